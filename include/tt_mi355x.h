@@ -1,0 +1,219 @@
+/*
+ * tt_mi355x.h — C ABI of libtt_mi355x.so, the MI355X-native (gfx950) sparse + tower hot path of
+ * the two-tower training step of alexmillerdb/two_tower_recommender_model.
+ *
+ * Every entry point takes raw device pointers, sizes and a hipStream_t (passed as void*), is
+ * asynchronous on that stream, never allocates, frees or synchronises, and returns 0 on success
+ * or a non-zero status (a hipError_t value, or one of the TT_E* codes below). The message of the
+ * last failure on the calling thread is returned by tt_last_error_string(). No C++ exception
+ * crosses this boundary. The caller owns every buffer, including workspaces (size queries first).
+ *
+ * What each entry point replaces (reference call site -> the pinned third-party op it reaches):
+ *   tt_kjt_build_mod_dropzero  <- transform_to_torchrec_batch, 03_model_training.py:353-382
+ *                                 (host loop :356-365 + KeyedJaggedTensor.from_lengths_sync :367-371)
+ *   tt_complete_cumsum         <- torch.ops.fbgemm.asynchronous_complete_cumsum (KJT offsets,
+ *                                 KeyedJaggedTensor built at 03_model_training.py:367-371)
+ *   tt_kjt_permute             <- torch.ops.fbgemm.permute_2D_sparse_data (KJT.permute inside
+ *                                 ShardedEmbeddingBagCollection.input_dist, reached from
+ *                                 DistributedModelParallel at 03_model_training.py:812-815)
+ *   tt_block_bucketize         <- torch.ops.fbgemm.block_bucketize_sparse_features (row-wise
+ *                                 input_dist, same call site)
+ *   tt_pooled_fwd              <- EmbeddingBagCollection.forward / FBGEMM TBE forward
+ *                                 (self.ebc(kjt), 03_model_training.py:417)
+ *   tt_bwd_prepare +
+ *   tt_bwd_rowwise_adagrad     <- TBE backward with EXACT_ROWWISE_ADAGRAD fused in backward
+ *                                 (_apply_optimizer_in_backward(RowWiseAdagrad, ...),
+ *                                 03_model_training.py:791-795)
+ *   tt_pooled_bwd_dense        <- nn.EmbeddingBag dense backward (unfused EBC, no optimizer in bwd)
+ *   tt_linear_fwd / _bwd_data /
+ *   tt_linear_bwd_weight       <- torchrec.modules.mlp.MLP / Perceptron (Linear + ReLU every layer),
+ *                                 query_proj / candidate_proj, 03_model_training.py:411-412,:420-436
+ *   tt_dot_bce_fwd_bwd         <- TwoTowerTrainTask.forward, 03_model_training.py:447-455
+ *                                 ((q*c).sum(1).squeeze() + BCEWithLogitsLoss(mean) + its backward)
+ *   tt_adam_step               <- KeyedOptimizerWrapper(torch.optim.Adam), 03_model_training.py:826-829
+ */
+#ifndef TT_MI355X_H
+#define TT_MI355X_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TT_ABI_VERSION 1
+
+/* status codes (besides hipError_t values, which are all < 1000) */
+#define TT_OK 0
+#define TT_EINVAL 1001      /* bad argument (shape, dtype, null pointer, limit exceeded) */
+#define TT_ECAPACITY 1002   /* workspace too small for the requested lookups */
+
+/* dtypes used at the boundary */
+#define TT_I32 0
+#define TT_I64 1
+#define TT_F32 2
+#define TT_BF16 3
+
+/* pooling modes (torchrec PoolingType) */
+#define TT_POOL_SUM 0
+#define TT_POOL_MEAN 1
+
+#define TT_MAX_FEATURES 64
+#define TT_MAX_TABLES 64
+
+/* One embedding table resident in a flat fp32 weight buffer (FBGEMM-TBE style "weights" +
+ * "weights_offsets"), with its row-wise optimizer state in a flat fp32 buffer. */
+typedef struct {
+  int64_t weight_offset; /* element offset of row 0 in the flat weight buffer */
+  int64_t state_offset;  /* element offset of row 0 in the flat row-wise state buffer */
+  int64_t num_rows;      /* rows held by this shard (local rows) */
+  int32_t dim;           /* embedding dim D (any value >= 1; D % 4 == 0 is the fast path) */
+  int32_t _pad;
+} tt_table_meta_t;
+
+/* One KJT key (feature) -> its table and its column range in the pooled [B, ldo] output. */
+typedef struct {
+  int32_t table;      /* index into the table array */
+  int32_t out_offset; /* first column of this feature in the pooled output row */
+} tt_feature_meta_t;
+
+const char* tt_last_error_string(void);
+int tt_abi_version(void);
+/* number of exported compute entry points (used by the loader to check the symbol table) */
+int tt_num_entry_points(void);
+
+/* ---- a1/a2: KeyedJaggedTensor build + offsets --------------------------------------------- */
+
+/* Workspace bytes needed by tt_kjt_build_mod_dropzero for n = F*B elements. */
+size_t tt_kjt_build_workspace_bytes(int64_t n);
+
+/* For key f in [0,F) and row b in [0,B): id = cols[f][b]. If id != 0 ("if value:",
+ * 03_model_training.py:358) the element contributes value id mod num_embeddings[f] (Python/torch
+ * floor-mod: result in [0, N)) and length 1, else length 0. Values are compacted key-major in
+ * (f, b) order, exactly like the reference's host loop. cols is a HOST array of F device pointers
+ * of dtype id_dtype; values_out (capacity F*B, dtype id_dtype), lengths_out [F*B] int32,
+ * offsets_out [F*B+1] int32 (complete cumsum), length_per_key_out [F] int64 (nullable). */
+int tt_kjt_build_mod_dropzero(int F, int64_t B, const void* const* cols, int id_dtype,
+                              const int64_t* num_embeddings, void* values_out,
+                              int32_t* lengths_out, int32_t* offsets_out,
+                              int64_t* length_per_key_out, void* workspace, size_t ws_bytes,
+                              void* stream);
+
+size_t tt_complete_cumsum_workspace_bytes(int64_t n);
+/* offsets[0] = 0, offsets[i+1] = sum(lengths[0..i]); n may be 0. */
+int tt_complete_cumsum(const int32_t* lengths, int64_t n, int32_t* offsets, void* workspace,
+                       size_t ws_bytes, void* stream);
+
+/* permute_2D_sparse_data: keys of a [F][B] jagged tensor reordered by perm (HOST array of F_out
+ * key indices, repeats allowed). out_offsets [F_out*B+1]. values may carry optional fp32
+ * per-value weights (weights/out_weights nullable). out_values capacity must be >= the permuted
+ * total, which the caller bounds (e.g. by the input total when perm is a permutation). */
+int tt_kjt_permute(int F, int64_t B, const int32_t* lengths, const int32_t* offsets,
+                   const void* values, int id_dtype, const float* weights, const int32_t* perm,
+                   int F_out, int32_t* out_lengths, int32_t* out_offsets, void* out_values,
+                   float* out_weights, void* stream);
+
+size_t tt_block_bucketize_workspace_bytes(int F, int64_t B, int W);
+/* block_bucketize_sparse_features (row-wise input_dist), keep_orig_idx = false:
+ * for id in bag (f,b): bs = block_sizes[f] (host); p = id < bs*W ? id / bs : id % W;
+ * local = id < bs*W ? id % bs : id / W. Output is bucket-major [W][F][B]: new_lengths
+ * [W*F*B], new_offsets [W*F*B+1], new_values (capacity = input total), order inside a
+ * (bucket, bag) = input order. */
+int tt_block_bucketize(int F, int64_t B, const int32_t* lengths, const int32_t* offsets,
+                       const void* values, int id_dtype, const int64_t* block_sizes, int W,
+                       int32_t* new_lengths, int32_t* new_offsets, void* new_values,
+                       void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a4: pooled (segmented gather + sum) forward ------------------------------------------- */
+
+/* out[b, features[f].out_offset + d] = pool_{i in bag(f,b)} W_t[values[i], d] for every key f and
+ * row b; empty bags give 0. offsets [F*B+1] int32 (key-major KJT offsets). ldo = row stride of out
+ * in elements. bounds_check: 0 = trust ids; 1 = ids outside [0, num_rows) read row 0 (FBGEMM
+ * BoundsCheckMode.WARNING) and are counted into *err_count (device int32, nullable). */
+int tt_pooled_fwd(const float* weights, const tt_table_meta_t* tables, int T,
+                  const tt_feature_meta_t* features, int F, int64_t B, const void* values,
+                  int id_dtype, const int32_t* offsets, int pooling, float* out, int64_t ldo,
+                  int bounds_check, int32_t* err_count, void* stream);
+
+/* ---- a8: deduplicated backward + fused exact row-wise Adagrad -------------------------------- */
+
+/* Workspace for up to max_lookups ids per step. Must be zeroed once by tt_bwd_workspace_init;
+ * tt_bwd_rowwise_adagrad leaves it clean again for the next step. */
+size_t tt_bwd_workspace_bytes(int64_t max_lookups);
+int tt_bwd_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
+
+/* Group the step's lookups by unique (table,row): hash insert, count, scan, scatter. Depends only
+ * on the ids, so it may run concurrently with the forward and the towers. */
+int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
+                   int64_t B, const void* values, int id_dtype, const int32_t* offsets,
+                   int bounds_check, void* workspace, size_t ws_bytes, int64_t max_lookups,
+                   void* stream);
+
+/* For every unique row r of table t touched this step:
+ *   G[r]   = sum over its lookups of grad_out[b, out_offset(f) : +D]  (x 1/len for MEAN pooling)
+ *   s[r]  += mean_d G[r,d]^2
+ *   W[r,d] = W[r,d] + (-lr * G[r,d]) / (sqrt(s[r]) + eps)
+ * (torchrec RowWiseAdagrad, lr_decay = weight_decay = 0). deterministic: 1 = segments of <= 64
+ * lookups are summed in sorted-bag order (bitwise reproducible), longer ones in fp64. */
+int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                           int F, int64_t B, const float* grad_out, int64_t ldg,
+                           const int32_t* offsets, int pooling, float* weights, float* state,
+                           float lr, float eps, void* workspace, size_t ws_bytes,
+                           int64_t max_lookups, void* stream);
+
+/* Unfused backward: grad_weights (flat, same layout as weights) += scatter of grad_out rows.
+ * Uses fp32 atomics (summation order not fixed). */
+int tt_pooled_bwd_dense(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                        int F, int64_t B, const float* grad_out, int64_t ldg, const void* values,
+                        int id_dtype, const int32_t* offsets, int pooling, float* grad_weights,
+                        int bounds_check, void* stream);
+
+/* ---- a6: tower GEMMs on bf16 MFMA (fp32 accumulate) ------------------------------------------ */
+
+/* A grouped launch runs `groups` (1 or 2: the two towers) independent problems of equal shape.
+ * Pointer arrays are HOST arrays of `groups` device pointers. */
+
+/* Y[m,n] = act(sum_k X[m,k] W[n,k] + bias[n]); X fp32 or bf16 (x_dtype), W [N,K] fp32 row-major
+ * (nn.Linear layout), bias nullable, act = relu if relu != 0. Y fp32 with row stride ldy. */
+int tt_linear_fwd(int groups, const void* const* X, int x_dtype, int64_t ldx,
+                  const float* const* W, const float* const* bias, int64_t M, int N, int K,
+                  float* const* Y, int64_t ldy, int relu, void* stream);
+
+/* dX[m,k] = sum_n dZ[m,n] W[n,k], dZ = dY * (Y > 0) if relu (Y nullable when relu == 0). */
+int tt_linear_bwd_data(int groups, const float* const* dY, const float* const* Y, int64_t ldy,
+                       const float* const* W, int64_t M, int N, int K, float* const* dX,
+                       int64_t ldx, int relu, void* stream);
+
+size_t tt_linear_bwd_weight_workspace_bytes(int groups, int64_t M, int N, int K);
+/* dW[n,k] = sum_m dZ[m,n] X[m,k]; db[n] = sum_m dZ[m,n] (db nullable). Split over M with fp32
+ * slabs in the workspace, summed in a fixed order (bitwise reproducible). */
+int tt_linear_bwd_weight(int groups, const float* const* dY, const float* const* Y, int64_t ldy,
+                         const void* const* X, int x_dtype, int64_t ldx, int64_t M, int N, int K,
+                         float* const* dW, float* const* db, int relu, void* workspace,
+                         size_t ws_bytes, void* stream);
+
+/* ---- a7: logits = sum_d q*c ; loss = mean BCEWithLogits ; dlogit = (sigmoid - y) / B ---------- */
+
+size_t tt_dot_bce_workspace_bytes(int64_t B);
+/* Must be zeroed once (tt_dot_bce_workspace_init); each call leaves it clean. labels: TT_I32,
+ * TT_I64 or TT_F32. logits [B] fp32; loss scalar fp32 (mean); dq/dc (nullable: forward only)
+ * receive dlogit*c and dlogit*q, scaled by grad_scale (d loss_total / d loss). */
+int tt_dot_bce_workspace_init(void* workspace, size_t ws_bytes, int64_t B, void* stream);
+int tt_dot_bce_fwd_bwd(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t B,
+                       int dim, const void* labels, int label_dtype, float* logits, float* loss,
+                       float* dq, int64_t lddq, float* dc, int64_t lddc, float grad_scale,
+                       void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a9: Adam on the flat dense-parameter buffer (torch.optim.Adam, amsgrad=False) ------------ */
+
+/* step_state: device int64[2] = {steps taken so far, arrival counter (0)}; the kernel uses
+ * t = step_state[0] + 1 and advances it, so the call is graph-replayable. */
+int tt_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                 float lr, float beta1, float beta2, float eps, float weight_decay,
+                 int64_t* step_state, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TT_MI355X_H */

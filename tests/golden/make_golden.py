@@ -1,0 +1,172 @@
+"""Generate the committed golden vectors by EXECUTING the reference's own hot-path code.
+
+Run in the build container only (it reads /root/reference, which does not exist on the GPU box):
+
+    python tests/golden/make_golden.py
+
+What it does: parses /root/reference/03_model_training.py with ``ast`` and executes, unmodified,
+the top-level definitions ``transform_to_torchrec_batch`` (03:353-380), ``TwoTower`` (03:395-437),
+``TwoTowerTrainTask`` (03:440-455) and ``batched`` (03:467-470) in a namespace whose torchrec names
+are bound to the CPU restatement in ``oracle/torchrec_cpu.py`` (torchrec itself is not installable
+offline). The training step around them follows ``TrainPipelineSparseDist.progress``: forward,
+``loss.backward()``, RowWiseAdagrad on the EBC tables (the in-backward optimizer of 03:791-795,
+restated in oracle/ref.py) and ``torch.optim.Adam`` on the MLPs (KeyedOptimizerWrapper, 03:826-829).
+Nothing from the reference is written out except these numeric inputs/outputs (npz fixtures).
+"""
+from __future__ import annotations
+
+import ast
+import itertools
+import sys
+from pathlib import Path
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+from torch import nn
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+
+from oracle import ref  # noqa: E402
+from oracle import torchrec_cpu as trc  # noqa: E402
+
+REF_FILE = Path("/root/reference/03_model_training.py")
+OUT = Path(__file__).resolve().parent
+WANT = ("transform_to_torchrec_batch", "TwoTower", "TwoTowerTrainTask", "batched")
+
+
+def load_reference_fragments(cat_cols):
+    tree = ast.parse(REF_FILE.read_text())
+    nodes = [n for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef)) and n.name in WANT]
+    assert sorted(n.name for n in nodes) == sorted(WANT), [n.name for n in nodes]
+    mod = ast.Module(body=nodes, type_ignores=[])
+    ns = dict(
+        torch=torch, nn=nn, List=List, Optional=Optional, Tuple=Tuple, itertools=itertools,
+        KeyedJaggedTensor=trc.KeyedJaggedTensor, Batch=trc.Batch,
+        EmbeddingBagCollection=trc.EmbeddingBagCollection, MLP=trc.MLP, cat_cols=cat_cols,
+    )
+    exec(compile(mod, str(REF_FILE), "exec"), ns)
+    return ns
+
+
+def kjt_cases():
+    """a1 golden vectors: the reference transform on int32/int64 columns with zeros, ids >= N,
+    negative ids, and an all-zero batch."""
+    cat_cols = ["user_id", "product_id"]
+    ns = load_reference_fragments(cat_cols)
+    g = torch.Generator().manual_seed(11)
+    cases = {}
+    specs = [
+        ("i32", torch.int32, 64, [1000, 1500], 0.1),
+        ("i64", torch.int64, 48, [777, 5], 0.2),
+        ("big", torch.int64, 32, [3, 2**33 + 7], 0.0),
+        ("allzero", torch.int32, 16, [10, 10], 1.0),
+    ]
+    for name, dt, B, N, pz in specs:
+        cols = {}
+        for ci, c in enumerate(cat_cols):
+            hi = N[ci] * 3 if name != "big" else 2**40
+            x = torch.randint(-N[ci], hi, (B,), generator=g, dtype=torch.int64)
+            x[torch.rand(B, generator=g) < pz] = 0
+            cols[c] = x.to(dt)
+        cols["label"] = torch.randint(0, 2, (B,), generator=g, dtype=torch.int64)
+        batch = ns["transform_to_torchrec_batch"](cols, num_embeddings_per_feature=N)
+        kjt = batch.sparse_features
+        cases[name] = dict(
+            user_id=cols["user_id"].numpy(), product_id=cols["product_id"].numpy(), label=cols["label"].numpy(),
+            num_embeddings=np.asarray(N, np.int64),
+            values=kjt.values().numpy(), lengths=kjt.lengths().numpy(), offsets=kjt.offsets().numpy(),
+            labels_out=batch.labels.numpy(),
+        )
+    for name, d in cases.items():
+        np.savez_compressed(OUT / f"kjt_{name}.npz", **d)
+    print("kjt cases:", list(cases))
+
+
+def train_case(name, num_users, num_items, D, B, layers, steps, seed, zipf=False, lr=0.01):
+    """a4-a9 golden vectors: ``steps`` training steps of the reference TwoTowerTrainTask."""
+    cat_cols = ["user_id", "product_id"]
+    ns = load_reference_fragments(cat_cols)
+    torch.manual_seed(seed)
+    g = torch.Generator().manual_seed(seed)
+    emb_counts = [num_users, num_items]
+    eb_configs = [
+        trc.EmbeddingBagConfig(name=f"t_{f}", embedding_dim=D, num_embeddings=emb_counts[i], feature_names=[f])
+        for i, f in enumerate(cat_cols)
+    ]
+    ebc = trc.EmbeddingBagCollection(tables=eb_configs)
+    with torch.no_grad():  # torchrec EBC default init U(-sqrt(1/N), sqrt(1/N))
+        for cfg in eb_configs:
+            a = (1.0 / cfg.num_embeddings) ** 0.5
+            ebc.embedding_bags[cfg.name].weight.uniform_(-a, a, generator=g)
+    two_tower = ns["TwoTower"](embedding_bag_collection=ebc, layer_sizes=layers, device=None)
+    task = ns["TwoTowerTrainTask"](two_tower)
+    dense = [p for n, p in task.named_parameters() if "embedding_bags" not in n]
+    adam = torch.optim.Adam(dense, lr=lr)
+    states = [torch.zeros(n) for n in emb_counts]
+    rec = {
+        "init_t_user_id": ebc.embedding_bags["t_user_id"].weight.detach().clone().numpy(),
+        "init_t_product_id": ebc.embedding_bags["t_product_id"].weight.detach().clone().numpy(),
+        "layers": np.asarray(layers, np.int64), "D": np.int64(D), "B": np.int64(B), "steps": np.int64(steps),
+        "num_embeddings": np.asarray(emb_counts, np.int64), "lr": np.float32(lr),
+    }
+    for n, p in task.named_parameters():
+        if "embedding_bags" not in n:
+            rec["init_" + n] = p.detach().clone().numpy()
+    for s in range(steps):
+        cols = {}
+        for ci, c in enumerate(cat_cols):
+            if zipf:
+                r = torch.distributions.Pareto(1.0, 0.35).sample((B,)).floor().to(torch.int64)
+                x = (r * 7919) % (emb_counts[ci] * 2)
+            else:
+                x = torch.randint(0, emb_counts[ci] * 2, (B,), generator=g, dtype=torch.int64)
+            x[torch.rand(B, generator=g) < 0.05] = 0
+            cols[c] = x
+        cols["label"] = torch.randint(0, 2, (B,), generator=g, dtype=torch.int64)
+        batch = ns["transform_to_torchrec_batch"](cols, num_embeddings_per_feature=emb_counts)
+        task.zero_grad(set_to_none=True)
+        kt_holder = {}
+        orig_fwd = ebc.forward
+
+        def hooked(kjt):
+            kt = orig_fwd(kjt)
+            kt.values.retain_grad()
+            kt_holder["kt"] = kt
+            return kt
+
+        ebc.forward = hooked
+        loss, (loss_d, logits, labels) = task(batch)
+        ebc.forward = orig_fwd
+        loss.backward()
+        pooled = kt_holder["kt"].values
+        for ti, cfg in enumerate(eb_configs):
+            wgt = ebc.embedding_bags[cfg.name].weight
+            with torch.no_grad():
+                ref.rowwise_adagrad(wgt.data, states[ti], wgt.grad, lr, 1e-10)
+        adam.step()
+        rec.update({
+            f"s{s}_user_id": cols["user_id"].numpy(), f"s{s}_product_id": cols["product_id"].numpy(),
+            f"s{s}_label": cols["label"].numpy(),
+            f"s{s}_values": batch.sparse_features.values().numpy(),
+            f"s{s}_offsets": batch.sparse_features.offsets().numpy(),
+            f"s{s}_loss": loss_d.numpy(), f"s{s}_logits": logits.numpy(),
+            f"s{s}_pooled": pooled.detach().numpy(), f"s{s}_pooled_grad": pooled.grad.numpy(),
+        })
+    for ti, cfg in enumerate(eb_configs):
+        rec[f"final_{cfg.name}"] = ebc.embedding_bags[cfg.name].weight.detach().numpy()
+        rec[f"final_state_{cfg.name}"] = states[ti].numpy()
+    for n, p in task.named_parameters():
+        if "embedding_bags" not in n:
+            rec["final_" + n] = p.detach().numpy()
+    np.savez_compressed(OUT / f"train_{name}.npz", **rec)
+    print("train case:", name, "final loss", float(rec[f"s{steps-1}_loss"]))
+
+
+if __name__ == "__main__":
+    kjt_cases()
+    # config-1 shape family (plumbing), shrunk to keep fixtures small
+    train_case("c1", num_users=1000, num_items=1200, D=16, B=256, layers=[16, 8], steps=3, seed=0)
+    train_case("zipf", num_users=500, num_items=800, D=32, B=128, layers=[32, 16], steps=3, seed=1, zipf=True)
+    train_case("d128", num_users=300, num_items=400, D=128, B=64, layers=[128, 64], steps=2, seed=2)

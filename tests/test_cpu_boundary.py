@@ -1,0 +1,64 @@
+"""The C-ABI library loads on a GPU-less host and exports exactly what include/tt_mi355x.h declares;
+argument validation errors come back as status codes with a message (no compute is launched)."""
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _declared():
+    text = (ROOT / "include" / "tt_mi355x.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tt_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from two_tower_recommender_model_amd import _lib
+    from two_tower_recommender_model_amd.build import LIB, build
+
+    build()
+    return _lib.load()
+
+
+def test_every_declared_symbol_exported(lib):
+    from two_tower_recommender_model_amd import _lib
+    from two_tower_recommender_model_amd.build import LIB
+
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (tt_[a-z0-9_]+)", out))
+    declared = _declared()
+    assert declared, "header parse failed"
+    missing = [d for d in declared if d not in exported]
+    assert not missing, missing
+    assert sorted(_lib.SIGNATURES) == declared
+    assert lib.tt_num_entry_points() == len(_lib.COMPUTE_ENTRY_POINTS)
+    assert lib.tt_abi_version() == 1
+
+
+def test_errors_are_status_codes(lib):
+    rc = lib.tt_pooled_fwd(None, None, 0, None, 0, 0, None, 0, None, 0, None, 0, 0, None, None)
+    assert rc == 1001
+    assert b"table count" in lib.tt_last_error_string()
+    rc = lib.tt_linear_fwd(3, None, 2, 0, None, None, 1, 1, 1, None, 0, 1, None)
+    assert rc == 1001 and b"groups" in lib.tt_last_error_string()
+
+
+def test_workspace_queries(lib):
+    assert lib.tt_bwd_workspace_bytes(16384) > 16384 * 4 * 5
+    assert lib.tt_linear_bwd_weight_workspace_bytes(2, 8192, 128, 128) > 0
+    assert lib.tt_dot_bce_workspace_bytes(8192) >= 8192 * 4
+
+
+def test_product_path_has_no_cpu_fallback():
+    import torch
+
+    from two_tower_recommender_model_amd import _lib, ops
+
+    with pytest.raises(_lib.TTError):
+        ops.complete_cumsum(torch.zeros(4, dtype=torch.int32))
+    src = "\n".join(p.read_text() for p in (ROOT / "two_tower_recommender_model_amd").rglob("*.py"))
+    assert "import oracle" not in src and "from oracle" not in src

@@ -1,0 +1,261 @@
+"""Parity of every C-ABI kernel against the oracle on the GPU (``-m gpu``).
+
+Tolerances: integer/index outputs bit-exact; fp32 embedding path rtol 1e-5 / atol 1e-6*max(1,L)
+(summation order); bf16-MFMA tower GEMMs vs fp32 torch: |err| <= 2e-2 * (|ref| + scale)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from two_tower_recommender_model_amd import ops as _ops
+
+    return _ops
+
+
+@pytest.mark.parametrize("case", ["i32", "i64", "big", "allzero"])
+def test_kjt_build_bit_exact_vs_reference_golden(ops, device, case):
+    g = load_golden(f"kjt_{case}.npz")
+    dt = torch.from_numpy(g["user_id"]).dtype
+    cols = [torch.from_numpy(g["user_id"]).to(device), torch.from_numpy(g["product_id"]).to(device)]
+    values, lengths, offsets, lpk = ops.kjt_build_mod_dropzero(cols, list(g["num_embeddings"]))
+    torch.cuda.synchronize()
+    n = int(offsets[-1])
+    np.testing.assert_array_equal(lengths.cpu().numpy(), g["lengths"])
+    np.testing.assert_array_equal(offsets.cpu().numpy(), g["offsets"])
+    if g["values"].size:
+        assert values.dtype == dt
+        np.testing.assert_array_equal(values[:n].cpu().numpy(), g["values"])
+    else:
+        assert n == 0
+    B = g["user_id"].size
+    np.testing.assert_array_equal(lpk.cpu().numpy(), [g["lengths"][:B].sum(), g["lengths"][B:].sum()])
+
+
+@pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 70000])
+def test_complete_cumsum(ops, device, n):
+    x = torch.randint(0, 5, (n,), dtype=torch.int32)
+    out = ops.complete_cumsum(x.to(device)).cpu().numpy()
+    np.testing.assert_array_equal(out, ref.complete_cumsum(x.numpy()))
+
+
+def test_kjt_build_large_scan(ops, device):
+    g = torch.Generator().manual_seed(3)
+    B = 50000
+    cols = [torch.randint(0, 5, (B,), generator=g, dtype=torch.int64) for _ in range(3)]
+    N = [3, 7, 2**31 + 11]
+    values, lengths, offsets, _ = ops.kjt_build_mod_dropzero([c.to(device) for c in cols], N)
+    v, l, o = ref.kjt_build([c.numpy() for c in cols], N)
+    np.testing.assert_array_equal(offsets.cpu().numpy(), o)
+    np.testing.assert_array_equal(values[: o[-1]].cpu().numpy(), v)
+
+
+@pytest.mark.parametrize("perm", [[2, 0, 1], [1, 1, 0, 2], [0]])
+def test_kjt_permute(ops, device, perm):
+    rng = np.random.default_rng(0)
+    F_, B = 3, 33
+    lengths = rng.integers(0, 5, F_ * B).astype(np.int32)
+    values = rng.integers(0, 10**6, int(lengths.sum())).astype(np.int64)
+    weights = rng.random(values.size).astype(np.float32)
+    L = torch.from_numpy(lengths).to(device)
+    O = ops.complete_cumsum(L)
+    ol, oo, ov, ow = ops.kjt_permute(L, O, torch.from_numpy(values).to(device), F_, B, perm,
+                                     weights=torch.from_numpy(weights).to(device))
+    rl, rv, rw = ref.kjt_permute(lengths, values, F_, B, perm, weights)
+    np.testing.assert_array_equal(ol.cpu().numpy(), rl)
+    np.testing.assert_array_equal(oo.cpu().numpy(), ref.complete_cumsum(rl))
+    np.testing.assert_array_equal(ov.cpu().numpy(), rv)
+    np.testing.assert_array_equal(ow.cpu().numpy(), rw)
+
+
+@pytest.mark.parametrize("W", [2, 8])
+def test_block_bucketize(ops, device, W):
+    rng = np.random.default_rng(W)
+    F_, B = 3, 40
+    N = [100, 1000, 7]
+    lengths = rng.integers(0, 6, F_ * B).astype(np.int32)
+    offs = ref.complete_cumsum(lengths)
+    vals = []
+    for i in range(F_ * B):
+        vals.extend(rng.integers(0, N[i // B] + 3, lengths[i]).tolist())
+    values = np.asarray(vals, np.int64)
+    bs = [(n + W - 1) // W for n in N]
+    L = torch.from_numpy(lengths).to(device)
+    nl, no, nv = ops.block_bucketize(L, ops.complete_cumsum(L), torch.from_numpy(values).to(device), F_, B, bs, W)
+    rl, rv = ref.block_bucketize(lengths, values, F_, B, bs, W)
+    np.testing.assert_array_equal(nl.cpu().numpy(), rl)
+    np.testing.assert_array_equal(no.cpu().numpy(), ref.complete_cumsum(rl))
+    np.testing.assert_array_equal(nv.cpu().numpy(), rv)
+
+
+def _make_kjt(rng, F_, B, rows, maxlen, zipf=False, dtype=np.int64):
+    lengths = rng.integers(0 if maxlen > 1 else 1, maxlen + 1, F_ * B).astype(np.int32)
+    vals = []
+    for i in range(F_ * B):
+        n = rows[i // B]
+        if zipf:
+            v = (rng.zipf(1.3, lengths[i]) - 1) % n
+        else:
+            v = rng.integers(0, n, lengths[i])
+        vals.extend(v.tolist())
+    return lengths, np.asarray(vals, dtype=dtype)
+
+
+CASES = [
+    # (name, T, feature_table, rows, dims, B, maxlen, zipf, dtype)
+    ("d64_single", 2, [0, 1], [5000, 3000], [64, 64], 257, 1, False, np.int64),
+    ("d128_single_i32", 2, [0, 1], [4000, 6000], [128, 128], 300, 1, False, np.int32),
+    ("d16_multi", 2, [0, 1], [50, 80], [16, 16], 64, 20, False, np.int64),
+    ("mixed_dims_shared", 3, [0, 1, 2, 0], [700, 300, 900], [36, 4, 128], 77, 7, True, np.int64),
+    ("t16_d128", 16, list(range(16)), [2000] * 16, [128] * 16, 96, 1, False, np.int64),
+    ("zipf_hot", 2, [0, 1], [100, 50], [128, 64], 512, 3, True, np.int64),
+    ("odd_dim", 2, [0, 1], [100, 100], [3, 10], 50, 4, False, np.int64),
+    ("d512", 1, [0], [300], [512], 40, 3, True, np.int64),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("pooling", ["sum", "mean"])
+def test_pooled_fwd_and_fused_rowwise_adagrad(ops, device, case, pooling):
+    name, T, ft, rows, dims, B, maxlen, zipf, dtype = case
+    rng = np.random.default_rng(abs(hash(name)) % 2**31)
+    F_ = len(ft)
+    lengths, values = _make_kjt(rng, F_, B, [rows[t] for t in ft], maxlen, zipf, dtype)
+    offsets = ref.complete_cumsum(lengths)
+    ts = ops.TableSet(rows, dims, ft, device)
+    ts.init_uniform_(torch.Generator(device=device).manual_seed(5))
+    tables0 = [ts.table_view(t).cpu().clone() for t in range(T)]
+    V = torch.from_numpy(values).to(device)
+    O = torch.from_numpy(offsets).to(device)
+    pool = 1 if pooling == "mean" else 0
+    out = ts.pooled_fwd(V, O, B, pooling=pool)
+    want = ref.pooled_fwd(tables0, ft, torch.from_numpy(values), torch.from_numpy(offsets), B, pooling)
+    atol = 1e-6 * max(1, maxlen)
+    np.testing.assert_allclose(out.cpu().numpy(), want.numpy(), rtol=1e-5, atol=atol)
+    if maxlen == 1 and pooling == "sum":
+        # single-hot sum pooling is a pure gather: bit-exact
+        np.testing.assert_array_equal(out.cpu().numpy(), want.numpy())
+    # backward with fused row-wise Adagrad, 2 steps
+    lr, eps = 0.05, 1e-10
+    tabs = [t.clone() for t in tables0]
+    states = [torch.zeros(r) for r in rows]
+    for step in range(2):
+        gout = torch.randn(B, ts.out_dim, generator=torch.Generator().manual_seed(step))
+        grads = ref.pooled_bwd_dense(tabs, ft, torch.from_numpy(values), torch.from_numpy(offsets), B, gout, pooling)
+        for t in range(T):
+            ref.rowwise_adagrad(tabs[t], states[t], grads[t], lr, eps)
+        ts.bwd_prepare(V, O, B, max_lookups=max(1, values.size))
+        ts.bwd_rowwise_adagrad(gout.to(device), O, B, lr, eps, pooling=pool)
+    torch.cuda.synchronize()
+    for t in range(T):
+        np.testing.assert_allclose(ts.table_view(t).cpu().numpy(), tabs[t].numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(ts.state_view(t).cpu().numpy(), states[t].numpy(), rtol=1e-5, atol=1e-9)
+
+
+def test_fused_adagrad_deterministic(ops, device):
+    rng = np.random.default_rng(7)
+    B, rows = 2048, [64, 4096]
+    lengths, values = _make_kjt(rng, 2, B, rows, 4, zipf=True)
+    offsets = torch.from_numpy(ref.complete_cumsum(lengths)).to(device)
+    V = torch.from_numpy(values).to(device)
+    gout = torch.randn(B, 256, device=device)
+    results = []
+    for _ in range(2):
+        ts = ops.TableSet(rows, [128, 128], [0, 1], device)
+        ts.init_uniform_(torch.Generator(device=device).manual_seed(1))
+        ts.bwd_prepare(V, offsets, B, values.size)
+        ts.bwd_rowwise_adagrad(gout, offsets, B, 0.1, 1e-10)
+        results.append(ts.weights.clone())
+    assert torch.equal(results[0], results[1])
+
+
+def test_pooled_bwd_dense(ops, device):
+    rng = np.random.default_rng(9)
+    B, rows, ft = 100, [300, 200], [0, 1, 1]
+    lengths, values = _make_kjt(rng, 3, B, [rows[t] for t in ft], 5)
+    offsets = ref.complete_cumsum(lengths)
+    ts = ops.TableSet(rows, [32, 32], ft, device)
+    ts.init_uniform_()
+    gout = torch.randn(B, ts.out_dim)
+    gw = torch.zeros_like(ts.weights)
+    ts.bwd_dense(gout.to(device), torch.from_numpy(values).to(device), torch.from_numpy(offsets).to(device), B, gw)
+    want = ref.pooled_bwd_dense([ts.table_view(t).cpu() for t in range(2)], ft, torch.from_numpy(values),
+                                torch.from_numpy(offsets), B, gout)
+    for t in range(2):
+        o = ts.weight_offsets[t]
+        got = gw[o:o + rows[t] * 32].view(rows[t], 32).cpu()
+        np.testing.assert_allclose(got.numpy(), want[t].numpy(), rtol=1e-5, atol=1e-5)
+
+
+def _bf16_close(got, want, tol=2e-2):
+    got = got.double()
+    want = want.double()
+    scale = want.abs().max().item() + 1e-6
+    err = (got - want).abs()
+    assert (err <= tol * (want.abs() + 0.1 * scale)).all(), f"max err {err.max().item()} scale {scale}"
+
+
+@pytest.mark.parametrize("M,N,K,groups,xbf16", [(4096, 128, 64, 2, False), (1000, 64, 128, 1, False),
+                                                 (513, 128, 1024, 2, False), (77, 5, 36, 1, True)])
+def test_linear_fwd_bwd_vs_fp32(ops, device, M, N, K, groups, xbf16):
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    xs = [torch.randn(M, K, generator=g) for _ in range(groups)]
+    ws = [torch.randn(N, K, generator=g) / K**0.5 for _ in range(groups)]
+    bs = [torch.randn(N, generator=g) for _ in range(groups)]
+    xd = [x.to(device).to(torch.bfloat16) if xbf16 else x.to(device) for x in xs]
+    ys = ops.linear_fwd(xd, [w.to(device) for w in ws], [b.to(device) for b in bs], relu=True)
+    for i in range(groups):
+        xr = xd[i].float().cpu()
+        want = torch.relu(xr @ ws[i].T + bs[i])
+        _bf16_close(ys[i].cpu(), want)
+    # backward
+    dys = [torch.randn(M, N, generator=g) for _ in range(groups)]
+    dxs = ops.linear_bwd_data([d.to(device) for d in dys], ys, [w.to(device) for w in ws], relu=True)
+    dws, dbs = ops.linear_bwd_weight([d.to(device) for d in dys], ys, xd, relu=True)
+    for i in range(groups):
+        y = ys[i].cpu()
+        dz = dys[i] * (y > 0)
+        _bf16_close(dxs[i].cpu(), dz @ ws[i])
+        _bf16_close(dws[i].cpu(), dz.T @ xd[i].float().cpu())
+        np.testing.assert_allclose(dbs[i].cpu().numpy(), dz.sum(0).numpy(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,dim,ldt", [(8192, 64, torch.int32), (1, 8, torch.int64), (1000, 33, torch.float32)])
+def test_dot_bce(ops, device, B, dim, ldt):
+    g = torch.Generator().manual_seed(B)
+    q = torch.rand(B, dim, generator=g)
+    c = torch.rand(B, dim, generator=g)
+    y = torch.randint(0, 2, (B,), generator=g).to(ldt)
+    qq = q.clone().requires_grad_(True)
+    cc = c.clone().requires_grad_(True)
+    logits, loss = ref.dot_bce(qq, cc, y)
+    loss.backward()
+    k = ops.DotBCE(device, B)
+    dq = torch.empty(B, dim, device=device)
+    dc = torch.empty(B, dim, device=device)
+    for _ in range(2):  # second call checks the arrival counter was reset
+        lg, ls = k(q.to(device), c.to(device), y.to(device), dq=dq, dc=dc)
+    np.testing.assert_allclose(lg.cpu().numpy().reshape(-1), logits.detach().numpy().reshape(-1), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(float(ls), float(loss), rtol=1e-5)
+    np.testing.assert_allclose(dq.cpu().numpy(), qq.grad.numpy(), rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(dc.cpu().numpy(), cc.grad.numpy(), rtol=1e-4, atol=1e-8)
+
+
+def test_adam(ops, device):
+    g = torch.Generator().manual_seed(0)
+    p = torch.randn(49536, generator=g)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    pd, md, vd = p.to(device), m.to(device), v.to(device)
+    st = torch.zeros(2, dtype=torch.int64, device=device)
+    for step in range(1, 4):
+        grad = torch.randn(49536, generator=g)
+        ref.adam([p], [grad], [m], [v], step, lr=0.01)
+        ops.adam_step(pd, grad.to(device), md, vd, st, lr=0.01)
+    np.testing.assert_allclose(pd.cpu().numpy(), p.numpy(), rtol=1e-5, atol=1e-6)
+    assert int(st[0]) == 3 and int(st[1]) == 0

@@ -1,0 +1,188 @@
+"""ctypes binding of the C ABI in ``include/tt_mi355x.h`` (libtt_mi355x.so, gfx950).
+
+The library is loaded after ``import torch`` so that its ``libamdhip64.so.7`` dependency resolves to
+the HIP runtime torch already loaded (one runtime per process: torch's streams and device pointers
+are then valid in our kernels). There is no CPU fallback: if the library is missing or does not
+export every symbol the header declares, loading raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libtt_mi355x.so"
+
+TT_OK = 0
+TT_I32, TT_I64, TT_F32, TT_BF16 = 0, 1, 2, 3
+TT_POOL_SUM, TT_POOL_MEAN = 0, 1
+TT_MAX_FEATURES = 64
+TT_MAX_TABLES = 64
+
+
+class TableMeta(C.Structure):
+    _fields_ = [
+        ("weight_offset", C.c_int64),
+        ("state_offset", C.c_int64),
+        ("num_rows", C.c_int64),
+        ("dim", C.c_int32),
+        ("_pad", C.c_int32),
+    ]
+
+
+class FeatureMeta(C.Structure):
+    _fields_ = [("table", C.c_int32), ("out_offset", C.c_int32)]
+
+
+_vp = C.c_void_p
+_i32 = C.c_int32
+_i64 = C.c_int64
+_f32 = C.c_float
+_sz = C.c_size_t
+_int = C.c_int
+_pvp = C.POINTER(C.c_void_p)
+_pi64 = C.POINTER(C.c_int64)
+_pi32 = C.POINTER(C.c_int32)
+_ptm = C.POINTER(TableMeta)
+_pfm = C.POINTER(FeatureMeta)
+
+# name -> (restype, argtypes); the compute entry points are exactly those counted by
+# tt_num_entry_points() in csrc/api.cpp.
+SIGNATURES = {
+    "tt_last_error_string": (C.c_char_p, []),
+    "tt_abi_version": (_int, []),
+    "tt_num_entry_points": (_int, []),
+    "tt_kjt_build_workspace_bytes": (_sz, [_i64]),
+    "tt_kjt_build_mod_dropzero": (
+        _int,
+        [_int, _i64, _pvp, _int, _pi64, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
+    ),
+    "tt_complete_cumsum_workspace_bytes": (_sz, [_i64]),
+    "tt_complete_cumsum": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
+    "tt_kjt_permute": (
+        _int,
+        [_int, _i64, _vp, _vp, _vp, _int, _vp, _pi32, _int, _vp, _vp, _vp, _vp, _vp],
+    ),
+    "tt_block_bucketize_workspace_bytes": (_sz, [_int, _i64, _int]),
+    "tt_block_bucketize": (
+        _int,
+        [_int, _i64, _vp, _vp, _vp, _int, _pi64, _int, _vp, _vp, _vp, _vp, _sz, _vp],
+    ),
+    "tt_pooled_fwd": (
+        _int,
+        [_vp, _ptm, _int, _pfm, _int, _i64, _vp, _int, _vp, _int, _vp, _i64, _int, _vp, _vp],
+    ),
+    "tt_bwd_workspace_bytes": (_sz, [_i64]),
+    "tt_bwd_workspace_init": (_int, [_vp, _sz, _i64, _vp]),
+    "tt_bwd_prepare": (
+        _int,
+        [_ptm, _int, _pfm, _int, _i64, _vp, _int, _vp, _int, _vp, _sz, _i64, _vp],
+    ),
+    "tt_bwd_rowwise_adagrad": (
+        _int,
+        [_ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _int, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
+    ),
+    "tt_pooled_bwd_dense": (
+        _int,
+        [_ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _int, _vp, _int, _vp, _int, _vp],
+    ),
+    "tt_linear_fwd": (_int, [_int, _pvp, _int, _i64, _pvp, _pvp, _i64, _int, _int, _pvp, _i64, _int, _vp]),
+    "tt_linear_bwd_data": (_int, [_int, _pvp, _pvp, _i64, _pvp, _i64, _int, _int, _pvp, _i64, _int, _vp]),
+    "tt_linear_bwd_weight_workspace_bytes": (_sz, [_int, _i64, _int, _int]),
+    "tt_linear_bwd_weight": (
+        _int,
+        [_int, _pvp, _pvp, _i64, _pvp, _int, _i64, _i64, _int, _int, _pvp, _pvp, _int, _vp, _sz, _vp],
+    ),
+    "tt_dot_bce_workspace_bytes": (_sz, [_i64]),
+    "tt_dot_bce_workspace_init": (_int, [_vp, _sz, _i64, _vp]),
+    "tt_dot_bce_fwd_bwd": (
+        _int,
+        [_vp, _i64, _vp, _i64, _i64, _int, _vp, _int, _vp, _vp, _vp, _i64, _vp, _i64, _f32, _vp, _sz, _vp],
+    ),
+    "tt_adam_step": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _vp, _vp]),
+}
+
+COMPUTE_ENTRY_POINTS = [
+    "tt_kjt_build_mod_dropzero",
+    "tt_complete_cumsum",
+    "tt_kjt_permute",
+    "tt_block_bucketize",
+    "tt_pooled_fwd",
+    "tt_bwd_workspace_init",
+    "tt_bwd_prepare",
+    "tt_bwd_rowwise_adagrad",
+    "tt_pooled_bwd_dense",
+    "tt_linear_fwd",
+    "tt_linear_bwd_data",
+    "tt_linear_bwd_weight",
+    "tt_dot_bce_workspace_init",
+    "tt_dot_bce_fwd_bwd",
+    "tt_adam_step",
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+class TTError(RuntimeError):
+    pass
+
+
+def load(path: os.PathLike | None = None):
+    """Load (once) and return the ctypes library with argtypes set. Raises if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = Path(path) if path else LIB_PATH
+        if not p.exists():
+            raise TTError(
+                f"libtt_mi355x.so not found at {p}: build it with "
+                "`python -m two_tower_recommender_model_amd.build` (no CPU fallback exists)"
+            )
+        lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)  # AttributeError if a declared symbol is missing
+            fn.restype = res
+            fn.argtypes = args
+        if lib.tt_num_entry_points() != len(COMPUTE_ENTRY_POINTS):
+            raise TTError("libtt_mi355x.so entry-point count does not match the header")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != TT_OK:
+        msg = load().tt_last_error_string()
+        msg = msg.decode() if msg else ""
+        raise TTError(f"{what or 'tt call'} failed (status {rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device (or host) address of a tensor, or 0 for None."""
+    if t is None:
+        return 0
+    return t.data_ptr()
+
+
+def ptr_array(ts):
+    arr = (C.c_void_p * len(ts))()
+    for i, t in enumerate(ts):
+        arr[i] = ptr(t) if t is not None else None
+    return arr
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def id_dtype_code(dtype: torch.dtype) -> int:
+    if dtype == torch.int64:
+        return TT_I64
+    if dtype == torch.int32:
+        return TT_I32
+    raise TTError(f"ids must be int32 or int64, got {dtype}")

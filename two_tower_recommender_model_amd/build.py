@@ -1,0 +1,98 @@
+"""Build recipe of libtt_mi355x.so (gfx950 only), compiled in-tree with hipcc.
+
+    python -m two_tower_recommender_model_amd.build          # incremental
+    python -m two_tower_recommender_model_amd.build --force
+
+Each translation unit is compiled to an object in ``build/`` (parallel), then linked into
+``two_tower_recommender_model_amd/lib/libtt_mi355x.so``. The library travels to the GPU box with the
+repository snapshot (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+INCLUDE = ROOT / "include"
+BUILD = ROOT / "build" / "tt_mi355x"
+LIB = PKG / "lib" / "libtt_mi355x.so"
+ARCH = "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["api.cpp", "kjt.hip", "embedding.hip", "gemm.hip", "loss_adam.hip"]
+HEADERS = [CSRC / "tt_common.h", INCLUDE / "tt_mi355x.h"]
+
+CFLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    f"--offload-arch={ARCH}",
+    "-munsafe-fp-atomics",
+    f"-I{INCLUDE}",
+    f"-I{CSRC}",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _compile(src: Path, obj: Path) -> None:
+    lang = ["-x", "hip"] if src.suffix == ".hip" else ["-x", "hip"]
+    cmd = [HIPCC, *CFLAGS, *lang, "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    objs = []
+    jobs = []
+    for s in SOURCES:
+        src = CSRC / s
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src, *HEADERS]):
+            jobs.append((src, obj))
+    if jobs:
+        workers = min(len(jobs), max(1, min(8, os.cpu_count() or 1)))
+        with cf.ThreadPoolExecutor(workers) as ex:
+            futs = [ex.submit(_compile, s, o) for s, o in jobs]
+            for f in futs:
+                f.result()
+        if verbose:
+            print("compiled:", ", ".join(s.name for s, _ in jobs))
+    if force or jobs or _stale(LIB, objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+        if verbose:
+            print("linked", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    args = ap.parse_args()
+    try:
+        build(force=args.force, verbose=True)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

@@ -1,0 +1,49 @@
+// Error plumbing and small host helpers of the C ABI (no kernels here).
+#include <hip/hip_runtime.h>
+#include <string>
+#include "tt_common.h"
+
+namespace tt {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int pack_meta(EmbMeta& m, const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+              int F, int64_t B) {
+  if (T < 1 || T > TT_MAX_TABLES) return fail(TT_EINVAL, "table count out of range [1, 64]");
+  if (F < 1 || F > TT_MAX_FEATURES) return fail(TT_EINVAL, "feature count out of range [1, 64]");
+  if (B < 0) return fail(TT_EINVAL, "negative batch size");
+  if (!tables || !features) return fail(TT_EINVAL, "null table/feature metadata");
+  for (int t = 0; t < T; ++t) {
+    if (tables[t].dim < 1) return fail(TT_EINVAL, "table dim must be >= 1");
+    if (tables[t].num_rows < 0) return fail(TT_EINVAL, "negative table rows");
+    m.tables[t] = tables[t];
+  }
+  for (int f = 0; f < F; ++f) {
+    if (features[f].table < 0 || features[f].table >= T)
+      return fail(TT_EINVAL, "feature references a table index out of range");
+    if (features[f].out_offset < 0) return fail(TT_EINVAL, "negative feature output offset");
+    m.features[f] = features[f];
+  }
+  m.T = T;
+  m.F = F;
+  m.B = B;
+  return TT_OK;
+}
+
+}  // namespace tt
+
+extern "C" {
+
+const char* tt_last_error_string(void) { return tt::g_last_error.c_str(); }
+
+int tt_abi_version(void) { return TT_ABI_VERSION; }
+
+// tt_kjt_build_mod_dropzero, tt_complete_cumsum, tt_kjt_permute, tt_block_bucketize, tt_pooled_fwd,
+// tt_bwd_workspace_init, tt_bwd_prepare, tt_bwd_rowwise_adagrad, tt_pooled_bwd_dense,
+// tt_linear_fwd, tt_linear_bwd_data, tt_linear_bwd_weight, tt_dot_bce_workspace_init,
+// tt_dot_bce_fwd_bwd, tt_adam_step
+int tt_num_entry_points(void) { return 15; }
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// Shared helpers for the gfx950 kernels of libtt_mi355x.so (wave64, CDNA4).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+#include "tt_mi355x.h"
+
+#define TT_WAVE 64
+
+namespace tt {
+
+// thread-local last error, set by the host-side launch functions
+void set_error(const std::string& msg);
+
+inline int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return (int)e;
+  }
+  return TT_OK;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Kernel-argument bundle of the table / feature metadata (passed by value: graph-capturable, no
+// host->device copy per call). 64 tables x 32 B + 64 features x 8 B + 16 = 2.6 KB < 4 KB limit.
+struct EmbMeta {
+  tt_table_meta_t tables[TT_MAX_TABLES];
+  tt_feature_meta_t features[TT_MAX_FEATURES];
+  int32_t T;
+  int32_t F;
+  int64_t B;
+};
+
+int pack_meta(EmbMeta& m, const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+              int F, int64_t B);
+
+// --- device helpers -------------------------------------------------------------------------
+
+__device__ __forceinline__ int64_t load_id(const void* values, int id_dtype, int64_t i) {
+  return id_dtype == TT_I64 ? reinterpret_cast<const int64_t*>(values)[i]
+                            : (int64_t)reinterpret_cast<const int32_t*>(values)[i];
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace tt

@@ -1,0 +1,371 @@
+"""torch-tensor wrappers over the C ABI (libtt_mi355x.so). Device tensors only; every call is
+asynchronous on the current HIP stream and raises ``TTError`` on a non-zero status. There is no
+CPU fallback: a CPU tensor is an error.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import (TT_BF16, TT_F32, TT_I32, TT_I64, TT_POOL_MEAN, TT_POOL_SUM, FeatureMeta, TableMeta,
+                   check, id_dtype_code, ptr, ptr_array, stream_handle)
+
+
+def _lib_():
+    return _lib.load()
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.TTError("libtt_mi355x ops take device (HIP) tensors only; got a CPU tensor")
+
+
+_WS_CACHE = {}
+
+
+def scratch(nbytes: int, device: torch.device, key: str) -> torch.Tensor:
+    """Per-(device, key) reusable uint8 workspace that only grows (stream-ordered reuse)."""
+    k = (device.index if device.index is not None else torch.cuda.current_device(), key)
+    buf = _WS_CACHE.get(k)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        _WS_CACHE[k] = buf
+    return buf
+
+
+# ---- a1/a2 ------------------------------------------------------------------------------------
+
+
+def kjt_build_mod_dropzero(cols: Sequence[torch.Tensor], num_embeddings: Sequence[int],
+                           values_out: Optional[torch.Tensor] = None,
+                           lengths_out: Optional[torch.Tensor] = None,
+                           offsets_out: Optional[torch.Tensor] = None,
+                           length_per_key_out: Optional[torch.Tensor] = None):
+    """Vectorised transform_to_torchrec_batch (03_model_training.py:353-371). Returns
+    (values[capacity F*B], lengths[F*B] int32, offsets[F*B+1] int32, length_per_key[F] int64);
+    the valid values are values[:offsets[-1]]."""
+    F = len(cols)
+    B = cols[0].numel()
+    dev = cols[0].device
+    dt = cols[0].dtype
+    _dev(*cols)
+    for c in cols:
+        if c.dtype != dt or c.numel() != B or not c.is_contiguous():
+            raise _lib.TTError("kjt_build: columns must be contiguous, same dtype and length")
+    if values_out is None:
+        values_out = torch.empty(F * B, dtype=dt, device=dev)
+    if lengths_out is None:
+        lengths_out = torch.empty(F * B, dtype=torch.int32, device=dev)
+    if offsets_out is None:
+        offsets_out = torch.empty(F * B + 1, dtype=torch.int32, device=dev)
+    if length_per_key_out is None:
+        length_per_key_out = torch.empty(F, dtype=torch.int64, device=dev)
+    lib = _lib_()
+    nbytes = lib.tt_kjt_build_workspace_bytes(F * B)
+    ws = scratch(nbytes, dev, "kjt_build")
+    colp = ptr_array(list(cols))
+    ne = (C.c_int64 * F)(*[int(n) for n in num_embeddings])
+    check(lib.tt_kjt_build_mod_dropzero(F, B, colp, id_dtype_code(dt), ne, ptr(values_out), ptr(lengths_out),
+                                        ptr(offsets_out), ptr(length_per_key_out), ptr(ws), ws.numel(),
+                                        stream_handle(dev)), "kjt_build_mod_dropzero")
+    return values_out, lengths_out, offsets_out, length_per_key_out
+
+
+def complete_cumsum(lengths: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(lengths)
+    if lengths.dtype != torch.int32:
+        raise _lib.TTError("complete_cumsum: lengths must be int32")
+    lengths = lengths.contiguous()
+    n = lengths.numel()
+    if out is None:
+        out = torch.empty(n + 1, dtype=torch.int32, device=lengths.device)
+    lib = _lib_()
+    ws = scratch(lib.tt_complete_cumsum_workspace_bytes(n), lengths.device, "cumsum")
+    check(lib.tt_complete_cumsum(ptr(lengths), n, ptr(out), ptr(ws), ws.numel(), stream_handle(lengths.device)),
+          "complete_cumsum")
+    return out
+
+
+def kjt_permute(lengths: torch.Tensor, offsets: torch.Tensor, values: torch.Tensor, F: int, B: int,
+                perm: Sequence[int], weights: Optional[torch.Tensor] = None,
+                total: Optional[int] = None):
+    """permute_2D_sparse_data. ``total`` = number of permuted values (computed with one device->host
+    read when not given and perm is not a permutation)."""
+    _dev(lengths, offsets, values, weights)
+    F_out = len(perm)
+    if total is None:
+        if sorted(perm) == list(range(F)):
+            total = values.numel()
+        else:
+            o = offsets.cpu()
+            total = int(sum(int(o[(p + 1) * B]) - int(o[p * B]) for p in perm))
+    dev = lengths.device
+    out_lengths = torch.empty(F_out * B, dtype=torch.int32, device=dev)
+    out_offsets = torch.empty(F_out * B + 1, dtype=torch.int32, device=dev)
+    out_values = torch.empty(total, dtype=values.dtype, device=dev)
+    out_weights = torch.empty(total, dtype=torch.float32, device=dev) if weights is not None else None
+    p = (C.c_int32 * max(1, F_out))(*[int(x) for x in perm])
+    check(_lib_().tt_kjt_permute(F, B, ptr(lengths), ptr(offsets), ptr(values), id_dtype_code(values.dtype),
+                                 ptr(weights), p, F_out, ptr(out_lengths), ptr(out_offsets), ptr(out_values),
+                                 ptr(out_weights), stream_handle(dev)), "kjt_permute")
+    return out_lengths, out_offsets, out_values, out_weights
+
+
+def block_bucketize(lengths: torch.Tensor, offsets: torch.Tensor, values: torch.Tensor, F: int, B: int,
+                    block_sizes: Sequence[int], W: int, capacity: Optional[int] = None):
+    """block_bucketize_sparse_features: bucket-major [W][F][B] lengths/offsets + local ids."""
+    _dev(lengths, offsets, values)
+    dev = lengths.device
+    cap = values.numel() if capacity is None else capacity
+    new_lengths = torch.empty(W * F * B, dtype=torch.int32, device=dev)
+    new_offsets = torch.empty(W * F * B + 1, dtype=torch.int32, device=dev)
+    new_values = torch.empty(cap, dtype=values.dtype, device=dev)
+    lib = _lib_()
+    ws = scratch(lib.tt_block_bucketize_workspace_bytes(F, B, W), dev, "bucketize")
+    bsz = (C.c_int64 * F)(*[int(b) for b in block_sizes])
+    check(lib.tt_block_bucketize(F, B, ptr(lengths), ptr(offsets), ptr(values), id_dtype_code(values.dtype), bsz, W,
+                                 ptr(new_lengths), ptr(new_offsets), ptr(new_values), ptr(ws), ws.numel(),
+                                 stream_handle(dev)), "block_bucketize")
+    return new_lengths, new_offsets, new_values
+
+
+# ---- a4 / a8: embedding tables ----------------------------------------------------------------
+
+
+class TableSet:
+    """Flat fp32 weight buffer + flat row-wise state for T local tables (FBGEMM-TBE-style layout:
+    one allocation, per-table element offsets), with the feature->table map of a KJT.
+
+    ``dims[t]``, ``rows[t]``: table shapes; ``feature_table[f]``: table of KJT key f;
+    ``out_offsets[f]``: first column of key f in the pooled output (default: cumulative)."""
+
+    def __init__(self, rows: Sequence[int], dims: Sequence[int], feature_table: Sequence[int],
+                 device: torch.device, out_offsets: Optional[Sequence[int]] = None,
+                 weights: Optional[torch.Tensor] = None, align: int = 4):
+        self.rows = [int(r) for r in rows]
+        self.dims = [int(d) for d in dims]
+        self.T = len(self.rows)
+        self.feature_table = [int(t) for t in feature_table]
+        self.F = len(self.feature_table)
+        if not (1 <= self.T <= _lib.TT_MAX_TABLES and 1 <= self.F <= _lib.TT_MAX_FEATURES):
+            raise _lib.TTError("TableSet: 1..64 tables and features supported")
+        self.device = torch.device(device)
+        woff, soff = [], []
+        w = s = 0
+        for r, d in zip(self.rows, self.dims):
+            woff.append(w)
+            soff.append(s)
+            w += (r * d + align - 1) // align * align
+            s += r
+        self.weight_offsets = woff
+        self.state_offsets = soff
+        self.total_weights = w
+        self.total_rows = s
+        if weights is None:
+            weights = torch.empty(max(1, w), dtype=torch.float32, device=self.device)
+        self.weights = weights
+        self.state = torch.zeros(max(1, s), dtype=torch.float32, device=self.device)
+        if out_offsets is None:
+            out_offsets, o = [], 0
+            for t in self.feature_table:
+                out_offsets.append(o)
+                o += self.dims[t]
+        self.out_offsets = [int(o) for o in out_offsets]
+        self.out_dim = max(o + self.dims[t] for o, t in zip(self.out_offsets, self.feature_table))
+        self._tm = (TableMeta * self.T)()
+        for t in range(self.T):
+            self._tm[t].weight_offset = self.weight_offsets[t]
+            self._tm[t].state_offset = self.state_offsets[t]
+            self._tm[t].num_rows = self.rows[t]
+            self._tm[t].dim = self.dims[t]
+        self._fm = (FeatureMeta * self.F)()
+        for f, t in enumerate(self.feature_table):
+            self._fm[f].table = t
+            self._fm[f].out_offset = self.out_offsets[f]
+        self._bwd_ws = None
+        self._bwd_cap = 0
+        self.err_count = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    def table_view(self, t: int) -> torch.Tensor:
+        o = self.weight_offsets[t]
+        return self.weights[o:o + self.rows[t] * self.dims[t]].view(self.rows[t], self.dims[t])
+
+    def state_view(self, t: int) -> torch.Tensor:
+        o = self.state_offsets[t]
+        return self.state[o:o + self.rows[t]]
+
+    def init_uniform_(self, generator: Optional[torch.Generator] = None) -> None:
+        """torchrec EmbeddingBagCollection default init: U(-sqrt(1/N), sqrt(1/N)) per table."""
+        for t in range(self.T):
+            a = (1.0 / max(1, self.rows[t])) ** 0.5
+            self.table_view(t).uniform_(-a, a, generator=generator)
+
+    # -- forward
+    def pooled_fwd(self, values: torch.Tensor, offsets: torch.Tensor, B: int, pooling: int = TT_POOL_SUM,
+                   out: Optional[torch.Tensor] = None, bounds_check: bool = False) -> torch.Tensor:
+        _dev(values, offsets)
+        if offsets.dtype != torch.int32:
+            raise _lib.TTError("pooled_fwd: offsets must be int32")
+        if out is None:
+            out = torch.empty(B, self.out_dim, dtype=torch.float32, device=self.device)
+        ldo = out.stride(0) if out.dim() == 2 else self.out_dim
+        idt = id_dtype_code(values.dtype) if values.numel() else TT_I64
+        check(_lib_().tt_pooled_fwd(ptr(self.weights), self._tm, self.T, self._fm, self.F, B, ptr(values), idt,
+                                    ptr(offsets), pooling, ptr(out), ldo, 1 if bounds_check else 0,
+                                    ptr(self.err_count), stream_handle(self.device)), "pooled_fwd")
+        return out
+
+    # -- backward (dedup + fused row-wise Adagrad)
+    def ensure_bwd_workspace(self, max_lookups: int) -> None:
+        max_lookups = max(1, int(max_lookups))
+        if self._bwd_ws is not None and max_lookups <= self._bwd_cap:
+            return
+        cap = 1
+        while cap < max_lookups:
+            cap <<= 1
+        lib = _lib_()
+        nbytes = lib.tt_bwd_workspace_bytes(cap)
+        self._bwd_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self._bwd_cap = cap
+        check(lib.tt_bwd_workspace_init(ptr(self._bwd_ws), nbytes, cap, stream_handle(self.device)), "bwd_ws_init")
+
+    def bwd_prepare(self, values: torch.Tensor, offsets: torch.Tensor, B: int, max_lookups: int,
+                    bounds_check: bool = False) -> None:
+        self.ensure_bwd_workspace(max_lookups)
+        idt = id_dtype_code(values.dtype) if values.numel() else TT_I64
+        check(_lib_().tt_bwd_prepare(self._tm, self.T, self._fm, self.F, B, ptr(values), idt, ptr(offsets),
+                                     1 if bounds_check else 0, ptr(self._bwd_ws), self._bwd_ws.numel(),
+                                     self._bwd_cap, stream_handle(self.device)), "bwd_prepare")
+
+    def bwd_rowwise_adagrad(self, grad_out: torch.Tensor, offsets: torch.Tensor, B: int, lr: float,
+                            eps: float, pooling: int = TT_POOL_SUM) -> None:
+        _dev(grad_out)
+        if grad_out.dtype != torch.float32 or grad_out.stride(1) != 1:
+            raise _lib.TTError("bwd: grad_out must be fp32 with unit column stride")
+        check(_lib_().tt_bwd_rowwise_adagrad(self._tm, self.T, self._fm, self.F, B, ptr(grad_out),
+                                             grad_out.stride(0), ptr(offsets), pooling, ptr(self.weights),
+                                             ptr(self.state), float(lr), float(eps), ptr(self._bwd_ws),
+                                             self._bwd_ws.numel(), self._bwd_cap, stream_handle(self.device)),
+              "bwd_rowwise_adagrad")
+
+    def bwd_dense(self, grad_out: torch.Tensor, values: torch.Tensor, offsets: torch.Tensor, B: int,
+                  grad_weights: torch.Tensor, pooling: int = TT_POOL_SUM) -> None:
+        _dev(grad_out, grad_weights)
+        idt = id_dtype_code(values.dtype) if values.numel() else TT_I64
+        check(_lib_().tt_pooled_bwd_dense(self._tm, self.T, self._fm, self.F, B, ptr(grad_out), grad_out.stride(0),
+                                          ptr(values), idt, ptr(offsets), pooling, ptr(grad_weights), 0,
+                                          stream_handle(self.device)), "pooled_bwd_dense")
+
+
+# ---- a6: tower GEMMs --------------------------------------------------------------------------
+
+
+def _x_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return TT_F32
+    if t.dtype == torch.bfloat16:
+        return TT_BF16
+    raise _lib.TTError("linear: X must be fp32 or bf16")
+
+
+def linear_fwd(xs: Sequence[torch.Tensor], ws: Sequence[torch.Tensor], bs: Sequence[Optional[torch.Tensor]],
+               relu: bool = True, outs: Optional[Sequence[torch.Tensor]] = None) -> List[torch.Tensor]:
+    """Grouped Y_g = act(X_g W_g^T + b_g) on bf16 MFMA (fp32 accumulate); X row stride may be > K
+    (column slices of a KeyedTensor are consumed in place)."""
+    G = len(xs)
+    M, K = xs[0].shape
+    N = ws[0].shape[0]
+    dev = xs[0].device
+    _dev(*xs, *ws)
+    for x, w in zip(xs, ws):
+        if x.shape != (M, K) or x.stride(1) != 1 or w.shape != (N, K) or not w.is_contiguous():
+            raise _lib.TTError("linear_fwd: shape/stride mismatch")
+    if outs is None:
+        outs = [torch.empty(M, N, dtype=torch.float32, device=dev) for _ in range(G)]
+    check(_lib_().tt_linear_fwd(G, ptr_array(xs), _x_code(xs[0]), xs[0].stride(0), ptr_array(ws), ptr_array(bs),
+                                M, N, K, ptr_array(outs), outs[0].stride(0), 1 if relu else 0,
+                                stream_handle(dev)), "linear_fwd")
+    return list(outs)
+
+
+def linear_bwd_data(dys: Sequence[torch.Tensor], ys: Sequence[Optional[torch.Tensor]], ws: Sequence[torch.Tensor],
+                    relu: bool = True, outs: Optional[Sequence[torch.Tensor]] = None) -> List[torch.Tensor]:
+    G = len(dys)
+    M, N = dys[0].shape
+    K = ws[0].shape[1]
+    dev = dys[0].device
+    _dev(*dys, *ws)
+    if outs is None:
+        outs = [torch.empty(M, K, dtype=torch.float32, device=dev) for _ in range(G)]
+    check(_lib_().tt_linear_bwd_data(G, ptr_array(dys), ptr_array(ys if relu else [None] * G), dys[0].stride(0),
+                                     ptr_array(ws), M, N, K, ptr_array(outs), outs[0].stride(0), 1 if relu else 0,
+                                     stream_handle(dev)), "linear_bwd_data")
+    return list(outs)
+
+
+def linear_bwd_weight(dys: Sequence[torch.Tensor], ys: Sequence[Optional[torch.Tensor]], xs: Sequence[torch.Tensor],
+                      relu: bool = True, dws: Optional[Sequence[torch.Tensor]] = None,
+                      dbs: Optional[Sequence[Optional[torch.Tensor]]] = None):
+    G = len(dys)
+    M, N = dys[0].shape
+    K = xs[0].shape[1]
+    dev = dys[0].device
+    _dev(*dys, *xs)
+    if dws is None:
+        dws = [torch.empty(N, K, dtype=torch.float32, device=dev) for _ in range(G)]
+    if dbs is None:
+        dbs = [torch.empty(N, dtype=torch.float32, device=dev) for _ in range(G)]
+    lib = _lib_()
+    ws = scratch(lib.tt_linear_bwd_weight_workspace_bytes(G, M, N, K), dev, "bwd_weight")
+    check(lib.tt_linear_bwd_weight(G, ptr_array(dys), ptr_array(ys if relu else [None] * G), dys[0].stride(0),
+                                   ptr_array(xs), _x_code(xs[0]), xs[0].stride(0), M, N, K, ptr_array(dws),
+                                   ptr_array(dbs), 1 if relu else 0, ptr(ws), ws.numel(), stream_handle(dev)),
+          "linear_bwd_weight")
+    return list(dws), list(dbs)
+
+
+# ---- a7 / a9 ----------------------------------------------------------------------------------
+
+
+class DotBCE:
+    """logits = (q*c).sum(1); loss = BCEWithLogits mean; optional dq, dc (k5). Owns its workspace."""
+
+    def __init__(self, device: torch.device, max_batch: int):
+        self.device = torch.device(device)
+        self.max_batch = int(max_batch)
+        lib = _lib_()
+        self.nbytes = lib.tt_dot_bce_workspace_bytes(self.max_batch)
+        self.ws = torch.empty(self.nbytes, dtype=torch.uint8, device=self.device)
+        check(lib.tt_dot_bce_workspace_init(ptr(self.ws), self.nbytes, self.max_batch, stream_handle(self.device)),
+              "dot_bce_ws_init")
+
+    def __call__(self, q, c, labels, logits=None, loss=None, dq=None, dc=None, grad_scale: float = 1.0):
+        B, dim = q.shape
+        if B > self.max_batch:
+            raise _lib.TTError("DotBCE: batch exceeds workspace")
+        _dev(q, c, labels)
+        if logits is None:
+            logits = torch.empty(B, dtype=torch.float32, device=q.device)
+        if loss is None:
+            loss = torch.empty((), dtype=torch.float32, device=q.device)
+        ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}.get(labels.dtype)
+        if ldt is None:
+            raise _lib.TTError("DotBCE: labels must be int32/int64/float32")
+        check(_lib_().tt_dot_bce_fwd_bwd(ptr(q), q.stride(0), ptr(c), c.stride(0), B, dim, ptr(labels), ldt,
+                                         ptr(logits), ptr(loss), ptr(dq), dq.stride(0) if dq is not None else 0,
+                                         ptr(dc), dc.stride(0) if dc is not None else 0, float(grad_scale),
+                                         ptr(self.ws), self.nbytes, stream_handle(q.device)), "dot_bce")
+        return logits, loss
+
+
+def adam_step(params: torch.Tensor, grads: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
+              step_state: torch.Tensor, lr: float, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,
+              weight_decay: float = 0.0) -> None:
+    _dev(params, grads, exp_avg, exp_avg_sq, step_state)
+    check(_lib_().tt_adam_step(ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), params.numel(), float(lr),
+                               float(beta1), float(beta2), float(eps), float(weight_decay), ptr(step_state),
+                               stream_handle(params.device)), "adam_step")
