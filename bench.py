@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Benchmark: training pairs/s of the two-tower step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload northstar|config2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (default = BASELINE.json north star): synthetic 100M-item x 50M-user two-tower, emb_dim
+128, batch 8192 per GPU, towers [128, 64], single-hot ids uniform over each table (ids kept in HBM),
+labels Bernoulli(0.5), random-init weights. One "step" = the full training step: device KJT build,
+pooled forward, towers fwd (bf16 MFMA), dot + BCE, towers bwd, fused dedup + row-wise Adagrad on the
+tables, Adam on the towers.
+
+N = 1: the fused step replayed as one HIP graph. N > 1: DistributedModelParallel over RCCL (the
+tables row-wise sharded, towers data-parallel) — eager launches. Timing: W untimed steps, barrier +
+synchronize, K timed steps, synchronize + barrier, max over ranks; rank 0 prints ONE JSON line.
+Also reported: the embedding path's dominant kernel against the HBM roofline (HIP events on its
+own stream) and the CPU restatement's pairs/s on this host (rank 0, N = 1, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    # name: (num_users, num_items, dim, batch, layer_sizes)
+    "northstar": (50_000_000, 100_000_000, 128, 8192, [128, 64]),
+    "config2": (5_000_000, 10_000_000, 64, 4096, [128, 64]),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
+    ap.add_argument("--ids", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=2_000_000, help="table rows of the CPU sample")
+    ap.add_argument("--cpu-steps", type=int, default=20)
+    ap.add_argument("--kernel-iters", type=int, default=50)
+    return ap.parse_args()
+
+
+def synth_batches(num_users, num_items, B, n, device, ids, seed):
+    g = torch.Generator(device=device).manual_seed(seed)
+    out = []
+    for _ in range(n):
+        if ids == "uniform":
+            u = torch.randint(0, num_users, (B,), generator=g, device=device, dtype=torch.int64)
+            it = torch.randint(0, num_items, (B,), generator=g, device=device, dtype=torch.int64)
+        else:  # Zipf-like (s ~ 1.05) over randomly permuted ranks: heavy hot rows
+            def zipf(N):
+                u01 = torch.rand(B, generator=g, device=device, dtype=torch.float64)
+                r = torch.floor(torch.exp(u01 * torch.log(torch.tensor(float(N), device=device, dtype=torch.float64))))
+                return ((r.to(torch.int64) * 2654435761) % N)
+            u, it = zipf(num_users), zipf(num_items)
+        lab = torch.randint(0, 2, (B,), generator=g, device=device, dtype=torch.int32)
+        out.append(([u, it], lab))
+    return out
+
+
+def algorithmic_bytes(step, nnz: int, uniq: int):
+    """Per-launch algorithmic bytes (SURVEY.md 8(d) accounting, per kernel):
+    pooled_fwd : per lookup id (8) + row (4D); per bag offset (4) + pooled write (4D)
+    adagrad k2d: per lookup bag index (4) + grad row (4D); per unique row read+write row (8D),
+                 read+write state (8), segment/slot/key bookkeeping (20)."""
+    D = step.dims[0]
+    idb = 8 if step.id_dtype == torch.int64 else 4
+    nb = step.F * step.B
+    fwd = nnz * (idb + 4 * D) + nb * (4 + 4 * D)
+    k2d = nnz * (4 + 4 * D) + uniq * (8 * D + 8 + 20)
+    return fwd, k2d
+
+
+def time_kernel(fn, iters, pre=None):
+    """Average device time of fn() measured with HIP events on the stream it launches on."""
+    st = torch.cuda.current_stream()
+    tot = 0.0
+    for _ in range(iters):
+        if pre is not None:
+            pre()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        fn()
+        b.record(st)
+        b.synchronize()
+        tot += a.elapsed_time(b)
+    return tot / iters  # ms
+
+
+def cpu_baseline(args, num_users, num_items, D, B, layers):
+    """The oracle (CPU restatement of TorchRec's unsharded CPU path, sparse touched-row update) on
+    this host's cores, bounded sample: full B, D, towers; tables scaled to --cpu-rows rows."""
+    from oracle import ref
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    rows = min(args.cpu_rows, num_users), min(args.cpu_rows, num_items)
+    st = ref.init_state(list(rows), [D, D], [0, 1], [0], [1], layers, seed=0)
+    g = torch.Generator().manual_seed(0)
+    batches = []
+    for _ in range(4):
+        cols = [torch.randint(0, rows[0], (B,), generator=g), torch.randint(0, rows[1], (B,), generator=g)]
+        lab = torch.randint(0, 2, (B,), generator=g)
+        v, l, o = ref.kjt_build([c.numpy() for c in cols], list(rows))
+        batches.append((torch.from_numpy(v), torch.from_numpy(o), lab))
+    for i in range(2):
+        v, o, lab = batches[i % 4]
+        ref.train_step(st, v, o, B, lab, 0.01, 0.01)
+    t0 = time.perf_counter()
+    n = args.cpu_steps
+    for i in range(n):
+        v, o, lab = batches[i % 4]
+        ref.train_step(st, v, o, B, lab, 0.01, 0.01)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(n * B / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+        "sample": f"{n} steps of the oracle train_step (torch CPU fp32: embedding_bag sum, towers "
+                  f"{layers}, BCE, sparse row-wise Adagrad, Adam) at B={B}, D={D}, tables scaled to "
+                  f"{rows[0]}x{D} / {rows[1]}x{D} rows; host CPU {platform.processor() or platform.machine()}",
+    }
+
+
+def run_single(args):
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
+                             lr_dense=0.01, id_dtype=torch.int64, seed=0)
+    batches = synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1)
+    step.load_batch(*batches[0])
+    step.capture()
+    for i in range(args.warmup):
+        step.load_batch(*batches[i % len(batches)])
+        step.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step.load_batch(*batches[i % len(batches)])
+        step.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms = dt / args.steps * 1e3
+    value = args.steps * B / dt
+    loss = float(step.loss)
+    # ---- dominant embedding kernels vs the HBM roofline (HIP events, same stream)
+    nnz = int(step.offsets[-1])
+    uniq = int(torch.unique(step.values[:nnz] + (torch.arange(nnz, device=dev) >= int(step.offsets[B])) * (1 << 40)).numel())
+    fwd_bytes, k2d_bytes = algorithmic_bytes(step, nnz, uniq)
+    t_fwd = time_kernel(lambda: step.tables.pooled_fwd(step.values, step.offsets, B, out=step.pooled), args.kernel_iters)
+    t_k2d = time_kernel(lambda: step.tables.bwd_rowwise_adagrad(step.gpooled, step.offsets, B, 0.0, 1e-10),
+                        args.kernel_iters,
+                        pre=lambda: step.tables.bwd_prepare(step.values, step.offsets, B, max_lookups=step.F * B))
+    kern = {
+        "pooled_fwd": {"ms": round(t_fwd, 5), "bytes": fwd_bytes, "GB/s": round(fwd_bytes / t_fwd / 1e6, 1)},
+        "bwd_rowwise_adagrad": {"ms": round(t_k2d, 5), "bytes": k2d_bytes, "GB/s": round(k2d_bytes / t_k2d / 1e6, 1)},
+    }
+    dom = max(kern, key=lambda k: kern[k]["ms"])
+    ach = kern[dom]["GB/s"]
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": kern[dom]["bytes"],
+                "kernels": kern, "lookups": nnz, "unique_rows": uniq}
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, num_users, num_items, D, B, layers)
+    return value, ms, loss, roofline, cpu
+
+
+def run_multi(args, world, rank, local_rank):
+    import two_tower_recommender_model_amd as tt
+    from two_tower_recommender_model_amd.task import TwoTower, TwoTowerTrainTask
+    from two_tower_recommender_model_amd.torchrec.datasets.utils import Batch
+    from two_tower_recommender_model_amd.torchrec.distributed.model_parallel import DistributedModelParallel
+    from two_tower_recommender_model_amd.torchrec.modules.embedding_configs import EmbeddingBagConfig
+    from two_tower_recommender_model_amd.torchrec.modules.embedding_modules import EmbeddingBagCollection
+    from two_tower_recommender_model_amd.torchrec.optim.rowwise_adagrad import RowWiseAdagrad
+    from two_tower_recommender_model_amd.torchrec.sparse.jagged_tensor import KeyedJaggedTensor
+    from torch.distributed.optim import _apply_optimizer_in_backward
+
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    dev = torch.device("cuda", local_rank)
+    cfgs = [EmbeddingBagConfig(name="t_user_id", embedding_dim=D, num_embeddings=num_users, feature_names=["user_id"]),
+            EmbeddingBagConfig(name="t_product_id", embedding_dim=D, num_embeddings=num_items,
+                               feature_names=["product_id"])]
+    ebc = EmbeddingBagCollection(tables=cfgs, device=torch.device("meta"))
+    task = TwoTowerTrainTask(TwoTower(ebc, layers, device=dev))
+    _apply_optimizer_in_backward(RowWiseAdagrad, task.two_tower.ebc.parameters(), {"lr": 0.01})
+    model = DistributedModelParallel(module=task, device=dev)
+    dense = [p for n, p in model.named_parameters() if "embedding_bags" not in n and p.numel() > 0]
+    opt = torch.optim.Adam(dense, lr=0.01)
+    from two_tower_recommender_model_amd import ops
+
+    batches = []
+    for cols, lab in synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1 + rank):
+        v, l, o, _ = ops.kjt_build_mod_dropzero(cols, [num_users, num_items])
+        n = int(o[-1])
+        kjt = KeyedJaggedTensor(["user_id", "product_id"], v[:n], lengths=l, offsets=o, stride=B)
+        batches.append(Batch(torch.zeros(1, device=dev), kjt, lab))
+
+    def one(i):
+        opt.zero_grad(set_to_none=True)
+        loss, _ = model(batches[i % len(batches)])
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = one(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], device=dev)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt)
+    return world * args.steps * B / dt, dt / args.steps * 1e3, float(loss)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    config = {"workload": f"{args.workload}: {num_items // 1_000_000}M items x {num_users // 1_000_000}M users, "
+                          f"emb_dim {D}, towers {layers}, single-hot {args.ids} ids",
+              "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D, "tower_dtype": "bf16 (MFMA, fp32 acc)",
+              "parallelism": "single-gpu hipgraph" if world == 1 else f"rw-sharded tables + dp towers x{world}"}
+    if world == 1:
+        value, ms, loss, roofline, cpu = run_single(args)
+    else:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        value, ms, loss = run_multi(args, world, rank, local_rank)
+        roofline, cpu = None, None
+    if rank == 0:
+        out = {"metric": "training pairs/sec at batch 8192 (per GPU)", "value": round(value, 1), "unit": "pairs/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 5),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic (uniform ids, Bernoulli labels), random-init weights", "config": config,
+               "loss": loss, "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

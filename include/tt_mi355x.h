@@ -72,10 +72,13 @@ typedef struct {
   int32_t _pad;
 } tt_table_meta_t;
 
-/* One KJT key (feature) -> its table and its column range in the pooled [B, ldo] output. */
+/* One KJT key (feature) -> its table and where its bags land in the pooled output: bag b of this
+ * key is row (out_row + b), columns [out_offset, out_offset + D). out_row = 0 for an ordinary
+ * [B, sum D] KeyedTensor; sharded lookups stack source ranks as row blocks (out_row = s * B). */
 typedef struct {
   int32_t table;      /* index into the table array */
   int32_t out_offset; /* first column of this feature in the pooled output row */
+  int64_t out_row;    /* first output row of this feature's bags */
 } tt_feature_meta_t;
 
 const char* tt_last_error_string(void);
@@ -169,29 +172,31 @@ int tt_pooled_bwd_dense(const tt_table_meta_t* tables, int T, const tt_feature_m
                         int id_dtype, const int32_t* offsets, int pooling, float* grad_weights,
                         int bounds_check, void* stream);
 
-/* ---- a6: tower GEMMs on bf16 MFMA (fp32 accumulate) ------------------------------------------ */
+/* ---- a6: tower GEMMs on MFMA (fp32 accumulate) ------------------------------------------------ */
 
 /* A grouped launch runs `groups` (1 or 2: the two towers) independent problems of equal shape.
- * Pointer arrays are HOST arrays of `groups` device pointers. */
+ * Pointer arrays are HOST arrays of `groups` device pointers. compute = TT_BF16 (operands rounded
+ * to bf16, v_mfma_f32_16x16x32_bf16: the production mode) or TT_F32 (exact fp32 operands,
+ * v_mfma_f32_16x16x4_f32: the fp32 parity mode). */
 
 /* Y[m,n] = act(sum_k X[m,k] W[n,k] + bias[n]); X fp32 or bf16 (x_dtype), W [N,K] fp32 row-major
  * (nn.Linear layout), bias nullable, act = relu if relu != 0. Y fp32 with row stride ldy. */
 int tt_linear_fwd(int groups, const void* const* X, int x_dtype, int64_t ldx,
                   const float* const* W, const float* const* bias, int64_t M, int N, int K,
-                  float* const* Y, int64_t ldy, int relu, void* stream);
+                  float* const* Y, int64_t ldy, int relu, int compute, void* stream);
 
 /* dX[m,k] = sum_n dZ[m,n] W[n,k], dZ = dY * (Y > 0) if relu (Y nullable when relu == 0). */
 int tt_linear_bwd_data(int groups, const float* const* dY, const float* const* Y, int64_t ldy,
                        const float* const* W, int64_t M, int N, int K, float* const* dX,
-                       int64_t ldx, int relu, void* stream);
+                       int64_t ldx, int relu, int compute, void* stream);
 
 size_t tt_linear_bwd_weight_workspace_bytes(int groups, int64_t M, int N, int K);
 /* dW[n,k] = sum_m dZ[m,n] X[m,k]; db[n] = sum_m dZ[m,n] (db nullable). Split over M with fp32
  * slabs in the workspace, summed in a fixed order (bitwise reproducible). */
 int tt_linear_bwd_weight(int groups, const float* const* dY, const float* const* Y, int64_t ldy,
                          const void* const* X, int x_dtype, int64_t ldx, int64_t M, int N, int K,
-                         float* const* dW, float* const* db, int relu, void* workspace,
-                         size_t ws_bytes, void* stream);
+                         float* const* dW, float* const* db, int relu, int compute,
+                         void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- a7: logits = sum_d q*c ; loss = mean BCEWithLogits ; dlogit = (sigmoid - y) / B ---------- */
 

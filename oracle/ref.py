@@ -243,7 +243,7 @@ def train_step(st: TwoTowerState, values: torch.Tensor, offsets: torch.Tensor, B
         feats = [f for f, tt in enumerate(st.feature_table) if tt == t]
         if not feats:
             continue
-        grad = torch.zeros_like(st.tables[t])
+        idxs, gs = [], []
         for f in feats:
             s, e = int(offs64[f * B]), int(offs64[(f + 1) * B])
             if e == s:
@@ -255,12 +255,21 @@ def train_step(st: TwoTowerState, values: torch.Tensor, offsets: torch.Tensor, B
             g = gpooled[bag, start:start + st.dims[f]]
             if pooling == "mean":
                 g = g / lens[bag].clamp(min=1).unsqueeze(1).to(g.dtype)
-            grad.index_add_(0, idx, g)
+            idxs.append(idx)
+            gs.append(g)
         if sparse_update:
-            rows = torch.unique(torch.cat([
-                values[int(offs64[f * B]):int(offs64[(f + 1) * B])].to(torch.int64) for f in feats]))
-            rowwise_adagrad_sparse(st.tables[t], st.states[t], rows, grad[rows], lr_emb, eps)
+            # compact [U, D] gradient of the touched rows only (same sums as the dense index_add)
+            if not idxs:
+                continue
+            idx = torch.cat(idxs)
+            rows, inv = torch.unique(idx, return_inverse=True)
+            grad_rows = torch.zeros(rows.numel(), st.tables[t].shape[1])
+            grad_rows.index_add_(0, inv, torch.cat(gs))
+            rowwise_adagrad_sparse(st.tables[t], st.states[t], rows, grad_rows, lr_emb, eps)
         else:
+            grad = torch.zeros_like(st.tables[t])
+            for idx, g in zip(idxs, gs):
+                grad.index_add_(0, idx, g)
             rowwise_adagrad(st.tables[t], st.states[t], grad, lr_emb, eps)
     # dense: Adam
     if not st.exp_avg:

@@ -43,7 +43,7 @@ def test_errors_are_status_codes(lib):
     rc = lib.tt_pooled_fwd(None, None, 0, None, 0, 0, None, 0, None, 0, None, 0, 0, None, None)
     assert rc == 1001
     assert b"table count" in lib.tt_last_error_string()
-    rc = lib.tt_linear_fwd(3, None, 2, 0, None, None, 1, 1, 1, None, 0, 1, None)
+    rc = lib.tt_linear_fwd(3, None, 2, 0, None, None, 1, 1, 1, None, 0, 1, 3, None)
     assert rc == 1001 and b"groups" in lib.tt_last_error_string()
 
 

@@ -1,0 +1,156 @@
+"""End-to-end parity of the training step on the GPU against the golden vectors produced by running
+the reference's own TwoTower / TwoTowerTrainTask / transform_to_torchrec_batch code
+(tests/golden/make_golden.py): (1) the fused single-GPU step, (2) the drop-in torchrec API path
+(DistributedModelParallel + TrainPipelineSparseDist + KeyedOptimizerWrapper(Adam) + RowWiseAdagrad
+in backward), in fp32-operand tower mode (tight tolerances) and bf16 mode (the production mode).
+
+Tolerances: fp32 mode — pooled rtol 1e-6, logits/loss rtol 1e-4, tables atol 1e-5, towers atol
+2e-4 (Adam divides by sqrt(v): near-zero gradients amplify the last-bit differences); bf16 mode —
+logits within 3e-2 * max|logit| + 1e-3, loss rtol 1e-2, tables atol 2e-3."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+TOL = {
+    "fp32": dict(logit=1e-4, loss=1e-4, table=1e-5, mlp=2e-4),
+    "bf16": dict(logit=3e-2, loss=1e-2, table=2e-3, mlp=3e-2),
+}
+
+
+def _logits_close(got, want, tol):
+    got, want = np.asarray(got, np.float64).reshape(-1), np.asarray(want, np.float64).reshape(-1)
+    scale = np.abs(want).max() + 1e-6
+    assert np.all(np.abs(got - want) <= tol * scale + 1e-5), np.abs(got - want).max()
+
+
+def _layers(g):
+    return [int(x) for x in g["layers"]]
+
+
+@pytest.mark.parametrize("case", ["c1", "zipf", "d128"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_fused_step_matches_reference_golden(device, case, precision):
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    g = load_golden(f"train_{case}.npz")
+    layers, D, B = _layers(g), int(g["D"]), int(g["B"])
+    ne = [int(x) for x in g["num_embeddings"]]
+    lr = float(g["lr"])
+    st = FusedTwoTowerStep(ne, [D, D], [0], [1], layers, B, device, lr_emb=lr, lr_dense=lr, precision=precision)
+    st.tables.table_view(0).copy_(torch.from_numpy(g["init_t_user_id"]))
+    st.tables.table_view(1).copy_(torch.from_numpy(g["init_t_product_id"]))
+    for l in range(len(layers)):
+        st.qW[l].copy_(torch.from_numpy(g[f"init_two_tower.query_proj._mlp.{l}._linear.weight"]))
+        st.qb[l].copy_(torch.from_numpy(g[f"init_two_tower.query_proj._mlp.{l}._linear.bias"]))
+        st.cW[l].copy_(torch.from_numpy(g[f"init_two_tower.candidate_proj._mlp.{l}._linear.weight"]))
+        st.cb[l].copy_(torch.from_numpy(g[f"init_two_tower.candidate_proj._mlp.{l}._linear.bias"]))
+    st.capture()
+    tol = TOL[precision]
+    for s in range(int(g["steps"])):
+        cols = [torch.from_numpy(g[f"s{s}_user_id"]).to(device), torch.from_numpy(g[f"s{s}_product_id"]).to(device)]
+        st.load_batch(cols, torch.from_numpy(g[f"s{s}_label"]).to(torch.int32).to(device))
+        st.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(st.pooled.cpu().numpy(), g[f"s{s}_pooled"], rtol=1e-6, atol=1e-7)
+        _logits_close(st.logits.cpu().numpy(), g[f"s{s}_logits"], tol["logit"])
+        np.testing.assert_allclose(float(st.loss), float(g[f"s{s}_loss"]), rtol=tol["loss"])
+        if precision == "fp32":
+            np.testing.assert_allclose(st.gpooled.cpu().numpy(), g[f"s{s}_pooled_grad"], rtol=1e-3, atol=1e-7)
+    np.testing.assert_allclose(st.tables.table_view(0).cpu().numpy(), g["final_t_user_id"], rtol=0, atol=tol["table"])
+    np.testing.assert_allclose(st.tables.table_view(1).cpu().numpy(), g["final_t_product_id"], rtol=0, atol=tol["table"])
+    np.testing.assert_allclose(st.tables.state_view(0).cpu().numpy(), g["final_state_t_user_id"], rtol=3e-2 if precision == "bf16" else 1e-3, atol=1e-12)
+    for l in range(len(layers)):
+        np.testing.assert_allclose(st.qW[l].cpu().numpy(), g[f"final_two_tower.query_proj._mlp.{l}._linear.weight"],
+                                   rtol=0, atol=tol["mlp"])
+        np.testing.assert_allclose(st.cb[l].cpu().numpy(), g[f"final_two_tower.candidate_proj._mlp.{l}._linear.bias"],
+                                   rtol=0, atol=tol["mlp"])
+
+
+@pytest.mark.parametrize("case", ["c1", "d128"])
+def test_dropin_torchrec_api_matches_reference_golden(device, case):
+    """The reference's main()/train() wiring on the torchrec-compatible API (world size 1)."""
+    import two_tower_recommender_model_amd as tt
+
+    tt.install_torchrec_alias()
+    from torch.distributed.optim import _apply_optimizer_in_backward
+
+    import two_tower_recommender_model_amd.torchrec.modules.mlp as mlp_mod
+    from torchrec.datasets.utils import Batch
+    from torchrec.distributed import TrainPipelineSparseDist
+    from torchrec.distributed.model_parallel import DistributedModelParallel
+    from torchrec.modules.embedding_configs import EmbeddingBagConfig
+    from torchrec.modules.embedding_modules import EmbeddingBagCollection
+    from torchrec.optim.keyed import KeyedOptimizerWrapper
+    from torchrec.optim.rowwise_adagrad import RowWiseAdagrad
+    from torchrec.sparse.jagged_tensor import KeyedJaggedTensor
+
+    from two_tower_recommender_model_amd.task import TwoTower, TwoTowerTrainTask
+
+    g = load_golden(f"train_{case}.npz")
+    layers, D, B = _layers(g), int(g["D"]), int(g["B"])
+    ne = [int(x) for x in g["num_embeddings"]]
+    lr = float(g["lr"])
+    cat_cols = ["user_id", "product_id"]
+    eb_configs = [EmbeddingBagConfig(name=f"t_{f}", embedding_dim=D, num_embeddings=ne[i], feature_names=[f])
+                  for i, f in enumerate(cat_cols)]
+    ebc = EmbeddingBagCollection(tables=eb_configs, device=torch.device("meta"))
+    old = mlp_mod.TOWER_PRECISION
+    mlp_mod.TOWER_PRECISION = "fp32"
+    try:
+        two_tower = TwoTower(embedding_bag_collection=ebc, layer_sizes=layers, device=device)
+    finally:
+        mlp_mod.TOWER_PRECISION = old
+    task = TwoTowerTrainTask(two_tower)
+    _apply_optimizer_in_backward(RowWiseAdagrad, task.two_tower.ebc.parameters(), {"lr": lr})
+    model = DistributedModelParallel(module=task, device=device)
+    sd = model.module.two_tower.state_dict()
+    with torch.no_grad():
+        sd["ebc.embedding_bags.t_user_id.weight"].copy_(torch.from_numpy(g["init_t_user_id"]))
+        sd["ebc.embedding_bags.t_product_id.weight"].copy_(torch.from_numpy(g["init_t_product_id"]))
+        for k in sd:
+            if "proj" in k:
+                sd[k].copy_(torch.from_numpy(g["init_two_tower." + k]))
+    optimizer = KeyedOptimizerWrapper(dict(model.named_parameters()), lambda params: torch.optim.Adam(params, lr=lr))
+    pipeline = TrainPipelineSparseDist(model, optimizer, device)
+
+    def batches():
+        for s in range(int(g["steps"])):
+            kjt = KeyedJaggedTensor.from_lengths_sync(
+                cat_cols, torch.from_numpy(g[f"s{s}_values"]),
+                torch.from_numpy(np.diff(g[f"s{s}_offsets"]).astype(np.int32)))
+            yield Batch(dense_features=torch.zeros(1), sparse_features=kjt,
+                        labels=torch.from_numpy(g[f"s{s}_label"]).to(torch.int32))
+
+    it = batches()
+    pipeline._model.train()
+    outs = []
+    while True:
+        try:
+            outs.append(pipeline.progress(it))
+        except StopIteration:
+            break
+    assert len(outs) == int(g["steps"])
+    tol = TOL["fp32"]
+    for s, (loss, logits, labels) in enumerate(outs):
+        _logits_close(logits.cpu().numpy(), g[f"s{s}_logits"], tol["logit"])
+        np.testing.assert_allclose(float(loss), float(g[f"s{s}_loss"]), rtol=tol["loss"])
+    sd = model.module.two_tower.state_dict()
+    np.testing.assert_allclose(sd["ebc.embedding_bags.t_user_id.weight"].cpu().numpy(), g["final_t_user_id"],
+                               rtol=0, atol=tol["table"])
+    np.testing.assert_allclose(sd["ebc.embedding_bags.t_product_id.weight"].cpu().numpy(), g["final_t_product_id"],
+                               rtol=0, atol=tol["table"])
+    for k in sd:
+        if "proj" in k:
+            np.testing.assert_allclose(sd[k].cpu().numpy(), g["final_two_tower." + k], rtol=0, atol=tol["mlp"])
+    # table params never receive a .grad (update fused into the backward, like FBGEMM's TBE)
+    assert model.module.two_tower.ebc.embedding_bags["t_user_id"].weight.grad is None
+    # eval mode: forward only, no update
+    before = sd["ebc.embedding_bags.t_user_id.weight"].clone()
+    pipeline._model.eval()
+    with torch.no_grad():
+        loss, logits, labels = pipeline.progress(batches())
+    assert torch.equal(before, model.module.two_tower.state_dict()["ebc.embedding_bags.t_user_id.weight"])

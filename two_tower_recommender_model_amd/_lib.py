@@ -34,7 +34,7 @@ class TableMeta(C.Structure):
 
 
 class FeatureMeta(C.Structure):
-    _fields_ = [("table", C.c_int32), ("out_offset", C.c_int32)]
+    _fields_ = [("table", C.c_int32), ("out_offset", C.c_int32), ("out_row", C.c_int64)]
 
 
 _vp = C.c_void_p
@@ -89,12 +89,12 @@ SIGNATURES = {
         _int,
         [_ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _int, _vp, _int, _vp, _int, _vp],
     ),
-    "tt_linear_fwd": (_int, [_int, _pvp, _int, _i64, _pvp, _pvp, _i64, _int, _int, _pvp, _i64, _int, _vp]),
-    "tt_linear_bwd_data": (_int, [_int, _pvp, _pvp, _i64, _pvp, _i64, _int, _int, _pvp, _i64, _int, _vp]),
+    "tt_linear_fwd": (_int, [_int, _pvp, _int, _i64, _pvp, _pvp, _i64, _int, _int, _pvp, _i64, _int, _int, _vp]),
+    "tt_linear_bwd_data": (_int, [_int, _pvp, _pvp, _i64, _pvp, _i64, _int, _int, _pvp, _i64, _int, _int, _vp]),
     "tt_linear_bwd_weight_workspace_bytes": (_sz, [_int, _i64, _int, _int]),
     "tt_linear_bwd_weight": (
         _int,
-        [_int, _pvp, _pvp, _i64, _pvp, _int, _i64, _i64, _int, _int, _pvp, _pvp, _int, _vp, _sz, _vp],
+        [_int, _pvp, _pvp, _i64, _pvp, _int, _i64, _i64, _int, _int, _pvp, _pvp, _int, _int, _vp, _sz, _vp],
     ),
     "tt_dot_bce_workspace_bytes": (_sz, [_i64]),
     "tt_dot_bce_workspace_init": (_int, [_vp, _sz, _i64, _vp]),

@@ -23,7 +23,7 @@ int pack_meta(EmbMeta& m, const tt_table_meta_t* tables, int T, const tt_feature
   for (int f = 0; f < F; ++f) {
     if (features[f].table < 0 || features[f].table >= T)
       return fail(TT_EINVAL, "feature references a table index out of range");
-    if (features[f].out_offset < 0) return fail(TT_EINVAL, "negative feature output offset");
+    if (features[f].out_offset < 0 || features[f].out_row < 0) return fail(TT_EINVAL, "negative feature output offset/row");
     m.features[f] = features[f];
   }
   m.T = T;

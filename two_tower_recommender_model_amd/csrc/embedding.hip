@@ -21,8 +21,8 @@ namespace tt {
 struct FwdArgs {
   EmbMeta m;
   int32_t block_start[TT_MAX_FEATURES + 1];  // first workgroup of each feature
-  int32_t group[TT_MAX_FEATURES];            // lanes per bag (power of two <= 64)
-  int32_t vec[TT_MAX_FEATURES];              // 4 = float4 path, 1 = scalar path
+  int8_t group[TT_MAX_FEATURES];             // lanes per bag (power of two <= 64)
+  int8_t vec[TT_MAX_FEATURES];               // 4 = float4 path, 1 = scalar path
 };
 
 template <int VEC>
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) pooled_fwd_kernel(const float* __restrict
   const int64_t s = offsets[bag], e = offsets[bag + 1];
   const float scale = (pooling == TT_POOL_MEAN && e > s) ? 1.0f / (float)(e - s) : 1.0f;
   const float* w = weights + tm.weight_offset;
-  float* o = out + b * ldo + fm.out_offset;
+  float* o = out + (fm.out_row + b) * ldo + fm.out_offset;
   if (a.vec[f] == 4)
     pool_bag_cols<4>(w, values, id_dtype, s, e, tm.num_rows, tm.dim, lane_g, G, scale, o, bounds_check, err);
   else
@@ -339,7 +339,7 @@ __device__ __forceinline__ void adagrad_row(const EmbMeta& m, const float* __res
   auto row_ptr = [&](int bag) -> const float* {
     const int f = bag / (int)B;
     const int64_t b = bag - (int64_t)f * B;
-    return grad_out + b * ldg + m.features[f].out_offset;
+    return grad_out + (m.features[f].out_row + b) * ldg + m.features[f].out_offset;
   };
   auto bag_scale = [&](int bag) -> float {
     if (pooling != TT_POOL_MEAN) return 1.f;
@@ -503,7 +503,7 @@ __global__ void __launch_bounds__(256) bwd_dense_kernel(EmbMeta m, const float* 
     const tt_table_meta_t tm = m.tables[m.features[f].table];
     const int64_t s = offsets[bag], e = offsets[bag + 1];
     const float sc = (pooling == TT_POOL_MEAN && e > s) ? 1.f / (float)(e - s) : 1.f;
-    const float* g = grad_out + b * ldg + m.features[f].out_offset;
+    const float* g = grad_out + (m.features[f].out_row + b) * ldg + m.features[f].out_offset;
     for (int64_t j = s; j < e; ++j) {
       int64_t id = load_id(values, id_dtype, j);
       if (bounds_check && (uint64_t)id >= (uint64_t)tm.num_rows) id = 0;

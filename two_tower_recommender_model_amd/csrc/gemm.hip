@@ -1,15 +1,16 @@
-// Tower GEMMs on gfx950 bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate).
+// Tower GEMMs on gfx950 MFMA: bf16 operands (v_mfma_f32_16x16x32_bf16) or exact fp32 operands
+// (v_mfma_f32_16x16x4_f32, the fp32 parity mode), fp32 accumulation in both.
 //
 // One template covers the three products of an MLP layer (torchrec Perceptron = Linear + ReLU on
 // every layer, 03_model_training.py:411-412):
 //   FWD         Y  = relu(X W^T + b)            A = X   [M,K] row-major,  B_c[n][k] = W[n][k]
 //   BWD_DATA    dX = (dY * (Y>0)) W             A = dZ  [M,N] row-major,  B_c[j][n] = W[n][j]
 //   BWD_WEIGHT  dW = (dY * (Y>0))^T X, db       A = dZ^T (transposed),    B_c[j][m] = X[m][j]
-// Operands are staged global -> registers (fp32 or bf16, relu mask applied, converted to bf16) ->
-// LDS in the canonical [row][k] layout with k contiguous, so every MFMA fragment is one 16-B
-// ds_read. 64x64 output tile per 256-thread workgroup (4 waves, 2x2 of 32x32), BK = 32.
-// BWD_WEIGHT splits the M reduction over workgroups into fp32 slabs, summed in a fixed order by a
-// second kernel (bitwise reproducible; no float atomics).
+// Operands are staged global -> registers (fp32 or bf16 source, ReLU mask applied, converted to
+// the compute type) -> LDS in the canonical [row][k] layout with k contiguous, so a bf16 MFMA
+// fragment is one 16-B ds_read. 64x64 output tile per 256-thread workgroup (4 waves, 2x2 of 32x32),
+// BK = 32. BWD_WEIGHT splits the M reduction over workgroups into fp32 slabs summed in a fixed
+// order by a second kernel (bitwise reproducible; no float atomics).
 #include "tt_common.h"
 
 namespace tt {
@@ -17,17 +18,23 @@ namespace tt {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int BM = 64, BN = 64, BK = 32, LDS_STRIDE = BK + 8;  // 80-B rows
+constexpr int BM = 64, BN = 64, BK = 32;
 
 enum { MODE_FWD = 0, MODE_BWD_DATA = 1, MODE_BWD_WEIGHT = 2 };
 
+template <bool F32>
+struct Tile {
+  typedef typename std::conditional<F32, float, __bf16>::type T;
+  static constexpr int STRIDE = F32 ? BK + 4 : BK + 8;  // 144-B / 80-B rows
+};
+
 struct GemmProblem {
-  const void* a;      // X (FWD), dY (BWD_DATA, BWD_WEIGHT)
-  const float* amask; // Y for the relu mask (BWD_*), else null
-  const void* b;      // W (FWD, BWD_DATA), X (BWD_WEIGHT)
-  const float* bias;  // FWD only, nullable
-  float* c;           // Y (FWD), dX (BWD_DATA), slab base (BWD_WEIGHT)
-  float* dbslab;      // BWD_WEIGHT: [S][N] partial bias grads (nullable)
+  const void* a;       // X (FWD), dY (BWD_DATA, BWD_WEIGHT)
+  const float* amask;  // Y for the relu mask (BWD_*), else null
+  const void* b;       // W (FWD, BWD_DATA), X (BWD_WEIGHT)
+  const float* bias;   // FWD only, nullable
+  float* c;            // Y (FWD), dX (BWD_DATA), slab base (BWD_WEIGHT)
+  float* dbslab;       // BWD_WEIGHT: [S][N] partial bias grads (nullable)
 };
 
 struct GemmArgs {
@@ -38,7 +45,7 @@ struct GemmArgs {
   int64_t lda, ldb, ldc, ldmask;
   int a_bf16, b_bf16;
   int relu;
-  int splits;    // BWD_WEIGHT: slices of K
+  int splits;      // BWD_WEIGHT: slices of K
   int64_t kslice;  // BWD_WEIGHT: K per slice (multiple of BK)
 };
 
@@ -50,23 +57,34 @@ __device__ __forceinline__ float ld_elem(const void* p, int bf, int64_t i) {
   return reinterpret_cast<const float*>(p)[i];
 }
 
-__device__ __forceinline__ __bf16 to_bf16(float x) { return (__bf16)x; }
+template <typename T>
+__device__ __forceinline__ void store8(T* dst, const float (&v)[8]) {
+  if constexpr (std::is_same<T, float>::value) {
+    reinterpret_cast<f32x4*>(dst)[0] = f32x4{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<f32x4*>(dst)[1] = f32x4{v[4], v[5], v[6], v[7]};
+  } else {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
+    *reinterpret_cast<bf16x8*>(dst) = o;
+  }
+}
 
 // Row-major source: tile element (r, k) = src[(r0 + r) * ld + k0 + k]. Thread t stages row t/4,
 // k-chunk (t%4)*8 .. +8 (8 consecutive elements: 32 B fp32 / 16 B bf16).
-__device__ __forceinline__ void stage_rowmajor(__bf16* lds, const void* src, int bf, int64_t ld,
-                                               const float* mask, int64_t ldm, int64_t rows, int64_t cols,
-                                               int64_t r0, int64_t k0) {
+template <typename T, int STRIDE>
+__device__ __forceinline__ void stage_rowmajor(T* lds, const void* src, int bf, int64_t ld, const float* mask,
+                                               int64_t ldm, int64_t rows, int64_t cols, int64_t r0, int64_t k0) {
   const int t = threadIdx.x;
   const int r = t >> 2, kc = (t & 3) * 8;
   const int64_t gr = r0 + r, gk = k0 + kc;
-  bf16x8 v;
+  float v[8];
   if (gr < rows && gk + 8 <= cols && !bf && mask == nullptr && ((ld & 3) == 0) &&
       ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
     const f32x4* s4 = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(src) + gr * ld + gk);
     const f32x4 x0 = s4[0], x1 = s4[1];
-    v[0] = to_bf16(x0[0]); v[1] = to_bf16(x0[1]); v[2] = to_bf16(x0[2]); v[3] = to_bf16(x0[3]);
-    v[4] = to_bf16(x1[0]); v[5] = to_bf16(x1[1]); v[6] = to_bf16(x1[2]); v[7] = to_bf16(x1[3]);
+    v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3];
+    v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -75,22 +93,22 @@ __device__ __forceinline__ void stage_rowmajor(__bf16* lds, const void* src, int
         x = ld_elem(src, bf, gr * ld + gk + j);
         if (mask && !(mask[gr * ldm + gk + j] > 0.f)) x = 0.f;
       }
-      v[j] = to_bf16(x);
+      v[j] = x;
     }
   }
-  *reinterpret_cast<bf16x8*>(lds + r * LDS_STRIDE + kc) = v;
+  store8(lds + r * STRIDE + kc, v);
 }
 
 // Transposed source: tile element (r, k) = src[(k0 + k) * ld + r0 + r]. Thread t stages row t%64,
 // k = (t/64)*8 .. +8; consecutive lanes read consecutive r (coalesced). Returns the fp32 sum of
-// the 8 staged values (pre-rounding) for the fused bias gradient.
-__device__ __forceinline__ float stage_transposed(__bf16* lds, const void* src, int bf, int64_t ld,
-                                                  const float* mask, int64_t ldm, int64_t rows, int64_t ks,
-                                                  int64_t r0, int64_t k0) {
+// the 8 staged values (before any rounding) for the fused bias gradient.
+template <typename T, int STRIDE>
+__device__ __forceinline__ float stage_transposed(T* lds, const void* src, int bf, int64_t ld, const float* mask,
+                                                  int64_t ldm, int64_t rows, int64_t ks, int64_t r0, int64_t k0) {
   const int t = threadIdx.x;
   const int r = t & 63, kc = (t >> 6) * 8;
   const int64_t gr = r0 + r;
-  bf16x8 v;
+  float v[8];
   float sum = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -101,16 +119,18 @@ __device__ __forceinline__ float stage_transposed(__bf16* lds, const void* src, 
       if (mask && !(mask[gk * ldm + gr] > 0.f)) x = 0.f;
     }
     sum += x;
-    v[j] = to_bf16(x);
+    v[j] = x;
   }
-  *reinterpret_cast<bf16x8*>(lds + r * LDS_STRIDE + kc) = v;
+  store8(lds + r * STRIDE + kc, v);
   return sum;
 }
 
-template <int MODE>
+template <int MODE, bool F32>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * LDS_STRIDE];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * LDS_STRIDE];
+  typedef typename Tile<F32>::T T;
+  constexpr int STRIDE = Tile<F32>::STRIDE;
+  __shared__ __attribute__((aligned(16))) T As[BM * STRIDE];
+  __shared__ __attribute__((aligned(16))) T Bs[BN * STRIDE];
   __shared__ float dbred[4][BM];
 
   int g, split = 0;
@@ -139,36 +159,53 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 
   for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
     if (MODE == MODE_FWD) {
-      stage_rowmajor(As, P.a, a.a_bf16, a.lda, nullptr, 0, a.M, a.K, m0, k0);
-      stage_rowmajor(Bs, P.b, a.b_bf16, a.ldb, nullptr, 0, a.N, a.K, n0, k0);
+      stage_rowmajor<T, STRIDE>(As, P.a, a.a_bf16, a.lda, nullptr, 0, a.M, a.K, m0, k0);
+      stage_rowmajor<T, STRIDE>(Bs, P.b, a.b_bf16, a.ldb, nullptr, 0, a.N, a.K, n0, k0);
     } else if (MODE == MODE_BWD_DATA) {
-      stage_rowmajor(As, P.a, 0, a.lda, a.relu ? P.amask : nullptr, a.ldmask, a.M, a.K, m0, k0);
-      stage_transposed(Bs, P.b, 0, a.ldb, nullptr, 0, a.N, a.K, n0, k0);
+      stage_rowmajor<T, STRIDE>(As, P.a, 0, a.lda, a.relu ? P.amask : nullptr, a.ldmask, a.M, a.K, m0, k0);
+      stage_transposed<T, STRIDE>(Bs, P.b, 0, a.ldb, nullptr, 0, a.N, a.K, n0, k0);
     } else {
-      const float s = stage_transposed(As, P.a, 0, a.lda, a.relu ? P.amask : nullptr, a.ldmask, a.M, kend, m0, k0);
+      const float s =
+          stage_transposed<T, STRIDE>(As, P.a, 0, a.lda, a.relu ? P.amask : nullptr, a.ldmask, a.M, kend, m0, k0);
       dbacc += s;
-      stage_transposed(Bs, P.b, a.b_bf16, a.ldb, nullptr, 0, a.N, kend, n0, k0);
+      stage_transposed<T, STRIDE>(Bs, P.b, a.b_bf16, a.ldb, nullptr, 0, a.N, kend, n0, k0);
     }
     __syncthreads();
-    bf16x8 af[2], bfr[2];
+    if constexpr (F32) {
+      // v_mfma_f32_16x16x4_f32: lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15]; 8 steps of K=4
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = wm * 32 + i * 16 + (lane & 15);
-      af[i] = *reinterpret_cast<const bf16x8*>(As + row * LDS_STRIDE + (lane >> 4) * 8);
+      for (int kk = 0; kk < BK; kk += 4) {
+        float af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = As[(wm * 32 + i * 16 + (lane & 15)) * STRIDE + kk + (lane >> 4)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr[j] = Bs[(wn * 32 + j * 16 + (lane & 15)) * STRIDE + kk + (lane >> 4)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 32 + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + row * STRIDE + (lane >> 4) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wn * 32 + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + col * STRIDE + (lane >> 4) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = wn * 32 + j * 16 + (lane & 15);
-      bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + col * LDS_STRIDE + (lane >> 4) * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     __syncthreads();
   }
 
-  // epilogue: C/D layout of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r
+  // epilogue: C/D layout of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -229,8 +266,9 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(ReduceArgs r) {
   }
 }
 
-static int check_groups(int groups) {
+static int check_common(int groups, int compute) {
   if (groups < 1 || groups > 2) return fail(TT_EINVAL, "gemm: groups must be 1 or 2");
+  if (compute != TT_BF16 && compute != TT_F32) return fail(TT_EINVAL, "gemm: compute dtype must be TT_BF16 or TT_F32");
   return TT_OK;
 }
 
@@ -241,6 +279,14 @@ static int bwd_weight_splits(int groups, int64_t M, int N, int K) {
   return (int)std::min<int64_t>(s, 256);
 }
 
+template <int MODE>
+static void launch(dim3 grid, const GemmArgs& a, int compute, hipStream_t st) {
+  if (compute == TT_F32)
+    gemm_kernel<MODE, true><<<grid, dim3(256), 0, st>>>(a);
+  else
+    gemm_kernel<MODE, false><<<grid, dim3(256), 0, st>>>(a);
+}
+
 }  // namespace tt
 
 using namespace tt;
@@ -249,8 +295,8 @@ extern "C" {
 
 int tt_linear_fwd(int groups, const void* const* X, int x_dtype, int64_t ldx, const float* const* W,
                   const float* const* bias, int64_t M, int N, int K, float* const* Y, int64_t ldy, int relu,
-                  void* stream) {
-  int rc = check_groups(groups);
+                  int compute, void* stream) {
+  int rc = check_common(groups, compute);
   if (rc) return rc;
   if (M < 0 || N < 1 || K < 1) return fail(TT_EINVAL, "linear_fwd: bad shape");
   if (x_dtype != TT_F32 && x_dtype != TT_BF16) return fail(TT_EINVAL, "linear_fwd: X must be fp32 or bf16");
@@ -267,15 +313,15 @@ int tt_linear_fwd(int groups, const void* const* X, int x_dtype, int64_t ldx, co
   a.M = M; a.N = N; a.K = K;
   a.lda = ldx; a.ldb = K; a.ldc = ldy;
   a.a_bf16 = x_dtype == TT_BF16; a.b_bf16 = 0; a.relu = relu;
-  dim3 grid((unsigned)ceil_div(M, BM), (unsigned)ceil_div(N, BN), (unsigned)groups);
-  gemm_kernel<MODE_FWD><<<grid, dim3(256), 0, as_stream(stream)>>>(a);
+  launch<MODE_FWD>(dim3((unsigned)ceil_div(M, BM), (unsigned)ceil_div(N, BN), (unsigned)groups), a, compute,
+                   as_stream(stream));
   return check_launch("linear_fwd");
 }
 
 int tt_linear_bwd_data(int groups, const float* const* dY, const float* const* Y, int64_t ldy,
                        const float* const* W, int64_t M, int N, int K, float* const* dX, int64_t ldx, int relu,
-                       void* stream) {
-  int rc = check_groups(groups);
+                       int compute, void* stream) {
+  int rc = check_common(groups, compute);
   if (rc) return rc;
   if (M < 0 || N < 1 || K < 1) return fail(TT_EINVAL, "linear_bwd_data: bad shape");
   if (!dY || !W || !dX || (relu && !Y)) return fail(TT_EINVAL, "linear_bwd_data: null pointer array");
@@ -292,8 +338,8 @@ int tt_linear_bwd_data(int groups, const float* const* dY, const float* const* Y
   a.M = M; a.N = K; a.K = N;
   a.lda = ldy; a.ldmask = ldy; a.ldb = K; a.ldc = ldx;
   a.relu = relu;
-  dim3 grid((unsigned)ceil_div(M, BM), (unsigned)ceil_div(K, BN), (unsigned)groups);
-  gemm_kernel<MODE_BWD_DATA><<<grid, dim3(256), 0, as_stream(stream)>>>(a);
+  launch<MODE_BWD_DATA>(dim3((unsigned)ceil_div(M, BM), (unsigned)ceil_div(K, BN), (unsigned)groups), a, compute,
+                        as_stream(stream));
   return check_launch("linear_bwd_data");
 }
 
@@ -305,9 +351,9 @@ size_t tt_linear_bwd_weight_workspace_bytes(int groups, int64_t M, int N, int K)
 
 int tt_linear_bwd_weight(int groups, const float* const* dY, const float* const* Y, int64_t ldy,
                          const void* const* X, int x_dtype, int64_t ldx, int64_t M, int N, int K,
-                         float* const* dW, float* const* db, int relu, void* workspace, size_t ws_bytes,
-                         void* stream) {
-  int rc = check_groups(groups);
+                         float* const* dW, float* const* db, int relu, int compute, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  int rc = check_common(groups, compute);
   if (rc) return rc;
   if (M < 0 || N < 1 || K < 1) return fail(TT_EINVAL, "linear_bwd_weight: bad shape");
   if (x_dtype != TT_F32 && x_dtype != TT_BF16) return fail(TT_EINVAL, "linear_bwd_weight: X must be fp32 or bf16");
@@ -350,8 +396,8 @@ int tt_linear_bwd_weight(int groups, const float* const* dY, const float* const*
   a.relu = relu;
   a.splits = S;
   a.kslice = ceil_div(ceil_div(M, S), BK) * BK;
-  dim3 grid((unsigned)ceil_div(N, BM), (unsigned)ceil_div(K, BN), (unsigned)(groups * S));
-  gemm_kernel<MODE_BWD_WEIGHT><<<grid, dim3(256), 0, st>>>(a);
+  launch<MODE_BWD_WEIGHT>(dim3((unsigned)ceil_div(N, BM), (unsigned)ceil_div(K, BN), (unsigned)(groups * S)), a,
+                          compute, st);
   r.MN = (int64_t)N * K;
   r.Mrows = N;
   r.splits = S;

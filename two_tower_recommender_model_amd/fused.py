@@ -1,0 +1,210 @@
+"""The whole two-tower training step on one MI355X as a fixed sequence of libtt_mi355x launches,
+replayable as one HIP graph.
+
+Semantics = one ``TrainPipelineSparseDist.progress`` of the reference (03_model_training.py:618)
+over ``transform_to_torchrec_batch`` (:353-382), ``TwoTowerTrainTask(TwoTower(ebc, layer_sizes))``
+(:395-455), RowWiseAdagrad applied in backward to the tables (:791-795) and Adam on the towers
+(:826-829) — with the reference's host KJT loop replaced by the device KJT builder and every
+intermediate kept in place:
+
+  side stream:  k2a-c  bwd_prepare (hash/count/scan/scatter)   <- depends on the ids only
+  main stream:  kjt_build -> pooled_fwd -> towers fwd (grouped bf16 MFMA, both towers per launch,
+                layer 0 reads the KeyedTensor column slices in place) -> dot+BCE(+grad)
+                -> towers bwd (dX into the pooled-gradient slices, dW/db split-K)
+                -> [join] k2d fused row-wise Adagrad -> Adam on the flat dense buffer
+
+No host synchronisation inside ``step()``: buffers are sized for the worst case (every id kept).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib, ops
+
+
+class FusedTwoTowerStep:
+    def __init__(self, num_embeddings: Sequence[int], embedding_dims: Sequence[int],
+                 query_features: Sequence[int], candidate_features: Sequence[int], layer_sizes: Sequence[int],
+                 batch_size: int, device: torch.device, lr_emb: float = 0.01, lr_dense: float = 0.01,
+                 eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
+                 overlap_prepare: bool = True, precision: str = "bf16"):
+        """One table per feature (feature f -> table f), features ordered as the KJT keys.
+        precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode)."""
+        self.device = torch.device(device)
+        self.precision = precision
+        self.F = len(num_embeddings)
+        self.B = int(batch_size)
+        self.num_embeddings = [int(n) for n in num_embeddings]
+        self.dims = [int(d) for d in embedding_dims]
+        self.qf = list(query_features)
+        self.cf = list(candidate_features)
+        self.layer_sizes = [int(x) for x in layer_sizes]
+        self.lr_emb, self.lr_dense, self.eps = float(lr_emb), float(lr_dense), float(eps)
+        self.id_dtype = id_dtype
+        dev = self.device
+        # tables (one flat HBM buffer) + row-wise state
+        self.tables = ops.TableSet(self.num_embeddings, self.dims, list(range(self.F)), dev)
+        gen = torch.Generator(device=dev).manual_seed(seed)
+        self.tables.init_uniform_(gen)
+        self.out_dim = sum(self.dims)
+        col = [0]
+        for d in self.dims:
+            col.append(col[-1] + d)
+        self.col = col
+        # the reference's towers take the concatenation of their features; with the KJT key order
+        # (query features, then candidate features) each tower input is one contiguous column slice
+        self.q_lo, self.q_hi = col[min(self.qf)], col[max(self.qf) + 1]
+        self.c_lo, self.c_hi = col[min(self.cf)], col[max(self.cf) + 1]
+        if sorted(self.qf) != list(range(min(self.qf), max(self.qf) + 1)) or \
+                sorted(self.cf) != list(range(min(self.cf), max(self.cf) + 1)):
+            raise _lib.TTError("fused step: tower features must be contiguous KJT keys")
+        self.in_q = self.q_hi - self.q_lo
+        self.in_c = self.c_hi - self.c_lo
+        # dense parameters: one flat fp32 buffer (towers' W, b), grads and Adam moments beside it
+        shapes = []
+        for tower_in in (self.in_q, self.in_c):
+            i = tower_in
+            for o in self.layer_sizes:
+                shapes.append((o, i))
+                shapes.append((o,))
+                i = o
+        n = sum(torch.Size(s).numel() for s in shapes)
+        self.params = torch.empty(n, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.adam_state = torch.zeros(2, dtype=torch.int64, device=dev)
+        views, gviews, o = [], [], 0
+        for s in shapes:
+            k = torch.Size(s).numel()
+            views.append(self.params[o:o + k].view(s))
+            gviews.append(self.grads[o:o + k].view(s))
+            o += k
+        L = len(self.layer_sizes)
+        self.qW = [views[2 * l] for l in range(L)]
+        self.qb = [views[2 * l + 1] for l in range(L)]
+        self.cW = [views[2 * L + 2 * l] for l in range(L)]
+        self.cb = [views[2 * L + 2 * l + 1] for l in range(L)]
+        self.gqW = [gviews[2 * l] for l in range(L)]
+        self.gqb = [gviews[2 * l + 1] for l in range(L)]
+        self.gcW = [gviews[2 * L + 2 * l] for l in range(L)]
+        self.gcb = [gviews[2 * L + 2 * l + 1] for l in range(L)]
+        g = torch.Generator().manual_seed(seed + 1)
+        for W_, b_ in list(zip(self.qW, self.qb)) + list(zip(self.cW, self.cb)):
+            bound = 1.0 / W_.shape[1] ** 0.5  # nn.Linear default init
+            W_.copy_(torch.empty(W_.shape).uniform_(-bound, bound, generator=g))
+            b_.copy_(torch.empty(b_.shape).uniform_(-bound, bound, generator=g))
+        self.grouped = self.in_q == self.in_c
+        # static step buffers
+        B, F = self.B, self.F
+        self.cols = [torch.zeros(B, dtype=id_dtype, device=dev) for _ in range(F)]
+        self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.values = torch.empty(F * B, dtype=id_dtype, device=dev)
+        self.lengths = torch.empty(F * B, dtype=torch.int32, device=dev)
+        self.offsets = torch.empty(F * B + 1, dtype=torch.int32, device=dev)
+        self.lpk = torch.empty(F, dtype=torch.int64, device=dev)
+        self.pooled = torch.empty(B, self.out_dim, dtype=torch.float32, device=dev)
+        self.gpooled = torch.empty(B, self.out_dim, dtype=torch.float32, device=dev)
+        self.qy = [torch.empty(B, n_, dtype=torch.float32, device=dev) for n_ in self.layer_sizes]
+        self.cy = [torch.empty(B, n_, dtype=torch.float32, device=dev) for n_ in self.layer_sizes]
+        self.qdy = [torch.empty(B, n_, dtype=torch.float32, device=dev) for n_ in self.layer_sizes]
+        self.cdy = [torch.empty(B, n_, dtype=torch.float32, device=dev) for n_ in self.layer_sizes]
+        self.logits = torch.empty(B, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros((), dtype=torch.float32, device=dev)
+        self.dot_bce = ops.DotBCE(dev, B)
+        self.tables.ensure_bwd_workspace(F * B)
+        self.side = torch.cuda.Stream(device=dev) if overlap_prepare else None
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        # warm every scratch workspace so graph capture allocates nothing new (the all-zero batch
+        # drops every id, so the tables are untouched; the towers' parameters are restored)
+        p0 = self.params.clone()
+        self.step()
+        torch.cuda.synchronize(dev)
+        self.params.copy_(p0)
+        self.reset_optimizer_state()
+
+    # ------------------------------------------------------------------------------------------
+    def reset_optimizer_state(self) -> None:
+        self.tables.state.zero_()
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        self.adam_state.zero_()
+
+    def load_batch(self, cols: Sequence[torch.Tensor], labels: torch.Tensor) -> None:
+        for dst, src in zip(self.cols, cols):
+            dst.copy_(src, non_blocking=True)
+        self.labels.copy_(labels, non_blocking=True)
+
+    def _towers_fwd(self):
+        L = len(self.layer_sizes)
+        pr = self.precision
+        xq = self.pooled[:, self.q_lo:self.q_hi]
+        xc = self.pooled[:, self.c_lo:self.c_hi]
+        for l in range(L):
+            if self.grouped:
+                ops.linear_fwd([xq, xc], [self.qW[l], self.cW[l]], [self.qb[l], self.cb[l]], relu=True,
+                               outs=[self.qy[l], self.cy[l]], precision=pr)
+            else:
+                ops.linear_fwd([xq], [self.qW[l]], [self.qb[l]], relu=True, outs=[self.qy[l]], precision=pr)
+                ops.linear_fwd([xc], [self.cW[l]], [self.cb[l]], relu=True, outs=[self.cy[l]], precision=pr)
+            xq, xc = self.qy[l], self.cy[l]
+
+    def _towers_bwd(self):
+        L = len(self.layer_sizes)
+        pr = self.precision
+        for l in reversed(range(L)):
+            xq = self.pooled[:, self.q_lo:self.q_hi] if l == 0 else self.qy[l - 1]
+            xc = self.pooled[:, self.c_lo:self.c_hi] if l == 0 else self.cy[l - 1]
+            dxq = self.gpooled[:, self.q_lo:self.q_hi] if l == 0 else self.qdy[l - 1]
+            dxc = self.gpooled[:, self.c_lo:self.c_hi] if l == 0 else self.cdy[l - 1]
+            if self.grouped:
+                ops.linear_bwd_data([self.qdy[l], self.cdy[l]], [self.qy[l], self.cy[l]], [self.qW[l], self.cW[l]],
+                                    relu=True, outs=[dxq, dxc], precision=pr)
+                ops.linear_bwd_weight([self.qdy[l], self.cdy[l]], [self.qy[l], self.cy[l]], [xq, xc], relu=True,
+                                      dws=[self.gqW[l], self.gcW[l]], dbs=[self.gqb[l], self.gcb[l]], precision=pr)
+            else:
+                for dy, y, W_, x, dx, gW, gb in ((self.qdy[l], self.qy[l], self.qW[l], xq, dxq, self.gqW[l], self.gqb[l]),
+                                                 (self.cdy[l], self.cy[l], self.cW[l], xc, dxc, self.gcW[l], self.gcb[l])):
+                    ops.linear_bwd_data([dy], [y], [W_], relu=True, outs=[dx], precision=pr)
+                    ops.linear_bwd_weight([dy], [y], [x], relu=True, dws=[gW], dbs=[gb], precision=pr)
+
+    def step(self) -> None:
+        """One training step on the batch currently in ``cols`` / ``labels``."""
+        B, F = self.B, self.F
+        main = torch.cuda.current_stream(self.device)
+        ops.kjt_build_mod_dropzero(self.cols, self.num_embeddings, self.values, self.lengths, self.offsets, self.lpk)
+        if self.side is not None:
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                self.tables.bwd_prepare(self.values, self.offsets, B, max_lookups=F * B)
+        else:
+            self.tables.bwd_prepare(self.values, self.offsets, B, max_lookups=F * B)
+        self.tables.pooled_fwd(self.values, self.offsets, B, out=self.pooled)
+        self._towers_fwd()
+        L = len(self.layer_sizes)
+        self.dot_bce(self.qy[L - 1], self.cy[L - 1], self.labels, logits=self.logits, loss=self.loss,
+                     dq=self.qdy[L - 1], dc=self.cdy[L - 1])
+        self._towers_bwd()
+        if self.side is not None:
+            main.wait_stream(self.side)
+        self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets, B, self.lr_emb, self.eps)
+        ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, self.lr_dense)
+
+    # ------------------------------------------------------------------------------------------
+    def capture(self) -> None:
+        """Record ``step()`` into a HIP graph (replayed by ``replay()``)."""
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self.step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.graph = g
+
+    def replay(self) -> None:
+        self.graph.replay()

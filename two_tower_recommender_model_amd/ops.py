@@ -145,7 +145,8 @@ class TableSet:
 
     def __init__(self, rows: Sequence[int], dims: Sequence[int], feature_table: Sequence[int],
                  device: torch.device, out_offsets: Optional[Sequence[int]] = None,
-                 weights: Optional[torch.Tensor] = None, align: int = 4):
+                 weights: Optional[torch.Tensor] = None, align: int = 4,
+                 out_rows: Optional[Sequence[int]] = None):
         self.rows = [int(r) for r in rows]
         self.dims = [int(d) for d in dims]
         self.T = len(self.rows)
@@ -176,6 +177,7 @@ class TableSet:
                 o += self.dims[t]
         self.out_offsets = [int(o) for o in out_offsets]
         self.out_dim = max(o + self.dims[t] for o, t in zip(self.out_offsets, self.feature_table))
+        self.out_rows = [int(r) for r in out_rows] if out_rows is not None else [0] * self.F
         self._tm = (TableMeta * self.T)()
         for t in range(self.T):
             self._tm[t].weight_offset = self.weight_offsets[t]
@@ -186,9 +188,18 @@ class TableSet:
         for f, t in enumerate(self.feature_table):
             self._fm[f].table = t
             self._fm[f].out_offset = self.out_offsets[f]
+            self._fm[f].out_row = self.out_rows[f]
         self._bwd_ws = None
         self._bwd_cap = 0
         self.err_count = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    def remap(self, feature_table: Sequence[int], out_offsets: Sequence[int],
+              out_rows: Optional[Sequence[int]] = None) -> "TableSet":
+        """Same tables and storage, another KJT key -> table / output-placement map."""
+        ts = TableSet(self.rows, self.dims, feature_table, self.device, out_offsets=out_offsets, weights=self.weights,
+                      out_rows=out_rows)
+        ts.state = self.state
+        return ts
 
     def table_view(self, t: int) -> torch.Tensor:
         o = self.weight_offsets[t]
@@ -211,7 +222,7 @@ class TableSet:
         if offsets.dtype != torch.int32:
             raise _lib.TTError("pooled_fwd: offsets must be int32")
         if out is None:
-            out = torch.empty(B, self.out_dim, dtype=torch.float32, device=self.device)
+            out = torch.empty(max(self.out_rows) + B, self.out_dim, dtype=torch.float32, device=self.device)
         ldo = out.stride(0) if out.dim() == 2 else self.out_dim
         idt = id_dtype_code(values.dtype) if values.numel() else TT_I64
         check(_lib_().tt_pooled_fwd(ptr(self.weights), self._tm, self.T, self._fm, self.F, B, ptr(values), idt,
@@ -272,8 +283,17 @@ def _x_code(t: torch.Tensor) -> int:
     raise _lib.TTError("linear: X must be fp32 or bf16")
 
 
+def _compute_code(precision: str) -> int:
+    if precision == "bf16":
+        return TT_BF16
+    if precision == "fp32":
+        return TT_F32
+    raise _lib.TTError("precision must be 'bf16' or 'fp32'")
+
+
 def linear_fwd(xs: Sequence[torch.Tensor], ws: Sequence[torch.Tensor], bs: Sequence[Optional[torch.Tensor]],
-               relu: bool = True, outs: Optional[Sequence[torch.Tensor]] = None) -> List[torch.Tensor]:
+               relu: bool = True, outs: Optional[Sequence[torch.Tensor]] = None,
+               precision: str = "bf16") -> List[torch.Tensor]:
     """Grouped Y_g = act(X_g W_g^T + b_g) on bf16 MFMA (fp32 accumulate); X row stride may be > K
     (column slices of a KeyedTensor are consumed in place)."""
     G = len(xs)
@@ -288,12 +308,13 @@ def linear_fwd(xs: Sequence[torch.Tensor], ws: Sequence[torch.Tensor], bs: Seque
         outs = [torch.empty(M, N, dtype=torch.float32, device=dev) for _ in range(G)]
     check(_lib_().tt_linear_fwd(G, ptr_array(xs), _x_code(xs[0]), xs[0].stride(0), ptr_array(ws), ptr_array(bs),
                                 M, N, K, ptr_array(outs), outs[0].stride(0), 1 if relu else 0,
-                                stream_handle(dev)), "linear_fwd")
+                                _compute_code(precision), stream_handle(dev)), "linear_fwd")
     return list(outs)
 
 
 def linear_bwd_data(dys: Sequence[torch.Tensor], ys: Sequence[Optional[torch.Tensor]], ws: Sequence[torch.Tensor],
-                    relu: bool = True, outs: Optional[Sequence[torch.Tensor]] = None) -> List[torch.Tensor]:
+                    relu: bool = True, outs: Optional[Sequence[torch.Tensor]] = None,
+                    precision: str = "bf16") -> List[torch.Tensor]:
     G = len(dys)
     M, N = dys[0].shape
     K = ws[0].shape[1]
@@ -303,13 +324,13 @@ def linear_bwd_data(dys: Sequence[torch.Tensor], ys: Sequence[Optional[torch.Ten
         outs = [torch.empty(M, K, dtype=torch.float32, device=dev) for _ in range(G)]
     check(_lib_().tt_linear_bwd_data(G, ptr_array(dys), ptr_array(ys if relu else [None] * G), dys[0].stride(0),
                                      ptr_array(ws), M, N, K, ptr_array(outs), outs[0].stride(0), 1 if relu else 0,
-                                     stream_handle(dev)), "linear_bwd_data")
+                                     _compute_code(precision), stream_handle(dev)), "linear_bwd_data")
     return list(outs)
 
 
 def linear_bwd_weight(dys: Sequence[torch.Tensor], ys: Sequence[Optional[torch.Tensor]], xs: Sequence[torch.Tensor],
                       relu: bool = True, dws: Optional[Sequence[torch.Tensor]] = None,
-                      dbs: Optional[Sequence[Optional[torch.Tensor]]] = None):
+                      dbs: Optional[Sequence[Optional[torch.Tensor]]] = None, precision: str = "bf16"):
     G = len(dys)
     M, N = dys[0].shape
     K = xs[0].shape[1]
@@ -323,7 +344,8 @@ def linear_bwd_weight(dys: Sequence[torch.Tensor], ys: Sequence[Optional[torch.T
     ws = scratch(lib.tt_linear_bwd_weight_workspace_bytes(G, M, N, K), dev, "bwd_weight")
     check(lib.tt_linear_bwd_weight(G, ptr_array(dys), ptr_array(ys if relu else [None] * G), dys[0].stride(0),
                                    ptr_array(xs), _x_code(xs[0]), xs[0].stride(0), M, N, K, ptr_array(dws),
-                                   ptr_array(dbs), 1 if relu else 0, ptr(ws), ws.numel(), stream_handle(dev)),
+                                   ptr_array(dbs), 1 if relu else 0, _compute_code(precision), ptr(ws), ws.numel(),
+                                   stream_handle(dev)),
           "linear_bwd_weight")
     return list(dws), list(dbs)
 
@@ -369,3 +391,26 @@ def adam_step(params: torch.Tensor, grads: torch.Tensor, exp_avg: torch.Tensor, 
     check(_lib_().tt_adam_step(ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), params.numel(), float(lr),
                                float(beta1), float(beta2), float(eps), float(weight_decay), ptr(step_state),
                                stream_handle(params.device)), "adam_step")
+
+
+class HipLookupBackend:
+    """The compute backend of the sharded lookup (ShardedEmbeddingBagCollection): table storage,
+    pooled forward, fused backward and the KJT integer ops, all on libtt_mi355x.so."""
+
+    name = "hip"
+
+    def table_set(self, rows, dims, feature_table, device, out_offsets=None, out_rows=None) -> TableSet:
+        return TableSet(rows, dims, feature_table, device, out_offsets=out_offsets, out_rows=out_rows)
+
+    def complete_cumsum(self, lengths: torch.Tensor) -> torch.Tensor:
+        return complete_cumsum(lengths)
+
+    def block_bucketize(self, lengths, offsets, values, F, B, block_sizes, W):
+        return block_bucketize(lengths, offsets, values, F, B, block_sizes, W)
+
+    def kjt_permute(self, lengths, offsets, values, F, B, perm, total=None):
+        l, o, v, _ = kjt_permute(lengths, offsets, values, F, B, perm, total=total)
+        return l, o, v
+
+
+HIP_BACKEND = HipLookupBackend()
