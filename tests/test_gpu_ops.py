@@ -240,7 +240,7 @@ def test_linear_fwd_bwd_vs_fp32(ops, device, M, N, K, groups, xbf16):
         np.testing.assert_allclose(dbs[i].cpu().numpy(), dz.sum(0).numpy(), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("B,dim,ldt", [(8192, 64, torch.int32), (1, 8, torch.int64), (1000, 33, torch.float32)])
+@pytest.mark.parametrize("B,dim,ldt", [(8192, 64, torch.int32), (2, 8, torch.int64), (1000, 33, torch.float32)])
 def test_dot_bce(ops, device, B, dim, ldt):
     g = torch.Generator().manual_seed(B)
     q = torch.rand(B, dim, generator=g)

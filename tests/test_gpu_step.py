@@ -55,7 +55,10 @@ def test_fused_step_matches_reference_golden(device, case, precision):
         st.load_batch(cols, torch.from_numpy(g[f"s{s}_label"]).to(torch.int32).to(device))
         st.replay()
         torch.cuda.synchronize()
-        np.testing.assert_allclose(st.pooled.cpu().numpy(), g[f"s{s}_pooled"], rtol=1e-6, atol=1e-7)
+        # step 0 pools the initial tables (bit-exact gather); later steps pool rows updated with
+        # tower gradients computed at this precision
+        np.testing.assert_allclose(st.pooled.cpu().numpy(), g[f"s{s}_pooled"], rtol=1e-6,
+                                   atol=1e-7 if s == 0 or precision == "fp32" else tol["table"])
         _logits_close(st.logits.cpu().numpy(), g[f"s{s}_logits"], tol["logit"])
         np.testing.assert_allclose(float(st.loss), float(g[f"s{s}_loss"]), rtol=tol["loss"])
         if precision == "fp32":
