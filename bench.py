@@ -86,12 +86,23 @@ def algorithmic_bytes(step, nnz: int, uniq: int):
 
 
 def time_kernel(fn, iters, pre=None):
-    """Average device time of fn() measured with HIP events on the stream it launches on."""
+    """Average device time of one fn() launch, HIP events on the stream it launches on: with no
+    per-launch prerequisite, `iters` back-to-back launches between two events; otherwise an event
+    pair around each launch (its prerequisite `pre` runs outside the pair)."""
     st = torch.cuda.current_stream()
+    if pre is None:
+        fn()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(iters):
+            fn()
+        b.record(st)
+        b.synchronize()
+        return a.elapsed_time(b) / iters
     tot = 0.0
     for _ in range(iters):
-        if pre is not None:
-            pre()
+        pre()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record(st)
@@ -144,29 +155,30 @@ def run_single(args):
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
     batches = synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1)
-    step.load_batch(*batches[0])
-    step.capture()
+    # one HIP graph per resident batch: replay i trains on batch i % 8 with no input copy
+    step.capture_pool(batches)
     for i in range(args.warmup):
-        step.load_batch(*batches[i % len(batches)])
-        step.replay()
+        step.replay(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step.load_batch(*batches[i % len(batches)])
-        step.replay()
+        step.replay(i)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ms = dt / args.steps * 1e3
     value = args.steps * B / dt
     loss = float(step.loss)
     # ---- dominant embedding kernels vs the HBM roofline (HIP events, same stream)
-    nnz = int(step.offsets[-1])
-    uniq = int(torch.unique(step.values[:nnz] + (torch.arange(nnz, device=dev) >= int(step.offsets[B])) * (1 << 40)).numel())
+    cols = batches[(args.steps - 1) % len(batches)][0]
+    ne = step.num_embeddings
+    keys = torch.cat([(c % n) + (t << 40) for t, (c, n) in enumerate(zip(cols, ne))])
+    nz = torch.cat([c != 0 for c in cols])
+    nnz = int(nz.sum())
+    uniq = int(torch.unique(keys[nz]).numel())
     fwd_bytes, k2d_bytes = algorithmic_bytes(step, nnz, uniq)
-    t_fwd = time_kernel(lambda: step.tables.pooled_fwd(step.values, step.offsets, B, out=step.pooled), args.kernel_iters)
-    t_k2d = time_kernel(lambda: step.tables.bwd_rowwise_adagrad(step.gpooled, step.offsets, B, 0.0, 1e-10),
-                        args.kernel_iters,
-                        pre=lambda: step.tables.bwd_prepare(step.values, step.offsets, B, max_lookups=step.F * B))
+    t_fwd = time_kernel(lambda: step.tables.pooled_fwd_cols(cols, ne, out=step.pooled), args.kernel_iters)
+    t_k2d = time_kernel(lambda: step.tables.bwd_rowwise_adagrad(step.gpooled, None, B, 0.0, 1e-10),
+                        args.kernel_iters, pre=lambda: step.tables.bwd_prepare_cols(cols, ne))
     kern = {
         "pooled_fwd": {"ms": round(t_fwd, 5), "bytes": fwd_bytes, "GB/s": round(fwd_bytes / t_fwd / 1e6, 1)},
         "bwd_rowwise_adagrad": {"ms": round(t_k2d, 5), "bytes": k2d_bytes, "GB/s": round(k2d_bytes / t_k2d / 1e6, 1)},

@@ -139,6 +139,16 @@ int tt_pooled_fwd(const float* weights, const tt_table_meta_t* tables, int T,
                   int id_dtype, const int32_t* offsets, int pooling, float* out, int64_t ldo,
                   int bounds_check, int32_t* err_count, void* stream);
 
+/* Single-hot column form of the reference's batch (one [B] id column per key, the loader's
+ * dict at 03_model_training.py:356-357): the transform of transform_to_torchrec_batch is applied
+ * inline (id 0 -> empty bag -> zero row; otherwise row = id mod num_embeddings[f], Python
+ * floor-mod), so the result equals tt_kjt_build_mod_dropzero followed by tt_pooled_fwd (SUM),
+ * without materialising the KJT. cols: HOST array of F device pointers. */
+int tt_pooled_fwd_cols(const float* weights, const tt_table_meta_t* tables, int T,
+                       const tt_feature_meta_t* features, int F, int64_t B, const void* const* cols,
+                       int id_dtype, const int64_t* num_embeddings, float* out, int64_t ldo,
+                       void* stream);
+
 /* ---- a8: deduplicated backward + fused exact row-wise Adagrad -------------------------------- */
 
 /* Workspace for up to max_lookups ids per step. Must be zeroed once by tt_bwd_workspace_init;
@@ -152,6 +162,14 @@ int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t
                    int64_t B, const void* values, int id_dtype, const int32_t* offsets,
                    int bounds_check, void* workspace, size_t ws_bytes, int64_t max_lookups,
                    void* stream);
+
+/* The same grouping for the single-hot column form (see tt_pooled_fwd_cols); lookup index =
+ * bag index, max_lookups >= F*B. Follow with tt_bwd_rowwise_adagrad (pooling SUM, offsets may
+ * be NULL). */
+int tt_bwd_prepare_cols(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                        int F, int64_t B, const void* const* cols, int id_dtype,
+                        const int64_t* num_embeddings, void* workspace, size_t ws_bytes,
+                        int64_t max_lookups, void* stream);
 
 /* For every unique row r of table t touched this step:
  *   G[r]   = sum over its lookups of grad_out[b, out_offset(f) : +D]  (x 1/len for MEAN pooling)
@@ -209,6 +227,44 @@ int tt_dot_bce_fwd_bwd(const float* q, int64_t ldq, const float* c, int64_t ldc,
                        int dim, const void* labels, int label_dtype, float* logits, float* loss,
                        float* dq, int64_t lddq, float* dc, int64_t lddc, float grad_scale,
                        void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a6+a7+a9 fused: both towers' MLP step, dot + BCE, Adam (3 launches) --------------------- */
+
+/* Two towers of L layers each (Linear + ReLU on every layer); tower t reads pooled columns
+ * [in_col[t], in_col[t] + in_dim[t]). Flat fp32 parameter layout: for t in (query, candidate),
+ * for l < L: W_(t,l) [width[l]][in_l] row-major, then b_(t,l) [width[l]]; in_0 = in_dim[t],
+ * in_l = width[l-1]. Limits: L <= 4; widths multiples of 32 in [32, 128]; in_dim multiples of
+ * 32 in [32, 1024]; in_col % 4 == 0; B % 8 == 0. bf16 MFMA operands, fp32 accumulation. */
+typedef struct {
+  int32_t L;
+  int32_t width[4];
+  int32_t in_dim[2];
+  int32_t in_col[2];
+  int32_t _pad;
+} tt_tower_shape_t;
+
+int64_t tt_tower_num_params(const tt_tower_shape_t* shape);
+size_t tt_tower_workspace_bytes(const tt_tower_shape_t* shape, int64_t B);
+/* Zero the workspace and upload the T2 tile list (synchronises `stream`: call at setup only).
+ * The workspace also holds the bf16 weight copies: run tt_tower_update(do_adam = 0) after
+ * (re)loading parameters. */
+int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* workspace, size_t ws_bytes,
+                            void* stream);
+/* T1: forward of both towers, logits, mean BCE (loss), its gradient back through every layer;
+ * dX written into gpooled's tower-input columns (ld = ldp). Also leaves, in the workspace, what
+ * T2 needs. */
+int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp,
+                     float* gpooled, const float* params, const void* labels, int label_dtype,
+                     float grad_scale, float* logits, float* loss, void* workspace, size_t ws_bytes,
+                     void* stream);
+/* T2: weight/bias gradients of every layer into the workspace (fixed-order partial slabs). */
+int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, void* workspace, size_t ws_bytes, void* stream);
+/* T3: fixed-order reduction of T2's partials, Adam (when do_adam; step_state as tt_adam_step),
+ * and the bf16 weight copies for the next T1. grads_out (nullable) receives the gradient. */
+int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
+                    float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, int64_t* step_state, int do_adam, float* grads_out,
+                    void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- a9: Adam on the flat dense-parameter buffer (torch.optim.Adam, amsgrad=False) ------------ */
 

@@ -1,10 +1,17 @@
+# tests -> smoke -> bench -> rocprofv3 kernel stats (each step time-limited; stop at first hard failure)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1; rc=$?
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -q -m gpu ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
 echo "pytest exit=$rc" >> gpurun_out/gpu_tests.log
-tail -30 gpurun_out/gpu_tests.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke exit=$?" >> gpurun_out/smoke.log
-tail -5 gpurun_out/smoke.log
-timeout -k 10 600 python bench.py --steps 50 --warmup 10 > gpurun_out/bench.log 2>&1; echo "bench exit=$?" >> gpurun_out/bench.log
-tail -5 gpurun_out/bench.log
+tail -25 gpurun_out/gpu_tests.log
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+echo "smoke exit=$rc" >> gpurun_out/smoke.log; tail -2 gpurun_out/smoke.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$?
+echo "bench exit=$rc" >> gpurun_out/bench.log; tail -3 gpurun_out/bench.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+mkdir -p gpurun_out/prof
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof_bench.log 2>&1
+echo "prof exit=$?" >> gpurun_out/prof_bench.log; tail -1 gpurun_out/prof_bench.log

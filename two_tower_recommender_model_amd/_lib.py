@@ -37,6 +37,16 @@ class FeatureMeta(C.Structure):
     _fields_ = [("table", C.c_int32), ("out_offset", C.c_int32), ("out_row", C.c_int64)]
 
 
+class TowerShape(C.Structure):
+    _fields_ = [
+        ("L", C.c_int32),
+        ("width", C.c_int32 * 4),
+        ("in_dim", C.c_int32 * 2),
+        ("in_col", C.c_int32 * 2),
+        ("_pad", C.c_int32),
+    ]
+
+
 _vp = C.c_void_p
 _i32 = C.c_int32
 _i64 = C.c_int64
@@ -48,6 +58,7 @@ _pi64 = C.POINTER(C.c_int64)
 _pi32 = C.POINTER(C.c_int32)
 _ptm = C.POINTER(TableMeta)
 _pfm = C.POINTER(FeatureMeta)
+_psh = C.POINTER(TowerShape)
 
 # name -> (restype, argtypes); the compute entry points are exactly those counted by
 # tt_num_entry_points() in csrc/api.cpp.
@@ -103,6 +114,17 @@ SIGNATURES = {
         [_vp, _i64, _vp, _i64, _i64, _int, _vp, _int, _vp, _vp, _vp, _i64, _vp, _i64, _f32, _vp, _sz, _vp],
     ),
     "tt_adam_step": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _vp, _vp]),
+    "tt_pooled_fwd_cols": (_int, [_vp, _ptm, _int, _pfm, _int, _i64, _pvp, _int, _pi64, _vp, _i64, _vp]),
+    "tt_bwd_prepare_cols": (_int, [_ptm, _int, _pfm, _int, _i64, _pvp, _int, _pi64, _vp, _sz, _i64, _vp]),
+    "tt_tower_num_params": (C.c_int64, [_psh]),
+    "tt_tower_workspace_bytes": (_sz, [_psh, _i64]),
+    "tt_tower_workspace_init": (_int, [_psh, _i64, _vp, _sz, _vp]),
+    "tt_tower_fwd_bwd": (_int, [_psh, _i64, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _vp, _sz, _vp]),
+    "tt_tower_wgrad": (_int, [_psh, _i64, _vp, _sz, _vp]),
+    "tt_tower_update": (
+        _int,
+        [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _int, _vp, _vp, _sz, _vp],
+    ),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -121,6 +143,12 @@ COMPUTE_ENTRY_POINTS = [
     "tt_dot_bce_workspace_init",
     "tt_dot_bce_fwd_bwd",
     "tt_adam_step",
+    "tt_tower_workspace_init",
+    "tt_tower_fwd_bwd",
+    "tt_tower_wgrad",
+    "tt_tower_update",
+    "tt_pooled_fwd_cols",
+    "tt_bwd_prepare_cols",
 ]
 
 _lib = None

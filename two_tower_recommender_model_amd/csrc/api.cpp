@@ -43,7 +43,9 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_kjt_build_mod_dropzero, tt_complete_cumsum, tt_kjt_permute, tt_block_bucketize, tt_pooled_fwd,
 // tt_bwd_workspace_init, tt_bwd_prepare, tt_bwd_rowwise_adagrad, tt_pooled_bwd_dense,
 // tt_linear_fwd, tt_linear_bwd_data, tt_linear_bwd_weight, tt_dot_bce_workspace_init,
-// tt_dot_bce_fwd_bwd, tt_adam_step
-int tt_num_entry_points(void) { return 15; }
+// tt_dot_bce_fwd_bwd, tt_adam_step, tt_tower_workspace_init, tt_tower_fwd_bwd, tt_tower_wgrad,
+// tt_tower_update
+// tt_pooled_fwd_cols, tt_bwd_prepare_cols
+int tt_num_entry_points(void) { return 21; }
 
 }  // extern "C"

@@ -5,16 +5,32 @@
 // row, so one D=128 fp32 row is one 512-B coalesced read by 32 lanes and a wave pools 2 bags at
 // once. Ids of a bag are read 4 at a time so 4 independent rows are in flight per group.
 // Algorithmic bytes per lookup: 4*D (row) + id bytes; per bag 4*D write + 4 (offset).
+// A column variant (k1c) reads single-hot ids straight from the loader's columns and applies the
+// reference transform inline (drop id 0, id mod N: transform_to_torchrec_batch semantics).
 //
-// Backward (k2a..k2d): lookups are grouped by unique (table,row) with an open-addressing hash in
-// the workspace (k2a), a reduce-then-scan over the hash slots assigns each unique row a segment
-// (k2b), the bag ids are scattered into their segments (k2c), and one wave per unique row sums the
-// pooled-output gradient rows of its segment and applies the row-wise Adagrad update in place
-// (k2d). k2a-k2c read only ids, so they can run concurrently with the forward and the towers.
-// k2d leaves the hash table clean for the next step (no per-step memset).
+// Backward: lookups are grouped by unique (table,row) with an open-addressing hash (k2a), a
+// reduce-then-scan over the hash slots gives every unique row a segment and a 16-B record
+// {key, start, count} and leaves the hash table clean for the next step (k2b), the bag ids are
+// scattered into their segments (k2c), then per unique row the pooled-gradient rows of its
+// segment are summed and the row-wise Adagrad update is applied in place (k2d). k2a-k2c read only
+// ids, so they run beside the forward and the towers.
+// k2d "narrow" (D <= 128, D % 4 == 0): a half-wave per unique row (32 lanes x float4 = one
+// 512-B row), two rows per wave; segments of <= 32 lookups are summed in ascending bag order
+// (bitwise reproducible), longer ones in fp64 (order-independent in practice). k2d "generic":
+// a wave per row for other dims.
 #include "tt_common.h"
 
 namespace tt {
+
+__device__ __forceinline__ int64_t py_mod64(int64_t a, int64_t n) {
+  int64_t r = a % n;
+  return (r != 0 && ((r < 0) != (n < 0))) ? r + n : r;
+}
+
+struct ColArgs {
+  const void* col[TT_MAX_FEATURES];
+  int64_t num_emb[TT_MAX_FEATURES];  // the transform's divisor (id mod N)
+};
 
 // ============================== forward =======================================================
 
@@ -33,7 +49,7 @@ __device__ __forceinline__ void pool_bag_cols(const float* __restrict__ w, const
   typedef __attribute__((ext_vector_type(VEC))) float vf;
   const int ncol = D / VEC;
   for (int c = lane_g; c < ncol; c += G) {
-    vf acc0 = (vf)(0.f), acc1 = (vf)(0.f);
+    vf acc0 = (vf)(0.f);
     int64_t j = s;
     for (; j + 4 <= e; j += 4) {
       int64_t id0 = load_id(values, id_dtype, j), id1 = load_id(values, id_dtype, j + 1);
@@ -62,10 +78,15 @@ __device__ __forceinline__ void pool_bag_cols(const float* __restrict__ w, const
       }
       acc0 += *reinterpret_cast<const vf*>(w + id * D + c * VEC);
     }
-    (void)acc1;
     acc0 *= scale;
     *reinterpret_cast<vf*>(out + c * VEC) = acc0;
   }
+}
+
+__device__ __forceinline__ int feature_of_block(const FwdArgs& a) {
+  int f = 0;
+  while (f + 1 < a.m.F && (int)blockIdx.x >= a.block_start[f + 1]) ++f;
+  return f;
 }
 
 __global__ void __launch_bounds__(256) pooled_fwd_kernel(const float* __restrict__ weights, FwdArgs a,
@@ -73,9 +94,7 @@ __global__ void __launch_bounds__(256) pooled_fwd_kernel(const float* __restrict
                                                          const int32_t* __restrict__ offsets, int pooling,
                                                          float* __restrict__ out, int64_t ldo,
                                                          int bounds_check, int32_t* __restrict__ err) {
-  // which feature does this workgroup serve (F <= 64, wave-uniform scalar search)
-  int f = 0;
-  while (f + 1 < a.m.F && (int)blockIdx.x >= a.block_start[f + 1]) ++f;
+  const int f = feature_of_block(a);  // wave-uniform scalar search (F <= 64)
   const tt_feature_meta_t fm = a.m.features[f];
   const tt_table_meta_t tm = a.m.tables[fm.table];
   const int G = a.group[f];
@@ -95,6 +114,37 @@ __global__ void __launch_bounds__(256) pooled_fwd_kernel(const float* __restrict
     pool_bag_cols<1>(w, values, id_dtype, s, e, tm.num_rows, tm.dim, lane_g, G, scale, o, bounds_check, err);
 }
 
+// k1c: single-hot columns -> pooled rows, transform applied inline (id 0 -> empty bag -> zeros)
+template <int VEC>
+__device__ __forceinline__ void copy_row(const float* __restrict__ src, float* __restrict__ dst, int D, int lane_g,
+                                         int G) {
+  typedef __attribute__((ext_vector_type(VEC))) float vf;
+  for (int c = lane_g; c < D / VEC; c += G) {
+    vf v = src ? *reinterpret_cast<const vf*>(src + c * VEC) : (vf)(0.f);
+    *reinterpret_cast<vf*>(dst + c * VEC) = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) pooled_fwd_cols_kernel(const float* __restrict__ weights, FwdArgs a, ColArgs ca,
+                                                              int id_dtype, float* __restrict__ out, int64_t ldo) {
+  const int f = feature_of_block(a);
+  const tt_feature_meta_t fm = a.m.features[f];
+  const tt_table_meta_t tm = a.m.tables[fm.table];
+  const int G = a.group[f];
+  const int64_t B = a.m.B;
+  const int64_t b = (int64_t)(blockIdx.x - a.block_start[f]) * (256 / G) + threadIdx.x / G;
+  if (b >= B) return;
+  const int lane_g = threadIdx.x & (G - 1);
+  const int64_t id = load_id(ca.col[f], id_dtype, b);
+  const float* src = nullptr;
+  if (id != 0) src = weights + tm.weight_offset + py_mod64(id, ca.num_emb[f]) * tm.dim;
+  float* o = out + (fm.out_row + b) * ldo + fm.out_offset;
+  if (a.vec[f] == 4)
+    copy_row<4>(src, o, tm.dim, lane_g, G);
+  else
+    copy_row<1>(src, o, tm.dim, lane_g, G);
+}
+
 // ============================== backward ======================================================
 
 constexpr uint64_t EMPTY_KEY = ~0ull;
@@ -109,15 +159,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+struct URec {
+  uint64_t key;
+  int32_t seg;
+  int32_t len;
+};
+
 struct BwdWs {
-  uint64_t* keys;   // [cap] hash keys (EMPTY when free)
-  int32_t* cnt;     // [cap] lookups per slot / scatter cursor
-  int32_t* seg;     // [cap] segment start per slot
-  int32_t* slot_of; // [L]   slot of each lookup
+  uint64_t* keys;   // [cap] hash keys (EMPTY when free; cleaned by k2b)
+  int32_t* cnt;     // [cap] lookups per slot (cleaned by k2b)
+  int32_t* cur;     // [cap] scatter cursor per slot (set by k2b)
+  int32_t* slot_of; // [L]   slot of each lookup (-1: none)
   int32_t* perm;    // [L]   bag ids grouped by unique row
-  int32_t* useg;    // [L]   segment start per unique
-  int32_t* ulen;    // [L]   segment length per unique
-  int32_t* uslot;   // [L]   slot per unique
+  URec* urec;       // [L]   per unique row
   int32_t* bsum_u;  // [nb]  scan partials (unique count)
   int32_t* bsum_c;  // [nb]  scan partials (lookup count)
   int32_t* U;       // [1]   number of unique rows this step
@@ -144,12 +198,10 @@ static size_t bwd_layout(void* base, int64_t L, BwdWs* w) {
   BwdWs t;
   t.keys = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * cap));
   t.cnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * cap));
-  t.seg = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * cap));
+  t.cur = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * cap));
   t.slot_of = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
   t.perm = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
-  t.useg = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
-  t.ulen = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
-  t.uslot = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
+  t.urec = reinterpret_cast<URec*>(take(sizeof(URec) * L));
   t.bsum_u = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
   t.bsum_c = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
   t.U = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
@@ -159,12 +211,28 @@ static size_t bwd_layout(void* base, int64_t L, BwdWs* w) {
   return off;
 }
 
+__device__ __forceinline__ int32_t hash_insert(BwdWs& ws, uint64_t key) {
+  const uint64_t mask = (uint64_t)ws.cap - 1;
+  uint64_t h = mix64(key) & mask;
+  while (true) {
+    const uint64_t c = __hip_atomic_load(&ws.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == key) break;
+    if (c == EMPTY_KEY) {
+      const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.keys[h]),
+                                      (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+      if (prev == EMPTY_KEY || prev == key) break;
+    }
+    h = (h + 1) & mask;
+  }
+  atomicAdd(&ws.cnt[h], 1);
+  return (int32_t)h;
+}
+
 // k2a: thread per bag: hash-insert every lookup's (table,row), count per slot
 __global__ void __launch_bounds__(256) bwd_hash_kernel(EmbMeta m, const void* __restrict__ values, int id_dtype,
                                                        const int32_t* __restrict__ offsets, int bounds_check,
                                                        BwdWs ws) {
   const int64_t nbag = (int64_t)m.F * m.B;
-  const uint64_t mask = (uint64_t)ws.cap - 1;
   for (int64_t bag = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; bag < nbag;
        bag += (int64_t)gridDim.x * blockDim.x) {
     const int f = (int)(bag / m.B);
@@ -174,21 +242,25 @@ __global__ void __launch_bounds__(256) bwd_hash_kernel(EmbMeta m, const void* __
     for (int64_t j = s; j < e; ++j) {
       int64_t id = load_id(values, id_dtype, j);
       if (bounds_check && (uint64_t)id >= (uint64_t)rows) id = 0;
-      const uint64_t key = ((uint64_t)t << KEY_TABLE_SHIFT) | (uint64_t)id;
-      uint64_t h = mix64(key) & mask;
-      while (true) {
-        uint64_t cur = __hip_atomic_load(&ws.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == key) break;
-        if (cur == EMPTY_KEY) {
-          uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.keys[h]),
-                                    (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-          if (prev == EMPTY_KEY || prev == key) break;
-        }
-        h = (h + 1) & mask;
-      }
-      ws.slot_of[j] = (int32_t)h;
-      atomicAdd(&ws.cnt[h], 1);
+      ws.slot_of[j] = hash_insert(ws, ((uint64_t)t << KEY_TABLE_SHIFT) | (uint64_t)id);
     }
+  }
+}
+
+// k2a (columns): lookup index = bag index; dropped ids get slot -1
+__global__ void __launch_bounds__(256) bwd_hash_cols_kernel(EmbMeta m, ColArgs ca, int id_dtype, BwdWs ws) {
+  const int64_t nbag = (int64_t)m.F * m.B;
+  for (int64_t bag = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; bag < nbag;
+       bag += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(bag / m.B);
+    const int64_t b = bag - (int64_t)f * m.B;
+    const int64_t id = load_id(ca.col[f], id_dtype, b);
+    int32_t h = -1;
+    if (id != 0) {
+      const int t = m.features[f].table;
+      h = hash_insert(ws, ((uint64_t)t << KEY_TABLE_SHIFT) | (uint64_t)py_mod64(id, ca.num_emb[f]));
+    }
+    ws.slot_of[bag] = h;
   }
 }
 
@@ -216,10 +288,10 @@ __global__ void __launch_bounds__(256) bwd_scan_reduce_kernel(BwdWs ws) {
   }
 }
 
-// k2b-2: exclusive scans -> unique index and segment start per occupied slot
+// k2b-2: exclusive scans -> record {key, segment start, count} per unique row; cursor per slot;
+// the slot's key and count are reset here, so the table is clean for the next step's k2a.
 __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
   __shared__ int lds[8];
-  // prefixes of the preceding tiles
   int pu = 0, pc = 0;
   for (int i = threadIdx.x; i < (int)blockIdx.x; i += 256) {
     pu += ws.bsum_u[i];
@@ -244,7 +316,6 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
     lu += c[j] > 0;
     lcnt += c[j];
   }
-  // two block scans at once (wave shuffles, then 4 wave totals)
   int iu = lu, ic = lcnt;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -273,11 +344,14 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
   for (int j = 0; j < 4; ++j) {
     if (c[j] > 0) {
       const int64_t h = base + j;
-      ws.useg[eu] = ec;
-      ws.ulen[eu] = c[j];
-      ws.uslot[eu] = (int32_t)h;
-      ws.seg[h] = ec;
-      ws.cnt[h] = 0;  // becomes the scatter cursor
+      URec rec;
+      rec.key = ws.keys[h];
+      rec.seg = ec;
+      rec.len = c[j];
+      ws.urec[eu] = rec;
+      ws.cur[h] = ec;
+      ws.keys[h] = EMPTY_KEY;
+      ws.cnt[h] = 0;
       eu += 1;
       ec += c[j];
     }
@@ -286,25 +360,26 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
 }
 
 // k2c: thread per bag: scatter bag ids into their unique row's segment
-__global__ void __launch_bounds__(256) bwd_scatter_kernel(EmbMeta m, const int32_t* __restrict__ offsets,
-                                                          BwdWs ws) {
+__global__ void __launch_bounds__(256) bwd_scatter_kernel(EmbMeta m, const int32_t* __restrict__ offsets, BwdWs ws) {
   const int64_t nbag = (int64_t)m.F * m.B;
   for (int64_t bag = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; bag < nbag;
        bag += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = offsets[bag], e = offsets[bag + 1];
+    const int64_t s = offsets ? offsets[bag] : bag, e = offsets ? offsets[bag + 1] : bag + 1;
     for (int64_t j = s; j < e; ++j) {
       const int h = ws.slot_of[j];
-      const int pos = ws.seg[h] + atomicAdd(&ws.cnt[h], 1);
+      if (h < 0) continue;
+      const int pos = atomicAdd(&ws.cur[h], 1);
       ws.perm[pos] = (int32_t)bag;
     }
   }
 }
 
-// 64-lane bitonic sort (ascending) of one int per lane
-__device__ __forceinline__ int wave_bitonic_sort(int v) {
-  const int lane = threadIdx.x & 63;
+// ascending bitonic sort of one int per lane over groups of W lanes (W = 32 or 64)
+template <int W>
+__device__ __forceinline__ int bitonic_sort(int v) {
+  const int lane = threadIdx.x & (W - 1);
 #pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
+  for (int k = 2; k <= W; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
       const int o = __shfl_xor(v, j, 64);
@@ -317,176 +392,196 @@ __device__ __forceinline__ int wave_bitonic_sort(int v) {
   return v;
 }
 
-constexpr int ADA_KMAX = 4;  // up to 4 x 64 x VEC columns per row (D <= 1024 with float4)
+struct BagRow {
+  const float* g;
+  int64_t B;
+  int64_t ldg;
+  const tt_feature_meta_t* feats;
+  __device__ __forceinline__ const float* row(int bag) const {
+    const int f = (int)(bag / B);
+    const int64_t b = bag - (int64_t)f * B;
+    return g + (feats[f].out_row + b) * ldg + feats[f].out_offset;
+  }
+};
+
+// ---- k2d narrow: half-wave per unique row, D <= 128, D % 4 == 0 ----------------------------
+__global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, const float* __restrict__ grad_out,
+                                                                 int64_t ldg, const int32_t* __restrict__ offsets,
+                                                                 int pooling, float* __restrict__ weights,
+                                                                 float* __restrict__ state, float lr, float eps,
+                                                                 BwdWs ws) {
+  const int U = ws.U[0];
+  const int lane = threadIdx.x & 63;
+  const int hl = lane & 31, half = lane >> 5;
+  const BagRow br{grad_out, m.B, ldg, m.features};
+  const int64_t nhalf = (int64_t)gridDim.x * 8;
+  for (int64_t u = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half; u - half < U; u += nhalf) {
+    const bool active = u < U;
+    URec rec{0, 0, 0};
+    if (active) rec = ws.urec[u];
+    const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
+    const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
+    const tt_table_meta_t tm = m.tables[active ? t : 0];
+    const int D = tm.dim;
+    const bool col_ok = active && hl * 4 < D;
+    // independent of the gradient: fetch the row and its state early
+    float* wrow = weights + tm.weight_offset + r * D;
+    float* srow = state + tm.state_offset + r;
+    f32x4v wv = col_ok ? *reinterpret_cast<const f32x4v*>(wrow + hl * 4) : (f32x4v)(0.f);
+    const float s_old = active ? *srow : 0.f;
+    const int n = rec.len;
+    f32x4v g = (f32x4v)(0.f);
+    // both halves must agree on the path for the shuffles: take the long path if either is long
+    const int nmax = max(n, __shfl_xor(n, 32, 64));
+    if (nmax <= 32) {
+      int mine = (active && hl < n) ? ws.perm[rec.seg + hl] : 0x7fffffff;
+      mine = bitonic_sort<32>(mine);
+      for (int i = 0; i < nmax; i += 2) {
+        const int b0 = __shfl(mine, (lane & 32) + i, 64);
+        const int b1 = __shfl(mine, (lane & 32) + min(i + 1, 31), 64);
+        const bool v0 = i < n, v1 = i + 1 < n;
+        f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
+        if (col_ok && v0) x0 = *reinterpret_cast<const f32x4v*>(br.row(b0) + hl * 4);
+        if (col_ok && v1) x1 = *reinterpret_cast<const f32x4v*>(br.row(b1) + hl * 4);
+        if (pooling == TT_POOL_MEAN) {
+          if (v0) x0 *= 1.f / (float)max(1, offsets[b0 + 1] - offsets[b0]);
+          if (v1) x1 *= 1.f / (float)max(1, offsets[b1 + 1] - offsets[b1]);
+        }
+        if (v0) g += x0;
+        if (v1) g += x1;
+      }
+    } else {
+      // hot row(s): fp64 accumulation, 32 bag ids per chunk
+      double d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+      for (int base = 0; base < nmax; base += 32) {
+        const int cnt = min(32, max(0, n - base));
+        const int mine = (hl < cnt) ? ws.perm[rec.seg + base + hl] : 0;
+        const int cmax = min(32, max(cnt, __shfl_xor(cnt, 32, 64)));
+        for (int i = 0; i < cmax; ++i) {
+          const int b0 = __shfl(mine, (lane & 32) + i, 64);
+          if (col_ok && i < cnt) {
+            f32x4v x = *reinterpret_cast<const f32x4v*>(br.row(b0) + hl * 4);
+            if (pooling == TT_POOL_MEAN) x *= 1.f / (float)max(1, offsets[b0 + 1] - offsets[b0]);
+            d0 += x[0];
+            d1 += x[1];
+            d2 += x[2];
+            d3 += x[3];
+          }
+        }
+      }
+      g = f32x4v{(float)d0, (float)d1, (float)d2, (float)d3};
+    }
+    // row-wise Adagrad: s += mean(G^2); w += (-lr * G) / (sqrt(s) + eps)
+    float sq = g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (active) {
+      const float snew = s_old + sq / (float)D;
+      const float stdv = sqrtf(snew) + eps;
+      if (col_ok) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
+        *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
+      }
+      if (hl == 0) *srow = snew;
+    }
+  }
+}
+
+// ---- k2d generic: a wave per unique row, any D <= 1024 ------------------------------------
+constexpr int ADA_KMAX = 4;  // up to 4 x 64 x VEC columns per row
 
 template <int VEC>
-__device__ __forceinline__ void adagrad_row(const EmbMeta& m, const float* __restrict__ grad_out, int64_t ldg,
-                                            const int32_t* __restrict__ offsets, int pooling,
-                                            float* __restrict__ weights, float* __restrict__ state, float lr,
-                                            float eps, const BwdWs& ws, int t, int64_t r, int s, int n) {
+__device__ __forceinline__ void adagrad_row(const EmbMeta& m, const BagRow& br, const int32_t* __restrict__ offsets,
+                                            int pooling, float* __restrict__ weights, float* __restrict__ state,
+                                            float lr, float eps, const BwdWs& ws, int t, int64_t r, int s, int n) {
   typedef __attribute__((ext_vector_type(VEC))) float vf;
   const int lane = threadIdx.x & 63;
   const tt_table_meta_t tm = m.tables[t];
   const int D = tm.dim;
-  const int ncol = D / VEC;  // VEC divides D
-  const int64_t B = m.B;
-  float g[ADA_KMAX][VEC];
-#pragma unroll
-  for (int k = 0; k < ADA_KMAX; ++k)
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) g[k][v] = 0.f;
-
-  auto row_ptr = [&](int bag) -> const float* {
-    const int f = bag / (int)B;
-    const int64_t b = bag - (int64_t)f * B;
-    return grad_out + (m.features[f].out_row + b) * ldg + m.features[f].out_offset;
-  };
-  auto bag_scale = [&](int bag) -> float {
-    if (pooling != TT_POOL_MEAN) return 1.f;
-    const int len = offsets[bag + 1] - offsets[bag];
-    return len > 0 ? 1.f / (float)len : 1.f;
-  };
-
-  if (n <= 64) {
-    // deterministic: sum in ascending bag order
-    int mine = lane < n ? ws.perm[s + lane] : 0x7fffffff;
-    mine = wave_bitonic_sort(mine);
-    int i = 0;
-    for (; i + 2 <= n; i += 2) {
-      const int b0 = __shfl(mine, i, 64), b1 = __shfl(mine, i + 1, 64);
-      const float* p0 = row_ptr(b0);
-      const float* p1 = row_ptr(b1);
-      const float s0 = bag_scale(b0), s1 = bag_scale(b1);
-#pragma unroll
-      for (int k = 0; k < ADA_KMAX; ++k) {
-        const int c = lane + k * 64;
-        if (c < ncol) {
-          const vf x0 = *reinterpret_cast<const vf*>(p0 + c * VEC);
-          const vf x1 = *reinterpret_cast<const vf*>(p1 + c * VEC);
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) {
-            g[k][v] += x0[v] * s0;
-            g[k][v] += x1[v] * s1;
-          }
-        }
-      }
-    }
-    if (i < n) {
-      const int b0 = __shfl(mine, i, 64);
-      const float* p0 = row_ptr(b0);
-      const float s0 = bag_scale(b0);
-#pragma unroll
-      for (int k = 0; k < ADA_KMAX; ++k) {
-        const int c = lane + k * 64;
-        if (c < ncol) {
-          const vf x0 = *reinterpret_cast<const vf*>(p0 + c * VEC);
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) g[k][v] += x0[v] * s0;
-        }
-      }
-    }
-  } else {
-    // hot row: fp64 accumulation (order-independent in practice), 64 bag ids per chunk
-    double gd[ADA_KMAX][VEC];
-#pragma unroll
-    for (int k = 0; k < ADA_KMAX; ++k)
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) gd[k][v] = 0.0;
-    for (int base = 0; base < n; base += 64) {
-      const int cnt = min(64, n - base);
-      const int mine = lane < cnt ? ws.perm[s + base + lane] : 0;
-      int i = 0;
-      for (; i + 4 <= cnt; i += 4) {
-        const int bb[4] = {__shfl(mine, i, 64), __shfl(mine, i + 1, 64), __shfl(mine, i + 2, 64),
-                           __shfl(mine, i + 3, 64)};
-#pragma unroll
-        for (int k = 0; k < ADA_KMAX; ++k) {
-          const int c = lane + k * 64;
-          if (c < ncol) {
-            vf x[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const vf*>(row_ptr(bb[q]) + c * VEC);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float sc = bag_scale(bb[q]);
-#pragma unroll
-              for (int v = 0; v < VEC; ++v) gd[k][v] += (double)(x[q][v] * sc);
-            }
-          }
-        }
-      }
-      for (; i < cnt; ++i) {
-        const int b0 = __shfl(mine, i, 64);
-        const float* p0 = row_ptr(b0);
-        const float s0 = bag_scale(b0);
-#pragma unroll
-        for (int k = 0; k < ADA_KMAX; ++k) {
-          const int c = lane + k * 64;
-          if (c < ncol) {
-            const vf x0 = *reinterpret_cast<const vf*>(p0 + c * VEC);
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) gd[k][v] += (double)(x0[v] * s0);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < ADA_KMAX; ++k)
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) g[k][v] = (float)gd[k][v];
-  }
-
-  // row-wise Adagrad: s += mean(G^2); w += (-lr * G) / (sqrt(s) + eps)
-  float sq = 0.f;
-#pragma unroll
-  for (int k = 0; k < ADA_KMAX; ++k)
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) sq += g[k][v] * g[k][v];
-  sq = wave_sum(sq);
+  const int ncol = D / VEC;
+  float* w = weights + tm.weight_offset + r * D;
   float* srow = state + tm.state_offset + r;
+  float sq = 0.f;
+  float gsave[ADA_KMAX][VEC];
+  int sorted = lane < n ? ws.perm[s + lane] : 0x7fffffff;
+  if (n <= 64) sorted = bitonic_sort<64>(sorted);
+#pragma unroll
+  for (int k = 0; k < ADA_KMAX; ++k) {
+    const int c = lane + k * 64;
+    double acc[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[v] = 0.0;
+    float accf[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) accf[v] = 0.f;
+    if (n <= 64) {
+      for (int i = 0; i < n; ++i) {  // ascending bag order, fp32 (bitwise reproducible)
+        const int b = __shfl(sorted, i, 64);
+        if (c < ncol) {
+          vf x = *reinterpret_cast<const vf*>(br.row(b) + c * VEC);
+          const float sc = pooling == TT_POOL_MEAN ? 1.f / (float)max(1, offsets[b + 1] - offsets[b]) : 1.f;
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) accf[v] += x[v] * sc;
+        }
+      }
+    } else {
+      for (int base = 0; base < n; base += 64) {  // hot row: fp64, 64 ids per chunk
+        const int cnt = min(64, n - base);
+        const int mine = lane < cnt ? ws.perm[s + base + lane] : 0;
+        for (int i = 0; i < cnt; ++i) {
+          const int b = __shfl(mine, i, 64);
+          if (c < ncol) {
+            vf x = *reinterpret_cast<const vf*>(br.row(b) + c * VEC);
+            const float sc = pooling == TT_POOL_MEAN ? 1.f / (float)max(1, offsets[b + 1] - offsets[b]) : 1.f;
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) acc[v] += (double)(x[v] * sc);
+          }
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) accf[v] = (float)acc[v];
+    }
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      gsave[k][v] = accf[v];
+      sq += accf[v] * accf[v];
+    }
+  }
+  sq = wave_sum(sq);
   const float snew = *srow + sq / (float)D;
   const float stdv = sqrtf(snew) + eps;
-  float* w = weights + tm.weight_offset + r * D;
 #pragma unroll
   for (int k = 0; k < ADA_KMAX; ++k) {
     const int c = lane + k * 64;
     if (c < ncol) {
       vf x = *reinterpret_cast<vf*>(w + c * VEC);
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) x[v] = x[v] + (-lr * g[k][v]) / stdv;
+      for (int v = 0; v < VEC; ++v) x[v] = x[v] + (-lr * gsave[k][v]) / stdv;
       *reinterpret_cast<vf*>(w + c * VEC) = x;
     }
   }
   if (lane == 0) *srow = snew;
 }
 
-// k2d: one wave per unique row (grid-stride over the device-side unique count)
-__global__ void __launch_bounds__(256) bwd_adagrad_kernel(EmbMeta m, const float* __restrict__ grad_out,
-                                                          int64_t ldg, const int32_t* __restrict__ offsets,
-                                                          int pooling, float* __restrict__ weights,
-                                                          float* __restrict__ state, float lr, float eps,
-                                                          BwdWs ws, int vec4_ok) {
+__global__ void __launch_bounds__(256) bwd_adagrad_kernel(EmbMeta m, const float* __restrict__ grad_out, int64_t ldg,
+                                                          const int32_t* __restrict__ offsets, int pooling,
+                                                          float* __restrict__ weights, float* __restrict__ state,
+                                                          float lr, float eps, BwdWs ws, int vec4_ok) {
   const int U = ws.U[0];
-  const int lane = threadIdx.x & 63;
+  const BagRow br{grad_out, m.B, ldg, m.features};
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += nwaves) {
-    const int h = ws.uslot[u];
-    const int s = ws.useg[u];
-    const int n = ws.ulen[u];
-    const uint64_t key = ws.keys[h];
-    const int t = (int)(key >> KEY_TABLE_SHIFT);
-    const int64_t r = (int64_t)(key & ((1ull << KEY_TABLE_SHIFT) - 1));
+    const URec rec = ws.urec[u];
+    const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
+    const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
     const int D = m.tables[t].dim;
     if (vec4_ok && (D & 3) == 0 && D >= 256)
-      adagrad_row<4>(m, grad_out, ldg, offsets, pooling, weights, state, lr, eps, ws, t, r, s, n);
+      adagrad_row<4>(m, br, offsets, pooling, weights, state, lr, eps, ws, t, r, rec.seg, rec.len);
     else if (vec4_ok && (D & 1) == 0)
-      adagrad_row<2>(m, grad_out, ldg, offsets, pooling, weights, state, lr, eps, ws, t, r, s, n);
+      adagrad_row<2>(m, br, offsets, pooling, weights, state, lr, eps, ws, t, r, rec.seg, rec.len);
     else
-      adagrad_row<1>(m, grad_out, ldg, offsets, pooling, weights, state, lr, eps, ws, t, r, s, n);
-    if (lane == 0) {
-      ws.keys[h] = EMPTY_KEY;  // leave the hash table clean for the next step
-      ws.cnt[h] = 0;
-    }
+      adagrad_row<1>(m, br, offsets, pooling, weights, state, lr, eps, ws, t, r, rec.seg, rec.len);
   }
 }
 
@@ -513,6 +608,43 @@ __global__ void __launch_bounds__(256) bwd_dense_kernel(EmbMeta m, const float* 
   }
 }
 
+// ---- host helpers ---------------------------------------------------------------------------
+
+static int fwd_geometry(FwdArgs& a, const float* weights, const float* out, int64_t ldo, int64_t B, int64_t* blocks) {
+  int64_t nb = 0;
+  for (int f = 0; f < a.m.F; ++f) {
+    const tt_table_meta_t& tm = a.m.tables[a.m.features[f].table];
+    if (a.m.features[f].out_offset + tm.dim > ldo) return fail(TT_EINVAL, "pooled_fwd: output row too short");
+    const bool v4 = (tm.dim % 4 == 0) && (tm.weight_offset % 4 == 0) && (a.m.features[f].out_offset % 4 == 0) &&
+                    (ldo % 4 == 0) && ((reinterpret_cast<uintptr_t>(weights) & 15) == 0) &&
+                    ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    a.vec[f] = v4 ? 4 : 1;
+    const int cols = tm.dim / a.vec[f];
+    int g = 1;
+    while (g < cols && g < 64) g <<= 1;
+    a.group[f] = (int8_t)g;
+    a.block_start[f] = (int32_t)nb;
+    nb += ceil_div(B, 256 / g);
+  }
+  a.block_start[a.m.F] = (int32_t)nb;
+  if (nb > INT32_MAX) return fail(TT_EINVAL, "pooled_fwd: grid too large");
+  *blocks = nb;
+  return TT_OK;
+}
+
+static int pack_cols(ColArgs& ca, int F, const void* const* cols, const int64_t* num_emb, int id_dtype) {
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "cols: ids must be int32/int64");
+  if (!cols || !num_emb) return fail(TT_EINVAL, "cols: null pointer");
+  for (int f = 0; f < F; ++f) {
+    if (!cols[f] || num_emb[f] < 1) return fail(TT_EINVAL, "cols: null column or num_embeddings < 1");
+    ca.col[f] = cols[f];
+    ca.num_emb[f] = num_emb[f];
+  }
+  return TT_OK;
+}
+
+static int check_ws(void* workspace, size_t ws_bytes, int64_t max_lookups, const char* what);
+
 }  // namespace tt
 
 using namespace tt;
@@ -531,26 +663,34 @@ int tt_pooled_fwd(const float* weights, const tt_table_meta_t* tables, int T,
   if (B == 0) return TT_OK;
   if (!weights || !offsets || !out) return fail(TT_EINVAL, "pooled_fwd: null pointer");
   if (bounds_check && !err_count) return fail(TT_EINVAL, "pooled_fwd: bounds_check needs err_count");
-  int64_t blocks = 0;
-  for (int f = 0; f < F; ++f) {
-    const tt_table_meta_t& tm = tables[features[f].table];
-    if (features[f].out_offset + tm.dim > ldo) return fail(TT_EINVAL, "pooled_fwd: output row too short");
-    const bool v4 = (tm.dim % 4 == 0) && (tm.weight_offset % 4 == 0) && (features[f].out_offset % 4 == 0) &&
-                    (ldo % 4 == 0) && ((reinterpret_cast<uintptr_t>(weights) & 15) == 0) &&
-                    ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-    a.vec[f] = v4 ? 4 : 1;
-    const int cols = tm.dim / a.vec[f];
-    int g = 1;
-    while (g < cols && g < 64) g <<= 1;
-    a.group[f] = g;
-    a.block_start[f] = (int32_t)blocks;
-    blocks += ceil_div(B, 256 / g);
-  }
-  a.block_start[F] = (int32_t)blocks;
-  if (blocks > INT32_MAX) return fail(TT_EINVAL, "pooled_fwd: grid too large");
+  int64_t blocks;
+  rc = fwd_geometry(a, weights, out, ldo, B, &blocks);
+  if (rc) return rc;
   pooled_fwd_kernel<<<dim3((unsigned)blocks), dim3(256), 0, as_stream(stream)>>>(
       weights, a, values, id_dtype, offsets, pooling, out, ldo, bounds_check, err_count);
   return check_launch("pooled_fwd");
+}
+
+int tt_pooled_fwd_cols(const float* weights, const tt_table_meta_t* tables, int T,
+                       const tt_feature_meta_t* features, int F, int64_t B, const void* const* cols,
+                       int id_dtype, const int64_t* num_embeddings, float* out, int64_t ldo, void* stream) {
+  FwdArgs a{};
+  int rc = pack_meta(a.m, tables, T, features, F, B);
+  if (rc) return rc;
+  ColArgs ca{};
+  rc = pack_cols(ca, F, cols, num_embeddings, id_dtype);
+  if (rc) return rc;
+  for (int f = 0; f < F; ++f)
+    if (num_embeddings[f] > tables[features[f].table].num_rows)
+      return fail(TT_EINVAL, "pooled_fwd_cols: num_embeddings exceeds the table's rows");
+  if (B == 0) return TT_OK;
+  if (!weights || !out) return fail(TT_EINVAL, "pooled_fwd_cols: null pointer");
+  int64_t blocks;
+  rc = fwd_geometry(a, weights, out, ldo, B, &blocks);
+  if (rc) return rc;
+  pooled_fwd_cols_kernel<<<dim3((unsigned)blocks), dim3(256), 0, as_stream(stream)>>>(weights, a, ca, id_dtype,
+                                                                                       out, ldo);
+  return check_launch("pooled_fwd_cols");
 }
 
 size_t tt_bwd_workspace_bytes(int64_t max_lookups) {
@@ -571,6 +711,14 @@ int tt_bwd_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookups,
   return TT_OK;
 }
 
+static int launch_scan_scatter(const EmbMeta& m, const int32_t* offsets, BwdWs& w, hipStream_t st, int gb) {
+  const int nb = (int)ceil_div(w.cap, 1024);
+  bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
+  bwd_scan_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
+  if ((int64_t)m.F * m.B > 0) bwd_scatter_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, offsets, w);
+  return check_launch("bwd_prepare");
+}
+
 int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
                    int64_t B, const void* values, int id_dtype, const int32_t* offsets,
                    int bounds_check, void* workspace, size_t ws_bytes, int64_t max_lookups,
@@ -580,9 +728,9 @@ int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t
   if (rc) return rc;
   if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "bwd_prepare: ids must be int32/int64");
   if (max_lookups < 1) max_lookups = 1;
-  if (max_lookups > INT32_MAX / 2) return fail(TT_EINVAL, "bwd_prepare: max_lookups too large");
-  if (!workspace || ws_bytes < tt_bwd_workspace_bytes(max_lookups))
-    return fail(TT_ECAPACITY, "bwd_prepare: workspace too small");
+  rc = check_ws(workspace, ws_bytes, max_lookups, "bwd_prepare");
+  if (rc) return rc;
+  if (!offsets) return fail(TT_EINVAL, "bwd_prepare: null offsets");
   for (int t = 0; t < T; ++t)
     if (tables[t].num_rows >= (1ll << KEY_TABLE_SHIFT)) return fail(TT_EINVAL, "bwd_prepare: table rows >= 2^40");
   BwdWs w;
@@ -591,11 +739,31 @@ int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t
   const int64_t nbag = (int64_t)F * B;
   const int gb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(nbag, 256)));
   if (nbag > 0) bwd_hash_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, values, id_dtype, offsets, bounds_check, w);
-  const int nb = (int)ceil_div(w.cap, 1024);
-  bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
-  bwd_scan_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
-  if (nbag > 0) bwd_scatter_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, offsets, w);
-  return check_launch("bwd_prepare");
+  return launch_scan_scatter(m, offsets, w, st, gb);
+}
+
+int tt_bwd_prepare_cols(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F, int64_t B,
+                        const void* const* cols, int id_dtype, const int64_t* num_embeddings, void* workspace,
+                        size_t ws_bytes, int64_t max_lookups, void* stream) {
+  EmbMeta m{};
+  int rc = pack_meta(m, tables, T, features, F, B);
+  if (rc) return rc;
+  ColArgs ca{};
+  rc = pack_cols(ca, F, cols, num_embeddings, id_dtype);
+  if (rc) return rc;
+  if (max_lookups < (int64_t)F * B) return fail(TT_ECAPACITY, "bwd_prepare_cols: max_lookups < F*B");
+  rc = check_ws(workspace, ws_bytes, max_lookups, "bwd_prepare_cols");
+  if (rc) return rc;
+  for (int f = 0; f < F; ++f)
+    if (num_embeddings[f] > tables[features[f].table].num_rows)
+      return fail(TT_EINVAL, "bwd_prepare_cols: num_embeddings exceeds the table's rows");
+  BwdWs w;
+  bwd_layout(workspace, max_lookups, &w);
+  hipStream_t st = as_stream(stream);
+  const int64_t nbag = (int64_t)F * B;
+  const int gb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(nbag, 256)));
+  if (nbag > 0) bwd_hash_cols_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, ca, id_dtype, w);
+  return launch_scan_scatter(m, nullptr, w, st, gb);
 }
 
 int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
@@ -607,20 +775,23 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
   int rc = pack_meta(m, tables, T, features, F, B);
   if (rc) return rc;
   if (max_lookups < 1) max_lookups = 1;
-  if (!workspace || ws_bytes < tt_bwd_workspace_bytes(max_lookups))
-    return fail(TT_ECAPACITY, "bwd_rowwise_adagrad: workspace too small");
+  rc = check_ws(workspace, ws_bytes, max_lookups, "bwd_rowwise_adagrad");
+  if (rc) return rc;
   if (pooling != TT_POOL_SUM && pooling != TT_POOL_MEAN) return fail(TT_EINVAL, "bwd_rowwise_adagrad: bad pooling");
-  if (!grad_out || !weights || !state || !offsets) return fail(TT_EINVAL, "bwd_rowwise_adagrad: null pointer");
+  if (!grad_out || !weights || !state) return fail(TT_EINVAL, "bwd_rowwise_adagrad: null pointer");
+  if (pooling == TT_POOL_MEAN && !offsets) return fail(TT_EINVAL, "bwd_rowwise_adagrad: MEAN pooling needs offsets");
   bool vec_ok = (ldg % 4 == 0) && ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0) &&
                 ((reinterpret_cast<uintptr_t>(weights) & 15) == 0);
   for (int t = 0; t < T; ++t)
     if (tables[t].weight_offset % 4) vec_ok = false;
   for (int f = 0; f < F; ++f)
     if (features[f].out_offset % 4) vec_ok = false;
-  // the kernel's per-row choice: float4 (D%4==0, D>=256, D<=1024), float2 (D even, D<=512),
-  // scalar (D<=256)
+  bool narrow = vec_ok;
   for (int t = 0; t < T; ++t) {
     const int D = tables[t].dim;
+    if (D > 128 || D % 4) narrow = false;
+    // generic path's per-row choice: float4 (D%4==0, D>=256, D<=1024), float2 (D even, D<=512),
+    // scalar (D<=256)
     const bool v4 = vec_ok && D % 4 == 0 && D >= 256;
     const bool v2 = vec_ok && D % 2 == 0 && !v4;
     const int cap = v4 ? 1024 : (v2 ? 512 : 256);
@@ -628,9 +799,16 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
   }
   BwdWs w;
   bwd_layout(workspace, max_lookups, &w);
-  const int grid = (int)std::min<int64_t>(16384, std::max<int64_t>(1, ceil_div(max_lookups, 4)));
-  bwd_adagrad_kernel<<<dim3(grid), dim3(256), 0, as_stream(stream)>>>(m, grad_out, ldg, offsets, pooling, weights,
-                                                                      state, lr, eps, w, vec_ok ? 1 : 0);
+  hipStream_t st = as_stream(stream);
+  if (narrow) {
+    const int grid = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(max_lookups, 8)));
+    bwd_adagrad_narrow_kernel<<<dim3(grid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
+                                                                lr, eps, w);
+  } else {
+    const int grid = (int)std::min<int64_t>(16384, std::max<int64_t>(1, ceil_div(max_lookups, 4)));
+    bwd_adagrad_kernel<<<dim3(grid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state, lr, eps,
+                                                         w, vec_ok ? 1 : 0);
+  }
   return check_launch("bwd_rowwise_adagrad");
 }
 
@@ -651,3 +829,12 @@ int tt_pooled_bwd_dense(const tt_table_meta_t* tables, int T, const tt_feature_m
 }
 
 }  // extern "C"
+
+namespace tt {
+static int check_ws(void* workspace, size_t ws_bytes, int64_t max_lookups, const char* what) {
+  if (max_lookups > INT32_MAX / 2) return fail(TT_EINVAL, std::string(what) + ": max_lookups too large");
+  if (!workspace || ws_bytes < tt_bwd_workspace_bytes(max_lookups))
+    return fail(TT_ECAPACITY, std::string(what) + ": workspace too small");
+  return TT_OK;
+}
+}  // namespace tt

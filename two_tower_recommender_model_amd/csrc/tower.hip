@@ -1,0 +1,795 @@
+// Fused two-tower MLP step on gfx950 bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate).
+//
+// Replaces ~9 per-layer launches of the towers (torchrec MLP = Linear + ReLU on every layer,
+// 03_model_training.py:411-412), the dot + BCE head (:452-453) and Adam (:826-829) with three:
+//
+//  T1 tower_fwd_bwd   one 256-thread workgroup per 32 rows: both towers' forward through all layers
+//                     (activations stay in LDS), logits + BCE + dlogit, the backward through all
+//                     layers down to dX, written straight into the pooled-embedding gradient
+//                     [B, sum D] that the fused row-wise Adagrad consumes. It also stores, for T2,
+//                     the layer inputs and the dZ of every layer TRANSPOSED ([feature][row], bf16),
+//                     and per-workgroup bias-gradient partials (fp32).
+//  T2 tower_wgrad     dW = dZ^T A over all rows: one wave per (32x32 tile, row slice), fragments
+//                     loaded straight from the transposed bf16 buffers (16 B per lane, no LDS),
+//                     partial tiles into fp32 slabs.
+//  T3 tower_update    per parameter: fixed-order sum of the slabs / bias partials, Adam
+//                     (torch.optim.Adam formula), and the bf16 weight copies T1 reads next step
+//                     (W [out][in] for the forward, W^T [in][out] for the backward).
+// Every reduction is in a fixed order: bitwise reproducible, independent of XCD placement.
+//
+// MFMA 16x16x32 operand maps (lane l, element j < 8): A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15];
+// result C[4(l>>4)+r][l&15], r < 4.
+#include <vector>
+
+#include "tt_common.h"
+
+namespace tt {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+constexpr int TR = 32;                // rows per workgroup
+constexpr int MAXW = 128;             // max layer width
+constexpr int XCH = 128;              // input columns per chunk
+constexpr int LSTR = MAXW + 8;        // bf16 LDS row stride (272 B: conflict-light ds_read_b128)
+constexpr int FSTR = MAXW + 4;        // fp32 LDS row stride
+constexpr int MAXL = 4;
+
+struct TowerArgs {
+  tt_tower_shape_t s;
+  int64_t B;
+  const float* pooled;  // [B, ldp]
+  int64_t ldp;
+  float* gpooled;       // [B, ldp] (tower-input columns written)
+  const float* params;  // flat fp32 (bias read from here)
+  const __bf16* wb;     // bf16 W  [out][in] per (t,l), flat like params' W blocks
+  const __bf16* wtb;    // bf16 W^T [in][out]
+  int64_t woff[2][MAXL];  // element offset of W_(t,l) in params
+  int64_t boff[2][MAXL];  // element offset of b_(t,l) in params
+  int64_t wcoff[2][MAXL]; // element offset of W_(t,l) in the bf16 copies
+  const void* labels;
+  int label_dtype;
+  float grad_scale;
+  float* logits;
+  float* loss;
+  // T1 -> T2 buffers
+  __bf16* xt;           // [2][in_max][B]
+  __bf16* act;          // [2][MAXL][MAXW][B]  (layer-l OUTPUT, transposed; layers 0..L-2 used)
+  __bf16* dzt;          // [2][MAXL][MAXW][B]
+  float* dbpart;        // [2][MAXL][nwg][MAXW]
+  float* loss_part;     // [nwg]
+  unsigned* counter;
+  int64_t in_max;
+  int nwg;
+};
+
+__device__ __forceinline__ float lbl(const void* p, int dt, int64_t i) {
+  if (dt == TT_I32) return (float)reinterpret_cast<const int32_t*>(p)[i];
+  if (dt == TT_I64) return (float)reinterpret_cast<const int64_t*>(p)[i];
+  return reinterpret_cast<const float*>(p)[i];
+}
+
+// acc[mt][j] += A(lds, rows 16*mt..) x B(global bf16, k-major rows) over K (multiple of 32)
+// B fragment: lane reads 8 consecutive k of "column" n from a [n][k]-layout matrix (ldb elems).
+__device__ __forceinline__ void mma_lds_global(f32x4 (&acc)[2][2], const __bf16* As, int lda_s,
+                                               const __bf16* Bg, int64_t ldb, int K, int n0a, int n0b,
+                                               bool has_b) {
+  // K <= 128 (4 k-steps): every B fragment (weights, L2-resident) is issued before the first
+  // MFMA so the GEMM pays one L2 round trip, not one per k-step.
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int nk = K >> 5;
+  bf16x8 b0[4], b1[4];
+  const __bf16* p0 = Bg + (int64_t)(n0a + r) * ldb + q * 8;
+  const __bf16* p1 = Bg + (int64_t)(n0b + r) * ldb + q * 8;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s < nk) {
+      b0[s] = *reinterpret_cast<const bf16x8*>(p0 + s * 32);
+      if (has_b) b1[s] = *reinterpret_cast<const bf16x8*>(p1 + s * 32);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s < nk) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(As + r * lda_s + s * 32 + q * 8);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(As + (16 + r) * lda_s + s * 32 + q * 8);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[s], acc[0][0], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0[s], acc[1][0], 0, 0, 0);
+      if (has_b) {
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1[s], acc[0][1], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[s], acc[1][1], 0, 0, 0);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
+  // LDS: X chunk, activations per (tower, layer) bf16, last-layer outputs fp32, dZ ping-pong
+  __shared__ __attribute__((aligned(16))) __bf16 xs[TR * LSTR];
+  __shared__ __attribute__((aligned(16))) __bf16 acts[2][MAXL][TR * LSTR];
+  __shared__ __attribute__((aligned(16))) float outf[2][TR * FSTR];
+  __shared__ __attribute__((aligned(16))) __bf16 dz[2][TR * LSTR];
+  __shared__ float dlog[TR];
+  __shared__ float lpart[TR];
+  __shared__ int last_flag;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int64_t B = a.B;
+  const int64_t m0 = (int64_t)blockIdx.x * TR;
+  const int L = a.s.L;
+
+  // ================= forward, both towers =================
+  for (int t = 0; t < 2; ++t) {
+    const int in = a.s.in_dim[t];
+    for (int l = 0; l < L; ++l) {
+      const int N = a.s.width[l];
+      const int K = l == 0 ? in : a.s.width[l - 1];
+      const int ntile = N / 16;
+      // this wave's n-tiles: wid and wid + 4
+      const bool h0 = wid < ntile, h1 = wid + 4 < ntile;
+      f32x4 acc[2][2];
+      for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
+      const __bf16* Wg = a.wb + a.wcoff[t][l];
+      if (l == 0) {
+        for (int k0 = 0; k0 < K; k0 += XCH) {
+          const int kc = min(XCH, K - k0);
+          // stage X[m0.., in_col + k0 ..] fp32 -> bf16 LDS, and X^T to global for T2
+          for (int e = threadIdx.x; e < TR * (kc / 4); e += 256) {
+            const int row = e / (kc / 4), c4 = (e % (kc / 4)) * 4;
+            const int64_t gm = m0 + row;
+            f32x4 v = (f32x4)(0.f);
+            if (gm < B) v = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + k0 + c4);
+            bf16x4 bv;
+            bv[0] = (__bf16)v[0]; bv[1] = (__bf16)v[1]; bv[2] = (__bf16)v[2]; bv[3] = (__bf16)v[3];
+            *reinterpret_cast<bf16x4*>(xs + row * LSTR + c4) = bv;
+          }
+          __syncthreads();
+          // X^T [t][k][B]: thread -> (k, 8 consecutive rows)
+          for (int e = threadIdx.x; e < kc * (TR / 8); e += 256) {
+            const int k = e / (TR / 8), rb = (e % (TR / 8)) * 8;
+            bf16x8 v;
+            for (int j = 0; j < 8; ++j) v[j] = xs[(rb + j) * LSTR + k];
+            const int64_t gm = m0 + rb;
+            __bf16* dst = a.xt + ((int64_t)t * a.in_max + k0 + k) * B + gm;
+            if (gm + 8 <= B) {
+              *reinterpret_cast<bf16x8*>(dst) = v;
+            } else {
+              for (int j = 0; j < 8; ++j)
+                if (gm + j < B) dst[j] = v[j];
+            }
+          }
+          if (h0) mma_lds_global(acc, xs, LSTR, Wg + k0, K, kc, wid * 16, (wid + 4) * 16, h1);
+          __syncthreads();
+        }
+      } else {
+        if (h0) mma_lds_global(acc, acts[t][l - 1], LSTR, Wg, K, K, wid * 16, (wid + 4) * 16, h1);
+      }
+      // epilogue: bias + relu -> LDS (bf16; fp32 too for the last layer), act^T -> global
+      const float* bias = a.params + a.boff[t][l];
+      for (int j = 0; j < 2; ++j) {
+        if (!(j == 0 ? h0 : h1)) continue;
+        const int col = (wid + 4 * j) * 16 + r16;
+        const float bv = bias[col];
+        for (int i = 0; i < 2; ++i) {
+          bf16x4 pk;
+          for (int rr = 0; rr < 4; ++rr) {
+            const int row = i * 16 + q4 * 4 + rr;
+            const float v = fmaxf(acc[i][j][rr] + bv, 0.f);
+            acts[t][l][row * LSTR + col] = (__bf16)v;
+            pk[rr] = (__bf16)v;
+            if (l == L - 1) outf[t][row * FSTR + col] = v;
+          }
+          if (l < L - 1) {
+            const int64_t gm = m0 + i * 16 + q4 * 4;
+            __bf16* dst = a.act + (((int64_t)t * MAXL + l) * MAXW + col) * B + gm;
+            if (gm + 4 <= B) {
+              *reinterpret_cast<bf16x4*>(dst) = pk;
+            } else {
+              for (int rr = 0; rr < 4; ++rr)
+                if (gm + rr < B) dst[rr] = pk[rr];
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ================= logits, BCE, dlogit =================
+  const int NL = a.s.width[L - 1];
+  {
+    // 8 threads per row
+    const int row = threadIdx.x >> 3, sub = threadIdx.x & 7;
+    float d = 0.f;
+    for (int c = sub; c < NL; c += 8) d += outf[0][row * FSTR + c] * outf[1][row * FSTR + c];
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    const int64_t gm = m0 + row;
+    float lo = 0.f, dl = 0.f;
+    if (gm < B) {
+      const float x = d, y = lbl(a.labels, a.label_dtype, gm);
+      const float lsig = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+      lo = (1.f - y) * x - lsig;
+      dl = (1.f / (1.f + expf(-x)) - y) / (float)B * a.grad_scale;
+      if (sub == 0) a.logits[gm] = x;
+    }
+    if (sub == 0) {
+      dlog[row] = dl;
+      lpart[row] = lo;
+    }
+  }
+  __syncthreads();
+
+  // ================= backward, tower by tower =================
+  for (int t = 0; t < 2; ++t) {
+    // dZ_{L-1} = dlogit * other * (self > 0): thread -> (8 consecutive rows, column), fp32
+    {
+      const float* self_ = outf[t];
+      const float* other = outf[1 - t];
+      float* dbp = a.dbpart + (((int64_t)t * MAXL + (L - 1)) * a.nwg + blockIdx.x) * MAXW;
+      for (int c = threadIdx.x >> 2; c < NL; c += 64) {
+        const int rb = (threadIdx.x & 3) * 8;
+        bf16x8 v;
+        float s = 0.f;
+        for (int j = 0; j < 8; ++j) {
+          const int row = rb + j;
+          float z = self_[row * FSTR + c] > 0.f ? dlog[row] * other[row * FSTR + c] : 0.f;
+          if (m0 + row >= B) z = 0.f;
+          s += z;
+          v[j] = (__bf16)z;
+          dz[0][row * LSTR + c] = (__bf16)z;
+        }
+        // bias-grad partial: 4 threads per column, fixed order
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        if ((threadIdx.x & 3) == 0) dbp[c] = s;
+        const int64_t gm = m0 + rb;
+        __bf16* dst = a.dzt + (((int64_t)t * MAXL + (L - 1)) * MAXW + c) * B + gm;
+        if (gm + 8 <= B) {
+          *reinterpret_cast<bf16x8*>(dst) = v;
+        } else {
+          for (int j = 0; j < 8; ++j)
+            if (gm + j < B) dst[j] = v[j];
+        }
+      }
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int l = L - 1; l >= 1; --l) {
+      // dA_{l-1} = dZ_l W_l : [TR, K=width[l]] x [width[l], width[l-1]], B from W^T [in][out]
+      const int Kd = a.s.width[l];
+      const int N = a.s.width[l - 1];
+      const int ntile = N / 16;
+      const bool h0 = wid < ntile, h1 = wid + 4 < ntile;
+      f32x4 acc[2][2];
+      for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
+      if (h0) mma_lds_global(acc, dz[cur], LSTR, a.wtb + a.wcoff[t][l], Kd, Kd, wid * 16, (wid + 4) * 16, h1);
+      // dZ_{l-1} = dA * (act_{l-1} > 0)
+      float* dbp = a.dbpart + (((int64_t)t * MAXL + (l - 1)) * a.nwg + blockIdx.x) * MAXW;
+      for (int j = 0; j < 2; ++j) {
+        if (!(j == 0 ? h0 : h1)) continue;
+        const int col = (wid + 4 * j) * 16 + r16;
+        float s = 0.f;
+        for (int i = 0; i < 2; ++i) {
+          bf16x4 pk;
+          for (int rr = 0; rr < 4; ++rr) {
+            const int row = i * 16 + q4 * 4 + rr;
+            float z = (float)acts[t][l - 1][row * LSTR + col] > 0.f ? acc[i][j][rr] : 0.f;
+            if (m0 + row >= B) z = 0.f;
+            s += z;
+            pk[rr] = (__bf16)z;
+            dz[cur ^ 1][row * LSTR + col] = (__bf16)z;
+          }
+          const int64_t gm = m0 + i * 16 + q4 * 4;
+          __bf16* dst = a.dzt + (((int64_t)t * MAXL + (l - 1)) * MAXW + col) * B + gm;
+          if (gm + 4 <= B) {
+            *reinterpret_cast<bf16x4*>(dst) = pk;
+          } else {
+            for (int rr = 0; rr < 4; ++rr)
+              if (gm + rr < B) dst[rr] = pk[rr];
+          }
+        }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (q4 == 0) dbp[col] = s;
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+    // dX = dZ_0 W_0 : [TR, width[0]] x [width[0], in] -> fp32 into the pooled gradient
+    {
+      const int in = a.s.in_dim[t];
+      const int Kd = a.s.width[0];
+      const __bf16* WT = a.wtb + a.wcoff[t][0];  // [in][width0]
+      for (int c0 = 0; c0 < in; c0 += XCH) {
+        const int nc = min(XCH, in - c0);
+        const int ntile = nc / 16;
+        const bool h0 = wid < ntile, h1 = wid + 4 < ntile;
+        f32x4 acc[2][2];
+        for (int i = 0; i < 2; ++i)
+          for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
+        if (h0) mma_lds_global(acc, dz[cur], LSTR, WT, Kd, Kd, c0 + wid * 16, c0 + (wid + 4) * 16, h1);
+        for (int j = 0; j < 2; ++j) {
+          if (!(j == 0 ? h0 : h1)) continue;
+          const int col = c0 + (wid + 4 * j) * 16 + r16;
+          for (int i = 0; i < 2; ++i)
+            for (int rr = 0; rr < 4; ++rr) {
+              const int64_t gm = m0 + i * 16 + q4 * 4 + rr;
+              if (gm < B) a.gpooled[gm * a.ldp + a.s.in_col[t] + col] = acc[i][j][rr];
+            }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ================= loss: per-workgroup partial, last arriver sums in order =================
+  if (threadIdx.x == 0) {
+    float p = 0.f;
+    for (int i = 0; i < TR; ++i) p += lpart[i];
+    a.loss_part[blockIdx.x] = p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = prev == gridDim.x - 1;
+    if (last_flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (last_flag) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) s += a.loss_part[i];
+    // fixed-order tree over the 256 thread sums
+    __shared__ float red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.loss[0] = red[0] / (float)B;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// T2: dW_(t,l)[n][k] = sum_m dZ_(t,l)[m][n] * A_(t,l)[m][k], A = X (l=0) or act_(t,l-1)
+
+struct WgradTile {
+  int32_t t, l, n0, k0;
+};
+
+constexpr int MAX_WTILES = 2 * MAXL * (MAXW / 32) * (1024 / 32);
+
+struct WgradArgs {
+  const __bf16* xt;
+  const __bf16* act;
+  const __bf16* dzt;
+  float* slab;  // [S][P]
+  int64_t P;
+  int64_t B;
+  int64_t in_max;
+  int S;
+  int64_t mslice;  // rows per slice (multiple of 32)
+  int ntiles;
+  int64_t woff[2][MAXL];
+  int64_t boff[2][MAXL];
+  int32_t K[2][MAXL];  // layer input width
+  int32_t width[MAXL];
+  int L;
+  const float* dbpart;
+  int nwg;
+};
+
+__global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const WgradTile* __restrict__ tiles) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)a.ntiles * a.S;
+  if (wave >= nw) {
+    // bias gradient of one output n of (t, l): sum of the T1 workgroups' partials, lanes strided
+    // over workgroups, then a fixed butterfly -> slab[0]
+    int64_t b = wave - nw;
+    for (int t = 0; t < 2; ++t)
+      for (int l = 0; l < a.L; ++l) {
+        if (b >= 0 && b < a.width[l]) {
+          const float* dbp = a.dbpart + ((int64_t)t * MAXL + l) * a.nwg * MAXW + b;
+          float s = 0.f;
+          for (int w = lane; w < a.nwg; w += 64) s += dbp[(int64_t)w * MAXW];
+          s = wave_sum(s);
+          if (lane == 0) a.slab[a.boff[t][l] + b] = s;
+        }
+        b -= a.width[l];
+      }
+    return;
+  }
+  const int s = (int)(wave / a.ntiles);
+  const WgradTile tl = tiles[wave % a.ntiles];
+  const int64_t B = a.B;
+  const __bf16* Z = a.dzt + ((int64_t)tl.t * MAXL + tl.l) * MAXW * B;  // [n][B]
+  const __bf16* A = tl.l == 0 ? a.xt + (int64_t)tl.t * a.in_max * B
+                              : a.act + ((int64_t)tl.t * MAXL + tl.l - 1) * MAXW * B;  // [k][B]
+  const int64_t mb = (int64_t)s * a.mslice;
+  const int64_t me = mb + a.mslice < B ? mb + a.mslice : B;
+  f32x4 acc[2][2];
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
+  const __bf16* z0 = Z + (int64_t)(tl.n0 + r) * B;
+  const __bf16* z1 = Z + (int64_t)(tl.n0 + 16 + r) * B;
+  const __bf16* a0 = A + (int64_t)(tl.k0 + r) * B;
+  const __bf16* a1 = A + (int64_t)(tl.k0 + 16 + r) * B;
+  int64_t m = mb;
+  for (; m + 32 <= me; m += 32) {
+    const int64_t o = m + q * 8;
+    const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(z0 + o);
+    const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(z1 + o);
+    const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(a0 + o);
+    const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(a1 + o);
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb1, acc[1][1], 0, 0, 0);
+  }
+  if (m < me) {  // ragged tail (B % 32 != 0): zero-padded fragments
+    bf16x8 fa0, fa1, fb0, fb1;
+    for (int j = 0; j < 8; ++j) {
+      const int64_t mm = m + q * 8 + j;
+      const bool ok = mm < me;
+      fa0[j] = ok ? z0[mm] : (__bf16)0.f;
+      fa1[j] = ok ? z1[mm] : (__bf16)0.f;
+      fb0[j] = ok ? a0[mm] : (__bf16)0.f;
+      fb1[j] = ok ? a1[mm] : (__bf16)0.f;
+    }
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb1, acc[1][1], 0, 0, 0);
+  }
+  // C[n][k]: row = n (4q + rr), col = k (r)
+  const int K = a.K[tl.t][tl.l];
+  float* dst = a.slab + (int64_t)s * a.P + a.woff[tl.t][tl.l];
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int rr = 0; rr < 4; ++rr) {
+        const int n = tl.n0 + i * 16 + q * 4 + rr;
+        const int k = tl.k0 + j * 16 + r;
+        dst[(int64_t)n * K + k] = acc[i][j][rr];
+      }
+}
+
+// ---------------------------------------------------------------------------------------------
+// T3: reduce + Adam + bf16 weight copies
+
+struct UpdateArgs {
+  float* params;
+  float* exp_avg;
+  float* exp_avg_sq;
+  const float* slab;
+  const float* dbpart;
+  int64_t P;
+  int S;
+  int nwg;
+  int nseg;
+  // segments of the flat parameter vector: W or b of (t, l)
+  int64_t seg_off[2 * 2 * MAXL + 1];
+  int32_t seg_t[2 * 2 * MAXL], seg_l[2 * 2 * MAXL], seg_isw[2 * 2 * MAXL], seg_n[2 * 2 * MAXL], seg_k[2 * 2 * MAXL];
+  int64_t seg_wc[2 * 2 * MAXL];  // bf16 copy offset for W segments
+  __bf16* wb;
+  __bf16* wtb;
+  float lr, beta1, beta2, eps, wd;
+  int64_t* step_state;
+  int do_adam;
+  float* grads_out;  // nullable: the reduced gradient (tests / inspection)
+};
+
+__global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t t_step = 0;
+  float step_size = 0.f, bc2_sqrt = 1.f;
+  if (a.do_adam) {
+    t_step = a.step_state[0] + 1;
+    const double bc1 = 1.0 - pow((double)a.beta1, (double)t_step);
+    const double bc2 = 1.0 - pow((double)a.beta2, (double)t_step);
+    step_size = (float)((double)a.lr / bc1);
+    bc2_sqrt = (float)sqrt(bc2);
+  }
+  if (i < a.P) {
+    int sg = 0;
+    while (sg + 1 < a.nseg && i >= a.seg_off[sg + 1]) ++sg;
+    const int64_t e = i - a.seg_off[sg];
+    float p = a.params[i];
+    float g = 0.f;
+    if (a.do_adam || a.grads_out) {
+      if (a.seg_isw[sg]) {
+#pragma unroll 8
+        for (int s = 0; s < a.S; ++s) g += a.slab[(int64_t)s * a.P + i];
+      } else {
+        g = a.slab[i];  // bias gradient, reduced over the T1 workgroups by T2's bias waves
+      }
+      if (a.grads_out) a.grads_out[i] = g;
+    }
+    if (a.do_adam) {
+      if (a.wd != 0.f) g = g + a.wd * p;
+      float m = a.exp_avg[i];
+      m = m + (1.f - a.beta1) * (g - m);
+      const float v = a.exp_avg_sq[i] * a.beta2 + (1.f - a.beta2) * g * g;
+      const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+      p = p + (-step_size) * m / denom;
+      a.exp_avg[i] = m;
+      a.exp_avg_sq[i] = v;
+      a.params[i] = p;
+    }
+    if (a.seg_isw[sg]) {
+      const int K = a.seg_k[sg], N = a.seg_n[sg];
+      const int64_t n = e / K, k = e - n * K;
+      a.wb[a.seg_wc[sg] + e] = (__bf16)p;
+      a.wtb[a.seg_wc[sg] + k * N + n] = (__bf16)p;
+    }
+  }
+  if (a.do_adam) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned* counter = reinterpret_cast<unsigned*>(a.step_state + 1);
+      const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1) {
+        __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.step_state), (unsigned long long)t_step,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+
+struct TowerLayout {
+  int64_t P;         // dense params
+  int64_t PW;        // weight elements (bf16 copies)
+  int64_t woff[2][MAXL], boff[2][MAXL], wcoff[2][MAXL];
+  int32_t K[2][MAXL];
+  int64_t in_max;
+  int nwg;
+  int S;
+  int64_t mslice;
+  int ntiles;
+  // workspace carve (bytes)
+  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_tiles, total;
+};
+
+static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) {
+  if (!s) return fail(TT_EINVAL, "tower: null shape");
+  if (s->L < 1 || s->L > MAXL) return fail(TT_EINVAL, "tower: 1..4 layers supported");
+  if (B < 8 || B % 8) return fail(TT_EINVAL, "tower: B must be a positive multiple of 8");
+  for (int l = 0; l < s->L; ++l)
+    if (s->width[l] < 16 || s->width[l] > MAXW || s->width[l] % 32)
+      return fail(TT_EINVAL, "tower: layer widths must be multiples of 32 in [32, 128]");
+  for (int t = 0; t < 2; ++t) {
+    if (s->in_dim[t] < 32 || s->in_dim[t] > 1024 || s->in_dim[t] % 32)
+      return fail(TT_EINVAL, "tower: input widths must be multiples of 32 in [32, 1024]");
+    if (s->in_col[t] < 0 || s->in_col[t] % 4) return fail(TT_EINVAL, "tower: input column must be >= 0, % 4 == 0");
+  }
+  TowerLayout L{};
+  int64_t o = 0, w = 0;
+  for (int t = 0; t < 2; ++t) {
+    int k = s->in_dim[t];
+    for (int l = 0; l < s->L; ++l) {
+      L.woff[t][l] = o;
+      L.wcoff[t][l] = w;
+      L.K[t][l] = k;
+      o += (int64_t)s->width[l] * k;
+      w += (int64_t)s->width[l] * k;
+      L.boff[t][l] = o;
+      o += s->width[l];
+      k = s->width[l];
+    }
+  }
+  L.P = o;
+  L.PW = w;
+  L.in_max = std::max(s->in_dim[0], s->in_dim[1]);
+  L.nwg = (int)ceil_div(B, TR);
+  int nt = 0;
+  for (int t = 0; t < 2; ++t)
+    for (int l = 0; l < s->L; ++l) nt += (s->width[l] / 32) * (L.K[t][l] / 32);
+  L.ntiles = nt;
+  // slices: aim for ~1024 waves, >= 256 rows per slice
+  int64_t S = std::max<int64_t>(1, 1024 / std::max(1, nt));
+  S = std::min<int64_t>(S, std::max<int64_t>(1, ceil_div(B, 256)));
+  S = std::min<int64_t>(S, 64);
+  L.S = (int)S;
+  L.mslice = ceil_div(ceil_div(B, S), 32) * 32;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t r = off;
+    off += align_up(bytes, 256);
+    return r;
+  };
+  L.o_xt = take(2 * (size_t)L.in_max * B * 2);
+  L.o_act = take(2 * (size_t)MAXL * MAXW * B * 2);
+  L.o_dzt = take(2 * (size_t)MAXL * MAXW * B * 2);
+  L.o_dbpart = take(2 * (size_t)MAXL * L.nwg * MAXW * 4);
+  L.o_slab = take((size_t)L.S * L.P * 4);
+  L.o_losspart = take((size_t)L.nwg * 4);
+  L.o_counter = take(64);
+  L.o_wb = take((size_t)L.PW * 2);
+  L.o_wtb = take((size_t)L.PW * 2);
+  L.o_tiles = take((size_t)nt * sizeof(WgradTile));
+  L.total = off;
+  *lay = L;
+  return TT_OK;
+}
+
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" {
+
+int64_t tt_tower_num_params(const tt_tower_shape_t* shape) {
+  TowerLayout L;
+  if (tower_layout(shape, 8, &L)) return -1;
+  return L.P;
+}
+
+size_t tt_tower_workspace_bytes(const tt_tower_shape_t* shape, int64_t B) {
+  TowerLayout L;
+  if (tower_layout(shape, B, &L)) return 0;
+  return L.total;
+}
+
+int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* workspace, size_t ws_bytes,
+                            void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  hipStream_t st = as_stream(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  if (hipMemsetAsync(ws, 0, L.total, st) != hipSuccess) return fail(TT_EINVAL, "tower: memset failed");
+  // the tile list of T2 (host-built, copied once)
+  std::vector<WgradTile> tiles;
+  for (int t = 0; t < 2; ++t)
+    for (int l = 0; l < shape->L; ++l)
+      for (int n0 = 0; n0 < shape->width[l]; n0 += 32)
+        for (int k0 = 0; k0 < L.K[t][l]; k0 += 32) tiles.push_back({t, l, n0, k0});
+  if (hipMemcpyAsync(ws + L.o_tiles, tiles.data(), tiles.size() * sizeof(WgradTile), hipMemcpyHostToDevice, st) !=
+      hipSuccess)
+    return fail(TT_EINVAL, "tower: tile upload failed");
+  return hipStreamSynchronize(st) == hipSuccess ? TT_OK : fail(TT_EINVAL, "tower: init sync failed");
+}
+
+int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp, float* gpooled,
+                     const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
+                     float* loss, void* workspace, size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  if (!pooled || !gpooled || !params || !labels || !logits || !loss) return fail(TT_EINVAL, "tower: null pointer");
+  if (label_dtype != TT_I32 && label_dtype != TT_I64 && label_dtype != TT_F32)
+    return fail(TT_EINVAL, "tower: labels must be int32/int64/float32");
+  if (ldp % 4 || (reinterpret_cast<uintptr_t>(pooled) & 15)) return fail(TT_EINVAL, "tower: pooled must be 16-B aligned rows");
+  for (int t = 0; t < 2; ++t)
+    if (shape->in_col[t] + shape->in_dim[t] > ldp) return fail(TT_EINVAL, "tower: input columns exceed the pooled row");
+  char* ws = reinterpret_cast<char*>(workspace);
+  TowerArgs a{};
+  a.s = *shape;
+  a.B = B;
+  a.pooled = pooled;
+  a.ldp = ldp;
+  a.gpooled = gpooled;
+  a.params = params;
+  a.wb = reinterpret_cast<const __bf16*>(ws + L.o_wb);
+  a.wtb = reinterpret_cast<const __bf16*>(ws + L.o_wtb);
+  for (int t = 0; t < 2; ++t)
+    for (int l = 0; l < MAXL; ++l) {
+      a.woff[t][l] = L.woff[t][l];
+      a.boff[t][l] = L.boff[t][l];
+      a.wcoff[t][l] = L.wcoff[t][l];
+    }
+  a.labels = labels;
+  a.label_dtype = label_dtype;
+  a.grad_scale = grad_scale;
+  a.logits = logits;
+  a.loss = loss;
+  a.xt = reinterpret_cast<__bf16*>(ws + L.o_xt);
+  a.act = reinterpret_cast<__bf16*>(ws + L.o_act);
+  a.dzt = reinterpret_cast<__bf16*>(ws + L.o_dzt);
+  a.dbpart = reinterpret_cast<float*>(ws + L.o_dbpart);
+  a.loss_part = reinterpret_cast<float*>(ws + L.o_losspart);
+  a.counter = reinterpret_cast<unsigned*>(ws + L.o_counter);
+  a.in_max = L.in_max;
+  a.nwg = L.nwg;
+  tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
+  return check_launch("tower_fwd_bwd");
+}
+
+int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, void* workspace, size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  char* ws = reinterpret_cast<char*>(workspace);
+  WgradArgs a{};
+  a.xt = reinterpret_cast<const __bf16*>(ws + L.o_xt);
+  a.act = reinterpret_cast<const __bf16*>(ws + L.o_act);
+  a.dzt = reinterpret_cast<const __bf16*>(ws + L.o_dzt);
+  a.slab = reinterpret_cast<float*>(ws + L.o_slab);
+  a.P = L.P;
+  a.B = B;
+  a.in_max = L.in_max;
+  a.S = L.S;
+  a.mslice = L.mslice;
+  a.ntiles = L.ntiles;
+  for (int t = 0; t < 2; ++t)
+    for (int l = 0; l < MAXL; ++l) {
+      a.woff[t][l] = L.woff[t][l];
+      a.boff[t][l] = L.boff[t][l];
+      a.K[t][l] = L.K[t][l];
+    }
+  int nbias = 0;
+  for (int l = 0; l < shape->L; ++l) {
+    a.width[l] = shape->width[l];
+    nbias += 2 * shape->width[l];
+  }
+  a.L = shape->L;
+  a.dbpart = reinterpret_cast<const float*>(ws + L.o_dbpart);
+  a.nwg = L.nwg;
+  const int64_t waves = (int64_t)L.ntiles * L.S + nbias;
+  tower_wgrad_kernel<<<dim3((unsigned)ceil_div(waves, 4)), dim3(256), 0, as_stream(stream)>>>(
+      a, reinterpret_cast<const WgradTile*>(ws + L.o_tiles));
+  return check_launch("tower_wgrad");
+}
+
+int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                    float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
+                    int do_adam, float* grads_out, void* workspace, size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  if (!params || (do_adam && (!exp_avg || !exp_avg_sq || !step_state))) return fail(TT_EINVAL, "tower: null pointer");
+  char* ws = reinterpret_cast<char*>(workspace);
+  UpdateArgs a{};
+  a.params = params;
+  a.exp_avg = exp_avg;
+  a.exp_avg_sq = exp_avg_sq;
+  a.slab = reinterpret_cast<const float*>(ws + L.o_slab);
+  a.dbpart = reinterpret_cast<const float*>(ws + L.o_dbpart);
+  a.P = L.P;
+  a.S = L.S;
+  a.nwg = L.nwg;
+  int sg = 0;
+  for (int t = 0; t < 2; ++t)
+    for (int l = 0; l < shape->L; ++l) {
+      a.seg_off[sg] = L.woff[t][l];
+      a.seg_t[sg] = t; a.seg_l[sg] = l; a.seg_isw[sg] = 1;
+      a.seg_n[sg] = shape->width[l]; a.seg_k[sg] = L.K[t][l];
+      a.seg_wc[sg] = L.wcoff[t][l];
+      ++sg;
+      a.seg_off[sg] = L.boff[t][l];
+      a.seg_t[sg] = t; a.seg_l[sg] = l; a.seg_isw[sg] = 0;
+      a.seg_n[sg] = shape->width[l]; a.seg_k[sg] = 1;
+      a.seg_wc[sg] = 0;
+      ++sg;
+    }
+  a.nseg = sg;
+  a.seg_off[sg] = L.P;
+  a.wb = reinterpret_cast<__bf16*>(ws + L.o_wb);
+  a.wtb = reinterpret_cast<__bf16*>(ws + L.o_wtb);
+  a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.wd = weight_decay;
+  a.step_state = step_state;
+  a.do_adam = do_adam;
+  a.grads_out = grads_out;
+  tower_update_kernel<<<dim3((unsigned)ceil_div(L.P, 256)), dim3(256), 0, as_stream(stream)>>>(a);
+  return check_launch("tower_update");
+}
+
+}  // extern "C"

@@ -9,6 +9,8 @@
 
 #define TT_WAVE 64
 
+typedef __attribute__((ext_vector_type(4))) float f32x4v;
+
 namespace tt {
 
 // thread-local last error, set by the host-side launch functions

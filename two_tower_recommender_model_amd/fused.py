@@ -29,11 +29,16 @@ class FusedTwoTowerStep:
                  query_features: Sequence[int], candidate_features: Sequence[int], layer_sizes: Sequence[int],
                  batch_size: int, device: torch.device, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
-                 overlap_prepare: bool = True, precision: str = "bf16"):
+                 overlap_prepare: bool = True, precision: str = "bf16", fused_towers: bool = True,
+                 kjt_mode: str = "cols"):
         """One table per feature (feature f -> table f), features ordered as the KJT keys.
         precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode)."""
         self.device = torch.device(device)
         self.precision = precision
+        if kjt_mode not in ("cols", "kjt"):
+            raise _lib.TTError("kjt_mode must be 'cols' or 'kjt'")
+        self.kjt_mode = kjt_mode
+        self.offsets_used = None
         self.F = len(num_embeddings)
         self.B = int(batch_size)
         self.num_embeddings = [int(n) for n in num_embeddings]
@@ -116,6 +121,14 @@ class FusedTwoTowerStep:
         self.dot_bce = ops.DotBCE(dev, B)
         self.tables.ensure_bwd_workspace(F * B)
         self.side = torch.cuda.Stream(device=dev) if overlap_prepare else None
+        # bf16 towers on the three fused kernels when the shape allows (else per-layer GEMMs)
+        self.towers = None
+        if precision == "bf16" and fused_towers and ops.FusedTowers.supported(
+                [self.in_q, self.in_c], self.layer_sizes, [self.q_lo, self.c_lo], B):
+            self.towers = ops.FusedTowers([self.in_q, self.in_c], self.layer_sizes, [self.q_lo, self.c_lo], B, dev)
+            assert self.towers.num_params == self.params.numel()
+            self.side2 = torch.cuda.Stream(device=dev)
+            self.sync_weights()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         # warm every scratch workspace so graph capture allocates nothing new (the all-zero batch
         # drops every id, so the tables are untouched; the towers' parameters are restored)
@@ -123,6 +136,7 @@ class FusedTwoTowerStep:
         self.step()
         torch.cuda.synchronize(dev)
         self.params.copy_(p0)
+        self.sync_weights()
         self.reset_optimizer_state()
 
     # ------------------------------------------------------------------------------------------
@@ -174,14 +188,39 @@ class FusedTwoTowerStep:
         """One training step on the batch currently in ``cols`` / ``labels``."""
         B, F = self.B, self.F
         main = torch.cuda.current_stream(self.device)
-        ops.kjt_build_mod_dropzero(self.cols, self.num_embeddings, self.values, self.lengths, self.offsets, self.lpk)
+        if self.kjt_mode == "kjt":
+            # materialise the KJT (values / lengths / offsets), then the KJT-form kernels
+            ops.kjt_build_mod_dropzero(self.cols, self.num_embeddings, self.values, self.lengths, self.offsets,
+                                       self.lpk)
+            prepare = lambda: self.tables.bwd_prepare(self.values, self.offsets, B, max_lookups=F * B)  # noqa: E731
+            self.offsets_used = self.offsets
+        else:
+            # single-hot columns: the transform (drop id 0, id mod N) is applied inside the kernels
+            prepare = lambda: self.tables.bwd_prepare_cols(self.cols, self.num_embeddings)  # noqa: E731
+            self.offsets_used = None
         if self.side is not None:
             self.side.wait_stream(main)
             with torch.cuda.stream(self.side):
-                self.tables.bwd_prepare(self.values, self.offsets, B, max_lookups=F * B)
+                prepare()
         else:
-            self.tables.bwd_prepare(self.values, self.offsets, B, max_lookups=F * B)
-        self.tables.pooled_fwd(self.values, self.offsets, B, out=self.pooled)
+            prepare()
+        if self.kjt_mode == "kjt":
+            self.tables.pooled_fwd(self.values, self.offsets, B, out=self.pooled)
+        else:
+            self.tables.pooled_fwd_cols(self.cols, self.num_embeddings, out=self.pooled)
+        if self.towers is not None:
+            # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update
+            self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits, self.loss)
+            self.side2.wait_stream(main)
+            with torch.cuda.stream(self.side2):
+                self.towers.wgrad()
+                self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
+                                   grads_out=self.grads)
+            if self.side is not None:
+                main.wait_stream(self.side)
+            self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, B, self.lr_emb, self.eps)
+            main.wait_stream(self.side2)
+            return
         self._towers_fwd()
         L = len(self.layer_sizes)
         self.dot_bce(self.qy[L - 1], self.cy[L - 1], self.labels, logits=self.logits, loss=self.loss,
@@ -189,12 +228,19 @@ class FusedTwoTowerStep:
         self._towers_bwd()
         if self.side is not None:
             main.wait_stream(self.side)
-        self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets, B, self.lr_emb, self.eps)
+        self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, B, self.lr_emb, self.eps)
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, self.lr_dense)
+
+    def sync_weights(self) -> None:
+        """Refresh the fused towers' bf16 weight copies after the fp32 parameters were changed
+        outside step() (initialisation, loading a checkpoint)."""
+        if self.towers is not None:
+            self.towers.update(self.params, do_adam=False)
 
     # ------------------------------------------------------------------------------------------
     def capture(self) -> None:
         """Record ``step()`` into a HIP graph (replayed by ``replay()``)."""
+        self.sync_weights()
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.device)
@@ -206,5 +252,22 @@ class FusedTwoTowerStep:
         torch.cuda.synchronize(self.device)
         self.graph = g
 
-    def replay(self) -> None:
-        self.graph.replay()
+    def replay(self, i: Optional[int] = None) -> None:
+        if i is None:
+            self.graph.replay()
+        else:
+            self.pool_graphs[i % len(self.pool_graphs)].replay()
+
+    def capture_pool(self, batches: Sequence) -> None:
+        """One graph per resident input batch ((cols, labels) device tensors): the graph's KJT
+        build reads that batch in place, so a replay needs no input copy."""
+        keep_cols, keep_labels = self.cols, self.labels
+        self.pool_graphs = []
+        for cols, labels in batches:
+            for c in cols:
+                if c.dtype != self.id_dtype or not c.is_contiguous() or c.numel() != self.B:
+                    raise _lib.TTError("capture_pool: batch columns must match the step's id dtype and batch")
+            self.cols, self.labels = list(cols), labels.to(torch.int32).contiguous()
+            self.capture()
+            self.pool_graphs.append(self.graph)
+        self.cols, self.labels = keep_cols, keep_labels

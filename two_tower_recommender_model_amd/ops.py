@@ -252,7 +252,28 @@ class TableSet:
                                      1 if bounds_check else 0, ptr(self._bwd_ws), self._bwd_ws.numel(),
                                      self._bwd_cap, stream_handle(self.device)), "bwd_prepare")
 
-    def bwd_rowwise_adagrad(self, grad_out: torch.Tensor, offsets: torch.Tensor, B: int, lr: float,
+    # -- single-hot column form (the loader's [B] id columns; transform applied inline)
+    def pooled_fwd_cols(self, cols: Sequence[torch.Tensor], num_embeddings: Sequence[int],
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        _dev(*cols)
+        B = cols[0].numel()
+        if out is None:
+            out = torch.empty(max(self.out_rows) + B, self.out_dim, dtype=torch.float32, device=self.device)
+        ne = (C.c_int64 * self.F)(*[int(n) for n in num_embeddings])
+        check(_lib_().tt_pooled_fwd_cols(ptr(self.weights), self._tm, self.T, self._fm, self.F, B, ptr_array(list(cols)),
+                                         id_dtype_code(cols[0].dtype), ne, ptr(out), out.stride(0),
+                                         stream_handle(self.device)), "pooled_fwd_cols")
+        return out
+
+    def bwd_prepare_cols(self, cols: Sequence[torch.Tensor], num_embeddings: Sequence[int]) -> None:
+        B = cols[0].numel()
+        self.ensure_bwd_workspace(self.F * B)
+        ne = (C.c_int64 * self.F)(*[int(n) for n in num_embeddings])
+        check(_lib_().tt_bwd_prepare_cols(self._tm, self.T, self._fm, self.F, B, ptr_array(list(cols)),
+                                          id_dtype_code(cols[0].dtype), ne, ptr(self._bwd_ws), self._bwd_ws.numel(),
+                                          self._bwd_cap, stream_handle(self.device)), "bwd_prepare_cols")
+
+    def bwd_rowwise_adagrad(self, grad_out: torch.Tensor, offsets: Optional[torch.Tensor], B: int, lr: float,
                             eps: float, pooling: int = TT_POOL_SUM) -> None:
         _dev(grad_out)
         if grad_out.dtype != torch.float32 or grad_out.stride(1) != 1:
@@ -414,3 +435,59 @@ class HipLookupBackend:
 
 
 HIP_BACKEND = HipLookupBackend()
+
+
+# ---- a6 + a7 + a9 fused: the towers' step in three launches -----------------------------------
+
+
+class FusedTowers:
+    """Both towers (L layers of Linear + ReLU), dot + BCE and Adam as three kernels (T1 fwd/bwd,
+    T2 weight gradients, T3 reduce + Adam + bf16 weight copies). Parameter layout: see
+    tt_tower_shape_t in include/tt_mi355x.h. bf16 operands, fp32 accumulation."""
+
+    @staticmethod
+    def supported(in_dims: Sequence[int], widths: Sequence[int], in_cols: Sequence[int], B: int) -> bool:
+        return (1 <= len(widths) <= 4 and all(w % 32 == 0 and 32 <= w <= 128 for w in widths)
+                and all(d % 32 == 0 and 32 <= d <= 1024 for d in in_dims) and all(c % 4 == 0 for c in in_cols)
+                and B % 8 == 0 and B >= 8)
+
+    def __init__(self, in_dims: Sequence[int], widths: Sequence[int], in_cols: Sequence[int], B: int,
+                 device: torch.device):
+        self.device = torch.device(device)
+        self.B = int(B)
+        sh = _lib.TowerShape()
+        sh.L = len(widths)
+        for i, w in enumerate(widths):
+            sh.width[i] = int(w)
+        for t in range(2):
+            sh.in_dim[t] = int(in_dims[t])
+            sh.in_col[t] = int(in_cols[t])
+        self.shape = sh
+        lib = _lib_()
+        self.num_params = lib.tt_tower_num_params(C.byref(sh))
+        if self.num_params < 0:
+            check(1001, "tower shape")
+        self.nbytes = lib.tt_tower_workspace_bytes(C.byref(sh), self.B)
+        if self.nbytes == 0:
+            check(1001, "tower shape")
+        self.ws = torch.empty(self.nbytes, dtype=torch.uint8, device=self.device)
+        check(lib.tt_tower_workspace_init(C.byref(sh), self.B, ptr(self.ws), self.nbytes,
+                                          stream_handle(self.device)), "tower_workspace_init")
+
+    def fwd_bwd(self, pooled, gpooled, params, labels, logits, loss, grad_scale: float = 1.0) -> None:
+        ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}[labels.dtype]
+        check(_lib_().tt_tower_fwd_bwd(C.byref(self.shape), self.B, ptr(pooled), pooled.stride(0), ptr(gpooled),
+                                       ptr(params), ptr(labels), ldt, float(grad_scale), ptr(logits), ptr(loss),
+                                       ptr(self.ws), self.nbytes, stream_handle(self.device)), "tower_fwd_bwd")
+
+    def wgrad(self) -> None:
+        check(_lib_().tt_tower_wgrad(C.byref(self.shape), self.B, ptr(self.ws), self.nbytes,
+                                     stream_handle(self.device)), "tower_wgrad")
+
+    def update(self, params, exp_avg=None, exp_avg_sq=None, step_state=None, lr: float = 0.01, beta1: float = 0.9,
+               beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0, do_adam: bool = True,
+               grads_out=None) -> None:
+        check(_lib_().tt_tower_update(C.byref(self.shape), self.B, ptr(params), ptr(exp_avg), ptr(exp_avg_sq),
+                                      float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+                                      ptr(step_state), 1 if do_adam else 0, ptr(grads_out), ptr(self.ws),
+                                      self.nbytes, stream_handle(self.device)), "tower_update")
