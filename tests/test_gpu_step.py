@@ -69,10 +69,10 @@ def test_fused_step_matches_reference_golden(device, case, precision):
     else:
         # bf16 operands can flip a ReLU mask where a pre-activation is within bf16 error of 0;
         # each flip moves that unit's whole gradient. Require 99% of elements within tolerance
-        # and every element within 3x it.
+        # and every element within 5x it.
         def check(got, want, atol):
             err = np.abs(got - want)
-            assert np.mean(err <= atol) >= 0.99 and err.max() <= 3 * atol, (np.mean(err <= atol), err.max())
+            assert np.mean(err <= atol) >= 0.99 and err.max() <= 5 * atol, (np.mean(err <= atol), err.max())
     check(st.tables.table_view(0).cpu().numpy(), g["final_t_user_id"], tol["table"])
     check(st.tables.table_view(1).cpu().numpy(), g["final_t_product_id"], tol["table"])
     np.testing.assert_allclose(st.tables.state_view(0).cpu().numpy(), g["final_state_t_user_id"],

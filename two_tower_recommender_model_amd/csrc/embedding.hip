@@ -212,16 +212,13 @@ static size_t bwd_layout(void* base, int64_t L, BwdWs* w) {
 }
 
 __device__ __forceinline__ int32_t hash_insert(BwdWs& ws, uint64_t key) {
+  // one returning CAS per probe: it claims an empty slot or reports who holds it
   const uint64_t mask = (uint64_t)ws.cap - 1;
   uint64_t h = mix64(key) & mask;
   while (true) {
-    const uint64_t c = __hip_atomic_load(&ws.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c == key) break;
-    if (c == EMPTY_KEY) {
-      const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.keys[h]),
-                                      (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-      if (prev == EMPTY_KEY || prev == key) break;
-    }
+    const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.keys[h]),
+                                    (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+    if (prev == EMPTY_KEY || prev == key) break;
     h = (h + 1) & mask;
   }
   atomicAdd(&ws.cnt[h], 1);
@@ -762,7 +759,9 @@ int tt_bwd_prepare_cols(const tt_table_meta_t* tables, int T, const tt_feature_m
   hipStream_t st = as_stream(stream);
   const int64_t nbag = (int64_t)F * B;
   const int gb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(nbag, 256)));
-  if (nbag > 0) bwd_hash_cols_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, ca, id_dtype, w);
+  // one wave per workgroup: the inserts are latency-bound round trips, spread them over all CUs
+  const int gh = (int)std::min<int64_t>(32768, std::max<int64_t>(1, ceil_div(nbag, 64)));
+  if (nbag > 0) bwd_hash_cols_kernel<<<dim3(gh), dim3(64), 0, st>>>(m, ca, id_dtype, w);
   return launch_scan_scatter(m, nullptr, w, st, gb);
 }
 

@@ -361,6 +361,277 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// T1 fast path: two layers per tower, every width <= 128. 512 threads: waves 0-3 run the query
+// tower, waves 4-7 the candidate tower, in lockstep. Every weight fragment a wave needs for the
+// whole step (fwd L0, fwd L1, bwd L1, bwd L0: up to 32 x 16 B per lane) is issued at kernel
+// entry together with the X rows, so the only global round trip on the chain is X itself; the rest
+// is LDS + MFMA.
+
+struct Frags {
+  bf16x8 f[4][2];
+};
+
+__device__ __forceinline__ void load_frags(Frags& fr, const __bf16* Wg, int ld, int K, int N, int w4) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int nk = K >> 5, nt = N >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int tile = w4 + 4 * j;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (tile < nt && s < nk)
+        fr.f[s][j] = *reinterpret_cast<const bf16x8*>(Wg + (int64_t)(tile * 16 + r) * ld + s * 32 + q * 8);
+  }
+}
+
+__device__ __forceinline__ void mma_frags(f32x4 (&acc)[2][2], const __bf16* As, const Frags& fr, int K, int N,
+                                          int w4) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int nk = K >> 5, nt = N >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s < nk) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(As + r * LSTR + s * 32 + q * 8);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(As + (16 + r) * LSTR + s * 32 + q * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (w4 + 4 * j < nt) {
+          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, fr.f[s][j], acc[0][j], 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, fr.f[s][j], acc[1][j], 0, 0, 0);
+        }
+    }
+  }
+}
+
+__device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int64_t gm, int64_t B) {
+  if (gm + 4 <= B) {
+    *reinterpret_cast<bf16x4*>(dst) = pk;
+  } else {
+    for (int rr = 0; rr < 4; ++rr)
+      if (gm + rr < B) dst[rr] = pk[rr];
+  }
+}
+
+__global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][TR * LSTR];   // X, later dZ0
+  __shared__ __attribute__((aligned(16))) __bf16 hs[2][TR * LSTR];   // hidden activation (bf16)
+  __shared__ __attribute__((aligned(16))) __bf16 dzs[2][TR * LSTR];  // dZ1
+  __shared__ __attribute__((aligned(16))) float outf[2][TR * FSTR];  // tower outputs (fp32)
+  __shared__ float dlog[TR];
+  __shared__ float lpart[TR];
+  __shared__ float red[256];
+  __shared__ int last_flag;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int t = wid >> 2, w4 = wid & 3;
+  const int tt = threadIdx.x & 255;  // thread index inside the tower group
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int64_t B = a.B;
+  const int64_t m0 = (int64_t)blockIdx.x * TR;
+  const int in = a.s.in_dim[t];
+  const int W0 = a.s.width[0], W1 = a.s.width[1];
+
+  // ---- 0. everything this wave will read from global: weight fragments, biases, X rows
+  Frags f0, f1, g1, g0;
+  load_frags(f0, a.wb + a.wcoff[t][0], in, in, W0, w4);      // W0 [W0][in]
+  load_frags(f1, a.wb + a.wcoff[t][1], W0, W0, W1, w4);      // W1 [W1][W0]
+  load_frags(g1, a.wtb + a.wcoff[t][1], W1, W1, W0, w4);     // W1^T [W0][W1]
+  load_frags(g0, a.wtb + a.wcoff[t][0], W0, W0, in, w4);     // W0^T [in][W0]
+  float bias0[2], bias1[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = (w4 + 4 * j) * 16 + r16;
+    bias0[j] = c < W0 ? a.params[a.boff[t][0] + c] : 0.f;
+    bias1[j] = c < W1 ? a.params[a.boff[t][1] + c] : 0.f;
+  }
+  for (int e = tt; e < TR * (in / 4); e += 256) {
+    const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
+    const int64_t gm = m0 + row;
+    f32x4 v = (f32x4)(0.f);
+    if (gm < B) v = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + c4);
+    bf16x4 bv;
+    bv[0] = (__bf16)v[0]; bv[1] = (__bf16)v[1]; bv[2] = (__bf16)v[2]; bv[3] = (__bf16)v[3];
+    *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
+  }
+  __syncthreads();
+  // X^T for T2's dW0 (fire-and-forget stores)
+  for (int e = tt; e < in * (TR / 8); e += 256) {
+    const int k = e / (TR / 8), rb = (e % (TR / 8)) * 8;
+    bf16x8 v;
+    for (int j = 0; j < 8; ++j) v[j] = xs[t][(rb + j) * LSTR + k];
+    const int64_t gm = m0 + rb;
+    __bf16* dst = a.xt + ((int64_t)t * a.in_max + k) * B + gm;
+    if (gm + 8 <= B) {
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (gm + j < B) dst[j] = v[j];
+    }
+  }
+  f32x4 acc[2][2];
+  // ---- 1. layer 0: h = relu(X W0^T + b0)
+  mma_frags(acc, xs[t], f0, in, W0, w4);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (w4 + 4 * j >= W0 / 16) continue;
+    const int col = (w4 + 4 * j) * 16 + r16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bf16x4 pk;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = i * 16 + q4 * 4 + rr;
+        const float v = fmaxf(acc[i][j][rr] + bias0[j], 0.f);
+        pk[rr] = (__bf16)v;
+        hs[t][row * LSTR + col] = pk[rr];
+      }
+      const int64_t gm = m0 + i * 16 + q4 * 4;
+      store_t4(a.act + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
+    }
+  }
+  __syncthreads();
+  // ---- 2. layer 1: out = relu(h W1^T + b1) (fp32)
+  mma_frags(acc, hs[t], f1, W0, W1, w4);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (w4 + 4 * j >= W1 / 16) continue;
+    const int col = (w4 + 4 * j) * 16 + r16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = i * 16 + q4 * 4 + rr;
+        outf[t][row * FSTR + col] = fmaxf(acc[i][j][rr] + bias1[j], 0.f);
+      }
+  }
+  __syncthreads();
+  // ---- 3. logits, BCE, dlogit: 16 threads per row
+  {
+    const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+    float d = 0.f;
+    for (int c = sub; c < W1; c += 16) d += outf[0][row * FSTR + c] * outf[1][row * FSTR + c];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) d += __shfl_xor(d, o, 64);
+    const int64_t gm = m0 + row;
+    float lo = 0.f, dl = 0.f;
+    if (gm < B) {
+      const float x = d, y = lbl(a.labels, a.label_dtype, gm);
+      const float lsig = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+      lo = (1.f - y) * x - lsig;
+      dl = (1.f / (1.f + expf(-x)) - y) / (float)B * a.grad_scale;
+      if (sub == 0) a.logits[gm] = x;
+    }
+    if (sub == 0) {
+      dlog[row] = dl;
+      lpart[row] = lo;
+    }
+  }
+  __syncthreads();
+  // ---- 4. dZ1 = dlogit * other * (self > 0): thread -> (column, 8 consecutive rows)
+  for (int c = tt >> 2; c < W1; c += 64) {
+    const int rb = (tt & 3) * 8;
+    bf16x8 v;
+    float s = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const int row = rb + j;
+      float z = outf[t][row * FSTR + c] > 0.f ? dlog[row] * outf[1 - t][row * FSTR + c] : 0.f;
+      if (m0 + row >= B) z = 0.f;
+      s += z;
+      v[j] = (__bf16)z;
+      dzs[t][row * LSTR + c] = v[j];
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if ((tt & 3) == 0) a.dbpart[(((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW + c] = s;
+    const int64_t gm = m0 + rb;
+    __bf16* dst = a.dzt + (((int64_t)t * MAXL + 1) * MAXW + c) * B + gm;
+    if (gm + 8 <= B) {
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (gm + j < B) dst[j] = v[j];
+    }
+  }
+  __syncthreads();
+  // ---- 5. dZ0 = (dZ1 W1) * (h > 0)  -> xs (X is no longer needed)
+  mma_frags(acc, dzs[t], g1, W1, W0, w4);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (w4 + 4 * j >= W0 / 16) continue;
+    const int col = (w4 + 4 * j) * 16 + r16;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bf16x4 pk;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = i * 16 + q4 * 4 + rr;
+        float z = (float)hs[t][row * LSTR + col] > 0.f ? acc[i][j][rr] : 0.f;
+        if (m0 + row >= B) z = 0.f;
+        s += z;
+        pk[rr] = (__bf16)z;
+        xs[t][row * LSTR + col] = pk[rr];
+      }
+      const int64_t gm = m0 + i * 16 + q4 * 4;
+      store_t4(a.dzt + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (q4 == 0) a.dbpart[(((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW + col] = s;
+  }
+  __syncthreads();
+  // ---- 6. dX = dZ0 W0 -> pooled gradient (fp32)
+  mma_frags(acc, xs[t], g0, W0, in, w4);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (w4 + 4 * j >= in / 16) continue;
+    const int col = (w4 + 4 * j) * 16 + r16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int64_t gm = m0 + i * 16 + q4 * 4 + rr;
+        if (gm < B) a.gpooled[gm * a.ldp + a.s.in_col[t] + col] = acc[i][j][rr];
+      }
+  }
+  // ---- 7. loss: per-workgroup partial, last arriver sums in a fixed order
+  if (threadIdx.x == 0) {
+    float p = 0.f;
+    for (int i = 0; i < TR; ++i) p += lpart[i];
+    a.loss_part[blockIdx.x] = p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = prev == gridDim.x - 1;
+    if (last_flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (last_flag && threadIdx.x < 256) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) s += a.loss_part[i];
+    red[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (last_flag) {
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.loss[0] = red[0] / (float)B;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // T2: dW_(t,l)[n][k] = sum_m dZ_(t,l)[m][n] * A_(t,l)[m][k], A = X (l=0) or act_(t,l-1)
 
 struct WgradTile {
@@ -707,7 +978,10 @@ int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pool
   a.counter = reinterpret_cast<unsigned*>(ws + L.o_counter);
   a.in_max = L.in_max;
   a.nwg = L.nwg;
-  tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
+  if (shape->L == 2 && shape->in_dim[0] <= 128 && shape->in_dim[1] <= 128)
+    tower_l2_kernel<<<dim3(L.nwg), dim3(512), 0, as_stream(stream)>>>(a);
+  else
+    tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_fwd_bwd");
 }
 
