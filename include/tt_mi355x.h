@@ -250,15 +250,16 @@ size_t tt_tower_workspace_bytes(const tt_tower_shape_t* shape, int64_t B);
  * (re)loading parameters. */
 int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* workspace, size_t ws_bytes,
                             void* stream);
-/* T1: forward of both towers, logits, mean BCE (loss), its gradient back through every layer;
- * dX written into gpooled's tower-input columns (ld = ldp). Also leaves, in the workspace, what
- * T2 needs. */
+/* T1: forward of both towers, logits, BCE and its gradient back through every layer; dX written
+ * into gpooled's tower-input columns (ld = ldp; pooled and gpooled 16-B aligned). Leaves, in the
+ * workspace, what T2 needs (transposed operands, bias and loss partials). */
 int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp,
                      float* gpooled, const float* params, const void* labels, int label_dtype,
-                     float grad_scale, float* logits, float* loss, void* workspace, size_t ws_bytes,
-                     void* stream);
-/* T2: weight/bias gradients of every layer into the workspace (fixed-order partial slabs). */
-int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, void* workspace, size_t ws_bytes, void* stream);
+                     float grad_scale, float* logits, void* workspace, size_t ws_bytes, void* stream);
+/* T2: weight/bias gradients of every layer into the workspace (fixed-order partial slabs), and
+ * the mean BCE of the preceding T1 into loss[0] (nullable; fixed-order sum of T1's partials). */
+int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                   void* stream);
 /* T3: fixed-order reduction of T2's partials, Adam (when do_adam; step_state as tt_adam_step),
  * and the bf16 weight copies for the next T1. grads_out (nullable) receives the gradient. */
 int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,

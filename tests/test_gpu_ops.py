@@ -162,20 +162,58 @@ def test_pooled_fwd_and_fused_rowwise_adagrad(ops, device, case, pooling):
 
 
 def test_fused_adagrad_deterministic(ops, device):
+    """Hot rows (up to ~2000 lookups of one row) included: every row's gradient is summed in
+    ascending bag order, so repeated runs agree bit for bit (the scatter's order does not)."""
     rng = np.random.default_rng(7)
     B, rows = 2048, [64, 4096]
     lengths, values = _make_kjt(rng, 2, B, rows, 4, zipf=True)
     offsets = torch.from_numpy(ref.complete_cumsum(lengths)).to(device)
     V = torch.from_numpy(values).to(device)
-    gout = torch.randn(B, 256, device=device)
+    gout = torch.randn(B, 256, generator=torch.Generator().manual_seed(3)).to(device)
     results = []
-    for _ in range(2):
+    for _ in range(3):
         ts = ops.TableSet(rows, [128, 128], [0, 1], device)
         ts.init_uniform_(torch.Generator(device=device).manual_seed(1))
         ts.bwd_prepare(V, offsets, B, values.size)
         ts.bwd_rowwise_adagrad(gout, offsets, B, 0.1, 1e-10)
         results.append(ts.weights.clone())
+    assert torch.equal(results[0], results[1]) and torch.equal(results[0], results[2])
+
+
+@pytest.mark.parametrize("pooling", ["sum", "mean"])
+def test_fused_adagrad_hot_rows(ops, device, pooling):
+    """Rows looked up thousands of times per step (several LDS passes of the hot-row kernel) and a
+    single bag holding one id 5000 times (the repeated-bag-id pass), narrow (D=128) and generic
+    (D=256) tables, against the oracle; and bitwise equal to a second run."""
+    rng = np.random.default_rng(11)
+    B, rows, dims = 1024, [3, 40], [128, 256]
+    lengths = rng.integers(0, 20, 2 * B).astype(np.int32)
+    lengths[5] = 5000
+    vals = []
+    for i in range(2 * B):
+        n = rows[i // B]
+        vals.extend([1] * lengths[i] if i == 5 else rng.integers(0, n, lengths[i]).tolist())
+    values = np.asarray(vals, np.int64)
+    offsets = ref.complete_cumsum(lengths)
+    pool = 1 if pooling == "mean" else 0
+    gout = torch.randn(B, sum(dims), generator=torch.Generator().manual_seed(4))
+    results = []
+    for _ in range(2):
+        ts = ops.TableSet(rows, dims, [0, 1], device)
+        ts.init_uniform_(torch.Generator(device=device).manual_seed(2))
+        tables0 = [ts.table_view(t).cpu().clone() for t in range(2)]
+        V, O = torch.from_numpy(values).to(device), torch.from_numpy(offsets).to(device)
+        ts.bwd_prepare(V, O, B, values.size)
+        ts.bwd_rowwise_adagrad(gout.to(device), O, B, 0.05, 1e-10, pooling=pool)
+        results.append(ts.weights.clone())
     assert torch.equal(results[0], results[1])
+    grads = ref.pooled_bwd_dense(tables0, [0, 1], torch.from_numpy(values), torch.from_numpy(offsets), B, gout,
+                                 pooling)
+    states = [torch.zeros(r) for r in rows]
+    for t in range(2):
+        ref.rowwise_adagrad(tables0[t], states[t], grads[t], 0.05, 1e-10)
+        np.testing.assert_allclose(ts.table_view(t).cpu().numpy(), tables0[t].numpy(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(ts.state_view(t).cpu().numpy(), states[t].numpy(), rtol=1e-4, atol=1e-9)
 
 
 def test_pooled_bwd_dense(ops, device):

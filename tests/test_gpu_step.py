@@ -168,8 +168,13 @@ def test_dropin_torchrec_api_matches_reference_golden(device, case):
     assert torch.equal(before, model.module.two_tower.state_dict()["ebc.embedding_bags.t_user_id.weight"])
 
 
-@pytest.mark.parametrize("B,in_dims,widths", [(8192, [128, 128], [128, 64]), (200, [64, 96], [128, 64, 32]),
-                                              (1024, [1024, 256], [128, 128])])
+@pytest.mark.parametrize("B,in_dims,widths", [
+    (8192, [128, 128], [128, 64]),    # T1 two-layer path, compile-time shape (north star)
+    (200, [64, 64], [128, 64]),       # compile-time shape (config 2), ragged last workgroup
+    (136, [96, 32], [96, 32]),        # two-layer path, run-time shape
+    (200, [64, 96], [128, 64, 32]),   # general T1
+    (1024, [1024, 256], [128, 128]),  # general T1, chunked wide input
+])
 def test_fused_towers_kernels_vs_fp32_autograd(device, B, in_dims, widths):
     """T1 (fwd + BCE + bwd-data), T2 (weight grads) and T3 (reduce, grads_out) against torch fp32
     autograd on the same parameters. bf16 operands: logits within 2e-2 relative (of max|logit|),
@@ -197,8 +202,8 @@ def test_fused_towers_kernels_vs_fp32_autograd(device, B, in_dims, widths):
     logits = torch.empty(B, device=device)
     loss = torch.empty((), device=device)
     grads = torch.zeros_like(P)
-    tw.fwd_bwd(Pd, gpd, P, labels.to(device), logits, loss)
-    tw.wgrad()
+    tw.fwd_bwd(Pd, gpd, P, labels.to(device), logits)
+    tw.wgrad(loss)
     tw.update(P, do_adam=False, grads_out=grads)
     torch.cuda.synchronize()
     # fp32 autograd reference

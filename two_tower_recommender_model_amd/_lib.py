@@ -119,8 +119,8 @@ SIGNATURES = {
     "tt_tower_num_params": (C.c_int64, [_psh]),
     "tt_tower_workspace_bytes": (_sz, [_psh, _i64]),
     "tt_tower_workspace_init": (_int, [_psh, _i64, _vp, _sz, _vp]),
-    "tt_tower_fwd_bwd": (_int, [_psh, _i64, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _vp, _sz, _vp]),
-    "tt_tower_wgrad": (_int, [_psh, _i64, _vp, _sz, _vp]),
+    "tt_tower_fwd_bwd": (_int, [_psh, _i64, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp]),
+    "tt_tower_wgrad": (_int, [_psh, _i64, _vp, _vp, _sz, _vp]),
     "tt_tower_update": (
         _int,
         [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _int, _vp, _vp, _sz, _vp],

@@ -165,6 +165,12 @@ struct URec {
   int32_t len;
 };
 
+// Rows looked up more than HOT_MIN - 1 times in a step are "hot": the per-row kernels (which sort
+// a segment of <= 32 bag ids in registers) skip them and bwd_adagrad_hot_kernel sums them in
+// ascending bag order through LDS, so every row's gradient is summed in one canonical order.
+constexpr int HOT_MIN = 33;
+constexpr int HOT_CAP = 4096;  // bag ids sorted in LDS per pass of the hot kernel
+
 struct BwdWs {
   uint64_t* keys;   // [cap] hash keys (EMPTY when free; cleaned by k2b)
   int32_t* cnt;     // [cap] lookups per slot (cleaned by k2b)
@@ -174,7 +180,8 @@ struct BwdWs {
   URec* urec;       // [L]   per unique row
   int32_t* bsum_u;  // [nb]  scan partials (unique count)
   int32_t* bsum_c;  // [nb]  scan partials (lookup count)
-  int32_t* U;       // [1]   number of unique rows this step
+  int32_t* hot;     // [L/HOT_MIN] unique indices whose segment is longer than HOT_MIN - 1
+  int32_t* U;       // [4]   {unique rows, -, hot rows, -}
   int64_t cap;
   int64_t L;
 };
@@ -204,7 +211,8 @@ static size_t bwd_layout(void* base, int64_t L, BwdWs* w) {
   t.urec = reinterpret_cast<URec*>(take(sizeof(URec) * L));
   t.bsum_u = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
   t.bsum_c = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
-  t.U = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
+  t.hot = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (L / HOT_MIN + 1)));
+  t.U =reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
   t.cap = cap;
   t.L = L;
   if (w) *w = t;
@@ -282,6 +290,7 @@ __global__ void __launch_bounds__(256) bwd_scan_reduce_kernel(BwdWs ws) {
   if (threadIdx.x == 0) {
     ws.bsum_u[blockIdx.x] = lu[0] + lu[1] + lu[2] + lu[3];
     ws.bsum_c[blockIdx.x] = lc[0] + lc[1] + lc[2] + lc[3];
+    if (blockIdx.x == 0) ws.U[2] = 0;  // hot list, filled by k2b-2
   }
 }
 
@@ -346,6 +355,7 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
       rec.seg = ec;
       rec.len = c[j];
       ws.urec[eu] = rec;
+      if (c[j] >= HOT_MIN) ws.hot[atomicAdd(&ws.U[2], 1)] = eu;
       ws.cur[h] = ec;
       ws.keys[h] = EMPTY_KEY;
       ws.cnt[h] = 0;
@@ -413,9 +423,10 @@ __global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, cons
   const BagRow br{grad_out, m.B, ldg, m.features};
   const int64_t nhalf = (int64_t)gridDim.x * 8;
   for (int64_t u = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half; u - half < U; u += nhalf) {
-    const bool active = u < U;
     URec rec{0, 0, 0};
-    if (active) rec = ws.urec[u];
+    if (u < U) rec = ws.urec[u];
+    const bool active = u < U && rec.len < HOT_MIN;  // hot rows: bwd_adagrad_hot_kernel
+    if (!active) rec = URec{0, 0, 0};
     const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
     const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
     const tt_table_meta_t tm = m.tables[active ? t : 0];
@@ -428,45 +439,23 @@ __global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, cons
     const float s_old = active ? *srow : 0.f;
     const int n = rec.len;
     f32x4v g = (f32x4v)(0.f);
-    // both halves must agree on the path for the shuffles: take the long path if either is long
+    // ascending bag order (bitonic over the half-wave), fp32: bitwise reproducible
     const int nmax = max(n, __shfl_xor(n, 32, 64));
-    if (nmax <= 32) {
-      int mine = (active && hl < n) ? ws.perm[rec.seg + hl] : 0x7fffffff;
-      mine = bitonic_sort<32>(mine);
-      for (int i = 0; i < nmax; i += 2) {
-        const int b0 = __shfl(mine, (lane & 32) + i, 64);
-        const int b1 = __shfl(mine, (lane & 32) + min(i + 1, 31), 64);
-        const bool v0 = i < n, v1 = i + 1 < n;
-        f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
-        if (col_ok && v0) x0 = *reinterpret_cast<const f32x4v*>(br.row(b0) + hl * 4);
-        if (col_ok && v1) x1 = *reinterpret_cast<const f32x4v*>(br.row(b1) + hl * 4);
-        if (pooling == TT_POOL_MEAN) {
-          if (v0) x0 *= 1.f / (float)max(1, offsets[b0 + 1] - offsets[b0]);
-          if (v1) x1 *= 1.f / (float)max(1, offsets[b1 + 1] - offsets[b1]);
-        }
-        if (v0) g += x0;
-        if (v1) g += x1;
+    int mine = (active && hl < n) ? ws.perm[rec.seg + hl] : 0x7fffffff;
+    mine = bitonic_sort<32>(mine);
+    for (int i = 0; i < nmax; i += 2) {
+      const int b0 = __shfl(mine, (lane & 32) + i, 64);
+      const int b1 = __shfl(mine, (lane & 32) + min(i + 1, 31), 64);
+      const bool v0 = i < n, v1 = i + 1 < n;
+      f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
+      if (col_ok && v0) x0 = *reinterpret_cast<const f32x4v*>(br.row(b0) + hl * 4);
+      if (col_ok && v1) x1 = *reinterpret_cast<const f32x4v*>(br.row(b1) + hl * 4);
+      if (pooling == TT_POOL_MEAN) {
+        if (v0) x0 *= 1.f / (float)max(1, offsets[b0 + 1] - offsets[b0]);
+        if (v1) x1 *= 1.f / (float)max(1, offsets[b1 + 1] - offsets[b1]);
       }
-    } else {
-      // hot row(s): fp64 accumulation, 32 bag ids per chunk
-      double d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-      for (int base = 0; base < nmax; base += 32) {
-        const int cnt = min(32, max(0, n - base));
-        const int mine = (hl < cnt) ? ws.perm[rec.seg + base + hl] : 0;
-        const int cmax = min(32, max(cnt, __shfl_xor(cnt, 32, 64)));
-        for (int i = 0; i < cmax; ++i) {
-          const int b0 = __shfl(mine, (lane & 32) + i, 64);
-          if (col_ok && i < cnt) {
-            f32x4v x = *reinterpret_cast<const f32x4v*>(br.row(b0) + hl * 4);
-            if (pooling == TT_POOL_MEAN) x *= 1.f / (float)max(1, offsets[b0 + 1] - offsets[b0]);
-            d0 += x[0];
-            d1 += x[1];
-            d2 += x[2];
-            d3 += x[3];
-          }
-        }
-      }
-      g = f32x4v{(float)d0, (float)d1, (float)d2, (float)d3};
+      if (v0) g += x0;
+      if (v1) g += x1;
     }
     // row-wise Adagrad: s += mean(G^2); w += (-lr * G) / (sqrt(s) + eps)
     float sq = g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
@@ -501,43 +490,23 @@ __device__ __forceinline__ void adagrad_row(const EmbMeta& m, const BagRow& br, 
   float* srow = state + tm.state_offset + r;
   float sq = 0.f;
   float gsave[ADA_KMAX][VEC];
+  // n < HOT_MIN (hot rows go to bwd_adagrad_hot_kernel): ascending bag order, fp32
   int sorted = lane < n ? ws.perm[s + lane] : 0x7fffffff;
-  if (n <= 64) sorted = bitonic_sort<64>(sorted);
+  sorted = bitonic_sort<64>(sorted);
 #pragma unroll
   for (int k = 0; k < ADA_KMAX; ++k) {
     const int c = lane + k * 64;
-    double acc[VEC];
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) acc[v] = 0.0;
     float accf[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) accf[v] = 0.f;
-    if (n <= 64) {
-      for (int i = 0; i < n; ++i) {  // ascending bag order, fp32 (bitwise reproducible)
-        const int b = __shfl(sorted, i, 64);
-        if (c < ncol) {
-          vf x = *reinterpret_cast<const vf*>(br.row(b) + c * VEC);
-          const float sc = pooling == TT_POOL_MEAN ? 1.f / (float)max(1, offsets[b + 1] - offsets[b]) : 1.f;
+    for (int i = 0; i < n; ++i) {
+      const int b = __shfl(sorted, i, 64);
+      if (c < ncol) {
+        vf x = *reinterpret_cast<const vf*>(br.row(b) + c * VEC);
+        const float sc = pooling == TT_POOL_MEAN ? 1.f / (float)max(1, offsets[b + 1] - offsets[b]) : 1.f;
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) accf[v] += x[v] * sc;
-        }
+        for (int v = 0; v < VEC; ++v) accf[v] += x[v] * sc;
       }
-    } else {
-      for (int base = 0; base < n; base += 64) {  // hot row: fp64, 64 ids per chunk
-        const int cnt = min(64, n - base);
-        const int mine = lane < cnt ? ws.perm[s + base + lane] : 0;
-        for (int i = 0; i < cnt; ++i) {
-          const int b = __shfl(mine, i, 64);
-          if (c < ncol) {
-            vf x = *reinterpret_cast<const vf*>(br.row(b) + c * VEC);
-            const float sc = pooling == TT_POOL_MEAN ? 1.f / (float)max(1, offsets[b + 1] - offsets[b]) : 1.f;
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) acc[v] += (double)(x[v] * sc);
-          }
-        }
-      }
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) accf[v] = (float)acc[v];
     }
 #pragma unroll
     for (int v = 0; v < VEC; ++v) {
@@ -570,6 +539,7 @@ __global__ void __launch_bounds__(256) bwd_adagrad_kernel(EmbMeta m, const float
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += nwaves) {
     const URec rec = ws.urec[u];
+    if (rec.len >= HOT_MIN) continue;  // bwd_adagrad_hot_kernel
     const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
     const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
     const int D = m.tables[t].dim;
@@ -579,6 +549,154 @@ __global__ void __launch_bounds__(256) bwd_adagrad_kernel(EmbMeta m, const float
       adagrad_row<2>(m, br, offsets, pooling, weights, state, lr, eps, ws, t, r, rec.seg, rec.len);
     else
       adagrad_row<1>(m, br, offsets, pooling, weights, state, lr, eps, ws, t, r, rec.seg, rec.len);
+  }
+}
+
+// ---- k2d hot rows: a workgroup per row looked up >= HOT_MIN times --------------------------
+// The segment's bag ids are summed in ascending order whatever order the scatter left them in:
+// passes over bag-id ranges [lo, hi) holding <= HOT_CAP ids each (hi found by halving, so the
+// ranges depend on the id multiset only), each range sorted in LDS; inside a range, group g of
+// HOT_G sums sorted positions g, g + HOT_G, ..., and the group partials are added in group order.
+// Every step of that is a function of the multiset of bag ids: bitwise reproducible.
+constexpr int HOT_TPR = 64;                 // threads per gradient row (columns strided by 64)
+constexpr int HOT_G = 256 / HOT_TPR;        // row groups
+constexpr int HOT_KC = 1024 / HOT_TPR;      // columns per thread at D = 1024
+
+__device__ __forceinline__ int block_sum_i(int v, int* red) {
+  v = wave_sum_i(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(256) bwd_adagrad_hot_kernel(EmbMeta m, const float* __restrict__ grad_out,
+                                                              int64_t ldg, const int32_t* __restrict__ offsets,
+                                                              int pooling, float* __restrict__ weights,
+                                                              float* __restrict__ state, float lr, float eps,
+                                                              BwdWs ws) {
+  __shared__ int ids[HOT_CAP];
+  __shared__ float part[HOT_G][1024];
+  __shared__ int redi[4];
+  __shared__ float redf[4];
+  __shared__ int fill;
+  const int tid = threadIdx.x;
+  const int cg = tid % HOT_TPR, gi = tid / HOT_TPR;
+  const int nhot = ws.U[2];
+  const BagRow br{grad_out, m.B, ldg, m.features};
+  for (int h = blockIdx.x; h < nhot; h += gridDim.x) {
+    const URec rec = ws.urec[ws.hot[h]];
+    const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
+    const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
+    const tt_table_meta_t tm = m.tables[t];
+    const int D = tm.dim;
+    const int32_t* seg = ws.perm + rec.seg;
+    const int n = rec.len;
+    float tot[4] = {0.f, 0.f, 0.f, 0.f};  // column tid + 256 k (D <= 1024)
+    const int64_t NB = (int64_t)m.F * m.B;  // bag ids are < F * B
+    int64_t lo = 0, width = 1;
+    while (width < NB) width <<= 1;
+    while (lo < NB) {
+      int64_t hi;
+      int c;
+      while (true) {  // shrink [lo, hi) until it holds <= HOT_CAP ids (or a single bag id)
+        hi = lo + width < NB ? lo + width : NB;
+        int k = 0;
+        for (int i = tid; i < n; i += 256) {
+          const int b = seg[i];
+          k += (b >= lo && b < hi);
+        }
+        c = block_sum_i(k, redi);
+        if (c <= HOT_CAP || hi - lo == 1) break;
+        width >>= 1;
+      }
+      if (c == 0) {
+        lo = hi;
+        width <<= 1;
+        continue;
+      }
+      const bool single = c > HOT_CAP;  // one bag id repeated c times: every position holds lo
+      if (!single) {
+        if (tid == 0) fill = 0;
+        __syncthreads();
+        for (int i = tid; i < n; i += 256) {
+          const int b = seg[i];
+          if (b >= lo && b < hi) ids[atomicAdd(&fill, 1)] = b;
+        }
+        int P = 1;
+        while (P < c) P <<= 1;
+        for (int i = c + tid; i < P; i += 256) ids[i] = 0x7fffffff;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1)
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < P; i += 256) {
+              const int x = i ^ j;
+              if (x > i) {
+                const int a = ids[i], b = ids[x];
+                if ((a > b) == ((i & k) == 0)) {
+                  ids[i] = b;
+                  ids[x] = a;
+                }
+              }
+            }
+            __syncthreads();
+          }
+      }
+      float acc[HOT_KC];
+#pragma unroll
+      for (int k = 0; k < HOT_KC; ++k) acc[k] = 0.f;
+      for (int i = gi; i < c; i += HOT_G) {
+        const int b = single ? (int)lo : ids[i];
+        const float* g = br.row(b);
+        const float sc = pooling == TT_POOL_MEAN ? 1.f / (float)max(1, offsets[b + 1] - offsets[b]) : 1.f;
+#pragma unroll
+        for (int k = 0; k < HOT_KC; ++k) {
+          const int col = cg + k * HOT_TPR;
+          if (col < D) acc[k] += g[col] * sc;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < HOT_KC; ++k) {
+        const int col = cg + k * HOT_TPR;
+        if (col < D) part[gi][col] = acc[k];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int col = tid + 256 * k;
+        if (col < D) {
+          float s = 0.f;
+#pragma unroll
+          for (int g = 0; g < HOT_G; ++g) s += part[g][col];
+          tot[k] += s;
+        }
+      }
+      __syncthreads();
+      lo = hi;
+      width <<= 1;  // the next range starts wider (still a function of the id multiset only)
+    }
+    // row-wise Adagrad on the summed row
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tid + 256 * k < D) sq += tot[k] * tot[k];
+    sq = wave_sum(sq);
+    __syncthreads();
+    if ((tid & 63) == 0) redf[tid >> 6] = sq;
+    __syncthreads();
+    sq = (redf[0] + redf[1]) + (redf[2] + redf[3]);
+    float* srow = state + tm.state_offset + r;
+    const float snew = *srow + sq / (float)D;
+    const float stdv = sqrtf(snew) + eps;
+    float* wrow = weights + tm.weight_offset + r * D;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int col = tid + 256 * k;
+      if (col < D) wrow[col] = wrow[col] + (-lr * tot[k]) / stdv;
+    }
+    __syncthreads();
+    if (tid == 0) *srow = snew;
   }
 }
 
@@ -807,6 +925,11 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
     const int grid = (int)std::min<int64_t>(16384, std::max<int64_t>(1, ceil_div(max_lookups, 4)));
     bwd_adagrad_kernel<<<dim3(grid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state, lr, eps,
                                                          w, vec_ok ? 1 : 0);
+  }
+  if (max_lookups >= HOT_MIN) {
+    const int hgrid = (int)std::min<int64_t>(512, max_lookups / HOT_MIN);
+    bwd_adagrad_hot_kernel<<<dim3(hgrid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
+                                                              lr, eps, w);
   }
   return check_launch("bwd_rowwise_adagrad");
 }

@@ -52,14 +52,12 @@ struct TowerArgs {
   int label_dtype;
   float grad_scale;
   float* logits;
-  float* loss;
   // T1 -> T2 buffers
   __bf16* xt;           // [2][in_max][B]
   __bf16* act;          // [2][MAXL][MAXW][B]  (layer-l OUTPUT, transposed; layers 0..L-2 used)
   __bf16* dzt;          // [2][MAXL][MAXW][B]
   float* dbpart;        // [2][MAXL][nwg][MAXW]
   float* loss_part;     // [nwg]
-  unsigned* counter;
   int64_t in_max;
   int nwg;
 };
@@ -113,7 +111,6 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 dz[2][TR * LSTR];
   __shared__ float dlog[TR];
   __shared__ float lpart[TR];
-  __shared__ int last_flag;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, q4 = lane >> 4;
@@ -329,34 +326,12 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
     __syncthreads();
   }
 
-  // ================= loss: per-workgroup partial, last arriver sums in order =================
+  // loss: per-workgroup partial; T2 sums the partials in a fixed order (no cross-workgroup
+  // hand-off inside T1: a release fence here costs more than the rest of the epilogue)
   if (threadIdx.x == 0) {
     float p = 0.f;
     for (int i = 0; i < TR; ++i) p += lpart[i];
     a.loss_part[blockIdx.x] = p;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_flag = prev == gridDim.x - 1;
-    if (last_flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  if (last_flag) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) s += a.loss_part[i];
-    // fixed-order tree over the 256 thread sums
-    __shared__ float red[256];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) a.loss[0] = red[0] / (float)B;
   }
 }
 
@@ -418,15 +393,17 @@ __device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int64_t 
   }
 }
 
+// IN_/W0_/W1_: compile-time tower input width and layer widths (0 = read from the shape at run
+// time). With them fixed every fragment load is unconditional, so the waitcnt that guards X (issued
+// first) does not also wait for the weight fragments issued behind it.
+template <int IN_, int W0_, int W1_>
 __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][TR * LSTR];   // X, later dZ0
   __shared__ __attribute__((aligned(16))) __bf16 hs[2][TR * LSTR];   // hidden activation (bf16)
   __shared__ __attribute__((aligned(16))) __bf16 dzs[2][TR * LSTR];  // dZ1
-  __shared__ __attribute__((aligned(16))) float outf[2][TR * FSTR];  // tower outputs (fp32)
+  __shared__ __attribute__((aligned(16))) float outf[2][TR * FSTR];  // tower outputs, later dX (fp32)
   __shared__ float dlog[TR];
   __shared__ float lpart[TR];
-  __shared__ float red[256];
-  __shared__ int last_flag;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int t = wid >> 2, w4 = wid & 3;
@@ -434,10 +411,24 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
   const int r16 = lane & 15, q4 = lane >> 4;
   const int64_t B = a.B;
   const int64_t m0 = (int64_t)blockIdx.x * TR;
-  const int in = a.s.in_dim[t];
-  const int W0 = a.s.width[0], W1 = a.s.width[1];
+  const int in = IN_ ? IN_ : a.s.in_dim[t];
+  const int W0 = W0_ ? W0_ : a.s.width[0];
+  const int W1 = W1_ ? W1_ : a.s.width[1];
 
-  // ---- 0. everything this wave will read from global: weight fragments, biases, X rows
+  // ---- 0. everything this wave will read from global: X rows first (the chain waits on them),
+  // then every weight fragment of the step in order of use, then the biases
+  f32x4 xv[4];
+  const int nxv = in / 32;  // f32x4 loads per thread: TR rows x in/4 vectors over 256 threads
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    xv[i] = (f32x4)(0.f);
+    if (i < nxv) {
+      const int e = tt + 256 * i;
+      const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
+      const int64_t gm = m0 + row;
+      if (gm < B) xv[i] = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + c4);
+    }
+  }
   Frags f0, f1, g1, g0;
   load_frags(f0, a.wb + a.wcoff[t][0], in, in, W0, w4);      // W0 [W0][in]
   load_frags(f1, a.wb + a.wcoff[t][1], W0, W0, W1, w4);      // W1 [W1][W0]
@@ -450,14 +441,15 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
     bias0[j] = c < W0 ? a.params[a.boff[t][0] + c] : 0.f;
     bias1[j] = c < W1 ? a.params[a.boff[t][1] + c] : 0.f;
   }
-  for (int e = tt; e < TR * (in / 4); e += 256) {
-    const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
-    const int64_t gm = m0 + row;
-    f32x4 v = (f32x4)(0.f);
-    if (gm < B) v = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + c4);
-    bf16x4 bv;
-    bv[0] = (__bf16)v[0]; bv[1] = (__bf16)v[1]; bv[2] = (__bf16)v[2]; bv[3] = (__bf16)v[3];
-    *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < nxv) {
+      const int e = tt + 256 * i;
+      const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
+      bf16x4 bv;
+      bv[0] = (__bf16)xv[i][0]; bv[1] = (__bf16)xv[i][1]; bv[2] = (__bf16)xv[i][2]; bv[3] = (__bf16)xv[i][3];
+      *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
+    }
   }
   __syncthreads();
   // X^T for T2's dW0 (fire-and-forget stores)
@@ -586,7 +578,7 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
     if (q4 == 0) a.dbpart[(((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW + col] = s;
   }
   __syncthreads();
-  // ---- 6. dX = dZ0 W0 -> pooled gradient (fp32)
+  // ---- 6. dX = dZ0 W0 -> LDS (outf is free since phase 4) -> pooled gradient, whole rows
   mma_frags(acc, xs[t], g0, W0, in, w4);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -595,39 +587,25 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int64_t gm = m0 + i * 16 + q4 * 4 + rr;
-        if (gm < B) a.gpooled[gm * a.ldp + a.s.in_col[t] + col] = acc[i][j][rr];
-      }
+      for (int rr = 0; rr < 4; ++rr) outf[t][(i * 16 + q4 * 4 + rr) * FSTR + col] = acc[i][j][rr];
   }
-  // ---- 7. loss: per-workgroup partial, last arriver sums in a fixed order
+  // ---- 7. loss: per-workgroup partial (T2 sums the partials in a fixed order)
   if (threadIdx.x == 0) {
     float p = 0.f;
     for (int i = 0; i < TR; ++i) p += lpart[i];
     a.loss_part[blockIdx.x] = p;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_flag = prev == gridDim.x - 1;
-    if (last_flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
   __syncthreads();
-  if (last_flag && threadIdx.x < 256) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) s += a.loss_part[i];
-    red[threadIdx.x] = s;
-  }
-  __syncthreads();
-  if (last_flag) {
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < nxv) {
+      const int e = tt + 256 * i;
+      const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
+      const int64_t gm = m0 + row;
+      if (gm < B)
+        *reinterpret_cast<f32x4*>(a.gpooled + gm * a.ldp + a.s.in_col[t] + c4) =
+            *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
     }
-    if (threadIdx.x == 0) a.loss[0] = red[0] / (float)B;
   }
 }
 
@@ -658,6 +636,9 @@ struct WgradArgs {
   int L;
   const float* dbpart;
   int nwg;
+  const float* loss_part;  // [nwg] T1 partials
+  float* loss;             // nullable
+  int nbias;
 };
 
 __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const WgradTile* __restrict__ tiles) {
@@ -669,6 +650,15 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
     // bias gradient of one output n of (t, l): sum of the T1 workgroups' partials, lanes strided
     // over workgroups, then a fixed butterfly -> slab[0]
     int64_t b = wave - nw;
+    if (b == a.nbias) {  // the scalar loss: T1's per-workgroup partials in a fixed order
+      if (a.loss) {
+        float s = 0.f;
+        for (int w = lane; w < a.nwg; w += 64) s += a.loss_part[w];
+        s = wave_sum(s);
+        if (lane == 0) a.loss[0] = s / (float)a.B;
+      }
+      return;
+    }
     for (int t = 0; t < 2; ++t)
       for (int l = 0; l < a.L; ++l) {
         if (b >= 0 && b < a.width[l]) {
@@ -938,15 +928,16 @@ int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* work
 
 int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp, float* gpooled,
                      const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
-                     float* loss, void* workspace, size_t ws_bytes, void* stream) {
+                     void* workspace, size_t ws_bytes, void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if (!pooled || !gpooled || !params || !labels || !logits || !loss) return fail(TT_EINVAL, "tower: null pointer");
+  if (!pooled || !gpooled || !params || !labels || !logits) return fail(TT_EINVAL, "tower: null pointer");
   if (label_dtype != TT_I32 && label_dtype != TT_I64 && label_dtype != TT_F32)
     return fail(TT_EINVAL, "tower: labels must be int32/int64/float32");
-  if (ldp % 4 || (reinterpret_cast<uintptr_t>(pooled) & 15)) return fail(TT_EINVAL, "tower: pooled must be 16-B aligned rows");
+  if (ldp % 4 || (reinterpret_cast<uintptr_t>(pooled) & 15) || (reinterpret_cast<uintptr_t>(gpooled) & 15))
+    return fail(TT_EINVAL, "tower: pooled and its gradient must be 16-B aligned rows");
   for (int t = 0; t < 2; ++t)
     if (shape->in_col[t] + shape->in_dim[t] > ldp) return fail(TT_EINVAL, "tower: input columns exceed the pooled row");
   char* ws = reinterpret_cast<char*>(workspace);
@@ -969,23 +960,28 @@ int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pool
   a.label_dtype = label_dtype;
   a.grad_scale = grad_scale;
   a.logits = logits;
-  a.loss = loss;
   a.xt = reinterpret_cast<__bf16*>(ws + L.o_xt);
   a.act = reinterpret_cast<__bf16*>(ws + L.o_act);
   a.dzt = reinterpret_cast<__bf16*>(ws + L.o_dzt);
   a.dbpart = reinterpret_cast<float*>(ws + L.o_dbpart);
   a.loss_part = reinterpret_cast<float*>(ws + L.o_losspart);
-  a.counter = reinterpret_cast<unsigned*>(ws + L.o_counter);
   a.in_max = L.in_max;
   a.nwg = L.nwg;
-  if (shape->L == 2 && shape->in_dim[0] <= 128 && shape->in_dim[1] <= 128)
-    tower_l2_kernel<<<dim3(L.nwg), dim3(512), 0, as_stream(stream)>>>(a);
+  const int i0 = shape->in_dim[0], i1 = shape->in_dim[1], w0 = shape->width[0], w1 = shape->width[1];
+  const dim3 g(L.nwg), b512(512);
+  if (shape->L == 2 && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
+    tower_l2_kernel<128, 128, 64><<<g, b512, 0, as_stream(stream)>>>(a);
+  else if (shape->L == 2 && i0 == 64 && i1 == 64 && w0 == 128 && w1 == 64)
+    tower_l2_kernel<64, 128, 64><<<g, b512, 0, as_stream(stream)>>>(a);
+  else if (shape->L == 2 && i0 <= 128 && i1 <= 128)
+    tower_l2_kernel<0, 0, 0><<<g, b512, 0, as_stream(stream)>>>(a);
   else
     tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_fwd_bwd");
 }
 
-int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, void* workspace, size_t ws_bytes, void* stream) {
+int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                   void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
@@ -1016,7 +1012,10 @@ int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, void* workspace, si
   a.L = shape->L;
   a.dbpart = reinterpret_cast<const float*>(ws + L.o_dbpart);
   a.nwg = L.nwg;
-  const int64_t waves = (int64_t)L.ntiles * L.S + nbias;
+  a.loss_part = reinterpret_cast<const float*>(ws + L.o_losspart);
+  a.loss = loss;
+  a.nbias = nbias;
+  const int64_t waves = (int64_t)L.ntiles * L.S + nbias + 1;
   tower_wgrad_kernel<<<dim3((unsigned)ceil_div(waves, 4)), dim3(256), 0, as_stream(stream)>>>(
       a, reinterpret_cast<const WgradTile*>(ws + L.o_tiles));
   return check_launch("tower_wgrad");

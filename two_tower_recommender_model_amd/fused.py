@@ -30,9 +30,11 @@ class FusedTwoTowerStep:
                  batch_size: int, device: torch.device, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
                  overlap_prepare: bool = True, precision: str = "bf16", fused_towers: bool = True,
-                 kjt_mode: str = "cols"):
+                 kjt_mode: str = "cols", overlap_towers: bool = True):
         """One table per feature (feature f -> table f), features ordered as the KJT keys.
-        precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode)."""
+        precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode).
+        overlap_prepare / overlap_towers: run the dedup prepare / the towers' weight-gradient and
+        Adam kernels on side streams (False: everything in order on the caller's stream)."""
         self.device = torch.device(device)
         self.precision = precision
         if kjt_mode not in ("cols", "kjt"):
@@ -127,7 +129,7 @@ class FusedTwoTowerStep:
                 [self.in_q, self.in_c], self.layer_sizes, [self.q_lo, self.c_lo], B):
             self.towers = ops.FusedTowers([self.in_q, self.in_c], self.layer_sizes, [self.q_lo, self.c_lo], B, dev)
             assert self.towers.num_params == self.params.numel()
-            self.side2 = torch.cuda.Stream(device=dev)
+            self.side2 = torch.cuda.Stream(device=dev) if overlap_towers else None
             self.sync_weights()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         # warm every scratch workspace so graph capture allocates nothing new (the all-zero batch
@@ -210,16 +212,19 @@ class FusedTwoTowerStep:
             self.tables.pooled_fwd_cols(self.cols, self.num_embeddings, out=self.pooled)
         if self.towers is not None:
             # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update
-            self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits, self.loss)
-            self.side2.wait_stream(main)
-            with torch.cuda.stream(self.side2):
-                self.towers.wgrad()
+            self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
+            s2 = self.side2 if self.side2 is not None else main
+            if self.side2 is not None:
+                self.side2.wait_stream(main)
+            with torch.cuda.stream(s2):
+                self.towers.wgrad(self.loss)
                 self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
                                    grads_out=self.grads)
             if self.side is not None:
                 main.wait_stream(self.side)
             self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, B, self.lr_emb, self.eps)
-            main.wait_stream(self.side2)
+            if self.side2 is not None:
+                main.wait_stream(self.side2)
             return
         self._towers_fwd()
         L = len(self.layer_sizes)
@@ -238,36 +243,52 @@ class FusedTwoTowerStep:
             self.towers.update(self.params, do_adam=False)
 
     # ------------------------------------------------------------------------------------------
-    def capture(self) -> None:
-        """Record ``step()`` into a HIP graph (replayed by ``replay()``)."""
+    def capture(self, batches: Optional[Sequence] = None) -> None:
+        """Record ``step()`` into a HIP graph (replayed by ``replay()``). With ``batches`` (a list of
+        resident (cols, labels) device batches) the graph holds one full step per batch, in order."""
         self.sync_weights()
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
+        keep_cols, keep_labels = self.cols, self.labels
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
-                self.step()
+                if batches is None:
+                    self.step()
+                else:
+                    for cols, labels in batches:
+                        self.cols, self.labels = list(cols), labels
+                        self.step()
+        self.cols, self.labels = keep_cols, keep_labels
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.graph = g
 
     def replay(self, i: Optional[int] = None) -> None:
+        """Replay the single-step graph, or pool graph ``i`` (which runs ``steps_per_graph`` steps)."""
         if i is None:
             self.graph.replay()
         else:
             self.pool_graphs[i % len(self.pool_graphs)].replay()
 
-    def capture_pool(self, batches: Sequence) -> None:
-        """One graph per resident input batch ((cols, labels) device tensors): the graph's KJT
-        build reads that batch in place, so a replay needs no input copy."""
-        keep_cols, keep_labels = self.cols, self.labels
-        self.pool_graphs = []
+    def capture_pool(self, batches: Sequence, steps_per_graph: int = 1) -> None:
+        """Graphs over resident input batches ((cols, labels) device tensors), read in place so a
+        replay needs no input copy. Graph j runs full steps on batches j*k .. j*k+k-1 (k =
+        ``steps_per_graph``, len(batches) % k == 0): k > 1 amortises the host cost of a graph
+        launch over k steps."""
+        k = int(steps_per_graph)
+        if k < 1 or len(batches) % k:
+            raise _lib.TTError("capture_pool: the batch count must be a multiple of steps_per_graph")
+        staged = []
         for cols, labels in batches:
             for c in cols:
                 if c.dtype != self.id_dtype or not c.is_contiguous() or c.numel() != self.B:
                     raise _lib.TTError("capture_pool: batch columns must match the step's id dtype and batch")
-            self.cols, self.labels = list(cols), labels.to(torch.int32).contiguous()
-            self.capture()
+            staged.append((list(cols), labels.to(torch.int32).contiguous()))
+        self._pool_batches = staged  # keep the inputs alive as long as the graphs
+        self.pool_graphs = []
+        for j in range(0, len(staged), k):
+            self.capture(staged[j:j + k])
             self.pool_graphs.append(self.graph)
-        self.cols, self.labels = keep_cols, keep_labels
+        self.steps_per_graph = k

@@ -474,14 +474,18 @@ class FusedTowers:
         check(lib.tt_tower_workspace_init(C.byref(sh), self.B, ptr(self.ws), self.nbytes,
                                           stream_handle(self.device)), "tower_workspace_init")
 
-    def fwd_bwd(self, pooled, gpooled, params, labels, logits, loss, grad_scale: float = 1.0) -> None:
+    def fwd_bwd(self, pooled, gpooled, params, labels, logits, grad_scale: float = 1.0) -> None:
+        """T1. The scalar loss of this pass is written by the following wgrad()."""
         ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}[labels.dtype]
+        if pooled.stride(0) != gpooled.stride(0):
+            raise ValueError("pooled and its gradient must share a row stride")
         check(_lib_().tt_tower_fwd_bwd(C.byref(self.shape), self.B, ptr(pooled), pooled.stride(0), ptr(gpooled),
-                                       ptr(params), ptr(labels), ldt, float(grad_scale), ptr(logits), ptr(loss),
+                                       ptr(params), ptr(labels), ldt, float(grad_scale), ptr(logits),
                                        ptr(self.ws), self.nbytes, stream_handle(self.device)), "tower_fwd_bwd")
 
-    def wgrad(self) -> None:
-        check(_lib_().tt_tower_wgrad(C.byref(self.shape), self.B, ptr(self.ws), self.nbytes,
+    def wgrad(self, loss=None) -> None:
+        """T2; also reduces T1's loss partials into loss[0] when given."""
+        check(_lib_().tt_tower_wgrad(C.byref(self.shape), self.B, ptr(loss), ptr(self.ws), self.nbytes,
                                      stream_handle(self.device)), "tower_wgrad")
 
     def update(self, params, exp_avg=None, exp_avg_sq=None, step_state=None, lr: float = 0.01, beta1: float = 0.9,
