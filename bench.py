@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA spec (same table; the 5 PF figure assumes 2:1 sparsity)
 
 WORKLOADS = {
     # name: (num_users, num_items, dim, batch, layer_sizes)
@@ -51,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=2_000_000, help="table rows of the CPU sample")
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--kernel-iters", type=int, default=50)
+    ap.add_argument("--steps-per-graph", type=int, default=8, choices=[1, 2, 4, 8])
     return ap.parse_args()
 
 
@@ -85,32 +87,28 @@ def algorithmic_bytes(step, nnz: int, uniq: int):
     return fwd, k2d
 
 
-def time_kernel(fn, iters, pre=None):
-    """Average device time of one fn() launch, HIP events on the stream it launches on: with no
-    per-launch prerequisite, `iters` back-to-back launches between two events; otherwise an event
-    pair around each launch (its prerequisite `pre` runs outside the pair)."""
+def time_kernel(fn, iters):
+    """Average device time of one fn() launch: `iters` launches captured back to back in one HIP
+    graph (no host launch gaps between them), replayed between two HIP events on the stream the
+    graph runs on (the current stream)."""
     st = torch.cuda.current_stream()
-    if pre is None:
-        fn()
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record(st)
-        for _ in range(iters):
-            fn()
-        b.record(st)
-        b.synchronize()
-        return a.elapsed_time(b) / iters
-    tot = 0.0
-    for _ in range(iters):
-        pre()
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record(st)
-        fn()
-        b.record(st)
-        b.synchronize()
-        tot += a.elapsed_time(b)
-    return tot / iters  # ms
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream()
+    cs.wait_stream(st)
+    with torch.cuda.stream(cs):
+        fn()  # warm (workspaces exist before capture)
+        with torch.cuda.graph(g, stream=cs):
+            for _ in range(iters):
+                fn()
+    st.wait_stream(cs)
+    g.replay()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    g.replay()
+    b.record(st)
+    b.synchronize()
+    return a.elapsed_time(b) / iters  # ms
 
 
 def cpu_baseline(args, num_users, num_items, D, B, layers):
@@ -155,18 +153,32 @@ def run_single(args):
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
     batches = synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1)
-    # one HIP graph per resident batch: replay i trains on batch i % 8 with no input copy
-    step.capture_pool(batches)
-    for i in range(args.warmup):
-        step.replay(i)
+    # HIP graphs over the 8 resident batches, k full steps per graph (no input copies): a graph
+    # launch costs the host ~35-55 us, more than a step's GPU time, so k > 1 keeps the GPU fed
+    # (graphs of k steps, plus single-step graphs for a remainder, so exactly K steps are timed)
+    k = args.steps_per_graph
+    step.capture_pool(batches, steps_per_graph=k)
+    big = step.pool_graphs
+    step.capture_pool(batches, steps_per_graph=1)
+    small = step.pool_graphs
+
+    def run(n, i=0):
+        while n >= k:
+            big[(i // k) % len(big)].replay()
+            i, n = i + k, n - k
+        while n > 0:
+            small[i % len(small)].replay()
+            i, n = i + 1, n - 1
+
+    run(args.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step.replay(i)
+    run(args.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ms = dt / args.steps * 1e3
-    value = args.steps * B / dt
+    steps_run = args.steps
+    ms = dt / steps_run * 1e3
+    value = steps_run * B / dt
     loss = float(step.loss)
     # ---- dominant embedding kernels vs the HBM roofline (HIP events, same stream)
     cols = batches[(args.steps - 1) % len(batches)][0]
@@ -177,21 +189,36 @@ def run_single(args):
     uniq = int(torch.unique(keys[nz]).numel())
     fwd_bytes, k2d_bytes = algorithmic_bytes(step, nnz, uniq)
     t_fwd = time_kernel(lambda: step.tables.pooled_fwd_cols(cols, ne, out=step.pooled), args.kernel_iters)
+    # the fused backward re-applied to one prepared dedup (lr 0: the tables are left unchanged);
+    # the op is the per-row kernel plus the hot-row kernel (idle for these ids)
+    step.tables.bwd_prepare_cols(cols, ne)
     t_k2d = time_kernel(lambda: step.tables.bwd_rowwise_adagrad(step.gpooled, None, B, 0.0, 1e-10),
-                        args.kernel_iters, pre=lambda: step.tables.bwd_prepare_cols(cols, ne))
+                        args.kernel_iters)
     kern = {
         "pooled_fwd": {"ms": round(t_fwd, 5), "bytes": fwd_bytes, "GB/s": round(fwd_bytes / t_fwd / 1e6, 1)},
         "bwd_rowwise_adagrad": {"ms": round(t_k2d, 5), "bytes": k2d_bytes, "GB/s": round(k2d_bytes / t_k2d / 1e6, 1)},
     }
     dom = max(kern, key=lambda k: kern[k]["ms"])
     ach = kern[dom]["GB/s"]
+    # the towers against the bf16 MFMA peak: T1 = forward + backward-data of both towers
+    # (2 x 2 x 2B x sum_l in_l * out_l flop), T2 = weight gradients (2 x 2B x sum_l in_l * out_l)
+    towers = {}
+    if step.towers is not None:
+        macs = sum(i * o for i, o in zip([D] + layers[:-1], layers))
+        t_t1 = time_kernel(lambda: step.towers.fwd_bwd(step.pooled, step.gpooled, step.params, step.labels,
+                                                       step.logits), args.kernel_iters)
+        t_t2 = time_kernel(lambda: step.towers.wgrad(step.loss), args.kernel_iters)
+        for name, t_ms, fl in (("tower_fwd_bwd", t_t1, 8 * B * macs), ("tower_wgrad", t_t2, 4 * B * macs)):
+            tf = fl / t_ms / 1e9
+            towers[name] = {"ms": round(t_ms, 5), "flop": fl, "TFLOP/s": round(tf, 1),
+                            "frac_of_bf16_peak": round(tf / MFMA_BF16_PEAK_TFS, 4)}
     roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": kern[dom]["bytes"],
-                "kernels": kern, "lookups": nnz, "unique_rows": uniq}
+                "kernels": kern, "lookups": nnz, "unique_rows": uniq, "towers_mfma": towers}
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(args, num_users, num_items, D, B, layers)
-    return value, ms, loss, roofline, cpu
+    return value, ms, loss, roofline, cpu, steps_run
 
 
 def run_multi(args, world, rank, local_rank):
@@ -258,15 +285,15 @@ def main():
               "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D, "tower_dtype": "bf16 (MFMA, fp32 acc)",
               "parallelism": "single-gpu hipgraph" if world == 1 else f"rw-sharded tables + dp towers x{world}"}
     if world == 1:
-        value, ms, loss, roofline, cpu = run_single(args)
+        value, ms, loss, roofline, cpu, steps_run = run_single(args)
     else:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         value, ms, loss = run_multi(args, world, rank, local_rank)
-        roofline, cpu = None, None
+        roofline, cpu, steps_run = None, None, args.steps
     if rank == 0:
         out = {"metric": "training pairs/sec at batch 8192 (per GPU)", "value": round(value, 1), "unit": "pairs/s",
-               "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 5),
+               "n_gpus": world, "steps": steps_run, "warmup": args.warmup, "ms_per_step": round(ms, 5),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (uniform ids, Bernoulli labels), random-init weights", "config": config,
                "loss": loss, "roofline": roofline, "cpu_baseline": cpu}

@@ -31,6 +31,13 @@
  *   tt_dot_bce_fwd_bwd         <- TwoTowerTrainTask.forward, 03_model_training.py:447-455
  *                                 ((q*c).sum(1).squeeze() + BCEWithLogitsLoss(mean) + its backward)
  *   tt_adam_step               <- KeyedOptimizerWrapper(torch.optim.Adam), 03_model_training.py:826-829
+ *   tt_pooled_fwd_cols +
+ *   tt_bwd_prepare_cols        <- transform_to_torchrec_batch (03:353-380) + EBC forward (03:417) +
+ *                                 the fused backward, for single-hot columns: the KJT is never built
+ *   tt_tower_fwd_bwd / tt_tower_wgrad / tt_tower_update
+ *                              <- both MLP towers (03:411-412, :420-436) + TwoTowerTrainTask
+ *                                 (03:447-455) + loss.backward() through the towers + the dense
+ *                                 Adam step (03:826-829), as three fused kernels
  */
 #ifndef TT_MI355X_H
 #define TT_MI355X_H

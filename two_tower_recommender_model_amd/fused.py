@@ -286,7 +286,7 @@ class FusedTwoTowerStep:
                 if c.dtype != self.id_dtype or not c.is_contiguous() or c.numel() != self.B:
                     raise _lib.TTError("capture_pool: batch columns must match the step's id dtype and batch")
             staged.append((list(cols), labels.to(torch.int32).contiguous()))
-        self._pool_batches = staged  # keep the inputs alive as long as the graphs
+        self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]  # alive as long as any graph
         self.pool_graphs = []
         for j in range(0, len(staged), k):
             self.capture(staged[j:j + k])
