@@ -263,6 +263,16 @@ int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* work
 int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp,
                      float* gpooled, const float* params, const void* labels, int label_dtype,
                      float grad_scale, float* logits, void* workspace, size_t ws_bytes, void* stream);
+/* T1 with the EBC forward fused in, for single-hot columns (one key per tower, L = 2, inputs
+ * <= 128 wide): tower t's input row m is row (cols[t][m] mod num_embeddings[t]) of the table
+ * starting at table_rows[t] ([rows][in_dim[t]] fp32, 16-B aligned), zeros when the id is 0
+ * (transform_to_torchrec_batch semantics, 03_model_training.py:356-365); the pooled rows are
+ * never materialised unless pooled_out (nullable, ld = ldp, columns in_col[t]) is given. */
+int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
+                            const int64_t* num_embeddings, const float* const* table_rows,
+                            float* pooled_out, int64_t ldp, float* gpooled, const float* params,
+                            const void* labels, int label_dtype, float grad_scale, float* logits,
+                            void* workspace, size_t ws_bytes, void* stream);
 /* T2: weight/bias gradients of every layer into the workspace (fixed-order partial slabs), and
  * the mean BCE of the preceding T1 into loss[0] (nullable; fixed-order sum of T1's partials). */
 int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,

@@ -18,11 +18,11 @@ def ops():
     return _ops
 
 
+@pytest.mark.parametrize("B", [3000, 9000])
 @pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
 @pytest.mark.parametrize("dims,zipf", [([128, 128], False), ([64, 64], True), ([36, 4], True), ([256, 16], False)])
-def test_cols_form_equals_kjt_form(ops, device, dtype, dims, zipf):
+def test_cols_form_equals_kjt_form(ops, device, dtype, dims, zipf, B):
     g = torch.Generator().manual_seed(sum(dims) + zipf)
-    B = 3000
     N = [5000, 700]
     cols = []
     for n in N:
@@ -59,12 +59,39 @@ def test_cols_form_equals_kjt_form(ops, device, dtype, dims, zipf):
     assert torch.equal(ts_a.state, ts_b.state)
 
 
+@pytest.mark.parametrize("B", [2000, 5000])
+def test_cols_form_shared_table(ops, device, B):
+    """Two keys on ONE table (each with its own id % N divisor): cols form == KJT form bitwise."""
+    g = torch.Generator().manual_seed(B)
+    rows, N = [6000], [6000, 2500]
+    cols = [torch.randint(0, 3 * n, (B,), generator=g).to(device) for n in N]
+    cols[1][:7] = 5  # shared rows between the keys, one of them hot
+    ts_a = ops.TableSet(rows, [64], [0, 0], device)
+    ts_a.init_uniform_(torch.Generator(device=device).manual_seed(4))
+    ts_b = ops.TableSet(rows, [64], [0, 0], device)
+    ts_b.weights.copy_(ts_a.weights)
+    out_c = ts_a.pooled_fwd_cols(cols, N)
+    values, lengths, offsets, _ = ops.kjt_build_mod_dropzero(cols, N)
+    out_k = ts_b.pooled_fwd(values, offsets, B)
+    assert torch.equal(out_c, out_k)
+    for step in range(2):
+        gout = torch.randn(B, 128, generator=torch.Generator().manual_seed(step)).to(device)
+        ts_a.bwd_prepare_cols(cols, N)
+        ts_a.bwd_rowwise_adagrad(gout, None, B, 0.05, 1e-10)
+        ts_b.bwd_prepare(values, offsets, B, max_lookups=2 * B)
+        ts_b.bwd_rowwise_adagrad(gout, offsets, B, 0.05, 1e-10)
+    torch.cuda.synchronize()
+    assert torch.equal(ts_a.weights, ts_b.weights)
+    assert torch.equal(ts_a.state, ts_b.state)
+
+
 @pytest.mark.parametrize("ids", ["uniform", "hot"])
 def test_fused_step_cols_equals_kjt_mode(device, ids):
     from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
 
     B, D, N = 1024, 128, [20000, 30000]
-    steps = [FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, kjt_mode=m, seed=5) for m in ("cols", "kjt")]
+    steps = [FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, kjt_mode=m, seed=5, materialize_pooled=True)
+             for m in ("cols", "kjt")]
     g = torch.Generator().manual_seed(1)
     for s in range(3):
         if ids == "uniform":
@@ -81,3 +108,32 @@ def test_fused_step_cols_equals_kjt_mode(device, ids):
     assert torch.equal(a.tables.weights, b.tables.weights)
     assert torch.equal(a.params, b.params)
     assert float(a.loss) == float(b.loss)
+
+
+@pytest.mark.parametrize("D,dtype", [(128, torch.int64), (64, torch.int32)])
+def test_fused_gather_equals_separate_forward(device, D, dtype):
+    """EBC forward fused into the tower kernel (rows gathered into its LDS tile) == the separate
+    pooled_fwd_cols + tower kernel, bit for bit, over 3 training steps (ids with zeros, negative
+    ids, ids >= N, a ragged last workgroup)."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    B, N = 1000, [5000, 7000]
+    steps = [FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=2, id_dtype=dtype,
+                               fuse_gather=fg, materialize_pooled=True) for fg in (True, False)]
+    assert steps[0].gather and not steps[1].gather
+    g = torch.Generator().manual_seed(9)
+    for s in range(3):
+        cols = [torch.randint(-n, 2 * n, (B,), generator=g) for n in N]
+        for c in cols:
+            c[torch.rand(B, generator=g) < 0.1] = 0
+        lab = torch.randint(0, 2, (B,), generator=g).to(torch.int32)
+        for st in steps:
+            st.load_batch([c.to(dtype).to(device) for c in cols], lab.to(device))
+            st.step()
+    torch.cuda.synchronize()
+    a, b = steps
+    assert torch.equal(a.pooled, b.pooled)
+    assert torch.equal(a.gpooled, b.gpooled)
+    assert torch.equal(a.logits, b.logits)
+    assert torch.equal(a.tables.weights, b.tables.weights)
+    assert torch.equal(a.params, b.params)

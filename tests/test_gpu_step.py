@@ -41,7 +41,8 @@ def test_fused_step_matches_reference_golden(device, case, precision):
     layers, D, B = _layers(g), int(g["D"]), int(g["B"])
     ne = [int(x) for x in g["num_embeddings"]]
     lr = float(g["lr"])
-    st = FusedTwoTowerStep(ne, [D, D], [0], [1], layers, B, device, lr_emb=lr, lr_dense=lr, precision=precision)
+    st = FusedTwoTowerStep(ne, [D, D], [0], [1], layers, B, device, lr_emb=lr, lr_dense=lr, precision=precision,
+                           materialize_pooled=True)
     st.tables.table_view(0).copy_(torch.from_numpy(g["init_t_user_id"]))
     st.tables.table_view(1).copy_(torch.from_numpy(g["init_t_product_id"]))
     for l in range(len(layers)):

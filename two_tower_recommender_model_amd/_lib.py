@@ -121,6 +121,10 @@ SIGNATURES = {
     "tt_tower_workspace_init": (_int, [_psh, _i64, _vp, _sz, _vp]),
     "tt_tower_fwd_bwd": (_int, [_psh, _i64, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp]),
     "tt_tower_wgrad": (_int, [_psh, _i64, _vp, _vp, _sz, _vp]),
+    "tt_tower_fwd_bwd_gather": (
+        _int,
+        [_psh, _i64, _pvp, _int, _pi64, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
+    ),
     "tt_tower_update": (
         _int,
         [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _int, _vp, _vp, _sz, _vp],
@@ -146,6 +150,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_workspace_init",
     "tt_tower_fwd_bwd",
     "tt_tower_wgrad",
+    "tt_tower_fwd_bwd_gather",
     "tt_tower_update",
     "tt_pooled_fwd_cols",
     "tt_bwd_prepare_cols",

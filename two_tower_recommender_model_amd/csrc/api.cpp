@@ -46,6 +46,6 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_dot_bce_fwd_bwd, tt_adam_step, tt_tower_workspace_init, tt_tower_fwd_bwd, tt_tower_wgrad,
 // tt_tower_update
 // tt_pooled_fwd_cols, tt_bwd_prepare_cols
-int tt_num_entry_points(void) { return 21; }
+int tt_num_entry_points(void) { return 22; }
 
 }  // extern "C"

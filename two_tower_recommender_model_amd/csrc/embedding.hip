@@ -16,16 +16,11 @@
 // ids, so they run beside the forward and the towers.
 // k2d "narrow" (D <= 128, D % 4 == 0): a half-wave per unique row (32 lanes x float4 = one
 // 512-B row), two rows per wave; segments of <= 32 lookups are summed in ascending bag order
-// (bitwise reproducible), longer ones in fp64 (order-independent in practice). k2d "generic":
-// a wave per row for other dims.
+// (bitwise reproducible). k2d "generic": a wave per row for other dims. Longer segments ("hot"
+// rows) go to a workgroup-per-row kernel that sorts their bag ids in LDS: same canonical order.
 #include "tt_common.h"
 
 namespace tt {
-
-__device__ __forceinline__ int64_t py_mod64(int64_t a, int64_t n) {
-  int64_t r = a % n;
-  return (r != 0 && ((r < 0) != (n < 0))) ? r + n : r;
-}
 
 struct ColArgs {
   const void* col[TT_MAX_FEATURES];

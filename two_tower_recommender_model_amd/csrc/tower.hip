@@ -60,6 +60,13 @@ struct TowerArgs {
   float* loss_part;     // [nwg]
   int64_t in_max;
   int nwg;
+  // fused single-hot gather (tt_tower_fwd_bwd_gather): tower t's input row m is table row
+  // (gcol[t][m] mod gmod[t]) of gtab[t] (zeros for id 0) instead of pooled row m
+  const void* gcol[2];
+  const float* gtab[2];
+  int64_t gmod[2];
+  int gid_dtype;
+  float* pooled_out;    // nullable: the gathered rows are also written here (ld = ldp)
 };
 
 __device__ __forceinline__ float lbl(const void* p, int dt, int64_t i) {
@@ -419,14 +426,35 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
   // then every weight fragment of the step in order of use, then the biases
   f32x4 xv[4];
   const int nxv = in / 32;  // f32x4 loads per thread: TR rows x in/4 vectors over 256 threads
+  const bool gather = a.gcol[t] != nullptr;
+  if (gather) {
+    // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros
+    const float* src[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    xv[i] = (f32x4)(0.f);
-    if (i < nxv) {
-      const int e = tt + 256 * i;
-      const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
-      const int64_t gm = m0 + row;
-      if (gm < B) xv[i] = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + c4);
+    for (int i = 0; i < 4; ++i) {
+      src[i] = nullptr;
+      if (i < nxv) {
+        const int e = tt + 256 * i;
+        const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
+        const int64_t gm = m0 + row;
+        if (gm < B) {
+          const int64_t id = load_id(a.gcol[t], a.gid_dtype, gm);
+          if (id != 0) src[i] = a.gtab[t] + py_mod64(id, a.gmod[t]) * in + c4;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xv[i] = src[i] ? *reinterpret_cast<const f32x4*>(src[i]) : (f32x4)(0.f);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xv[i] = (f32x4)(0.f);
+      if (i < nxv) {
+        const int e = tt + 256 * i;
+        const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
+        const int64_t gm = m0 + row;
+        if (gm < B) xv[i] = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + c4);
+      }
     }
   }
   Frags f0, f1, g1, g0;
@@ -449,6 +477,9 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
       bf16x4 bv;
       bv[0] = (__bf16)xv[i][0]; bv[1] = (__bf16)xv[i][1]; bv[2] = (__bf16)xv[i][2]; bv[3] = (__bf16)xv[i][3];
       *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
+      const int64_t gm = m0 + row;
+      if (a.pooled_out && gm < B)
+        *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + a.s.in_col[t] + c4) = xv[i];
     }
   }
   __syncthreads();
@@ -642,14 +673,17 @@ struct WgradArgs {
 };
 
 __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const WgradTile* __restrict__ tiles) {
-  const int lane = threadIdx.x & 63;
+  // workgroups [0, ntiles * S): one (32x32 tile of dW, batch slice) each, its 4 waves on 4
+  // consecutive quarters of the slice, reduced through LDS in wave order -> one slab row.
+  // Workgroups beyond: one wave per bias output (+ one for the loss).
+  __shared__ float red[3][64 * 16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
-  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t nw = (int64_t)a.ntiles * a.S;
-  if (wave >= nw) {
+  const int64_t nwg_tiles = (int64_t)a.ntiles * a.S;
+  if ((int64_t)blockIdx.x >= nwg_tiles) {
     // bias gradient of one output n of (t, l): sum of the T1 workgroups' partials, lanes strided
     // over workgroups, then a fixed butterfly -> slab[0]
-    int64_t b = wave - nw;
+    int64_t b = ((int64_t)blockIdx.x - nwg_tiles) * 4 + wid;
     if (b == a.nbias) {  // the scalar loss: T1's per-workgroup partials in a fixed order
       if (a.loss) {
         float s = 0.f;
@@ -672,14 +706,17 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
       }
     return;
   }
-  const int s = (int)(wave / a.ntiles);
-  const WgradTile tl = tiles[wave % a.ntiles];
+  const int s = (int)(blockIdx.x / a.ntiles);
+  const WgradTile tl = tiles[blockIdx.x % a.ntiles];
   const int64_t B = a.B;
   const __bf16* Z = a.dzt + ((int64_t)tl.t * MAXL + tl.l) * MAXW * B;  // [n][B]
   const __bf16* A = tl.l == 0 ? a.xt + (int64_t)tl.t * a.in_max * B
                               : a.act + ((int64_t)tl.t * MAXL + tl.l - 1) * MAXW * B;  // [k][B]
-  const int64_t mb = (int64_t)s * a.mslice;
-  const int64_t me = mb + a.mslice < B ? mb + a.mslice : B;
+  const int64_t mw = a.mslice / 4;
+  int64_t mb = (int64_t)s * a.mslice + wid * mw;
+  int64_t me = mb + mw;
+  if (mb > B) mb = B;
+  if (me > B) me = B;
   f32x4 acc[2][2];
   for (int i = 0; i < 2; ++i)
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
@@ -688,6 +725,25 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
   const __bf16* a0 = A + (int64_t)(tl.k0 + r) * B;
   const __bf16* a1 = A + (int64_t)(tl.k0 + 16 + r) * B;
   int64_t m = mb;
+  // 4 k-steps per iteration: their 16 fragment loads are issued before the first MFMA
+  for (; m + 128 <= me; m += 128) {
+    bf16x8 fa0[4], fa1[4], fb0[4], fb1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t o = m + 32 * u + q * 8;
+      fa0[u] = *reinterpret_cast<const bf16x8*>(z0 + o);
+      fa1[u] = *reinterpret_cast<const bf16x8*>(z1 + o);
+      fb0[u] = *reinterpret_cast<const bf16x8*>(a0 + o);
+      fb1[u] = *reinterpret_cast<const bf16x8*>(a1 + o);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[u], fb0[u], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[u], fb1[u], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[u], fb0[u], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[u], fb1[u], acc[1][1], 0, 0, 0);
+    }
+  }
   for (; m + 32 <= me; m += 32) {
     const int64_t o = m + q * 8;
     const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(z0 + o);
@@ -714,6 +770,25 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
     acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb0, acc[1][0], 0, 0, 0);
     acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb1, acc[1][1], 0, 0, 0);
   }
+  // fixed-order reduction of the 4 waves' tiles: wave 0 adds waves 1, 2, 3 in that order
+  if (wid > 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) red[wid - 1][((i * 2 + j) * 4 + rr) * 64 + lane] = acc[i][j][rr];
+  }
+  __syncthreads();
+  if (wid > 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[i][j][rr] += red[w][((i * 2 + j) * 4 + rr) * 64 + lane];
   // C[n][k]: row = n (4q + rr), col = k (r)
   const int K = a.K[tl.t][tl.l];
   float* dst = a.slab + (int64_t)s * a.P + a.woff[tl.t][tl.l];
@@ -860,12 +935,13 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   for (int t = 0; t < 2; ++t)
     for (int l = 0; l < s->L; ++l) nt += (s->width[l] / 32) * (L.K[t][l] / 32);
   L.ntiles = nt;
-  // slices: aim for ~1024 waves, >= 256 rows per slice
-  int64_t S = std::max<int64_t>(1, 1024 / std::max(1, nt));
-  S = std::min<int64_t>(S, std::max<int64_t>(1, ceil_div(B, 256)));
+  // slices (one T2 workgroup each per tile, 4 waves of mslice/4 rows): aim for ~400 workgroups,
+  // >= 512 rows per slice; the slice count is also the slab depth T3 reduces over
+  int64_t S = std::max<int64_t>(1, 400 / std::max(1, nt));
+  S = std::min<int64_t>(S, std::max<int64_t>(1, ceil_div(B, 512)));
   S = std::min<int64_t>(S, 64);
   L.S = (int)S;
-  L.mslice = ceil_div(ceil_div(B, S), 32) * 32;
+  L.mslice = ceil_div(ceil_div(B, S), 128) * 128;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t r = off;
@@ -926,22 +1002,27 @@ int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* work
   return hipStreamSynchronize(st) == hipSuccess ? TT_OK : fail(TT_EINVAL, "tower: init sync failed");
 }
 
-int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp, float* gpooled,
-                     const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
-                     void* workspace, size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace tt {
+// shared by tt_tower_fwd_bwd / tt_tower_fwd_bwd_gather: checks, T1 arguments, launch
+static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, const float* pooled, int64_t ldp,
+                     float* gpooled, const float* params, const void* labels, int label_dtype, float grad_scale,
+                     float* logits, void* workspace, size_t ws_bytes, void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if (!pooled || !gpooled || !params || !labels || !logits) return fail(TT_EINVAL, "tower: null pointer");
+  if ((!pooled && !a.gcol[0]) || !gpooled || !params || !labels || !logits)
+    return fail(TT_EINVAL, "tower: null pointer");
   if (label_dtype != TT_I32 && label_dtype != TT_I64 && label_dtype != TT_F32)
     return fail(TT_EINVAL, "tower: labels must be int32/int64/float32");
-  if (ldp % 4 || (reinterpret_cast<uintptr_t>(pooled) & 15) || (reinterpret_cast<uintptr_t>(gpooled) & 15))
-    return fail(TT_EINVAL, "tower: pooled and its gradient must be 16-B aligned rows");
+  if (ldp % 4 || (reinterpret_cast<uintptr_t>(pooled) & 15) || (reinterpret_cast<uintptr_t>(gpooled) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.pooled_out) & 15))
+    return fail(TT_EINVAL, "tower: pooled rows and their gradient must be 16-B aligned");
   for (int t = 0; t < 2; ++t)
     if (shape->in_col[t] + shape->in_dim[t] > ldp) return fail(TT_EINVAL, "tower: input columns exceed the pooled row");
   char* ws = reinterpret_cast<char*>(workspace);
-  TowerArgs a{};
   a.s = *shape;
   a.B = B;
   a.pooled = pooled;
@@ -969,15 +1050,48 @@ int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pool
   a.nwg = L.nwg;
   const int i0 = shape->in_dim[0], i1 = shape->in_dim[1], w0 = shape->width[0], w1 = shape->width[1];
   const dim3 g(L.nwg), b512(512);
-  if (shape->L == 2 && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
+  const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
+  if (a.gcol[0] && !two) return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
+  if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
     tower_l2_kernel<128, 128, 64><<<g, b512, 0, as_stream(stream)>>>(a);
-  else if (shape->L == 2 && i0 == 64 && i1 == 64 && w0 == 128 && w1 == 64)
+  else if (two && i0 == 64 && i1 == 64 && w0 == 128 && w1 == 64)
     tower_l2_kernel<64, 128, 64><<<g, b512, 0, as_stream(stream)>>>(a);
-  else if (shape->L == 2 && i0 <= 128 && i1 <= 128)
+  else if (two)
     tower_l2_kernel<0, 0, 0><<<g, b512, 0, as_stream(stream)>>>(a);
   else
     tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_fwd_bwd");
+}
+}  // namespace tt
+
+extern "C" {
+
+int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp, float* gpooled,
+                     const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
+                     void* workspace, size_t ws_bytes, void* stream) {
+  TowerArgs a{};
+  return launch_t1(shape, B, a, pooled, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
+                   ws_bytes, stream);
+}
+
+int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
+                            const int64_t* num_embeddings, const float* const* table_rows, float* pooled_out,
+                            int64_t ldp, float* gpooled, const float* params, const void* labels, int label_dtype,
+                            float grad_scale, float* logits, void* workspace, size_t ws_bytes, void* stream) {
+  if (!cols || !num_embeddings || !table_rows) return fail(TT_EINVAL, "tower_gather: null pointer");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_gather: ids must be int32/int64");
+  TowerArgs a{};
+  for (int t = 0; t < 2; ++t) {
+    if (!cols[t] || !table_rows[t] || num_embeddings[t] < 1) return fail(TT_EINVAL, "tower_gather: bad column");
+    if (reinterpret_cast<uintptr_t>(table_rows[t]) & 15) return fail(TT_EINVAL, "tower_gather: rows not 16-B aligned");
+    a.gcol[t] = cols[t];
+    a.gtab[t] = table_rows[t];
+    a.gmod[t] = num_embeddings[t];
+  }
+  a.gid_dtype = id_dtype;
+  a.pooled_out = pooled_out;
+  return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
+                   ws_bytes, stream);
 }
 
 int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
@@ -1015,8 +1129,8 @@ int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* 
   a.loss_part = reinterpret_cast<const float*>(ws + L.o_losspart);
   a.loss = loss;
   a.nbias = nbias;
-  const int64_t waves = (int64_t)L.ntiles * L.S + nbias + 1;
-  tower_wgrad_kernel<<<dim3((unsigned)ceil_div(waves, 4)), dim3(256), 0, as_stream(stream)>>>(
+  const int64_t wgs = (int64_t)L.ntiles * L.S + ceil_div(nbias + 1, 4);
+  tower_wgrad_kernel<<<dim3((unsigned)wgs), dim3(256), 0, as_stream(stream)>>>(
       a, reinterpret_cast<const WgradTile*>(ws + L.o_tiles));
   return check_launch("tower_wgrad");
 }

@@ -56,6 +56,13 @@ __device__ __forceinline__ int64_t load_id(const void* values, int id_dtype, int
                             : (int64_t)reinterpret_cast<const int32_t*>(values)[i];
 }
 
+// Python's a % n (result takes the divisor's sign): transform_to_torchrec_batch's `id % N`,
+// 03_model_training.py:361, on tensors of either sign
+__device__ __forceinline__ int64_t py_mod64(int64_t a, int64_t n) {
+  int64_t r = a % n;
+  return (r != 0 && ((r < 0) != (n < 0))) ? r + n : r;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

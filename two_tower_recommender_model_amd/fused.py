@@ -30,11 +30,15 @@ class FusedTwoTowerStep:
                  batch_size: int, device: torch.device, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
                  overlap_prepare: bool = True, precision: str = "bf16", fused_towers: bool = True,
-                 kjt_mode: str = "cols", overlap_towers: bool = True):
+                 kjt_mode: str = "cols", overlap_towers: bool = True, fuse_gather: bool = True,
+                 materialize_pooled: bool = False):
         """One table per feature (feature f -> table f), features ordered as the KJT keys.
         precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode).
         overlap_prepare / overlap_towers: run the dedup prepare / the towers' weight-gradient and
-        Adam kernels on side streams (False: everything in order on the caller's stream)."""
+        Adam kernels on side streams (False: everything in order on the caller's stream).
+        fuse_gather: with single-hot columns, one key per tower and two-layer towers, the EBC
+        forward runs inside the tower kernel (rows gathered straight into its LDS tile); the
+        pooled rows are then written to ``self.pooled`` only when ``materialize_pooled``."""
         self.device = torch.device(device)
         self.precision = precision
         if kjt_mode not in ("cols", "kjt"):
@@ -131,6 +135,10 @@ class FusedTwoTowerStep:
             assert self.towers.num_params == self.params.numel()
             self.side2 = torch.cuda.Stream(device=dev) if overlap_towers else None
             self.sync_weights()
+        self.materialize_pooled = bool(materialize_pooled)
+        self.gather = (fuse_gather and self.towers is not None and kjt_mode == "cols" and self.F == 2
+                       and self.qf == [0] and self.cf == [1] and len(self.layer_sizes) == 2
+                       and max(self.dims) <= 128)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         # warm every scratch workspace so graph capture allocates nothing new (the all-zero batch
         # drops every id, so the tables are untouched; the towers' parameters are restored)
@@ -206,13 +214,20 @@ class FusedTwoTowerStep:
                 prepare()
         else:
             prepare()
-        if self.kjt_mode == "kjt":
+        if self.gather:
+            # EBC forward fused into T1
+            self.towers.fwd_bwd_gather(self.cols, self.num_embeddings,
+                                       [self.tables.table_view(0), self.tables.table_view(1)], self.gpooled,
+                                       self.params, self.labels, self.logits,
+                                       pooled_out=self.pooled if self.materialize_pooled else None)
+        elif self.kjt_mode == "kjt":
             self.tables.pooled_fwd(self.values, self.offsets, B, out=self.pooled)
         else:
             self.tables.pooled_fwd_cols(self.cols, self.num_embeddings, out=self.pooled)
         if self.towers is not None:
             # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update
-            self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
+            if not self.gather:
+                self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
             s2 = self.side2 if self.side2 is not None else main
             if self.side2 is not None:
                 self.side2.wait_stream(main)

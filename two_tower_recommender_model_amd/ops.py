@@ -483,6 +483,24 @@ class FusedTowers:
                                        ptr(params), ptr(labels), ldt, float(grad_scale), ptr(logits),
                                        ptr(self.ws), self.nbytes, stream_handle(self.device)), "tower_fwd_bwd")
 
+    def fwd_bwd_gather(self, cols, num_embeddings, table_rows, gpooled, params, labels, logits,
+                       pooled_out=None, grad_scale: float = 1.0) -> None:
+        """T1 with the single-hot EBC forward fused in: tower t's input rows are gathered from the
+        table view ``table_rows[t]`` ([rows, in_dim[t]] fp32) by ``cols[t] % num_embeddings[t]``
+        (id 0 -> zeros). ``pooled_out`` (optional) receives the gathered rows."""
+        ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}[labels.dtype]
+        for t in range(2):
+            if table_rows[t].shape[1] != self.shape.in_dim[t] or int(num_embeddings[t]) > table_rows[t].shape[0]:
+                raise _lib.TTError("fwd_bwd_gather: table view does not match the tower input")
+        if pooled_out is not None and pooled_out.stride(0) != gpooled.stride(0):
+            raise ValueError("pooled_out and the gradient must share a row stride")
+        ne = (C.c_int64 * 2)(*[int(n) for n in num_embeddings])
+        check(_lib_().tt_tower_fwd_bwd_gather(C.byref(self.shape), self.B, ptr_array(list(cols)),
+                                              id_dtype_code(cols[0].dtype), ne, ptr_array(list(table_rows)),
+                                              ptr(pooled_out), gpooled.stride(0), ptr(gpooled), ptr(params),
+                                              ptr(labels), ldt, float(grad_scale), ptr(logits), ptr(self.ws),
+                                              self.nbytes, stream_handle(self.device)), "tower_fwd_bwd_gather")
+
     def wgrad(self, loss=None) -> None:
         """T2; also reduces T1's loss partials into loss[0] when given."""
         check(_lib_().tt_tower_wgrad(C.byref(self.shape), self.B, ptr(loss), ptr(self.ws), self.nbytes,
