@@ -74,19 +74,6 @@ def synth_batches(num_users, num_items, B, n, device, ids, seed):
     return out
 
 
-def algorithmic_bytes(step, nnz: int, uniq: int):
-    """Per-launch algorithmic bytes (SURVEY.md 8(d) accounting, per kernel):
-    pooled_fwd : per lookup id (8) + row (4D); per bag offset (4) + pooled write (4D)
-    adagrad k2d: per lookup bag index (4) + grad row (4D); per unique row read+write row (8D),
-                 read+write state (8), segment/slot/key bookkeeping (20)."""
-    D = step.dims[0]
-    idb = 8 if step.id_dtype == torch.int64 else 4
-    nb = step.F * step.B
-    fwd = nnz * (idb + 4 * D) + nb * (4 + 4 * D)
-    k2d = nnz * (4 + 4 * D) + uniq * (8 * D + 8 + 20)
-    return fwd, k2d
-
-
 def time_kernel(fn, iters):
     """Average device time of one fn() launch: `iters` launches captured back to back in one HIP
     graph (no host launch gaps between them), replayed between two HIP events on the stream the
@@ -144,6 +131,93 @@ def cpu_baseline(args, num_users, num_items, D, B, layers):
     }
 
 
+def lookup_stats(step, batches):
+    """Kept lookups and unique (table, row) pairs per step, averaged over the resident batches."""
+    nnz = uniq = 0
+    for cols, _ in batches:
+        keys = torch.cat([(c % n) + (t << 40) for t, (c, n) in enumerate(zip(cols, step.num_embeddings))])
+        nz = torch.cat([c != 0 for c in cols])
+        nnz += int(nz.sum())
+        uniq += int(torch.unique(keys[nz]).numel())
+    return nnz // len(batches), uniq // len(batches)
+
+
+def launch_bytes(step, nnz: int, uniq: int):
+    """Algorithmic HBM bytes (and MFMA flops) per launch of the one-stream step:
+    t1 = gather + towers fwd/bwd + dedup insert; k2 = T2 weight gradients + fused row-wise Adagrad;
+    t3 = Adam. The embedding-path total follows SURVEY.md 8(d)."""
+    D, B, F = step.dims[0], step.B, step.F
+    L = step.layer_sizes
+    idb = 8 if step.id_dtype == torch.int64 else 4
+    ins = [step.in_q, step.in_c]
+    macs = sum(i * o for i, o in zip([D] + L[:-1], L))
+    opnd = 2 * B * 2 * (D + L[0] + (L[0] + L[1]))  # bf16 X^T, act^T, dZ^T of both towers (T1 -> T2)
+    P = step.params.numel()
+    S = max(1, min(400 // max(1, sum((w // 32) * (k // 32) for w, k in zip(L, [D] + L[:-1])) * 2), -(-B // 512), 64))
+    t1 = (F * B * idb + B * 4 + nnz * 4 * D + B * 4 + F * B * 4 * D + opnd + nnz * 20)
+    emb_upd = uniq * (64 + 8 * D + 8) + nnz * 4 * D
+    k2 = emb_upd + opnd + S * P * 4
+    t3 = S * P * 4 + 6 * P * 4 + 4 * P
+    emb_path = F * B * (1 * (8 + 8 + 4 * D) + 4 + 4 * D + 4 * D) + uniq * (8 * D + 8)  # 8(d), L = 1
+    return {"t1": {"bytes": t1, "flop": 8 * B * macs, "what": "tower_l2_kernel: EBC gather + both towers fwd/bwd "
+                                                              "+ dedup insert"},
+            "k2": {"bytes": k2, "flop": 4 * B * macs, "emb_bytes": emb_upd,
+                   "what": "tower_wgrad_dedup_kernel: T2 weight gradients + fused row-wise Adagrad"},
+            "t3": {"bytes": t3, "flop": 0, "what": "tower_update_kernel: slab reduction + Adam + bf16 copies"},
+            "_emb_path_bytes": emb_path}
+
+
+def pmc_traffic(kernel_name: str):
+    """HBM bytes per launch of `kernel_name` from the newest committed PMC summary (profiles/*pmc*.json,
+    FETCH_SIZE/WRITE_SIZE passes of scripts/pmc_traffic.sh, gfx950-corrected), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for k, v in d.get("kernels", {}).items():
+        if kernel_name in k:
+            return v.get("hbm_bytes"), os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
+KERNEL_NAMES = {"t1": "tower_l2_kernel", "k2": "tower_wgrad_dedup_kernel", "t3": "tower_update_kernel"}
+
+
+def roofline_report(kern, timed, nnz, uniq, step, B):
+    emb_path_bytes = kern.pop("_emb_path_bytes")
+    out = {}
+    for name, k in kern.items():
+        ms = timed.get(name) if timed else None
+        e = dict(k)
+        e["kernel"] = KERNEL_NAMES[name]
+        if ms:
+            e["ms"] = round(ms, 5)
+            e["GB/s"] = round(k["bytes"] / ms / 1e6, 1)
+            if k["flop"]:
+                e["TFLOP/s"] = round(k["flop"] / ms / 1e9, 1)
+                e["frac_of_bf16_peak"] = round(k["flop"] / ms / 1e9 / MFMA_BF16_PEAK_TFS, 4)
+        out[name] = e
+    if not timed:
+        return {"bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq}
+    dom = max((n for n in out if "ms" in out[n]), key=lambda n: out[n]["ms"])
+    traffic, src = pmc_traffic(KERNEL_NAMES[dom])
+    emb_ms = timed.get("t1", 0.0) + timed.get("k2", 0.0)
+    ach = out[dom]["GB/s"]
+    return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "bytes_per_launch": out[dom]["bytes"], "ms_per_launch": out[dom]["ms"],
+            "timing": "HIP external events around each launch inside the replayed step graphs",
+            "kernels": out, "lookups": nnz, "unique_rows": uniq,
+            "embedding_path": {"bytes_per_step": emb_path_bytes, "ms": round(emb_ms, 5),
+                               "GB/s": round(emb_path_bytes / emb_ms / 1e6, 1) if emb_ms else None,
+                               "frac": round(emb_path_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4) if emb_ms else None,
+                               "note": "SURVEY 8(d) bytes over the in-step time of the launches that carry the "
+                                       "embedding work (T1 gather+insert, K2 Adagrad); both also run tower work"}}
+
+
 def run_single(args):
     from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
 
@@ -180,41 +254,29 @@ def run_single(args):
     ms = dt / steps_run * 1e3
     value = steps_run * B / dt
     loss = float(step.loss)
-    # ---- dominant embedding kernels vs the HBM roofline (HIP events, same stream)
-    cols = batches[(args.steps - 1) % len(batches)][0]
-    ne = step.num_embeddings
-    keys = torch.cat([(c % n) + (t << 40) for t, (c, n) in enumerate(zip(cols, ne))])
-    nz = torch.cat([c != 0 for c in cols])
-    nnz = int(nz.sum())
-    uniq = int(torch.unique(keys[nz]).numel())
-    fwd_bytes, k2d_bytes = algorithmic_bytes(step, nnz, uniq)
-    t_fwd = time_kernel(lambda: step.tables.pooled_fwd_cols(cols, ne, out=step.pooled), args.kernel_iters)
-    # the fused backward re-applied to one prepared dedup (lr 0: the tables are left unchanged);
-    # the op is the per-row kernel plus the hot-row kernel (idle for these ids)
-    step.tables.bwd_prepare_cols(cols, ne)
-    t_k2d = time_kernel(lambda: step.tables.bwd_rowwise_adagrad(step.gpooled, None, B, 0.0, 1e-10),
-                        args.kernel_iters)
-    kern = {
-        "pooled_fwd": {"ms": round(t_fwd, 5), "bytes": fwd_bytes, "GB/s": round(fwd_bytes / t_fwd / 1e6, 1)},
-        "bwd_rowwise_adagrad": {"ms": round(t_k2d, 5), "bytes": k2d_bytes, "GB/s": round(k2d_bytes / t_k2d / 1e6, 1)},
-    }
-    dom = max(kern, key=lambda k: kern[k]["ms"])
-    ach = kern[dom]["GB/s"]
-    # the towers against the bf16 MFMA peak: T1 = forward + backward-data of both towers
-    # (2 x 2 x 2B x sum_l in_l * out_l flop), T2 = weight gradients (2 x 2B x sum_l in_l * out_l)
-    towers = {}
-    if step.towers is not None:
-        macs = sum(i * o for i, o in zip([D] + layers[:-1], layers))
-        t_t1 = time_kernel(lambda: step.towers.fwd_bwd(step.pooled, step.gpooled, step.params, step.labels,
-                                                       step.logits), args.kernel_iters)
-        t_t2 = time_kernel(lambda: step.towers.wgrad(step.loss), args.kernel_iters)
-        for name, t_ms, fl in (("tower_fwd_bwd", t_t1, 8 * B * macs), ("tower_wgrad", t_t2, 4 * B * macs)):
-            tf = fl / t_ms / 1e9
-            towers[name] = {"ms": round(t_ms, 5), "flop": fl, "TFLOP/s": round(tf, 1),
-                            "frac_of_bf16_peak": round(tf / MFMA_BF16_PEAK_TFS, 4)}
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": kern[dom]["bytes"],
-                "kernels": kern, "lookups": nnz, "unique_rows": uniq, "towers_mfma": towers}
+    # ---- per-launch device time inside the step: a second set of graphs over the same batches
+    # with an external-event pair around every launch (event-record nodes on the launching
+    # stream), replayed for the same number of steps
+    nnz, uniq = lookup_stats(step, batches)
+    kern = launch_bytes(step, nnz, uniq)
+    timed = None
+    try:
+        marks = step.capture_timed_pool(batches, steps_per_graph=k)
+        acc, cnt = {}, {}
+        n_done, j = 0, 0
+        while n_done < args.steps:
+            step.pool_graphs[j % len(step.pool_graphs)].replay()
+            torch.cuda.synchronize()
+            for m in marks[j % len(marks)]:
+                for name, (a, b) in m.items():
+                    acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
+                    cnt[name] = cnt.get(name, 0) + 1
+            n_done += k
+            j += 1
+        timed = {name: acc[name] / cnt[name] for name in acc}
+    except Exception as e:  # noqa: BLE001 - timing is reported, never fatal
+        print(f"in-graph event timing unavailable ({e}); per-launch times omitted", file=sys.stderr)
+    roofline = roofline_report(kern, timed, nnz, uniq, step, B)
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(args, num_users, num_items, D, B, layers)

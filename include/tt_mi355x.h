@@ -267,22 +267,67 @@ int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pool
  * <= 128 wide): tower t's input row m is row (cols[t][m] mod num_embeddings[t]) of the table
  * starting at table_rows[t] ([rows][in_dim[t]] fp32, 16-B aligned), zeros when the id is 0
  * (transform_to_torchrec_batch semantics, 03_model_training.py:356-365); the pooled rows are
- * never materialised unless pooled_out (nullable, ld = ldp, columns in_col[t]) is given. */
+ * never materialised unless pooled_out (nullable, ld = ldp, columns in_col[t]) is given.
+ * With dedup_ws (nullable; a tt_dedup workspace) every kept lookup (tower t, row m) is also
+ * inserted as lookup t * B + m with key dedup_tables[t] << 40 | row, ready for
+ * tt_dedup_rowwise_adagrad over gpooled (features t -> columns in_col[t]). */
 int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
                             const int64_t* num_embeddings, const float* const* table_rows,
                             float* pooled_out, int64_t ldp, float* gpooled, const float* params,
                             const void* labels, int label_dtype, float grad_scale, float* logits,
-                            void* workspace, size_t ws_bytes, void* stream);
+                            const int32_t* dedup_tables, void* dedup_ws, size_t dedup_ws_bytes,
+                            int64_t dedup_max_lookups, void* workspace, size_t ws_bytes, void* stream);
+/* T1 for the sharded step (row-wise / table-wise shards, single-hot): tower t's input row m is row
+ * pos[t][m] of rows_in[t] ([*][in_dim[t]] fp32: the rows returned by the owners' all-to-all; -1
+ * -> zeros, a dropped id), and its gradient row dX is written to row pos[t][m] of grad_rows_out[t]
+ * (the buffer the gradient all-to-all sends back to the owners). Replaces the EBC lookup's output
+ * KeyedTensor + the towers (03_model_training.py:417-455) on the sharded path. */
+int tt_tower_fwd_bwd_indexed(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos,
+                             const float* const* rows_in, float* const* grad_rows_out, const float* params,
+                             const void* labels, int label_dtype, float grad_scale, float* logits,
+                             void* workspace, size_t ws_bytes, void* stream);
 /* T2: weight/bias gradients of every layer into the workspace (fixed-order partial slabs), and
  * the mean BCE of the preceding T1 into loss[0] (nullable; fixed-order sum of T1's partials). */
 int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
                    void* stream);
+/* T2 and the embedding backward in ONE launch: tt_tower_wgrad + tt_dedup_rowwise_adagrad (same
+ * arguments as those two calls; emb_B = the dedup's lookups-per-feature B). One launch boundary after
+ * T1 instead of two, no cross-stream join: the tile workgroups (MFMA / L2) and the row-update
+ * workgroups (HBM) share the CUs. */
+int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                   size_t ws_bytes, const tt_table_meta_t* tables, int T,
+                                   const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
+                                   int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
+                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 /* T3: fixed-order reduction of T2's partials, Adam (when do_adam; step_state as tt_adam_step),
  * and the bf16 weight copies for the next T1. grads_out (nullable) receives the gradient. */
 int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
                     float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
                     float weight_decay, int64_t* step_state, int do_adam, float* grads_out,
                     void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a8 (single-hot): two-launch dedup + fused row-wise Adagrad --------------------------------
+ * For single-hot lookups (the fused step's id columns; the sharded step's received ids) this
+ * replaces tt_bwd_prepare(_cols) + tt_bwd_rowwise_adagrad (TBE backward with EXACT_ROWWISE_ADAGRAD,
+ * _apply_optimizer_in_backward(RowWiseAdagrad, ...), 03_model_training.py:791-795) with one insert
+ * launch and one update launch. Lookup i of the step maps to pooled-gradient row
+ * (features[f].out_row + b) * ldg + features[f].out_offset with f = i / B, b = i % B.
+ * The workspace is clean between steps (the update resets what the insert wrote); initialise it
+ * once with tt_dedup_workspace_init (synchronises `stream`). 64-B aligned. */
+size_t tt_dedup_workspace_bytes(int64_t max_lookups);
+int tt_dedup_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
+/* lookups i = f * B + b: key (table of feature f, cols[f][b] mod num_embeddings[f]); id 0 dropped */
+int tt_dedup_insert_cols(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F, int64_t B,
+                         const void* const* cols, int id_dtype, const int64_t* num_embeddings, void* workspace,
+                         size_t ws_bytes, int64_t max_lookups, void* stream);
+/* lookups i = s * seg_capacity + k, k < counts[s]: keys[i] = local table << 40 | local row */
+int tt_dedup_insert_segments(const int64_t* keys, const int32_t* counts, int64_t num_segments, int64_t seg_capacity,
+                             void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
+/* sum every unique row's gradient rows (ascending lookup order; rows with > 14 lookups: fixed
+ * 8-way interleave), then s += mean(G^2), w -= lr * G / (sqrt(s) + eps). D % 4 == 0, D <= 128. */
+int tt_dedup_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
+                             int64_t B, const float* grad, int64_t ldg, float* weights, float* state, float lr,
+                             float eps, void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
 
 /* ---- a9: Adam on the flat dense-parameter buffer (torch.optim.Adam, amsgrad=False) ------------ */
 

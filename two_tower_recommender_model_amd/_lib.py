@@ -116,6 +116,14 @@ SIGNATURES = {
     "tt_adam_step": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _vp, _vp]),
     "tt_pooled_fwd_cols": (_int, [_vp, _ptm, _int, _pfm, _int, _i64, _pvp, _int, _pi64, _vp, _i64, _vp]),
     "tt_bwd_prepare_cols": (_int, [_ptm, _int, _pfm, _int, _i64, _pvp, _int, _pi64, _vp, _sz, _i64, _vp]),
+    "tt_dedup_workspace_bytes": (_sz, [_i64]),
+    "tt_dedup_workspace_init": (_int, [_vp, _sz, _i64, _vp]),
+    "tt_dedup_insert_cols": (_int, [_ptm, _int, _pfm, _int, _i64, _pvp, _int, _pi64, _vp, _sz, _i64, _vp]),
+    "tt_dedup_insert_segments": (_int, [_vp, _vp, _i64, _i64, _vp, _sz, _i64, _vp]),
+    "tt_dedup_rowwise_adagrad": (
+        _int,
+        [_ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
+    ),
     "tt_tower_num_params": (C.c_int64, [_psh]),
     "tt_tower_workspace_bytes": (_sz, [_psh, _i64]),
     "tt_tower_workspace_init": (_int, [_psh, _i64, _vp, _sz, _vp]),
@@ -123,7 +131,17 @@ SIGNATURES = {
     "tt_tower_wgrad": (_int, [_psh, _i64, _vp, _vp, _sz, _vp]),
     "tt_tower_fwd_bwd_gather": (
         _int,
-        [_psh, _i64, _pvp, _int, _pi64, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
+        [_psh, _i64, _pvp, _int, _pi64, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _pi32, _vp, _sz, _i64,
+         _vp, _sz, _vp],
+    ),
+    "tt_tower_wgrad_rowwise_adagrad": (
+        _int,
+        [_psh, _i64, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64,
+         _vp],
+    ),
+    "tt_tower_fwd_bwd_indexed": (
+        _int,
+        [_psh, _i64, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
     ),
     "tt_tower_update": (
         _int,
@@ -154,6 +172,12 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_update",
     "tt_pooled_fwd_cols",
     "tt_bwd_prepare_cols",
+    "tt_dedup_workspace_init",
+    "tt_dedup_insert_cols",
+    "tt_dedup_insert_segments",
+    "tt_dedup_rowwise_adagrad",
+    "tt_tower_fwd_bwd_indexed",
+    "tt_tower_wgrad_rowwise_adagrad",
 ]
 
 _lib = None

@@ -46,6 +46,8 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_dot_bce_fwd_bwd, tt_adam_step, tt_tower_workspace_init, tt_tower_fwd_bwd, tt_tower_wgrad,
 // tt_tower_update
 // tt_pooled_fwd_cols, tt_bwd_prepare_cols
-int tt_num_entry_points(void) { return 22; }
+// tt_dedup_workspace_init, tt_dedup_insert_cols, tt_dedup_insert_segments, tt_dedup_rowwise_adagrad
+// tt_tower_fwd_bwd_indexed, tt_tower_wgrad_rowwise_adagrad
+int tt_num_entry_points(void) { return 28; }
 
 }  // extern "C"

@@ -1,0 +1,319 @@
+// Single-pass dedup of single-hot lookups for the fused row-wise Adagrad (gfx950).
+//
+// A lookup i (one id of a single-hot bag) is inserted into an open-addressing table of 64-B slots
+// {word = key << 18 | count, items[14]}: a first-time key claims a free slot with ONE returning
+// 64-bit CAS that also sets its count to 1 (the common case: a single atomic round trip); a
+// repeated key finds its slot and takes a position with one atomicAdd on the same word. Positions
+// < 14 store the lookup index inline, so after the insert pass every unique (table, row) owns ONE
+// cache line holding everything its update needs, read in one hop. Rows looked up more than 14
+// times in a step ("hot") are listed by the lookup that takes position 14 and are summed by a
+// workgroup that finds their lookups by scanning the per-lookup key array in index order.
+#pragma once
+
+#include "tt_common.h"
+
+namespace tt {
+
+constexpr uint64_t DD_EMPTY = ~0ull;
+constexpr int DD_TABLE_SHIFT = 40;  // key = table << 40 | row (table < 64, rows < 2^40 per shard)
+constexpr int DD_CNT_BITS = 18;     // slot word = key << 18 | count; a step has < 2^18 lookups
+constexpr uint64_t DD_CNT_MASK = (1ull << DD_CNT_BITS) - 1;
+constexpr int DD_INL = 14;          // lookups stored inline per slot
+
+struct __attribute__((aligned(64))) DSlot {
+  uint64_t word;  // DD_EMPTY when free, else key << 18 | lookups of this key in the step
+  int32_t item[DD_INL];
+};
+
+struct DedupWs {
+  DSlot* slots;    // [cap], clean (key EMPTY, cnt 0) between steps
+  uint64_t* lkey;  // [L] key of each lookup (DD_EMPTY: dropped / padding)
+  int32_t* hot;    // [L / (DD_INL + 1) + 1] slots with cnt > DD_INL
+  int32_t* ctr;    // [4] {hot rows, hot-workgroup ticket, -, -}
+  int64_t cap;
+  int64_t L;
+  int32_t hot_cap;  // entries of `hot` (a step inserts <= L lookups: <= L / 14 hot rows)
+};
+
+__device__ __forceinline__ uint64_t dd_mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// Insert in two halves so a kernel can issue the claiming CAS early and finish late (the tower
+// kernel overlaps the CAS round trip with its MFMA chain): begin stores the lookup's key and
+// issues one returning CAS on the key's home slot; finish resolves the result (claimed -> position
+// 0; same key -> atomicAdd for a position; other key -> linear probing) and files the lookup.
+struct DdPend {
+  uint64_t key;
+  uint64_t prev;
+  uint64_t h;
+};
+
+__device__ __forceinline__ void dd_insert_begin(const DedupWs& ws, uint64_t key, int32_t i, DdPend& p) {
+  ws.lkey[i] = key;
+  p.key = key;
+  p.prev = 0;
+  p.h = 0;
+  if (key == DD_EMPTY) return;
+  p.h = dd_mix64(key) & ((uint64_t)ws.cap - 1);
+  p.prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.slots[p.h].word), (unsigned long long)DD_EMPTY,
+                     (unsigned long long)((key << DD_CNT_BITS) | 1ull));
+}
+
+__device__ __forceinline__ void dd_insert_finish(const DedupWs& ws, const DdPend& p, int32_t i) {
+  if (p.key == DD_EMPTY) return;
+  const uint64_t mask = (uint64_t)ws.cap - 1;
+  const uint64_t mine = (p.key << DD_CNT_BITS) | 1ull;
+  uint64_t h = p.h, prev = p.prev;
+  int k;
+  while (true) {
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(&ws.slots[h].word);
+    if (prev == DD_EMPTY) {
+      k = 0;
+      break;
+    }
+    if ((prev >> DD_CNT_BITS) == p.key) {
+      k = (int)(atomicAdd(w, 1ull) & DD_CNT_MASK);
+      break;
+    }
+    h = (h + 1) & mask;
+    prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.slots[h].word), (unsigned long long)DD_EMPTY,
+                     (unsigned long long)mine);
+  }
+  if (k < DD_INL) {
+    ws.slots[h].item[k] = i;
+  } else if (k == DD_INL) {
+    const int q = atomicAdd(&ws.ctr[0], 1);
+    if (q < ws.hot_cap) ws.hot[q] = (int32_t)h;  // bound holds unless inserts skip an update
+  }
+}
+
+// lookup i of the step has key `key` (DD_EMPTY: the lookup contributes nothing)
+__device__ __forceinline__ void dd_insert(const DedupWs& ws, uint64_t key, int32_t i) {
+  DdPend p;
+  dd_insert_begin(ws, key, i, p);
+  dd_insert_finish(ws, p, i);
+}
+
+size_t dedup_layout(void* base, int64_t L, DedupWs* w);
+
+// arguments of the update launch (dd_adagrad_kernel, or a role of a combined launch)
+struct DdUpdateArgs {
+  EmbMeta m;           // tables; features map lookup i = f * B + b to its gradient row
+  const float* grad;   // pooled gradient, row (features[f].out_row + b), cols features[f].out_offset..
+  int64_t ldg;
+  int64_t n;           // lookups inserted this step (F * B)
+  float* weights;
+  float* state;
+  float lr, eps;
+  DedupWs ws;
+  int hot_wgs;         // workgroups of the hot role; the slot role has ws.cap / 8 more
+};
+
+struct GradMap {
+  const float* g;
+  int64_t ldg;
+  int64_t B;
+  const tt_feature_meta_t* feats;
+  __device__ __forceinline__ const float* row(int i) const {
+    const int f = (int)(i / B);
+    const int64_t b = i - (int64_t)f * B;
+    return g + (feats[f].out_row + b) * ldg + feats[f].out_offset;
+  }
+};
+
+template <int W>
+__device__ __forceinline__ int dd_bitonic(int v) {
+  const int lane = threadIdx.x & (W - 1);
+#pragma unroll
+  for (int k = 2; k <= W; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int o = __shfl_xor(v, j, 64);
+      const bool up = (lane & k) == 0;
+      const bool lower = (lane & j) == 0;
+      const int mn = v < o ? v : o, mx = v < o ? o : v;
+      v = (lower == up) ? mn : mx;
+    }
+  }
+  return v;
+}
+
+constexpr int DD_HOT_CH = 4096;  // lookups scanned per pass of a hot workgroup
+
+__device__ __forceinline__ void dd_hot_role(const EmbMeta& m, const GradMap& gm, int64_t n,
+                                            float* __restrict__ weights, float* __restrict__ state, float lr,
+                                            float eps, const DedupWs& ws, int hot_wgs, int bid) {
+  __shared__ int list[DD_HOT_CH];
+  __shared__ int wtot[4];
+  __shared__ f32x4v part[8][32];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = tid >> 5, hl = tid & 31;
+  const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
+  for (int j = bid; j < nh; j += hot_wgs) {
+    const int32_t h = ws.hot[j];
+    const uint64_t key = ws.slots[h].word >> DD_CNT_BITS;
+    const int t = (int)(key >> DD_TABLE_SHIFT);
+    const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
+    const tt_table_meta_t tm = m.tables[t];
+    const int D = tm.dim;
+    const bool col_ok = hl * 4 < D;
+    f32x4v acc = (f32x4v)(0.f);
+    int seen = 0;  // matches before this pass (global position of list[0])
+    for (int64_t c0 = 0; c0 < n; c0 += DD_HOT_CH) {
+      // thread tid covers lookups [c0 + 16 tid, c0 + 16 tid + 16): 16-bit match mask
+      const int64_t i0 = c0 + 16 * tid;
+      uint32_t mask = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (i0 + q < n && ws.lkey[i0 + q] == key) mask |= 1u << q;
+      const int mc = __popc(mask);
+      int inc = mc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) wtot[wid] = inc;
+      __syncthreads();
+      int base = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if (w < wid) base += wtot[w];
+        total += wtot[w];
+      }
+      int pos = base + inc - mc;
+      for (int q = 0; q < 16; ++q)
+        if (mask & (1u << q)) list[pos++] = (int)(i0 + q);
+      __syncthreads();
+      // group grp takes global positions == grp (mod 8), ascending
+      int p = (grp - (seen & 7) + 8) & 7;
+      for (; p + 8 < total; p += 16) {
+        f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
+        if (col_ok) {
+          x0 = *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
+          x1 = *reinterpret_cast<const f32x4v*>(gm.row(list[p + 8]) + hl * 4);
+        }
+        acc += x0;
+        acc += x1;
+      }
+      if (p < total && col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
+      seen += total;
+      __syncthreads();
+    }
+    part[grp][hl] = acc;
+    __syncthreads();
+    if (wid == 0) {
+      f32x4v g = part[0][hl];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) g += part[q][hl];
+      float sq = col_ok ? g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3] : 0.f;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+      if (lane < 32) {
+        float* wrow = weights + tm.weight_offset + r * D;
+        float* srow = state + tm.state_offset + r;
+        const float snew = *srow + sq / (float)D;
+        const float stdv = sqrtf(snew) + eps;
+        if (col_ok) {
+          f32x4v wv = *reinterpret_cast<const f32x4v*>(wrow + hl * 4);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
+          *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          *srow = snew;
+          ws.slots[h].word = DD_EMPTY;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int tk = atomicAdd(&ws.ctr[1], 1);
+    if (tk == hot_wgs - 1) {
+      atomicExch(&ws.ctr[0], 0);
+      atomicExch(&ws.ctr[1], 0);
+    }
+  }
+}
+
+// host: validate + fill the update launch's arguments; *grid = its workgroup count
+int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F, int64_t B,
+                      const float* grad, int64_t ldg, float* weights, float* state, float lr, float eps,
+                      void* workspace, size_t ws_bytes, int64_t max_lookups, DdUpdateArgs& a, int64_t* grid);
+
+// One workgroup (256 threads) of the update launch: bid < hot_wgs -> hot role, else 8 slots.
+__device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) {
+  const EmbMeta& m = a.m;
+  const DedupWs& ws = a.ws;
+  float* __restrict__ weights = a.weights;
+  float* __restrict__ state = a.state;
+  const float lr = a.lr, eps = a.eps;
+  const GradMap gm{a.grad, a.ldg, m.B, m.features};
+  if (bid < a.hot_wgs) {
+    dd_hot_role(m, gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int hl = lane & 31, hb = lane & 32;
+  const int64_t h = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
+  // the grid covers exactly cap slots (cap is a multiple of 1024): every half-wave has a slot
+  DSlot* sp = ws.slots + h;
+  const int dw = hl < 16 ? reinterpret_cast<const int32_t*>(sp)[hl] : 0;
+  const uint64_t word = ((uint64_t)(uint32_t)__shfl(dw, hb + 1, 64) << 32) | (uint32_t)__shfl(dw, hb, 64);
+  const uint64_t key = word >> DD_CNT_BITS;
+  const int cnt = (int)(word & DD_CNT_MASK);
+  const int item = __shfl(dw, hb + 2 + (hl < DD_INL ? hl : 0), 64);
+  // hot slots (reset by the hot role, one 8-B store) are never taken here
+  const bool active = word != DD_EMPTY && cnt <= DD_INL;
+  const int t = active ? (int)(key >> DD_TABLE_SHIFT) : 0;
+  const int64_t r = active ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
+  const tt_table_meta_t tm = m.tables[t];
+  const int D = tm.dim;
+  const bool col_ok = active && hl * 4 < D;
+  float* wrow = weights + tm.weight_offset + r * D;
+  float* srow = state + tm.state_offset + r;
+  f32x4v wv = col_ok ? *reinterpret_cast<const f32x4v*>(wrow + hl * 4) : (f32x4v)(0.f);
+  const float s_old = active ? *srow : 0.f;
+  const int c = active ? cnt : 0;
+  const int cmax = max(c, __shfl_xor(c, 32, 64));
+  int mine = hl < c ? item : 0x7fffffff;
+  if (cmax > 1) mine = dd_bitonic<32>(mine);
+  f32x4v g = (f32x4v)(0.f);
+  for (int i = 0; i < cmax; i += 2) {
+    const int b0 = __shfl(mine, hb + i, 64);
+    const int b1 = __shfl(mine, hb + min(i + 1, 31), 64);
+    f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
+    if (col_ok && i < c) x0 = *reinterpret_cast<const f32x4v*>(gm.row(b0) + hl * 4);
+    if (col_ok && i + 1 < c) x1 = *reinterpret_cast<const f32x4v*>(gm.row(b1) + hl * 4);
+    if (i < c) g += x0;
+    if (i + 1 < c) g += x1;
+  }
+  float sq = g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+  if (active) {
+    const float snew = s_old + sq / (float)D;
+    const float stdv = sqrtf(snew) + eps;
+    if (col_ok) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
+      *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
+    }
+    if (hl == 0) {
+      *srow = snew;
+      sp->word = DD_EMPTY;
+    }
+  }
+}
+
+
+
+}  // namespace tt

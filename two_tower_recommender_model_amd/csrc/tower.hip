@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "tt_common.h"
+#include "dedup.h"
 
 namespace tt {
 
@@ -67,6 +68,16 @@ struct TowerArgs {
   int64_t gmod[2];
   int gid_dtype;
   float* pooled_out;    // nullable: the gathered rows are also written here (ld = ldp)
+  // dedup insert of the gathered lookups (lookup i = t * B + m, key = dd_table[t] << 40 | row)
+  DedupWs dd;
+  int dd_on;
+  int dd_table[2];
+  // indexed gather (sharded step, tt_tower_fwd_bwd_indexed): tower t's input row m is row
+  // gpos[t][m] of gsrc[t] ([*][in_dim[t]] fp32; -1 -> zeros) and its dX row goes to row gpos[t][m]
+  // of gdst[t] instead of gpooled
+  const int32_t* gpos[2];
+  const float* gsrc[2];
+  float* gdst[2];
 };
 
 __device__ __forceinline__ float lbl(const void* p, int dt, int64_t i) {
@@ -427,20 +438,45 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
   f32x4 xv[4];
   const int nxv = in / 32;  // f32x4 loads per thread: TR rows x in/4 vectors over 256 threads
   const bool gather = a.gcol[t] != nullptr;
-  if (gather) {
+  const bool indexed = a.gpos[t] != nullptr;
+  int32_t rpos[4];  // indexed: the source/destination row of each xv
+  uint64_t dkey[4];  // gather + dedup: the key of the (tower, row) lookup this thread files (c4 == 0)
+  bool down[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rpos[i] = -1;
+    dkey[i] = DD_EMPTY;
+    down[i] = false;
+  }
+  if (gather || indexed) {
     // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros
     const float* src[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       src[i] = nullptr;
+      rpos[i] = -1;
+      down[i] = false;
+      dkey[i] = DD_EMPTY;
       if (i < nxv) {
         const int e = tt + 256 * i;
         const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
         const int64_t gm = m0 + row;
+        uint64_t key = DD_EMPTY;
         if (gm < B) {
-          const int64_t id = load_id(a.gcol[t], a.gid_dtype, gm);
-          if (id != 0) src[i] = a.gtab[t] + py_mod64(id, a.gmod[t]) * in + c4;
+          if (indexed) {
+            rpos[i] = a.gpos[t][gm];
+            if (rpos[i] >= 0) src[i] = a.gsrc[t] + (int64_t)rpos[i] * in + c4;
+          } else {
+            const int64_t id = load_id(a.gcol[t], a.gid_dtype, gm);
+            if (id != 0) {
+              const int64_t r = py_mod64(id, a.gmod[t]);
+              src[i] = a.gtab[t] + r * in + c4;
+              key = ((uint64_t)a.dd_table[t] << DD_TABLE_SHIFT) | (uint64_t)r;
+            }
+          }
         }
+        dkey[i] = key;
+        down[i] = a.dd_on && c4 == 0 && gm < B;
       }
     }
 #pragma unroll
@@ -469,6 +505,14 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
     bias0[j] = c < W0 ? a.params[a.boff[t][0] + c] : 0.f;
     bias1[j] = c < W1 ? a.params[a.boff[t][1] + c] : 0.f;
   }
+  // the label of the row this thread scores in phase 3 (loaded now: no global load after the CAS)
+  const int64_t lrow = m0 + (threadIdx.x >> 4);
+  const float ylab = lrow < B ? lbl(a.labels, a.label_dtype, lrow) : 0.f;
+  // dedup: the claiming CAS of every lookup goes out now and is resolved at the very end
+  DdPend pend[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (down[i]) dd_insert_begin(a.dd, dkey[i], (int32_t)(t * B + m0 + (tt + 256 * i) / (in / 4)), pend[i]);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i < nxv) {
@@ -544,7 +588,7 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
     const int64_t gm = m0 + row;
     float lo = 0.f, dl = 0.f;
     if (gm < B) {
-      const float x = d, y = lbl(a.labels, a.label_dtype, gm);
+      const float x = d, y = ylab;
       const float lsig = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
       lo = (1.f - y) * x - lsig;
       dl = (1.f / (1.f + expf(-x)) - y) / (float)B * a.grad_scale;
@@ -633,11 +677,21 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
       const int e = tt + 256 * i;
       const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
       const int64_t gm = m0 + row;
-      if (gm < B)
-        *reinterpret_cast<f32x4*>(a.gpooled + gm * a.ldp + a.s.in_col[t] + c4) =
-            *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
+      float* dst = nullptr;
+      if (gm < B) {
+        if (indexed)
+          dst = rpos[i] >= 0 ? a.gdst[t] + (int64_t)rpos[i] * in + c4 : nullptr;
+        else
+          dst = a.gpooled + gm * a.ldp + a.s.in_col[t] + c4;
+      }
+      if (dst) *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
     }
   }
+  // ---- 8. dedup: resolve the CASes issued at entry (the row-wise Adagrad launch that follows
+  // reads the slots)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (down[i]) dd_insert_finish(a.dd, pend[i], (int32_t)(t * B + m0 + (tt + 256 * i) / (in / 4)));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -670,9 +724,10 @@ struct WgradArgs {
   const float* loss_part;  // [nwg] T1 partials
   float* loss;             // nullable
   int nbias;
+  int64_t tiles_off;       // byte offset of the tile list in the workspace (host side)
 };
 
-__global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const WgradTile* __restrict__ tiles) {
+__device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile* __restrict__ tiles, int bid) {
   // workgroups [0, ntiles * S): one (32x32 tile of dW, batch slice) each, its 4 waves on 4
   // consecutive quarters of the slice, reduced through LDS in wave order -> one slab row.
   // Workgroups beyond: one wave per bias output (+ one for the loss).
@@ -680,10 +735,10 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int64_t nwg_tiles = (int64_t)a.ntiles * a.S;
-  if ((int64_t)blockIdx.x >= nwg_tiles) {
+  if ((int64_t)bid >= nwg_tiles) {
     // bias gradient of one output n of (t, l): sum of the T1 workgroups' partials, lanes strided
     // over workgroups, then a fixed butterfly -> slab[0]
-    int64_t b = ((int64_t)blockIdx.x - nwg_tiles) * 4 + wid;
+    int64_t b = ((int64_t)bid - nwg_tiles) * 4 + wid;
     if (b == a.nbias) {  // the scalar loss: T1's per-workgroup partials in a fixed order
       if (a.loss) {
         float s = 0.f;
@@ -706,8 +761,8 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
       }
     return;
   }
-  const int s = (int)(blockIdx.x / a.ntiles);
-  const WgradTile tl = tiles[blockIdx.x % a.ntiles];
+  const int s = (int)(bid / a.ntiles);
+  const WgradTile tl = tiles[bid % a.ntiles];
   const int64_t B = a.B;
   const __bf16* Z = a.dzt + ((int64_t)tl.t * MAXL + tl.l) * MAXW * B;  // [n][B]
   const __bf16* A = tl.l == 0 ? a.xt + (int64_t)tl.t * a.in_max * B
@@ -799,6 +854,22 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
         const int k = tl.k0 + j * 16 + r;
         dst[(int64_t)n * K + k] = acc[i][j][rr];
       }
+}
+
+__global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const WgradTile* __restrict__ tiles) {
+  wgrad_block(a, tiles, (int)blockIdx.x);
+}
+
+// T2 + the embedding path's fused row-wise Adagrad (dedup.h) in ONE launch: workgroups
+// [0, n_t2) are T2's, the rest run dd_update_block. Both read only what T1 wrote, so one launch
+// boundary (and no cross-stream join) separates them from T1, and the MFMA/L2-bound tiles overlap
+// the HBM-bound row updates on the same CUs.
+__global__ void __launch_bounds__(256) tower_wgrad_dedup_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
+                                                                DdUpdateArgs d, int n_t2) {
+  if ((int)blockIdx.x < n_t2)
+    wgrad_block(a, tiles, (int)blockIdx.x);
+  else
+    dd_update_block(d, (int)blockIdx.x - n_t2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1013,7 +1084,7 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if ((!pooled && !a.gcol[0]) || !gpooled || !params || !labels || !logits)
+  if ((!pooled && !a.gcol[0] && !a.gpos[0]) || (!gpooled && !a.gpos[0]) || !params || !labels || !logits)
     return fail(TT_EINVAL, "tower: null pointer");
   if (label_dtype != TT_I32 && label_dtype != TT_I64 && label_dtype != TT_F32)
     return fail(TT_EINVAL, "tower: labels must be int32/int64/float32");
@@ -1051,7 +1122,8 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   const int i0 = shape->in_dim[0], i1 = shape->in_dim[1], w0 = shape->width[0], w1 = shape->width[1];
   const dim3 g(L.nwg), b512(512);
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
-  if (a.gcol[0] && !two) return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
+  if ((a.gcol[0] || a.gpos[0]) && !two)
+    return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
   if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
     tower_l2_kernel<128, 128, 64><<<g, b512, 0, as_stream(stream)>>>(a);
   else if (two && i0 == 64 && i1 == 64 && w0 == 128 && w1 == 64)
@@ -1062,46 +1134,15 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
     tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_fwd_bwd");
 }
-}  // namespace tt
 
-extern "C" {
-
-int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp, float* gpooled,
-                     const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
-                     void* workspace, size_t ws_bytes, void* stream) {
-  TowerArgs a{};
-  return launch_t1(shape, B, a, pooled, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
-                   ws_bytes, stream);
-}
-
-int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
-                            const int64_t* num_embeddings, const float* const* table_rows, float* pooled_out,
-                            int64_t ldp, float* gpooled, const float* params, const void* labels, int label_dtype,
-                            float grad_scale, float* logits, void* workspace, size_t ws_bytes, void* stream) {
-  if (!cols || !num_embeddings || !table_rows) return fail(TT_EINVAL, "tower_gather: null pointer");
-  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_gather: ids must be int32/int64");
-  TowerArgs a{};
-  for (int t = 0; t < 2; ++t) {
-    if (!cols[t] || !table_rows[t] || num_embeddings[t] < 1) return fail(TT_EINVAL, "tower_gather: bad column");
-    if (reinterpret_cast<uintptr_t>(table_rows[t]) & 15) return fail(TT_EINVAL, "tower_gather: rows not 16-B aligned");
-    a.gcol[t] = cols[t];
-    a.gtab[t] = table_rows[t];
-    a.gmod[t] = num_embeddings[t];
-  }
-  a.gid_dtype = id_dtype;
-  a.pooled_out = pooled_out;
-  return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
-                   ws_bytes, stream);
-}
-
-int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
-                   void* stream) {
+// T2 arguments from the shape + workspace (shared by tt_tower_wgrad and the combined launch)
+static int wgrad_args(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                      WgradArgs& a, int64_t* wgs) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
   char* ws = reinterpret_cast<char*>(workspace);
-  WgradArgs a{};
   a.xt = reinterpret_cast<const __bf16*>(ws + L.o_xt);
   a.act = reinterpret_cast<const __bf16*>(ws + L.o_act);
   a.dzt = reinterpret_cast<const __bf16*>(ws + L.o_dzt);
@@ -1129,10 +1170,106 @@ int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* 
   a.loss_part = reinterpret_cast<const float*>(ws + L.o_losspart);
   a.loss = loss;
   a.nbias = nbias;
-  const int64_t wgs = (int64_t)L.ntiles * L.S + ceil_div(nbias + 1, 4);
+  a.tiles_off = (int64_t)L.o_tiles;
+  *wgs = (int64_t)L.ntiles * L.S + ceil_div(nbias + 1, 4);
+  return TT_OK;
+}
+}  // namespace tt
+
+extern "C" {
+
+int tt_tower_fwd_bwd(const tt_tower_shape_t* shape, int64_t B, const float* pooled, int64_t ldp, float* gpooled,
+                     const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
+                     void* workspace, size_t ws_bytes, void* stream) {
+  TowerArgs a{};
+  return launch_t1(shape, B, a, pooled, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
+                   ws_bytes, stream);
+}
+
+int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
+                            const int64_t* num_embeddings, const float* const* table_rows, float* pooled_out,
+                            int64_t ldp, float* gpooled, const float* params, const void* labels, int label_dtype,
+                            float grad_scale, float* logits, const int32_t* dedup_tables, void* dedup_ws,
+                            size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* workspace, size_t ws_bytes,
+                            void* stream) {
+  if (!cols || !num_embeddings || !table_rows) return fail(TT_EINVAL, "tower_gather: null pointer");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_gather: ids must be int32/int64");
+  TowerArgs a{};
+  for (int t = 0; t < 2; ++t) {
+    if (!cols[t] || !table_rows[t] || num_embeddings[t] < 1) return fail(TT_EINVAL, "tower_gather: bad column");
+    if (reinterpret_cast<uintptr_t>(table_rows[t]) & 15) return fail(TT_EINVAL, "tower_gather: rows not 16-B aligned");
+    a.gcol[t] = cols[t];
+    a.gtab[t] = table_rows[t];
+    a.gmod[t] = num_embeddings[t];
+  }
+  a.gid_dtype = id_dtype;
+  a.pooled_out = pooled_out;
+  if (dedup_ws) {
+    if (!dedup_tables) return fail(TT_EINVAL, "tower_gather: dedup needs the key table of each tower");
+    if (dedup_max_lookups < 2 * B || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+        dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
+        (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
+      return fail(TT_ECAPACITY, "tower_gather: dedup workspace too small / misaligned");
+    for (int t = 0; t < 2; ++t) {
+      if (dedup_tables[t] < 0 || dedup_tables[t] >= TT_MAX_TABLES || num_embeddings[t] >= (1ll << DD_TABLE_SHIFT))
+        return fail(TT_EINVAL, "tower_gather: bad dedup table");
+      a.dd_table[t] = dedup_tables[t];
+    }
+    dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
+    a.dd_on = 1;
+  }
+  return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
+                   ws_bytes, stream);
+}
+
+int tt_tower_fwd_bwd_indexed(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos,
+                             const float* const* rows_in, float* const* grad_rows_out, const float* params,
+                             const void* labels, int label_dtype, float grad_scale, float* logits, void* workspace,
+                             size_t ws_bytes, void* stream) {
+  if (!pos || !rows_in || !grad_rows_out) return fail(TT_EINVAL, "tower_indexed: null pointer");
+  TowerArgs a{};
+  for (int t = 0; t < 2; ++t) {
+    if (!pos[t] || !rows_in[t] || !grad_rows_out[t]) return fail(TT_EINVAL, "tower_indexed: null pointer");
+    if ((reinterpret_cast<uintptr_t>(rows_in[t]) & 15) || (reinterpret_cast<uintptr_t>(grad_rows_out[t]) & 15))
+      return fail(TT_EINVAL, "tower_indexed: rows not 16-B aligned");
+    a.gpos[t] = pos[t];
+    a.gsrc[t] = rows_in[t];
+    a.gdst[t] = grad_rows_out[t];
+  }
+  return launch_t1(shape, B, a, nullptr,
+                   std::max(shape->in_col[0] + shape->in_dim[0], shape->in_col[1] + shape->in_dim[1]), nullptr, params, labels, label_dtype,
+                   grad_scale, logits, workspace, ws_bytes, stream);
+}
+
+int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                   void* stream) {
+  WgradArgs a{};
+  int64_t wgs = 0;
+  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
+  if (rc) return rc;
   tower_wgrad_kernel<<<dim3((unsigned)wgs), dim3(256), 0, as_stream(stream)>>>(
-      a, reinterpret_cast<const WgradTile*>(ws + L.o_tiles));
+      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off));
   return check_launch("tower_wgrad");
+}
+
+int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                   size_t ws_bytes, const tt_table_meta_t* tables, int T,
+                                   const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
+                                   int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
+                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+  WgradArgs a{};
+  int64_t wgs = 0;
+  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
+  if (rc) return rc;
+  DdUpdateArgs d{};
+  int64_t dd_grid = 0;
+  rc = dedup_update_args(tables, T, features, F, emb_B, grad, ldg, weights, state, lr, eps, dedup_ws, dedup_ws_bytes,
+                         dedup_max_lookups, d, &dd_grid);
+  if (rc) return rc;
+  if (wgs + dd_grid > INT32_MAX) return fail(TT_EINVAL, "tower_wgrad_rowwise_adagrad: grid too large");
+  tower_wgrad_dedup_kernel<<<dim3((unsigned)(wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
+      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), d, (int)wgs);
+  return check_launch("tower_wgrad_rowwise_adagrad");
 }
 
 int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,

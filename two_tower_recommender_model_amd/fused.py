@@ -31,14 +31,21 @@ class FusedTwoTowerStep:
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
                  overlap_prepare: bool = True, precision: str = "bf16", fused_towers: bool = True,
                  kjt_mode: str = "cols", overlap_towers: bool = True, fuse_gather: bool = True,
-                 materialize_pooled: bool = False):
+                 materialize_pooled: bool = False, dedup: str = "single", combined_bwd: bool = True):
         """One table per feature (feature f -> table f), features ordered as the KJT keys.
         precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode).
         overlap_prepare / overlap_towers: run the dedup prepare / the towers' weight-gradient and
         Adam kernels on side streams (False: everything in order on the caller's stream).
         fuse_gather: with single-hot columns, one key per tower and two-layer towers, the EBC
         forward runs inside the tower kernel (rows gathered straight into its LDS tile); the
-        pooled rows are then written to ``self.pooled`` only when ``materialize_pooled``."""
+        pooled rows are then written to ``self.pooled`` only when ``materialize_pooled``.
+        dedup: "single" — single-hot columns use the two-launch dedup (csrc/dedup.hip: the insert
+        fused into the tower kernel, one update launch); "kjt" — the KJT-form hash/scan/scatter
+        kernels (always used in kjt_mode "kjt").
+        combined_bwd: with the fused gather and the single-hot dedup, run the whole step on ONE
+        stream as three launches — T1 (gather + towers + dedup insert), T2 + row-wise Adagrad in
+        one launch, T3 (Adam) — instead of side streams (cross-stream joins inside a HIP graph
+        cost several microseconds each)."""
         self.device = torch.device(device)
         self.precision = precision
         if kjt_mode not in ("cols", "kjt"):
@@ -135,7 +142,16 @@ class FusedTwoTowerStep:
             assert self.towers.num_params == self.params.numel()
             self.side2 = torch.cuda.Stream(device=dev) if overlap_towers else None
             self.sync_weights()
+        if dedup not in ("single", "kjt"):
+            raise _lib.TTError("dedup must be 'single' or 'kjt'")
+        self.dedup_single = dedup == "single" and kjt_mode == "cols" and max(self.dims) <= 128 and \
+            all(d % 4 == 0 for d in self.dims)
+        if self.dedup_single:
+            self.tables.ensure_dedup_workspace(F * B)
         self.materialize_pooled = bool(materialize_pooled)
+        self.combined_bwd = bool(combined_bwd)
+        # in-graph kernel timing (bench): while a list, step() records an event pair per launch
+        self._timing: Optional[list] = None
         self.gather = (fuse_gather and self.towers is not None and kjt_mode == "cols" and self.F == 2
                        and self.qf == [0] and self.cf == [1] and len(self.layer_sizes) == 2
                        and max(self.dims) <= 128)
@@ -204,26 +220,46 @@ class FusedTwoTowerStep:
                                        self.lpk)
             prepare = lambda: self.tables.bwd_prepare(self.values, self.offsets, B, max_lookups=F * B)  # noqa: E731
             self.offsets_used = self.offsets
+        elif self.dedup_single:
+            # single-hot columns, two-launch dedup: the insert runs inside T1 (gather) or here
+            prepare = None if self.gather else (lambda: self.tables.dedup_insert_cols(self.cols, self.num_embeddings))
+            self.offsets_used = None
         else:
             # single-hot columns: the transform (drop id 0, id mod N) is applied inside the kernels
             prepare = lambda: self.tables.bwd_prepare_cols(self.cols, self.num_embeddings)  # noqa: E731
             self.offsets_used = None
-        if self.side is not None:
-            self.side.wait_stream(main)
-            with torch.cuda.stream(self.side):
+        if prepare is not None:
+            if self.side is not None:
+                self.side.wait_stream(main)
+                with torch.cuda.stream(self.side):
+                    prepare()
+            else:
                 prepare()
-        else:
-            prepare()
         if self.gather:
-            # EBC forward fused into T1
+            # EBC forward (and, with the single-hot dedup, its insert) fused into T1
+            if self._timing is not None:
+                self._timing.append({})
+            self._mark("t1", 0)
             self.towers.fwd_bwd_gather(self.cols, self.num_embeddings,
                                        [self.tables.table_view(0), self.tables.table_view(1)], self.gpooled,
                                        self.params, self.labels, self.logits,
-                                       pooled_out=self.pooled if self.materialize_pooled else None)
+                                       pooled_out=self.pooled if self.materialize_pooled else None,
+                                       dedup=self.tables if self.dedup_single else None, dedup_tables=(0, 1))
         elif self.kjt_mode == "kjt":
             self.tables.pooled_fwd(self.values, self.offsets, B, out=self.pooled)
         else:
             self.tables.pooled_fwd_cols(self.cols, self.num_embeddings, out=self.pooled)
+        if self.towers is not None and self.gather and self.dedup_single and self.combined_bwd:
+            # one stream: T1 -> [T2 + fused row-wise Adagrad] -> T3
+            self._mark("t1", 1)
+            self._mark("k2", 0)
+            self.towers.wgrad_rowwise_adagrad(self.loss, self.tables, self.gpooled, B, self.lr_emb, self.eps)
+            self._mark("k2", 1)
+            self._mark("t3", 0)
+            self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
+                               grads_out=self.grads)
+            self._mark("t3", 1)
+            return
         if self.towers is not None:
             # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update
             if not self.gather:
@@ -235,9 +271,9 @@ class FusedTwoTowerStep:
                 self.towers.wgrad(self.loss)
                 self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
                                    grads_out=self.grads)
-            if self.side is not None:
+            if self.side is not None and prepare is not None:
                 main.wait_stream(self.side)
-            self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, B, self.lr_emb, self.eps)
+            self._emb_update()
             if self.side2 is not None:
                 main.wait_stream(self.side2)
             return
@@ -246,10 +282,27 @@ class FusedTwoTowerStep:
         self.dot_bce(self.qy[L - 1], self.cy[L - 1], self.labels, logits=self.logits, loss=self.loss,
                      dq=self.qdy[L - 1], dc=self.cdy[L - 1])
         self._towers_bwd()
-        if self.side is not None:
+        if self.side is not None and prepare is not None:
             main.wait_stream(self.side)
-        self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, B, self.lr_emb, self.eps)
+        self._emb_update()
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, self.lr_dense)
+
+    def _mark(self, name: str, end: int) -> None:
+        """Record the start (end=0) / end (end=1) event of launch `name` of the current step when
+        in-graph timing is on (external events: they become event-record nodes of the graph)."""
+        if self._timing is None or not self._timing:
+            return
+        ev = torch.cuda.Event(enable_timing=True, external=True)
+        ev.record()
+        self._timing[-1].setdefault(name, [None, None])[end] = ev
+
+    def _emb_update(self) -> None:
+        """EBC backward + in-backward RowWiseAdagrad (03_model_training.py:791-795) on the pooled
+        gradient of this step."""
+        if self.dedup_single:
+            self.tables.dedup_rowwise_adagrad(self.gpooled, self.B, self.lr_emb, self.eps)
+        else:
+            self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, self.B, self.lr_emb, self.eps)
 
     def sync_weights(self) -> None:
         """Refresh the fused towers' bf16 weight copies after the fp32 parameters were changed
@@ -286,6 +339,17 @@ class FusedTwoTowerStep:
             self.graph.replay()
         else:
             self.pool_graphs[i % len(self.pool_graphs)].replay()
+
+    def capture_timed_pool(self, batches: Sequence, steps_per_graph: int = 1) -> list:
+        """capture_pool with a start/end event around every launch of every step (bench): returns,
+        per graph, the list of per-step {launch name: [start, end]} event pairs."""
+        self._timing = []
+        try:
+            self.capture_pool(batches, steps_per_graph)
+        finally:
+            marks, self._timing = self._timing, None
+        k = self.steps_per_graph
+        return [marks[j:j + k] for j in range(0, len(marks), k)]
 
     def capture_pool(self, batches: Sequence, steps_per_graph: int = 1) -> None:
         """Graphs over resident input batches ((cols, labels) device tensors), read in place so a

@@ -284,6 +284,58 @@ class TableSet:
                                              self._bwd_ws.numel(), self._bwd_cap, stream_handle(self.device)),
               "bwd_rowwise_adagrad")
 
+    # -- single-hot two-launch dedup + fused row-wise Adagrad (csrc/dedup.hip)
+    def ensure_dedup_workspace(self, max_lookups: int) -> None:
+        max_lookups = max(1, int(max_lookups))
+        if getattr(self, "_dd_ws", None) is not None and max_lookups <= self._dd_cap:
+            return
+        lib = _lib_()
+        nbytes = lib.tt_dedup_workspace_bytes(max_lookups)
+        self._dd_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self._dd_cap = max_lookups
+        check(lib.tt_dedup_workspace_init(ptr(self._dd_ws), nbytes, max_lookups, stream_handle(self.device)),
+              "dedup_workspace_init")
+
+    def dedup_insert_cols(self, cols: Sequence[torch.Tensor], num_embeddings: Sequence[int]) -> None:
+        """Lookup i = f*B + b of the single-hot columns (id 0 dropped, id mod N) joins its row's slot."""
+        _dev(*cols)
+        B = cols[0].numel()
+        self.ensure_dedup_workspace(self.F * B)
+        ne = (C.c_int64 * self.F)(*[int(n) for n in num_embeddings])
+        check(_lib_().tt_dedup_insert_cols(self._tm, self.T, self._fm, self.F, B, ptr_array(list(cols)),
+                                           id_dtype_code(cols[0].dtype), ne, ptr(self._dd_ws), self._dd_ws.numel(),
+                                           self._dd_cap, stream_handle(self.device)), "dedup_insert_cols")
+
+    def dedup_insert_segments(self, keys: torch.Tensor, counts: torch.Tensor, seg_capacity: int) -> None:
+        """Lookup i = s*C + k (k < counts[s]) with key keys[i] = table << 40 | local row."""
+        _dev(keys, counts)
+        if keys.dtype != torch.int64 or counts.dtype != torch.int32:
+            raise _lib.TTError("dedup_insert_segments: int64 keys and int32 counts expected")
+        nseg = counts.numel()
+        if keys.numel() < nseg * seg_capacity:
+            raise _lib.TTError("dedup_insert_segments: keys shorter than segments x capacity")
+        self.ensure_dedup_workspace(nseg * seg_capacity)
+        check(_lib_().tt_dedup_insert_segments(ptr(keys), ptr(counts), nseg, int(seg_capacity), ptr(self._dd_ws),
+                                               self._dd_ws.numel(), self._dd_cap, stream_handle(self.device)),
+              "dedup_insert_segments")
+
+    def dedup_rowwise_adagrad(self, grad: torch.Tensor, B: int, lr: float, eps: float, flat: bool = False) -> None:
+        """Fused row-wise Adagrad over the rows inserted since the last call. Gradient row of lookup
+        i: the KeyedTensor row of (feature i // B, bag i % B) — or, with ``flat``, row i of ``grad``."""
+        _dev(grad)
+        if grad.dtype != torch.float32 or grad.stride(-1) != 1:
+            raise _lib.TTError("dedup_rowwise_adagrad: grad must be fp32 with unit column stride")
+        if flat:
+            fm = (FeatureMeta * 1)()
+            fm[0].table, fm[0].out_offset, fm[0].out_row = 0, 0, 0
+            F = 1
+        else:
+            fm, F = self._fm, self.F
+        check(_lib_().tt_dedup_rowwise_adagrad(self._tm, self.T, fm, F, int(B), ptr(grad), grad.stride(0),
+                                               ptr(self.weights), ptr(self.state), float(lr), float(eps),
+                                               ptr(self._dd_ws), self._dd_ws.numel(), self._dd_cap,
+                                               stream_handle(self.device)), "dedup_rowwise_adagrad")
+
     def bwd_dense(self, grad_out: torch.Tensor, values: torch.Tensor, offsets: torch.Tensor, B: int,
                   grad_weights: torch.Tensor, pooling: int = TT_POOL_SUM) -> None:
         _dev(grad_out, grad_weights)
@@ -484,10 +536,13 @@ class FusedTowers:
                                        ptr(self.ws), self.nbytes, stream_handle(self.device)), "tower_fwd_bwd")
 
     def fwd_bwd_gather(self, cols, num_embeddings, table_rows, gpooled, params, labels, logits,
-                       pooled_out=None, grad_scale: float = 1.0) -> None:
+                       pooled_out=None, grad_scale: float = 1.0, dedup: Optional["TableSet"] = None,
+                       dedup_tables: Sequence[int] = (0, 1)) -> None:
         """T1 with the single-hot EBC forward fused in: tower t's input rows are gathered from the
         table view ``table_rows[t]`` ([rows, in_dim[t]] fp32) by ``cols[t] % num_embeddings[t]``
-        (id 0 -> zeros). ``pooled_out`` (optional) receives the gathered rows."""
+        (id 0 -> zeros). ``pooled_out`` (optional) receives the gathered rows. With ``dedup`` (the
+        TableSet whose dedup workspace the next ``dedup_rowwise_adagrad`` reads) the lookups are
+        also inserted (tower t -> table ``dedup_tables[t]``)."""
         ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}[labels.dtype]
         for t in range(2):
             if table_rows[t].shape[1] != self.shape.in_dim[t] or int(num_embeddings[t]) > table_rows[t].shape[0]:
@@ -495,16 +550,54 @@ class FusedTowers:
         if pooled_out is not None and pooled_out.stride(0) != gpooled.stride(0):
             raise ValueError("pooled_out and the gradient must share a row stride")
         ne = (C.c_int64 * 2)(*[int(n) for n in num_embeddings])
+        dd_tab, dd_ws, dd_bytes, dd_cap = None, None, 0, 0
+        if dedup is not None:
+            dedup.ensure_dedup_workspace(2 * self.B)
+            dd_tab = (C.c_int32 * 2)(*[int(t) for t in dedup_tables])
+            dd_ws, dd_bytes, dd_cap = dedup._dd_ws, dedup._dd_ws.numel(), dedup._dd_cap
         check(_lib_().tt_tower_fwd_bwd_gather(C.byref(self.shape), self.B, ptr_array(list(cols)),
                                               id_dtype_code(cols[0].dtype), ne, ptr_array(list(table_rows)),
                                               ptr(pooled_out), gpooled.stride(0), ptr(gpooled), ptr(params),
-                                              ptr(labels), ldt, float(grad_scale), ptr(logits), ptr(self.ws),
-                                              self.nbytes, stream_handle(self.device)), "tower_fwd_bwd_gather")
+                                              ptr(labels), ldt, float(grad_scale), ptr(logits), dd_tab, ptr(dd_ws),
+                                              dd_bytes, dd_cap, ptr(self.ws), self.nbytes,
+                                              stream_handle(self.device)), "tower_fwd_bwd_gather")
+
+    def fwd_bwd_indexed(self, pos, rows_in, grad_rows_out, params, labels, logits, grad_scale: float = 1.0) -> None:
+        """T1 of the sharded step: tower t's input row m is ``rows_in[t][pos[t][m]]`` (-1: zeros) and
+        its input gradient goes to ``grad_rows_out[t][pos[t][m]]``."""
+        ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}[labels.dtype]
+        for t in range(2):
+            if pos[t].dtype != torch.int32 or pos[t].numel() < self.B:
+                raise _lib.TTError("fwd_bwd_indexed: pos must be int32 [B]")
+            for x in (rows_in[t], grad_rows_out[t]):
+                if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != self.shape.in_dim[t] or not x.is_contiguous():
+                    raise _lib.TTError("fwd_bwd_indexed: row buffers must be contiguous fp32 [*, in_dim]")
+        check(_lib_().tt_tower_fwd_bwd_indexed(C.byref(self.shape), self.B, ptr_array(list(pos)),
+                                               ptr_array(list(rows_in)), ptr_array(list(grad_rows_out)), ptr(params),
+                                               ptr(labels), ldt, float(grad_scale), ptr(logits), ptr(self.ws),
+                                               self.nbytes, stream_handle(self.device)), "tower_fwd_bwd_indexed")
 
     def wgrad(self, loss=None) -> None:
         """T2; also reduces T1's loss partials into loss[0] when given."""
         check(_lib_().tt_tower_wgrad(C.byref(self.shape), self.B, ptr(loss), ptr(self.ws), self.nbytes,
                                      stream_handle(self.device)), "tower_wgrad")
+
+    def wgrad_rowwise_adagrad(self, loss, tables: "TableSet", grad: torch.Tensor, emb_B: int, lr: float, eps: float,
+                              flat: bool = False) -> None:
+        """T2 and ``tables.dedup_rowwise_adagrad(grad, emb_B, lr, eps, flat)`` in one launch."""
+        _dev(grad)
+        if flat:
+            fm = (FeatureMeta * 1)()
+            fm[0].table, fm[0].out_offset, fm[0].out_row = 0, 0, 0
+            F = 1
+        else:
+            fm, F = tables._fm, tables.F
+        check(_lib_().tt_tower_wgrad_rowwise_adagrad(C.byref(self.shape), self.B, ptr(loss), ptr(self.ws), self.nbytes,
+                                                     tables._tm, tables.T, fm, F, int(emb_B), ptr(grad),
+                                                     grad.stride(0), ptr(tables.weights), ptr(tables.state), float(lr),
+                                                     float(eps), ptr(tables._dd_ws), tables._dd_ws.numel(),
+                                                     tables._dd_cap, stream_handle(self.device)),
+              "tower_wgrad_rowwise_adagrad")
 
     def update(self, params, exp_avg=None, exp_avg_sq=None, step_state=None, lr: float = 0.01, beta1: float = 0.9,
                beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0, do_adam: bool = True,
