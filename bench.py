@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--steps-per-graph", type=int, default=8, choices=[1, 2, 4, 8])
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
     return ap.parse_args()
 
 
@@ -209,7 +211,7 @@ def roofline_report(kern, timed, nnz, uniq, step, B):
     return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "bytes_per_launch": out[dom]["bytes"], "ms_per_launch": out[dom]["ms"],
-            "timing": "HIP external events around each launch inside the replayed step graphs",
+            "timing": "HIP events around each launch on its stream over K eager steps of the same sequence",
             "kernels": out, "lookups": nnz, "unique_rows": uniq,
             "embedding_path": {"bytes_per_step": emb_path_bytes, "ms": round(emb_ms, 5),
                                "GB/s": round(emb_path_bytes / emb_ms / 1e6, 1) if emb_ms else None,
@@ -254,28 +256,11 @@ def run_single(args):
     ms = dt / steps_run * 1e3
     value = steps_run * B / dt
     loss = float(step.loss)
-    # ---- per-launch device time inside the step: a second set of graphs over the same batches
-    # with an external-event pair around every launch (event-record nodes on the launching
-    # stream), replayed for the same number of steps
+    # ---- per-launch device time: K more steps of the same launch sequence, eager, with a HIP
+    # event pair around every launch on the stream it runs on
     nnz, uniq = lookup_stats(step, batches)
     kern = launch_bytes(step, nnz, uniq)
-    timed = None
-    try:
-        marks = step.capture_timed_pool(batches, steps_per_graph=k)
-        acc, cnt = {}, {}
-        n_done, j = 0, 0
-        while n_done < args.steps:
-            step.pool_graphs[j % len(step.pool_graphs)].replay()
-            torch.cuda.synchronize()
-            for m in marks[j % len(marks)]:
-                for name, (a, b) in m.items():
-                    acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
-                    cnt[name] = cnt.get(name, 0) + 1
-            n_done += k
-            j += 1
-        timed = {name: acc[name] / cnt[name] for name in acc}
-    except Exception as e:  # noqa: BLE001 - timing is reported, never fatal
-        print(f"in-graph event timing unavailable ({e}); per-launch times omitted", file=sys.stderr)
+    timed = step.timed_steps(batches, args.steps)
     roofline = roofline_report(kern, timed, nnz, uniq, step, B)
     cpu = None
     if not args.no_cpu_baseline:
@@ -284,56 +269,64 @@ def run_single(args):
 
 
 def run_multi(args, world, rank, local_rank):
-    import two_tower_recommender_model_amd as tt
-    from two_tower_recommender_model_amd.task import TwoTower, TwoTowerTrainTask
-    from two_tower_recommender_model_amd.torchrec.datasets.utils import Batch
-    from two_tower_recommender_model_amd.torchrec.distributed.model_parallel import DistributedModelParallel
-    from two_tower_recommender_model_amd.torchrec.modules.embedding_configs import EmbeddingBagConfig
-    from two_tower_recommender_model_amd.torchrec.modules.embedding_modules import EmbeddingBagCollection
-    from two_tower_recommender_model_amd.torchrec.optim.rowwise_adagrad import RowWiseAdagrad
-    from two_tower_recommender_model_amd.torchrec.sparse.jagged_tensor import KeyedJaggedTensor
-    from torch.distributed.optim import _apply_optimizer_in_backward
+    """N >= 1 ranks, one per GPU: the sharded single-hot step (row-wise shards of both tables,
+    id-level all-to-alls over RCCL, data-parallel towers), replayed as HIP graphs with the
+    collectives inside (eager launches if capture is refused)."""
+    from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, TorchComm
 
     num_users, num_items, D, B, layers = WORKLOADS[args.workload]
     dev = torch.device("cuda", local_rank)
-    cfgs = [EmbeddingBagConfig(name="t_user_id", embedding_dim=D, num_embeddings=num_users, feature_names=["user_id"]),
-            EmbeddingBagConfig(name="t_product_id", embedding_dim=D, num_embeddings=num_items,
-                               feature_names=["product_id"])]
-    ebc = EmbeddingBagCollection(tables=cfgs, device=torch.device("meta"))
-    task = TwoTowerTrainTask(TwoTower(ebc, layers, device=dev))
-    _apply_optimizer_in_backward(RowWiseAdagrad, task.two_tower.ebc.parameters(), {"lr": 0.01})
-    model = DistributedModelParallel(module=task, device=dev)
-    dense = [p for n, p in model.named_parameters() if "embedding_bags" not in n and p.numel() > 0]
-    opt = torch.optim.Adam(dense, lr=0.01)
-    from two_tower_recommender_model_amd import ops
+    comm = TorchComm(always_collective=True)
+    step = FusedShardedTwoTowerStep(comm, [num_users, num_items], D, layers, B, dev, lr_emb=0.01, lr_dense=0.01,
+                                    seed=0)
+    batches = synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1 + rank)
+    step.load_batch(*batches[0])
+    step.step()  # creates the RCCL communicators before any capture
+    torch.cuda.synchronize()
+    k = args.steps_per_graph
+    mode = "hipgraph"
+    try:
+        step.capture_pool(batches, steps_per_graph=k)
+        big = step.pool_graphs
+        step.capture_pool(batches, steps_per_graph=1)
+        small = step.pool_graphs
+    except Exception as e:  # noqa: BLE001 - fall back to eager launches, same work per step
+        print(f"rank {rank}: graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
+        mode = "eager"
+        torch.cuda.synchronize()
+        dist.barrier()
 
-    batches = []
-    for cols, lab in synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1 + rank):
-        v, l, o, _ = ops.kjt_build_mod_dropzero(cols, [num_users, num_items])
-        n = int(o[-1])
-        kjt = KeyedJaggedTensor(["user_id", "product_id"], v[:n], lengths=l, offsets=o, stride=B)
-        batches.append(Batch(torch.zeros(1, device=dev), kjt, lab))
+    def run(n, i=0):
+        if mode == "eager":
+            for j in range(n):
+                cols, lab = batches[(i + j) % len(batches)]
+                step.cols, step.labels = cols, lab
+                step.step()
+            return
+        while n >= k:
+            big[(i // k) % len(big)].replay()
+            i, n = i + k, n - k
+        while n > 0:
+            small[i % len(small)].replay()
+            i, n = i + 1, n - 1
 
-    def one(i):
-        opt.zero_grad(set_to_none=True)
-        loss, _ = model(batches[i % len(batches)])
-        loss.backward()
-        opt.step()
-        return loss
-
-    for i in range(args.warmup):
-        one(i)
+    run(args.warmup)
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = one(i)
+    run(args.steps)
     torch.cuda.synchronize()
     dist.barrier()
     dt = torch.tensor([time.perf_counter() - t0], device=dev)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt)
-    return world * args.steps * B / dt, dt / args.steps * 1e3, float(loss)
+    step.check()  # a segment over capacity would have invalidated the run
+    loss = float(step.loss)
+    big = small = None
+    step.release_graphs()  # before the process group is destroyed
+    info = {"capacity": step.C, "exchange_bytes_per_step": 2 * 4 * step.nslots * D + 8 * step.send.numel(),
+            "mode": mode}
+    return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info
 
 
 def main():
@@ -345,14 +338,22 @@ def main():
     config = {"workload": f"{args.workload}: {num_items // 1_000_000}M items x {num_users // 1_000_000}M users, "
                           f"emb_dim {D}, towers {layers}, single-hot {args.ids} ids",
               "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D, "tower_dtype": "bf16 (MFMA, fp32 acc)",
-              "parallelism": "single-gpu hipgraph" if world == 1 else f"rw-sharded tables + dp towers x{world}"}
-    if world == 1:
+              "parallelism": "single-gpu hipgraph"}
+    sharded_info = None
+    if world == 1 and not args.sharded:
         value, ms, loss, roofline, cpu, steps_run = run_single(args)
     else:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        value, ms, loss = run_multi(args, world, rank, local_rank)
+        if "RANK" in os.environ:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:  # --sharded without a launcher (e.g. under rocprofv3): a one-rank group
+            dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
+                                    device_id=torch.device("cuda", local_rank))
+        value, ms, loss, sharded_info = run_multi(args, world, rank, local_rank)
         roofline, cpu, steps_run = None, None, args.steps
+        config["parallelism"] = (f"row-wise sharded tables (id all-to-all over RCCL) + data-parallel towers x{world}, "
+                                 f"{sharded_info['mode']}")
+        config["sharded"] = sharded_info
     if rank == 0:
         out = {"metric": "training pairs/sec at batch 8192 (per GPU)", "value": round(value, 1), "unit": "pairs/s",
                "n_gpus": world, "steps": steps_run, "warmup": args.warmup, "ms_per_step": round(ms, 5),
@@ -360,7 +361,7 @@ def main():
                "data": "synthetic (uniform ids, Bernoulli labels), random-init weights", "config": config,
                "loss": loss, "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

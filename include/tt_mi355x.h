@@ -329,6 +329,36 @@ int tt_dedup_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feat
                              int64_t B, const float* grad, int64_t ldg, float* weights, float* state, float lr,
                              float eps, void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
 
+/* ---- a10 (single-hot): sharded lookups with fixed-size exchanges (csrc/shard.hip) ------------------
+ * Replace ShardedEmbeddingBagCollection's input_dist (KJT permute + block_bucketize_sparse_features
+ * + lengths/values all-to-all) and output_dist (pooled all-to-all / reduce-scatter), reached from
+ * DistributedModelParallel at 03_model_training.py:812-815, for single-hot features, with an id
+ * exchange (ids out, rows back, gradient rows out) whose buffers have a fixed size, so RCCL
+ * all-to-alls sit inside one HIP graph. Segment (d, f) of capacity C holds the lookups of feature f
+ * owned by rank d, in ascending bag order. */
+/* requester: send[d] = {count(d, f) for f < F; keys (f << 40 | local row) of segment (d, f) at
+ * F + f * C + k}; pos[f * B + b] = (d * F + f) * C + k, or -1 (id 0). block_sizes[f] > 0: row-wise
+ * (owner = (id mod N) / block); 0: table-wise (owner = owners[f]). W <= 16. A segment over capacity
+ * sets *overflow (sticky; results invalid). */
+size_t tt_shard_route_workspace_bytes(int F, int64_t B);
+int tt_shard_route_cols(int F, int64_t B, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
+                        const int64_t* block_sizes, const int32_t* owners, int W, int64_t seg_capacity,
+                        int64_t* send, int32_t* pos, int32_t* overflow, void* workspace, size_t ws_bytes,
+                        void* stream);
+/* owner: rows_out[(s * F + f) * C + k] = local table f's row of the received key (all tables one
+ * dim D, D % 4 == 0), and, with dedup_ws, that slot inserted as lookup (s * F + f) * C + k (then
+ * tt_dedup_rowwise_adagrad(F = 1, B = W * F * C) on the received gradient rows). A key outside the
+ * local shard sets *bad (sticky). */
+int tt_shard_gather_rows(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                         int64_t seg_capacity, const int64_t* recv, float* rows_out, int32_t* bad, void* dedup_ws,
+                         size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
+
+/* T3 with the gradient taken from `grads` (data-parallel towers: the all-reduced gradient) instead
+ * of T2's partials: Adam + the bf16 weight copies. */
+int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
+                        float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                        float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes, void* stream);
+
 /* ---- a9: Adam on the flat dense-parameter buffer (torch.optim.Adam, amsgrad=False) ------------ */
 
 /* step_state: device int64[2] = {steps taken so far, arrival counter (0)}; the kernel uses

@@ -307,3 +307,57 @@ def init_state(num_embeddings: Sequence[int], dims: Sequence[int], feature_table
     cin = sum(dims[f] for f in cand_features)
     return TwoTowerState(tables, states, list(feature_table), list(query_features), list(cand_features),
                          list(dims), mlp(qin), mlp(cin))
+
+
+# ----------------------------------------------------------------------------------------------
+# a10 (single-hot): sharded lookups — DistributedModelParallel + ShardedEmbeddingBagCollection
+# (03_model_training.py:798-815): torchrec block_bucketize_sparse_features row-wise semantics
+# (owner = row // ceil(N / W), local row = row - owner * block; EXTERNAL fbgemm-gpu 0.7.0
+# sparse_ops block_bucketize, restated) or table-wise (whole table on one rank), with the
+# fixed-capacity id exchange of csrc/shard.hip.
+# ----------------------------------------------------------------------------------------------
+
+
+def shard_route(cols: Sequence[np.ndarray], num_embeddings: Sequence[int], block_sizes: Sequence[int],
+                owners: Sequence[int], W: int, C: int):
+    """Returns (send [W, F + F*C] int64 — counts then keys f << 40 | local row, unused slots 0 —,
+    pos [F*B] int32, overflow bool). Slot k of segment (d, f) = k-th kept lookup of feature f owned
+    by d in ascending bag order (transform_to_torchrec_batch: id 0 dropped, id % N, 03:356-365)."""
+    F = len(cols)
+    B = len(cols[0])
+    send = np.zeros((W, F + F * C), dtype=np.int64)
+    pos = np.full(F * B, -1, dtype=np.int32)
+    overflow = False
+    for f in range(F):
+        ids = np.asarray(cols[f]).astype(np.int64)
+        cnt = np.zeros(W, dtype=np.int64)
+        for b in range(B):
+            if ids[b] == 0:
+                continue
+            row = int(np.mod(ids[b], num_embeddings[f]))
+            if block_sizes[f] > 0:
+                d, lr = row // block_sizes[f], row - (row // block_sizes[f]) * block_sizes[f]
+            else:
+                d, lr = owners[f], row
+            k = cnt[d]
+            cnt[d] += 1
+            if k < C:
+                send[d, F + f * C + k] = (f << 40) | lr
+                pos[f * B + b] = (d * F + f) * C + k
+            else:
+                overflow = True
+        for d in range(W):
+            send[d, f] = min(cnt[d], C)
+    return send, pos, overflow
+
+
+def rowwise_adagrad_from_lookups(table: torch.Tensor, state: torch.Tensor, rows: torch.Tensor,
+                                 grad_rows: torch.Tensor, lr: float, eps: float = 1e-10) -> None:
+    """Fused backward of single-hot lookups: lookup j (row rows[j]) contributes grad_rows[j]; a
+    row's lookups are summed in index order (dense index_add), then RowWiseAdagrad (03:791-795)."""
+    if rows.numel() == 0:
+        return
+    u, inv = torch.unique(rows, return_inverse=True)
+    g = torch.zeros(u.numel(), table.shape[1])
+    g.index_add_(0, inv, grad_rows)
+    rowwise_adagrad_sparse(table, state, u, g, lr, eps)

@@ -78,7 +78,7 @@ def _assert_clean(ts):
     """After every update the workspace is clean: every slot free, hot-row counters zero."""
     L = ts._dd_cap
     cap = 1024
-    while cap < 2 * L:
+    while cap < L + L // 2:
         cap <<= 1
     al = lambda x: (x + 255) // 256 * 256  # noqa: E731
     sl = ts._dd_ws[:cap * 64].view(torch.int64).view(cap, 8).cpu()

@@ -139,6 +139,16 @@ SIGNATURES = {
         [_psh, _i64, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64,
          _vp],
     ),
+    "tt_shard_route_workspace_bytes": (_sz, [_int, _i64]),
+    "tt_shard_route_cols": (
+        _int,
+        [_int, _i64, _pvp, _int, _pi64, _pi64, _pi32, _int, _i64, _vp, _vp, _vp, _vp, _sz, _vp],
+    ),
+    "tt_shard_gather_rows": (_int, [_vp, _ptm, _int, _int, _int, _i64, _vp, _vp, _vp, _vp, _sz, _i64, _vp]),
+    "tt_tower_adam_grads": (
+        _int,
+        [_psh, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp],
+    ),
     "tt_tower_fwd_bwd_indexed": (
         _int,
         [_psh, _i64, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
@@ -178,6 +188,9 @@ COMPUTE_ENTRY_POINTS = [
     "tt_dedup_rowwise_adagrad",
     "tt_tower_fwd_bwd_indexed",
     "tt_tower_wgrad_rowwise_adagrad",
+    "tt_shard_route_cols",
+    "tt_shard_gather_rows",
+    "tt_tower_adam_grads",
 ]
 
 _lib = None

@@ -28,9 +28,10 @@ struct ColArgsD {
   int64_t num_emb[TT_MAX_FEATURES];
 };
 
+// slots: a power of two >= 1.5 x the lookups (load factor <= 2/3 even if every lookup is unique)
 static int64_t dedup_cap(int64_t L) {
   int64_t c = 1024;
-  while (c < 2 * L) c <<= 1;
+  while (c < L + L / 2) c <<= 1;
   return c;
 }
 

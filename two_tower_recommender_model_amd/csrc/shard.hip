@@ -1,0 +1,281 @@
+// Sharded single-hot lookups on gfx950: input_dist / output_dist of the sharded two-tower step.
+//
+// Replaces, for single-hot bags, what DistributedModelParallel's ShardedEmbeddingBagCollection does
+// around the local lookups (03_model_training.py:798-815, torchrec input_dist: KJT permute +
+// block_bucketize_sparse_features + lengths/values all-to-all; output_dist: pooled all-to-all
+// (table-wise) or reduce-scatter (row-wise)) with an id-level exchange whose buffers have a FIXED
+// size, so the whole sharded step is one HIP graph with RCCL collectives inside:
+//
+//   route (requester)   lookup (f, b): id 0 dropped, row = id mod N_f (transform_to_torchrec_batch,
+//                       03:356-365); owner d = row / block (row-wise, torchrec block_bucketize
+//                       semantics: block = ceil(N / W)) or the table's rank (table-wise); local
+//                       row = row - d * block. Lookups are filed into segment (d, f) in ascending
+//                       bag order (slot k), capacity C per segment; send[d] = {count(d, f) for f,
+//                       then the F segments of C keys (f << 40 | local row)}; pos[f][b] =
+//                       (d * F + f) * C + k, the row of this lookup in the returned-rows buffer
+//                       (-1: dropped). More than C lookups for one segment set the sticky overflow
+//                       flag (the step's results are then invalid: the host checks it).
+//   all-to-all          send -> recv, W equal blocks of F + F * C int64.
+//   gather (owner)      slot i = (s * F + f) * C + k < count: rows_out[i] = table_f[local row]; the
+//                       slot is also inserted into the dedup table (dedup.h) as lookup i, so the
+//                       owner's fused row-wise Adagrad after the gradient all-to-all reads it.
+//   all-to-all          rows_out -> rows_in ([W * F * C][D]); T1 reads rows_in[pos] (tower.hip,
+//                       indexed mode) and writes its input gradient to grad_out[pos]; the reverse
+//                       all-to-all takes grad_out to the owners, whose gradient row of lookup i is
+//                       row i: tt_dedup_rowwise_adagrad(flat) sums a row's lookups in ascending i =
+//                       (source rank, bag) order — the order of the single-process batch
+//                       concatenated over ranks.
+#include "dedup.h"
+
+namespace tt {
+
+constexpr int RT_BLOCK = 256;  // bags per workgroup of the two route kernels
+constexpr int RT_MAXW = 16;
+
+struct RouteArgs {
+  const void* col[TT_MAX_FEATURES];
+  int64_t num_emb[TT_MAX_FEATURES];  // id mod N divisor
+  int64_t block[TT_MAX_FEATURES];    // row-wise block size (> 0), or 0: table-wise
+  int32_t owner[TT_MAX_FEATURES];    // table-wise owner rank
+  int id_dtype;
+  int F;
+  int W;
+  int64_t B;
+  int64_t C;
+  int nblk;           // workgroups per feature = ceil(B / RT_BLOCK)
+  int64_t* send;      // [W][F + F * C]
+  int32_t* pos;       // [F][B]
+  int32_t* overflow;  // sticky flag
+  int64_t* dl;        // [F][B] workspace: owner << 48 | local row, -1 = dropped
+  int32_t* cnt;       // [F][nblk][RT_MAXW] workspace: lookups per (block, owner)
+};
+
+// route pass 1 (thread per bag, coalesced): owner + local row of every lookup, and per-workgroup
+// per-owner counts (wave ballots, summed in wave order)
+__global__ void __launch_bounds__(RT_BLOCK) shard_route_count_kernel(RouteArgs a) {
+  __shared__ int wc[RT_BLOCK / 64][RT_MAXW];
+  const int f = blockIdx.y, blk = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blk * RT_BLOCK + threadIdx.x;
+  int d = -1;
+  int64_t lr = 0;
+  if (b < a.B) {
+    const int64_t id = load_id(a.col[f], a.id_dtype, b);
+    if (id != 0) {
+      const int64_t row = py_mod64(id, a.num_emb[f]);
+      if (a.block[f] > 0) {
+        d = (int)udiv64(row, a.block[f]);
+        lr = row - (int64_t)d * a.block[f];
+      } else {
+        d = a.owner[f];
+        lr = row;
+      }
+    }
+    a.dl[(int64_t)f * a.B + b] = d >= 0 ? (int64_t)(((uint64_t)d << 48) | (uint64_t)lr) : -1;
+  }
+  for (int w = 0; w < a.W; ++w) {
+    const uint64_t m = __ballot(d == w);
+    if (lane == 0) wc[wid][w] = __popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < a.W) {
+    int t = 0;
+    for (int v = 0; v < RT_BLOCK / 64; ++v) t += wc[v][threadIdx.x];
+    a.cnt[((int64_t)f * a.nblk + blk) * RT_MAXW + threadIdx.x] = t;
+  }
+}
+
+// route pass 2: slot k = (lookups of the same owner in earlier workgroups) + (earlier waves) +
+// (earlier lanes): ascending bag order inside each (owner, feature) segment
+__global__ void __launch_bounds__(RT_BLOCK) shard_route_place_kernel(RouteArgs a) {
+  __shared__ int base[RT_MAXW];
+  __shared__ int wc[RT_BLOCK / 64][RT_MAXW];
+  const int f = blockIdx.y, blk = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t seg_stride = (int64_t)a.F + (int64_t)a.F * a.C;
+  const int32_t* cf = a.cnt + (int64_t)f * a.nblk * RT_MAXW;
+  if (threadIdx.x < a.W) {
+    int t = 0, all = 0;
+    for (int q = 0; q < a.nblk; ++q) {
+      const int c = cf[q * RT_MAXW + threadIdx.x];
+      if (q < blk) t += c;
+      all += c;
+    }
+    base[threadIdx.x] = t;
+    if (blk == 0) {  // the segment header: lookups kept for this (owner, feature)
+      if (all > a.C) atomicOr(a.overflow, 1);
+      a.send[(int64_t)threadIdx.x * seg_stride + f] = all < a.C ? all : a.C;
+    }
+  }
+  const int64_t b = (int64_t)blk * RT_BLOCK + threadIdx.x;
+  int64_t v = -1;
+  if (b < a.B) v = a.dl[(int64_t)f * a.B + b];
+  const int d = v >= 0 ? (int)(v >> 48) : -1;
+  int rank = 0;
+  for (int w = 0; w < a.W; ++w) {
+    const uint64_t m = __ballot(d == w);
+    if (d == w) rank = __popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wc[wid][w] = __popcll(m);
+  }
+  __syncthreads();
+  if (b >= a.B) return;
+  int32_t p = -1;
+  if (d >= 0) {
+    int k = base[d] + rank;
+    for (int v2 = 0; v2 < wid; ++v2) k += wc[v2][d];
+    if (k < a.C) {
+      a.send[(int64_t)d * seg_stride + a.F + (int64_t)f * a.C + k] =
+          (int64_t)(((uint64_t)f << DD_TABLE_SHIFT) | ((uint64_t)v & ((1ull << 48) - 1)));
+      p = (int32_t)(((int64_t)d * a.F + f) * a.C + k);
+    } else {
+      atomicOr(a.overflow, 1);
+    }
+  }
+  a.pos[(int64_t)f * a.B + b] = p;
+}
+
+struct GatherArgs {
+  const float* weights;
+  tt_table_meta_t tables[TT_MAX_TABLES];
+  int T;
+  int F;
+  int W;
+  int64_t C;
+  int D;
+  const int64_t* recv;  // [W][F + F * C]
+  float* rows_out;      // [W * F * C][D]
+  DedupWs dd;
+  int dd_on;
+  int32_t* bad;         // sticky: a received key outside the local shard
+};
+
+// owner side: a half-wave per received slot: copy the row, file the lookup for the Adagrad update
+__global__ void __launch_bounds__(256) shard_gather_rows_kernel(GatherArgs a) {
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t n = (int64_t)a.W * a.F * a.C;
+  const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (i >= n) return;
+  const int64_t fc = (int64_t)a.F * a.C;
+  const int64_t s = i / fc, f = (i / a.C) % a.F, k = i % a.C;
+  const int64_t* blk = a.recv + s * (a.F + fc);
+  const int64_t cnt = blk[f];
+  uint64_t key = DD_EMPTY;
+  const float* src = nullptr;
+  if (k < cnt) {
+    key = (uint64_t)blk[a.F + f * a.C + k];
+    const int t = (int)(key >> DD_TABLE_SHIFT);
+    const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
+    if (t < a.T && r < a.tables[t].num_rows && a.tables[t].dim == a.D) {
+      src = a.weights + a.tables[t].weight_offset + r * a.D;
+    } else {
+      key = DD_EMPTY;
+      if (hl == 0) atomicOr(a.bad, 1);
+    }
+  }
+  DdPend pend;
+  if (a.dd_on && hl == 0) dd_insert_begin(a.dd, key, (int32_t)i, pend);
+  float* dst = a.rows_out + i * a.D;
+  if (src) {
+    for (int c = hl * 4; c < a.D; c += 128)
+      *reinterpret_cast<f32x4v*>(dst + c) = *reinterpret_cast<const f32x4v*>(src + c);
+  }
+  if (a.dd_on && hl == 0) dd_insert_finish(a.dd, pend, (int32_t)i);
+}
+
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" {
+
+size_t tt_shard_route_workspace_bytes(int F, int64_t B) {
+  const int64_t nblk = ceil_div(std::max<int64_t>(B, 1), RT_BLOCK);
+  return align_up(sizeof(int64_t) * (size_t)F * (size_t)std::max<int64_t>(B, 1), 256) +
+         align_up(sizeof(int32_t) * (size_t)F * (size_t)nblk * RT_MAXW, 256);
+}
+
+int tt_shard_route_cols(int F, int64_t B, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
+                        const int64_t* block_sizes, const int32_t* owners, int W, int64_t seg_capacity,
+                        int64_t* send, int32_t* pos, int32_t* overflow, void* workspace, size_t ws_bytes,
+                        void* stream) {
+  if (F < 1 || F > TT_MAX_FEATURES) return fail(TT_EINVAL, "shard_route: feature count out of range");
+  if (W < 1 || W > RT_MAXW) return fail(TT_EINVAL, "shard_route: 1..16 ranks supported");
+  if (B < 0 || seg_capacity < 1 || seg_capacity > INT32_MAX / ((int64_t)W * F))
+    return fail(TT_EINVAL, "shard_route: bad batch / segment capacity");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "shard_route: ids must be int32/int64");
+  if (!cols || !num_embeddings || !block_sizes || !owners || !send || !pos || !overflow)
+    return fail(TT_EINVAL, "shard_route: null pointer");
+  if (!workspace || ws_bytes < tt_shard_route_workspace_bytes(F, B))
+    return fail(TT_ECAPACITY, "shard_route: workspace too small");
+  RouteArgs a{};
+  for (int f = 0; f < F; ++f) {
+    if (!cols[f] || num_embeddings[f] < 1) return fail(TT_EINVAL, "shard_route: bad column");
+    if (block_sizes[f] < 0 || (block_sizes[f] == 0 && (owners[f] < 0 || owners[f] >= W)))
+      return fail(TT_EINVAL, "shard_route: bad sharding of a feature");
+    if (block_sizes[f] > 0 && (num_embeddings[f] + block_sizes[f] - 1) / block_sizes[f] > W)
+      return fail(TT_EINVAL, "shard_route: row blocks exceed the rank count");
+    if ((block_sizes[f] > 0 ? block_sizes[f] : num_embeddings[f]) >= (1ll << DD_TABLE_SHIFT))
+      return fail(TT_EINVAL, "shard_route: local rows >= 2^40");
+    a.col[f] = cols[f];
+    a.num_emb[f] = num_embeddings[f];
+    a.block[f] = block_sizes[f];
+    a.owner[f] = owners[f];
+  }
+  if (B == 0) return TT_OK;
+  a.id_dtype = id_dtype;
+  a.F = F;
+  a.W = W;
+  a.B = B;
+  a.C = seg_capacity;
+  a.nblk = (int)ceil_div(B, RT_BLOCK);
+  a.send = send;
+  a.pos = pos;
+  a.overflow = overflow;
+  char* ws = reinterpret_cast<char*>(workspace);
+  a.dl = reinterpret_cast<int64_t*>(ws);
+  a.cnt = reinterpret_cast<int32_t*>(ws + align_up(sizeof(int64_t) * (size_t)F * (size_t)B, 256));
+  const dim3 grid(a.nblk, F);
+  shard_route_count_kernel<<<grid, dim3(RT_BLOCK), 0, as_stream(stream)>>>(a);
+  shard_route_place_kernel<<<grid, dim3(RT_BLOCK), 0, as_stream(stream)>>>(a);
+  return check_launch("shard_route");
+}
+
+int tt_shard_gather_rows(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                         int64_t seg_capacity, const int64_t* recv, float* rows_out, int32_t* bad, void* dedup_ws,
+                         size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+  if (T < 1 || T > TT_MAX_TABLES || F < 1 || F > TT_MAX_FEATURES || W < 1 || seg_capacity < 1)
+    return fail(TT_EINVAL, "shard_gather_rows: bad sizes");
+  if (!weights || !tables || !recv || !rows_out || !bad) return fail(TT_EINVAL, "shard_gather_rows: null pointer");
+  GatherArgs a{};
+  a.D = tables[0].dim;
+  for (int t = 0; t < T; ++t) {
+    if (tables[t].dim != a.D) return fail(TT_EINVAL, "shard_gather_rows: tables must share one dim");
+    if (tables[t].weight_offset % 4) return fail(TT_EINVAL, "shard_gather_rows: rows must be 16-B aligned");
+    a.tables[t] = tables[t];
+  }
+  if (a.D % 4 || (reinterpret_cast<uintptr_t>(weights) & 15) || (reinterpret_cast<uintptr_t>(rows_out) & 15))
+    return fail(TT_EINVAL, "shard_gather_rows: D % 4 == 0 and 16-B aligned buffers required");
+  const int64_t n = (int64_t)W * F * seg_capacity;
+  if (n > INT32_MAX) return fail(TT_EINVAL, "shard_gather_rows: too many slots");
+  a.weights = weights;
+  a.T = T;
+  a.F = F;
+  a.W = W;
+  a.C = seg_capacity;
+  a.recv = recv;
+  a.rows_out = rows_out;
+  a.bad = bad;
+  if (dedup_ws) {
+    if (dedup_max_lookups < n || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+        dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
+        (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
+      return fail(TT_ECAPACITY, "shard_gather_rows: dedup workspace too small / misaligned");
+    dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
+    a.dd_on = 1;
+  }
+  const int64_t grid = ceil_div(n, 8);
+  shard_gather_rows_kernel<<<dim3((unsigned)grid), dim3(256), 0, as_stream(stream)>>>(a);
+  return check_launch("shard_gather_rows");
+}
+
+}  // extern "C"

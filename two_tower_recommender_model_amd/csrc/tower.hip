@@ -895,6 +895,7 @@ struct UpdateArgs {
   int64_t* step_state;
   int do_adam;
   float* grads_out;  // nullable: the reduced gradient (tests / inspection)
+  const float* grads_in;  // nullable: take the gradient from here (data-parallel: all-reduced)
 };
 
 __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
@@ -914,7 +915,9 @@ __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
     const int64_t e = i - a.seg_off[sg];
     float p = a.params[i];
     float g = 0.f;
-    if (a.do_adam || a.grads_out) {
+    if (a.grads_in) {
+      g = a.grads_in[i];
+    } else if (a.do_adam || a.grads_out) {
       if (a.seg_isw[sg]) {
 #pragma unroll 8
         for (int s = 0; s < a.S; ++s) g += a.slab[(int64_t)s * a.P + i];
@@ -1272,9 +1275,10 @@ int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, flo
   return check_launch("tower_wgrad_rowwise_adagrad");
 }
 
-int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
-                    float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
-                    int do_adam, float* grads_out, void* workspace, size_t ws_bytes, void* stream) {
+static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                     float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
+                     int do_adam, float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes,
+                     void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
@@ -1312,8 +1316,24 @@ int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, flo
   a.step_state = step_state;
   a.do_adam = do_adam;
   a.grads_out = grads_out;
+  a.grads_in = grads_in;
   tower_update_kernel<<<dim3((unsigned)ceil_div(L.P, 256)), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_update");
+}
+
+int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                    float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
+                    int do_adam, float* grads_out, void* workspace, size_t ws_bytes, void* stream) {
+  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, do_adam,
+                   grads_out, nullptr, workspace, ws_bytes, stream);
+}
+
+int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
+                        float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                        float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes, void* stream) {
+  if (!grads) return fail(TT_EINVAL, "tower_adam_grads: null gradient");
+  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, 1,
+                   nullptr, grads, workspace, ws_bytes, stream);
 }
 
 }  // extern "C"

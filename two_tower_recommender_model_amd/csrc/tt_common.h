@@ -59,8 +59,17 @@ __device__ __forceinline__ int64_t load_id(const void* values, int id_dtype, int
 // Python's a % n (result takes the divisor's sign): transform_to_torchrec_batch's `id % N`,
 // 03_model_training.py:361, on tensors of either sign
 __device__ __forceinline__ int64_t py_mod64(int64_t a, int64_t n) {
+  // 32-bit fast path (ids and table sizes below 2^32: the usual case): a 64-bit remainder is a
+  // long emulated sequence on CDNA, a 32-bit one a short float-reciprocal sequence
+  if ((uint64_t)a <= 0xffffffffull && (uint64_t)n <= 0xffffffffull && n > 0) return (int64_t)((uint32_t)a % (uint32_t)n);
   int64_t r = a % n;
   return (r != 0 && ((r < 0) != (n < 0))) ? r + n : r;
+}
+
+// a / b for 0 <= a, 0 < b (32-bit fast path as py_mod64)
+__device__ __forceinline__ int64_t udiv64(int64_t a, int64_t b) {
+  if ((uint64_t)a <= 0xffffffffull && (uint64_t)b <= 0xffffffffull) return (int64_t)((uint32_t)a / (uint32_t)b);
+  return a / b;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

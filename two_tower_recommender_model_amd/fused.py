@@ -237,8 +237,6 @@ class FusedTwoTowerStep:
                 prepare()
         if self.gather:
             # EBC forward (and, with the single-hot dedup, its insert) fused into T1
-            if self._timing is not None:
-                self._timing.append({})
             self._mark("t1", 0)
             self.towers.fwd_bwd_gather(self.cols, self.num_embeddings,
                                        [self.tables.table_view(0), self.tables.table_view(1)], self.gpooled,
@@ -288,11 +286,11 @@ class FusedTwoTowerStep:
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, self.lr_dense)
 
     def _mark(self, name: str, end: int) -> None:
-        """Record the start (end=0) / end (end=1) event of launch `name` of the current step when
-        in-graph timing is on (external events: they become event-record nodes of the graph)."""
+        """Record the start (end=0) / end (end=1) HIP event of launch `name` of the current step
+        on the launching stream, when per-launch timing is on (bench: eager steps)."""
         if self._timing is None or not self._timing:
             return
-        ev = torch.cuda.Event(enable_timing=True, external=True)
+        ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         self._timing[-1].setdefault(name, [None, None])[end] = ev
 
@@ -340,16 +338,26 @@ class FusedTwoTowerStep:
         else:
             self.pool_graphs[i % len(self.pool_graphs)].replay()
 
-    def capture_timed_pool(self, batches: Sequence, steps_per_graph: int = 1) -> list:
-        """capture_pool with a start/end event around every launch of every step (bench): returns,
-        per graph, the list of per-step {launch name: [start, end]} event pairs."""
+    def timed_steps(self, batches: Sequence, n: int) -> dict:
+        """Run n eager steps over the resident batches with a HIP event pair around every launch on
+        its stream; returns the mean device time (ms) per launch name."""
+        keep = self.cols, self.labels
         self._timing = []
         try:
-            self.capture_pool(batches, steps_per_graph)
+            for i in range(n):
+                cols, labels = batches[i % len(batches)]
+                self.cols, self.labels = list(cols), labels.to(torch.int32)
+                self._timing.append({})
+                self.step()
+            torch.cuda.synchronize(self.device)
+            acc = {}
+            for m in self._timing:
+                for name, (a, b) in m.items():
+                    acc.setdefault(name, []).append(a.elapsed_time(b))
         finally:
-            marks, self._timing = self._timing, None
-        k = self.steps_per_graph
-        return [marks[j:j + k] for j in range(0, len(marks), k)]
+            self._timing = None
+            self.cols, self.labels = keep
+        return {k: sum(v) / len(v) for k, v in acc.items()}
 
     def capture_pool(self, batches: Sequence, steps_per_graph: int = 1) -> None:
         """Graphs over resident input batches ((cols, labels) device tensors), read in place so a

@@ -599,6 +599,14 @@ class FusedTowers:
                                                      tables._dd_cap, stream_handle(self.device)),
               "tower_wgrad_rowwise_adagrad")
 
+    def adam_grads(self, params, grads, exp_avg, exp_avg_sq, step_state, lr: float = 0.01, beta1: float = 0.9,
+                   beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0) -> None:
+        """T3 from an explicit gradient (the all-reduced one of the data-parallel towers)."""
+        check(_lib_().tt_tower_adam_grads(C.byref(self.shape), self.B, ptr(params), ptr(grads), ptr(exp_avg),
+                                          ptr(exp_avg_sq), float(lr), float(beta1), float(beta2), float(eps),
+                                          float(weight_decay), ptr(step_state), ptr(self.ws), self.nbytes,
+                                          stream_handle(self.device)), "tower_adam_grads")
+
     def update(self, params, exp_avg=None, exp_avg_sq=None, step_state=None, lr: float = 0.01, beta1: float = 0.9,
                beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0, do_adam: bool = True,
                grads_out=None) -> None:
