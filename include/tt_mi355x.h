@@ -293,12 +293,19 @@ int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* 
 /* T2 and the embedding backward in ONE launch: tt_tower_wgrad + tt_dedup_rowwise_adagrad (same
  * arguments as those two calls; emb_B = the dedup's lookups-per-feature B). One launch boundary after
  * T1 instead of two, no cross-stream join: the tile workgroups (MFMA / L2) and the row-update
- * workgroups (HBM) share the CUs. */
+ * workgroups (HBM) share the CUs. With adam_step_state (nullable) it also advances the Adam step
+ * and precomputes the step's bias-correction scalars for tt_tower_update_pre. */
 int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
                                    size_t ws_bytes, const tt_table_meta_t* tables, int T,
                                    const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
                                    int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
-                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
+                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, int64_t* adam_step_state,
+                                   float adam_lr, float adam_beta1, float adam_beta2, void* stream);
+/* T3 after tt_tower_wgrad_rowwise_adagrad(adam_step_state != NULL): reduction + Adam with the
+ * precomputed scalars + bf16 copies. */
+int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                        float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
+                        size_t ws_bytes, void* stream);
 /* T3: fixed-order reduction of T2's partials, Adam (when do_adam; step_state as tt_adam_step),
  * and the bf16 weight copies for the next T1. grads_out (nullable) receives the gradient. */
 int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,

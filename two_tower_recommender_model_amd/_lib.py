@@ -137,8 +137,9 @@ SIGNATURES = {
     "tt_tower_wgrad_rowwise_adagrad": (
         _int,
         [_psh, _i64, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64,
-         _vp],
+         _vp, _f32, _f32, _f32, _vp],
     ),
+    "tt_tower_update_pre": (_int, [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp]),
     "tt_shard_route_workspace_bytes": (_sz, [_int, _i64]),
     "tt_shard_route_cols": (
         _int,
@@ -191,6 +192,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_shard_route_cols",
     "tt_shard_gather_rows",
     "tt_tower_adam_grads",
+    "tt_tower_update_pre",
 ]
 
 _lib = None

@@ -144,7 +144,8 @@ __device__ __forceinline__ int dd_bitonic(int v) {
   return v;
 }
 
-constexpr int DD_HOT_CH = 4096;  // lookups scanned per pass of a hot workgroup
+constexpr int DD_HOT_PT = 4;                 // lookups per thread per scan pass
+constexpr int DD_HOT_CH = 256 * DD_HOT_PT;  // lookups scanned per pass of a hot workgroup (LDS list)
 
 __device__ __forceinline__ void dd_hot_role(const EmbMeta& m, const GradMap& gm, int64_t n,
                                             float* __restrict__ weights, float* __restrict__ state, float lr,
@@ -166,11 +167,11 @@ __device__ __forceinline__ void dd_hot_role(const EmbMeta& m, const GradMap& gm,
     f32x4v acc = (f32x4v)(0.f);
     int seen = 0;  // matches before this pass (global position of list[0])
     for (int64_t c0 = 0; c0 < n; c0 += DD_HOT_CH) {
-      // thread tid covers lookups [c0 + 16 tid, c0 + 16 tid + 16): 16-bit match mask
-      const int64_t i0 = c0 + 16 * tid;
+      // thread tid covers lookups [c0 + PT tid, c0 + PT tid + PT): PT-bit match mask
+      const int64_t i0 = c0 + DD_HOT_PT * tid;
       uint32_t mask = 0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q)
+      for (int q = 0; q < DD_HOT_PT; ++q)
         if (i0 + q < n && ws.lkey[i0 + q] == key) mask |= 1u << q;
       const int mc = __popc(mask);
       int inc = mc;
@@ -188,7 +189,7 @@ __device__ __forceinline__ void dd_hot_role(const EmbMeta& m, const GradMap& gm,
         total += wtot[w];
       }
       int pos = base + inc - mc;
-      for (int q = 0; q < 16; ++q)
+      for (int q = 0; q < DD_HOT_PT; ++q)
         if (mask & (1u << q)) list[pos++] = (int)(i0 + q);
       __syncthreads();
       // group grp takes global positions == grp (mod 8), ascending

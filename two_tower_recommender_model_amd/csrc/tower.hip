@@ -414,8 +414,12 @@ __device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int64_t 
 // IN_/W0_/W1_: compile-time tower input width and layer widths (0 = read from the shape at run
 // time). With them fixed every fragment load is unconditional, so the waitcnt that guards X (issued
 // first) does not also wait for the weight fragments issued behind it.
+// 8 compute waves + 1 dedup wave; the compute path has exactly T1_BARRIERS __syncthreads
+constexpr int T1_THREADS = 576;
+constexpr int T1_BARRIERS = 7;
+
 template <int IN_, int W0_, int W1_>
-__global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
+__global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][TR * LSTR];   // X, later dZ0
   __shared__ __attribute__((aligned(16))) __bf16 hs[2][TR * LSTR];   // hidden activation (bf16)
   __shared__ __attribute__((aligned(16))) __bf16 dzs[2][TR * LSTR];  // dZ1
@@ -424,6 +428,26 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
   __shared__ float lpart[TR];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (wid == 8) {
+    // ---- the dedup wave: files this workgroup's 2 x TR lookups (gather + dedup) into the hash
+    // table; its CAS round trips count only in ITS vmcnt, so the 8 compute waves never wait on
+    // them. It passes the compute waves' barriers (T1_BARRIERS, all unconditional) in step.
+    const int tq = lane / TR, row = lane % TR;
+    const int64_t gm = (int64_t)blockIdx.x * TR + row;
+    const bool own = a.dd_on && gm < a.B;
+    DdPend p;
+    if (own) {
+      const int64_t id = load_id(a.gcol[tq], a.gid_dtype, gm);
+      const uint64_t key = id != 0 ? (((uint64_t)a.dd_table[tq] << DD_TABLE_SHIFT) |
+                                      (uint64_t)py_mod64(id, a.gmod[tq]))
+                                   : DD_EMPTY;
+      dd_insert_begin(a.dd, key, (int32_t)(tq * a.B + gm), p);
+    }
+#pragma unroll 1
+    for (int k = 0; k < T1_BARRIERS; ++k) __syncthreads();
+    if (own) dd_insert_finish(a.dd, p, (int32_t)(tq * a.B + gm));
+    return;
+  }
   const int t = wid >> 2, w4 = wid & 3;
   const int tt = threadIdx.x & 255;  // thread index inside the tower group
   const int r16 = lane & 15, q4 = lane >> 4;
@@ -439,15 +463,10 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
   const int nxv = in / 32;  // f32x4 loads per thread: TR rows x in/4 vectors over 256 threads
   const bool gather = a.gcol[t] != nullptr;
   const bool indexed = a.gpos[t] != nullptr;
-  int32_t rpos[4];  // indexed: the source/destination row of each xv
-  uint64_t dkey[4];  // gather + dedup: the key of the (tower, row) lookup this thread files (c4 == 0)
-  bool down[4];
+  const int incol = a.s.in_col[t];  // read once, before any store (no vmcnt waits mid-chain)
+  int32_t rpos[4];                   // indexed: the source/destination row of each xv
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rpos[i] = -1;
-    dkey[i] = DD_EMPTY;
-    down[i] = false;
-  }
+  for (int i = 0; i < 4; ++i) rpos[i] = -1;
   if (gather || indexed) {
     // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros
     const float* src[4];
@@ -455,28 +474,19 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
     for (int i = 0; i < 4; ++i) {
       src[i] = nullptr;
       rpos[i] = -1;
-      down[i] = false;
-      dkey[i] = DD_EMPTY;
       if (i < nxv) {
         const int e = tt + 256 * i;
         const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
         const int64_t gm = m0 + row;
-        uint64_t key = DD_EMPTY;
         if (gm < B) {
           if (indexed) {
             rpos[i] = a.gpos[t][gm];
             if (rpos[i] >= 0) src[i] = a.gsrc[t] + (int64_t)rpos[i] * in + c4;
           } else {
             const int64_t id = load_id(a.gcol[t], a.gid_dtype, gm);
-            if (id != 0) {
-              const int64_t r = py_mod64(id, a.gmod[t]);
-              src[i] = a.gtab[t] + r * in + c4;
-              key = ((uint64_t)a.dd_table[t] << DD_TABLE_SHIFT) | (uint64_t)r;
-            }
+            if (id != 0) src[i] = a.gtab[t] + py_mod64(id, a.gmod[t]) * in + c4;
           }
         }
-        dkey[i] = key;
-        down[i] = a.dd_on && c4 == 0 && gm < B;
       }
     }
 #pragma unroll
@@ -489,7 +499,7 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
         const int e = tt + 256 * i;
         const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
         const int64_t gm = m0 + row;
-        if (gm < B) xv[i] = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + c4);
+        if (gm < B) xv[i] = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + incol + c4);
       }
     }
   }
@@ -508,11 +518,7 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
   // the label of the row this thread scores in phase 3 (loaded now: no global load after the CAS)
   const int64_t lrow = m0 + (threadIdx.x >> 4);
   const float ylab = lrow < B ? lbl(a.labels, a.label_dtype, lrow) : 0.f;
-  // dedup: the claiming CAS of every lookup goes out now and is resolved at the very end
-  DdPend pend[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (down[i]) dd_insert_begin(a.dd, dkey[i], (int32_t)(t * B + m0 + (tt + 256 * i) / (in / 4)), pend[i]);
+
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i < nxv) {
@@ -523,7 +529,7 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
       *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
       const int64_t gm = m0 + row;
       if (a.pooled_out && gm < B)
-        *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + a.s.in_col[t] + c4) = xv[i];
+        *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + incol + c4) = xv[i];
     }
   }
   __syncthreads();
@@ -682,16 +688,11 @@ __global__ void __launch_bounds__(512) tower_l2_kernel(TowerArgs a) {
         if (indexed)
           dst = rpos[i] >= 0 ? a.gdst[t] + (int64_t)rpos[i] * in + c4 : nullptr;
         else
-          dst = a.gpooled + gm * a.ldp + a.s.in_col[t] + c4;
+          dst = a.gpooled + gm * a.ldp + incol + c4;
       }
       if (dst) *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
     }
   }
-  // ---- 8. dedup: resolve the CASes issued at entry (the row-wise Adagrad launch that follows
-  // reads the slots)
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (down[i]) dd_insert_finish(a.dd, pend[i], (int32_t)(t * B + m0 + (tt + 256 * i) / (in / 4)));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -725,6 +726,12 @@ struct WgradArgs {
   float* loss;             // nullable
   int nbias;
   int64_t tiles_off;       // byte offset of the tile list in the workspace (host side)
+  // Adam's per-step scalars for the T3 that follows (nullable): t = ++step_state[0];
+  // adam_pre = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} — one thread, once, instead of every T3
+  // thread evaluating pow() and an arrival ticket advancing the counter
+  int64_t* step_state;
+  float* adam_pre;
+  float lr, beta1, beta2;
 };
 
 __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile* __restrict__ tiles, int bid) {
@@ -745,6 +752,14 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
         for (int w = lane; w < a.nwg; w += 64) s += a.loss_part[w];
         s = wave_sum(s);
         if (lane == 0) a.loss[0] = s / (float)a.B;
+      }
+      if (a.adam_pre && lane == 0) {
+        const int64_t t_step = a.step_state[0] + 1;
+        a.step_state[0] = t_step;
+        const double bc1 = 1.0 - pow((double)a.beta1, (double)t_step);
+        const double bc2 = 1.0 - pow((double)a.beta2, (double)t_step);
+        a.adam_pre[0] = (float)((double)a.lr / bc1);
+        a.adam_pre[1] = (float)sqrt(bc2);
       }
       return;
     }
@@ -896,13 +911,18 @@ struct UpdateArgs {
   int do_adam;
   float* grads_out;  // nullable: the reduced gradient (tests / inspection)
   const float* grads_in;  // nullable: take the gradient from here (data-parallel: all-reduced)
+  const float* adam_pre;  // nullable: step size / sqrt(bias correction 2) precomputed by T2 (which
+                          // also advanced step_state): no pow() and no arrival ticket here
 };
 
 __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   int64_t t_step = 0;
   float step_size = 0.f, bc2_sqrt = 1.f;
-  if (a.do_adam) {
+  if (a.do_adam && a.adam_pre) {
+    step_size = a.adam_pre[0];
+    bc2_sqrt = a.adam_pre[1];
+  } else if (a.do_adam) {
     t_step = a.step_state[0] + 1;
     const double bc1 = 1.0 - pow((double)a.beta1, (double)t_step);
     const double bc2 = 1.0 - pow((double)a.beta2, (double)t_step);
@@ -944,7 +964,7 @@ __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
       a.wtb[a.seg_wc[sg] + k * N + n] = (__bf16)p;
     }
   }
-  if (a.do_adam) {
+  if (a.do_adam && !a.adam_pre) {
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned* counter = reinterpret_cast<unsigned*>(a.step_state + 1);
@@ -1123,7 +1143,7 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   a.in_max = L.in_max;
   a.nwg = L.nwg;
   const int i0 = shape->in_dim[0], i1 = shape->in_dim[1], w0 = shape->width[0], w1 = shape->width[1];
-  const dim3 g(L.nwg), b512(512);
+  const dim3 g(L.nwg), b512(T1_THREADS);
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
   if ((a.gcol[0] || a.gpos[0]) && !two)
     return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
@@ -1259,11 +1279,21 @@ int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, flo
                                    size_t ws_bytes, const tt_table_meta_t* tables, int T,
                                    const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
                                    int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
-                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, int64_t* adam_step_state,
+                                   float adam_lr, float adam_beta1, float adam_beta2, void* stream) {
   WgradArgs a{};
   int64_t wgs = 0;
   int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
   if (rc) return rc;
+  if (adam_step_state) {  // T2 advances the Adam step and precomputes its scalars for T3
+    TowerLayout L;
+    tower_layout(shape, B, &L);
+    a.step_state = adam_step_state;
+    a.adam_pre = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + L.o_counter);
+    a.lr = adam_lr;
+    a.beta1 = adam_beta1;
+    a.beta2 = adam_beta2;
+  }
   DdUpdateArgs d{};
   int64_t dd_grid = 0;
   rc = dedup_update_args(tables, T, features, F, emb_B, grad, ldg, weights, state, lr, eps, dedup_ws, dedup_ws_bytes,
@@ -1278,12 +1308,13 @@ int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, flo
 static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
                      float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
                      int do_adam, float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes,
-                     void* stream) {
+                     void* stream, const float* adam_pre = nullptr) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if (!params || (do_adam && (!exp_avg || !exp_avg_sq || !step_state))) return fail(TT_EINVAL, "tower: null pointer");
+  if (!params || (do_adam && (!exp_avg || !exp_avg_sq || (!step_state && !adam_pre))))
+    return fail(TT_EINVAL, "tower: null pointer");
   char* ws = reinterpret_cast<char*>(workspace);
   UpdateArgs a{};
   a.params = params;
@@ -1317,6 +1348,7 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
   a.do_adam = do_adam;
   a.grads_out = grads_out;
   a.grads_in = grads_in;
+  a.adam_pre = adam_pre;
   tower_update_kernel<<<dim3((unsigned)ceil_div(L.P, 256)), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_update");
 }
@@ -1326,6 +1358,18 @@ int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, flo
                     int do_adam, float* grads_out, void* workspace, size_t ws_bytes, void* stream) {
   return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, do_adam,
                    grads_out, nullptr, workspace, ws_bytes, stream);
+}
+
+int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                        float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
+                        size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
+  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
+                   nullptr, workspace, ws_bytes, stream, pre);
 }
 
 int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,

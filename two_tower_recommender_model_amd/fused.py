@@ -251,11 +251,11 @@ class FusedTwoTowerStep:
             # one stream: T1 -> [T2 + fused row-wise Adagrad] -> T3
             self._mark("t1", 1)
             self._mark("k2", 0)
-            self.towers.wgrad_rowwise_adagrad(self.loss, self.tables, self.gpooled, B, self.lr_emb, self.eps)
+            self.towers.wgrad_rowwise_adagrad(self.loss, self.tables, self.gpooled, B, self.lr_emb, self.eps,
+                                              adam_step_state=self.adam_state, adam_lr=self.lr_dense)
             self._mark("k2", 1)
             self._mark("t3", 0)
-            self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
-                               grads_out=self.grads)
+            self.towers.update_pre(self.params, self.exp_avg, self.exp_avg_sq, grads_out=self.grads)
             self._mark("t3", 1)
             return
         if self.towers is not None:

@@ -583,8 +583,10 @@ class FusedTowers:
                                      stream_handle(self.device)), "tower_wgrad")
 
     def wgrad_rowwise_adagrad(self, loss, tables: "TableSet", grad: torch.Tensor, emb_B: int, lr: float, eps: float,
-                              flat: bool = False) -> None:
-        """T2 and ``tables.dedup_rowwise_adagrad(grad, emb_B, lr, eps, flat)`` in one launch."""
+                              flat: bool = False, adam_step_state=None, adam_lr: float = 0.01, adam_beta1: float = 0.9,
+                              adam_beta2: float = 0.999) -> None:
+        """T2 and ``tables.dedup_rowwise_adagrad(grad, emb_B, lr, eps, flat)`` in one launch; with
+        ``adam_step_state`` it also advances the Adam step for a following ``update_pre``."""
         _dev(grad)
         if flat:
             fm = (FeatureMeta * 1)()
@@ -596,8 +598,17 @@ class FusedTowers:
                                                      tables._tm, tables.T, fm, F, int(emb_B), ptr(grad),
                                                      grad.stride(0), ptr(tables.weights), ptr(tables.state), float(lr),
                                                      float(eps), ptr(tables._dd_ws), tables._dd_ws.numel(),
-                                                     tables._dd_cap, stream_handle(self.device)),
+                                                     tables._dd_cap, ptr(adam_step_state), float(adam_lr),
+                                                     float(adam_beta1), float(adam_beta2), stream_handle(self.device)),
               "tower_wgrad_rowwise_adagrad")
+
+    def update_pre(self, params, exp_avg, exp_avg_sq, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,
+                   weight_decay: float = 0.0, grads_out=None) -> None:
+        """T3 with the Adam scalars the preceding wgrad_rowwise_adagrad(adam_step_state=...) computed."""
+        check(_lib_().tt_tower_update_pre(C.byref(self.shape), self.B, ptr(params), ptr(exp_avg), ptr(exp_avg_sq),
+                                          float(eps), float(beta1), float(beta2), float(weight_decay),
+                                          ptr(grads_out), ptr(self.ws), self.nbytes, stream_handle(self.device)),
+              "tower_update_pre")
 
     def adam_grads(self, params, grads, exp_avg, exp_avg_sq, step_state, lr: float = 0.01, beta1: float = 0.9,
                    beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0) -> None:
