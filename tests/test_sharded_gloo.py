@@ -92,7 +92,22 @@ def _worker(rank, world, port, out_q, sharding):
             outs.append((kt.values().detach().numpy().copy(), gout.numpy().copy()))
         local = {n: mod.embedding_bags[n].weight.detach().numpy().copy() for n in mod.embedding_bags}
         blocks = dict(mod._rw_block)
-        out_q.put((rank, outs, local, {cfgs[t].name: bs for t, bs in blocks.items()}, plan.plan[""]))
+        # checkpoint: state_dict() holds torch ShardedTensors that the reference's
+        # gather_and_get_state_dict (03_model_training.py:474-495, restated) gathers on rank 0
+        from torch.distributed._sharded_tensor import ShardedTensor
+
+        gathered = {}
+        for k, v in mod.state_dict().items():
+            if isinstance(v, ShardedTensor):
+                full = torch.zeros(v.size()) if rank == 0 else None
+                v.gather(0, full)
+                if rank == 0:
+                    gathered[k] = full.numpy().copy()
+        # and a gathered (full) dict loads back: every rank keeps its rows
+        mod.load_state_dict({f"embedding_bags.{n}.weight": t for n, t in _full_tables().items()})
+        reloaded = {n: mod.embedding_bags[n].weight.detach().numpy().copy() for n in mod.embedding_bags}
+        out_q.put((rank, outs, local, {cfgs[t].name: bs for t, bs in blocks.items()}, plan.plan[""], gathered,
+                   reloaded))
     finally:
         dist.destroy_process_group()
 
@@ -106,8 +121,8 @@ def _run(world, sharding):
         p.start()
     res = {}
     for _ in range(world):
-        rank, outs, local, blocks, plan = q.get(timeout=180)
-        res[rank] = (outs, local, blocks, plan)
+        rank, outs, local, blocks, plan, gathered, reloaded = q.get(timeout=180)
+        res[rank] = (outs, local, blocks, plan, gathered, reloaded)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -145,9 +160,19 @@ def test_sharded_ebc_matches_oracle(world, sharding):
                 grads[t] += g[t]
         for t in range(len(tabs)):
             ref.rowwise_adagrad(tabs[t], states[t], grads[t], LR, 1e-10)
+    # the gathered checkpoint (rank 0) holds the oracle's full tables
+    gathered = res[0][4]
+    assert sorted(gathered) == sorted(f"embedding_bags.{n}.weight" for n in names)
+    for n in names:
+        np.testing.assert_allclose(gathered[f"embedding_bags.{n}.weight"], tabs[names.index(n)].numpy(),
+                                   rtol=1e-5, atol=1e-6)
     # every rank's local shards equal the oracle's rows
     for rank in range(world):
-        _, local, blocks, plan = res[rank]
+        _, local, blocks, plan, _, reloaded = res[rank]
+        for n, w in reloaded.items():
+            ps = plan[n]
+            lo = 0 if ps.sharding_type == "table_wise" else min(rank * blocks[n], full[n].shape[0])
+            np.testing.assert_array_equal(w, full[n][lo:lo + w.shape[0]].numpy())
         for n, w in local.items():
             t = names.index(n)
             ps = plan[n]

@@ -302,6 +302,21 @@ class FusedTwoTowerStep:
         else:
             self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, self.B, self.lr_emb, self.eps)
 
+    def eval_step(self, cols: Sequence[torch.Tensor], labels: torch.Tensor):
+        """Forward only (pipeline.progress in eval mode, 03_model_training.py:545): pooled lookup of
+        the single-hot columns, both towers (bf16 MFMA GEMMs, or fp32 in the parity precision), dot +
+        BCE. Tables and towers are not touched. Returns (mean loss, logits) device tensors."""
+        B = self.B
+        if cols[0].numel() != B:
+            raise _lib.TTError("eval_step: batch size differs from the step's")
+        self.tables.pooled_fwd_cols(list(cols), self.num_embeddings, out=self.pooled)
+        self._towers_fwd()
+        L = len(self.layer_sizes)
+        loss = torch.empty((), dtype=torch.float32, device=self.device)
+        logits = torch.empty(B, dtype=torch.float32, device=self.device)
+        self.dot_bce(self.qy[L - 1], self.cy[L - 1], labels, logits=logits, loss=loss)
+        return loss, logits
+
     def sync_weights(self) -> None:
         """Refresh the fused towers' bf16 weight copies after the fp32 parameters were changed
         outside step() (initialisation, loading a checkpoint)."""

@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import ctypes as C
 import threading
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -65,6 +65,27 @@ class TorchComm:
             return _Done()
         w = dist.all_to_all_single(out, inp, group=self.group, async_op=async_op)
         return w if async_op else _Done()
+
+    def gather_rows(self, local: torch.Tensor, spans: Sequence[Tuple[int, int]], full_rows: int):
+        """Rank 0 receives every rank's row block (spans[r] = (first row, rows)) into one
+        [full_rows, D] tensor (returned on rank 0, None elsewhere); point-to-point, so no rank
+        ever holds more than its own shard plus, on rank 0, the result."""
+        D = local.shape[1]
+        if self.rank == 0:
+            full = torch.empty(full_rows, D, dtype=local.dtype, device=local.device)
+            lo, n = spans[0]
+            full[lo:lo + n].copy_(local[:n])
+            for r in range(1, self.world):
+                lo, n = spans[r]
+                if n:
+                    buf = torch.empty(n, D, dtype=local.dtype, device=local.device)
+                    dist.recv(buf, src=r, group=self.group)
+                    full[lo:lo + n].copy_(buf)
+            return full
+        lo, n = spans[self.rank]
+        if n:
+            dist.send(local[:n].contiguous(), dst=0, group=self.group)
+        return None
 
     def all_reduce_mean(self, t: torch.Tensor, async_op: bool = False):
         if self.world == 1 and not self.always:
@@ -110,6 +131,18 @@ class ThreadComm:
         torch.cuda.current_stream().synchronize()
         self.shared.barrier.wait()
         return _Done()
+
+    def gather_rows(self, local: torch.Tensor, spans: Sequence[Tuple[int, int]], full_rows: int):
+        self._exchange(local)
+        full = None
+        if self.rank == 0:
+            full = torch.empty(full_rows, local.shape[1], dtype=local.dtype, device=local.device)
+            for r in range(self.world):
+                lo, n = spans[r]
+                full[lo:lo + n].copy_(self.shared.slots[r][:n])
+        torch.cuda.current_stream().synchronize()
+        self.shared.barrier.wait()
+        return full
 
     def all_reduce_mean(self, t: torch.Tensor, async_op: bool = False):
         self._exchange(t.clone())
@@ -289,6 +322,50 @@ class FusedShardedTwoTowerStep:
         ts.dedup_rowwise_adagrad(self.grad_in, self.nslots, self.lr_emb, self.eps, flat=True)
         h_dense.wait()
         tw.adam_grads(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense)
+
+    # ---- checkpoint (03_model_training.py:474-502 / :1015-1054 format) -------------------------
+    def spans(self, f: int) -> List[Tuple[int, int]]:
+        """(first row, rows) of table f held by each rank."""
+        out = []
+        for r in range(self.W):
+            if self.sharding[f] == "row_wise":
+                bs = self.block[f]
+                lo = min(r * bs, self.N[f])
+                out.append((lo, max(0, min(bs, self.N[f] - lo))))
+            else:
+                out.append((0, self.N[f] if self.owner[f] == r else 0))
+        return out
+
+    def gathered_state_dict(self, feature_names: Sequence[str] = ("user_id", "product_id"),
+                            prefix: str = "two_tower.") -> Dict[str, torch.Tensor]:
+        """Collective: rank 0 returns the full state dict the reference's gather_and_get_state_dict
+        writes (full tables + towers), other ranks {}."""
+        from .lifecycle import _dense_items, _tower_views
+
+        sd = {}
+        for f, name in enumerate(feature_names):
+            full = self.comm.gather_rows(self.tables.table_view(f), self.spans(f), self.N[f])
+            if self.rank == 0:
+                sd[f"{prefix}ebc.embedding_bags.t_{name}.weight"] = full
+        if self.rank == 0:
+            towers = _tower_views(self.params, [self.D, self.D], self.layer_sizes)
+            sd.update({k: v.clone() for k, v in _dense_items(towers, prefix).items()})
+        return sd
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], feature_names: Sequence[str] = ("user_id", "product_id"),
+                        prefix: str = "two_tower.") -> None:
+        """Every rank takes its blocks of the full tables and the towers from a gathered dict."""
+        from .lifecycle import _dense_items, _tower_views
+
+        with torch.no_grad():
+            for f, name in enumerate(feature_names):
+                lo, n = self.spans(f)[self.rank]
+                if n:
+                    self.tables.table_view(f)[:n].copy_(sd[f"{prefix}ebc.embedding_bags.t_{name}.weight"][lo:lo + n])
+            towers = _tower_views(self.params, [self.D, self.D], self.layer_sizes)
+            for k, v in _dense_items(towers, prefix).items():
+                v.copy_(sd[k])
+        self.towers.update(self.params, do_adam=False)
 
     def check(self) -> None:
         """Raise if any step so far overflowed a segment or received a key outside its shard."""

@@ -84,6 +84,48 @@ class _ShardedLookup(torch.autograd.Function):
         return (None, None, None, None) + (None,) * len(ctx.mod._local_params())
 
 
+def _sharded_state_dict_hook(module, state_dict, prefix, local_metadata):
+    """state_dict() of a sharded EBC holds one torch ShardedTensor per table (collective: every rank
+    builds every table's, with no local shard where it holds none), as torchrec's does — what the
+    reference's gather_and_get_state_dict (03_model_training.py:474-495) expects:
+    ``isinstance(t, ShardedTensor)`` then ``t.gather(0, full)`` on rank 0."""
+    from torch.distributed._shard.metadata import ShardMetadata
+    from torch.distributed._shard.sharded_tensor import Shard, ShardedTensor
+
+    dev = module._device
+    place = f"rank:{module._rank}/{dev.type}" + (f":{dev.index if dev.index is not None else 0}"
+                                                 if dev.type == "cuda" else "")
+    for c in module._embedding_bag_configs:  # same key order on every rank (collective gathers follow it)
+        state_dict.pop(f"{prefix}embedding_bags.{c.name}.weight", None)
+    for t, c in enumerate(module._embedding_bag_configs):
+        key = f"{prefix}embedding_bags.{c.name}.weight"
+        shards = []
+        lo, n = module._shard_of.get(t, (0, 0))
+        if n > 0:
+            w = module.embedding_bags[c.name].weight.detach()
+            shards.append(Shard(tensor=w, metadata=ShardMetadata(shard_offsets=[lo, 0],
+                                                                 shard_sizes=[n, c.embedding_dim],
+                                                                 placement=place)))
+        state_dict[key] = ShardedTensor._init_from_local_shards(shards, c.num_embeddings, c.embedding_dim,
+                                                                process_group=module._pg)
+    state_dict.pop(prefix + "_grad_anchor", None)
+    return state_dict
+
+
+def _sharded_load_pre_hook(module, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                           error_msgs):
+    """load_state_dict() of a sharded EBC takes full (gathered) tables: each rank keeps its rows."""
+    for t, c in enumerate(module._embedding_bag_configs):
+        key = f"{prefix}embedding_bags.{c.name}.weight"
+        if key not in state_dict:
+            continue
+        full = state_dict.pop(key)
+        if c.name in module.embedding_bags:  # this rank's rows replace the full table
+            lo, n = module._shard_of.get(t, (0, 0))
+            state_dict[key] = full[lo:lo + n]
+    state_dict.setdefault(prefix + "_grad_anchor", module._grad_anchor.detach())
+
+
 class ShardedEmbeddingBagCollection(nn.Module):
     def __init__(self, ebc: EmbeddingBagCollection, module_plan: Dict[str, ParameterSharding], pg,
                  device: torch.device, backend=None):
@@ -164,6 +206,9 @@ class ShardedEmbeddingBagCollection(nn.Module):
         self._f_table = f_table
         self._ts_cache: Dict[Tuple[str, int], object] = {}
         self._grad_anchor = nn.Parameter(torch.zeros(0, device=self._device))
+        self._shard_of = {t: (lo, n) for (t, lo, n) in local_tables}
+        self._register_state_dict_hook(_sharded_state_dict_hook)
+        self._register_load_state_dict_pre_hook(_sharded_load_pre_hook, with_module=True)
 
     @staticmethod
     def _prefix(ds: Sequence[int]) -> List[int]:
