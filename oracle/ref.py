@@ -361,3 +361,31 @@ def rowwise_adagrad_from_lookups(table: torch.Tensor, state: torch.Tensor, rows:
     g = torch.zeros(u.numel(), table.shape[1])
     g.index_add_(0, inv, grad_rows)
     rowwise_adagrad_sparse(table, state, u, g, lr, eps)
+
+
+# ----------------------------------------------------------------------------------------------
+# 8(f) row 3: evaluate() of 03_model_training.py:504-566 — forward only; AUROC of sigmoid(logits)
+# over all batches (torchmetrics binary AUROC = scikit-learn roc_auc_score); average loss = the SUM
+# of per-batch mean losses divided by the number of samples (the reference's quirk, 03:550-559)
+# ----------------------------------------------------------------------------------------------
+
+
+def evaluate(st: TwoTowerState, batches, num_embeddings: Sequence[int], limit_batches: Optional[int] = None):
+    """batches: [(user ids, item ids, labels) numpy]; returns (avg_loss, auroc)."""
+    from sklearn.metrics import roc_auc_score
+
+    total, n, ps, ys = 0.0, 0, [], []
+    for i, (u, it, lab) in enumerate(batches):
+        if limit_batches is not None and i >= limit_batches:
+            break
+        v, _, o = kjt_build([u, it], num_embeddings)
+        B = len(lab)
+        pooled = pooled_fwd(st.tables, st.feature_table, torch.from_numpy(v).to(torch.int64), torch.from_numpy(o), B)
+        q = mlp_fwd(pooled[:, feature_columns(st.dims, st.query_features)], st.query_layers)
+        c = mlp_fwd(pooled[:, feature_columns(st.dims, st.cand_features)], st.cand_layers)
+        logits, loss = dot_bce(q, c, torch.from_numpy(np.asarray(lab)))
+        total += float(loss)
+        n += B
+        ps.append(torch.sigmoid(logits).numpy())
+        ys.append(np.asarray(lab))
+    return (total / n if n else 0.0), float(roc_auc_score(np.concatenate(ys), np.concatenate(ps)))

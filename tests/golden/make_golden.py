@@ -164,7 +164,102 @@ def train_case(name, num_users, num_items, D, B, layers, steps, seed, zipf=False
     print("train case:", name, "final loss", float(rec[f"s{steps-1}_loss"]))
 
 
+class _SklearnAUROC:
+    """Stand-in for torchmetrics.AUROC(task="binary") (not installable offline): exact binary AUROC
+    of the accumulated scores via scikit-learn's roc_auc_score (same definition: trapezoidal ROC
+    over distinct thresholds)."""
+
+    def __init__(self, task="binary"):
+        self.p, self.y = [], []
+
+    def to(self, device):
+        return self
+
+    def __call__(self, preds, target):
+        self.p.append(preds.detach().numpy().ravel())
+        self.y.append(target.detach().numpy().ravel())
+
+    def compute(self):
+        from sklearn.metrics import roc_auc_score
+
+        return torch.tensor(roc_auc_score(np.concatenate(self.y), np.concatenate(self.p)))
+
+
+class _EvalPipeline:
+    """What evaluate() touches of TrainPipelineSparseDist in eval mode: _model, _device, progress()."""
+
+    def __init__(self, model):
+        self._model = model
+        self._device = torch.device("cpu")
+
+    def progress(self, it):
+        batch = next(it)
+        with torch.no_grad():
+            return self._model(batch)[1]
+
+
+def eval_case(name, num_users, num_items, D, B, layers, n_batches, seed, limit_batches=None):
+    """03:504-566 golden: the reference's own evaluate() (AST-extracted) on a fixed model state and
+    fixed raw eval batches; records its (average loss, AUROC) return."""
+    import functools
+    import os
+    import types
+
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    cat_cols = ["user_id", "product_id"]
+    ns = load_reference_fragments(cat_cols)
+    tree = ast.parse(REF_FILE.read_text())
+    node = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "evaluate"][0]
+    from tqdm import tqdm
+
+    ns.update(dict(metrics=types.SimpleNamespace(AUROC=_SklearnAUROC), dist=dist, tqdm=tqdm,
+                   TrainPipelineSparseDist=object, DataLoader=list, partial=functools.partial))
+    exec(compile(ast.Module(body=[node], type_ignores=[]), str(REF_FILE), "exec"), ns)
+    g = torch.Generator().manual_seed(seed)
+    emb_counts = [num_users, num_items]
+    eb_configs = [trc.EmbeddingBagConfig(name=f"t_{f}", embedding_dim=D, num_embeddings=emb_counts[i],
+                                         feature_names=[f]) for i, f in enumerate(cat_cols)]
+    ebc = trc.EmbeddingBagCollection(tables=eb_configs)
+    with torch.no_grad():
+        for cfg in eb_configs:
+            ebc.embedding_bags[cfg.name].weight.uniform_(-0.3, 0.3, generator=g)
+    torch.manual_seed(seed)
+    task = ns["TwoTowerTrainTask"](ns["TwoTower"](embedding_bag_collection=ebc, layer_sizes=layers, device=None))
+    task.eval()
+    rec = {"D": np.int64(D), "B": np.int64(B), "layers": np.asarray(layers, np.int64),
+           "num_embeddings": np.asarray(emb_counts, np.int64), "n_batches": np.int64(n_batches),
+           "limit_batches": np.int64(-1 if limit_batches is None else limit_batches)}
+    for n, p in task.named_parameters():
+        rec["state_" + n] = p.detach().clone().numpy()
+    raw = []
+    for b in range(n_batches):
+        cols = {c: torch.randint(0, 2 * emb_counts[i], (B,), generator=g, dtype=torch.int64)
+                for i, c in enumerate(cat_cols)}
+        cols["label"] = torch.randint(0, 2, (B,), generator=g, dtype=torch.int64)
+        raw.append(cols)
+        for k, v in cols.items():
+            rec[f"b{b}_{k}"] = v.numpy()
+    transform = functools.partial(ns["transform_to_torchrec_batch"], num_embeddings_per_feature=emb_counts)
+    avg_loss, auroc = ns["evaluate"](limit_batches, _EvalPipeline(task), raw, "test", transform)
+    rec["avg_loss"] = np.float64(avg_loss)
+    rec["auroc"] = np.float64(auroc)
+    np.savez_compressed(OUT / f"eval_{name}.npz", **rec)
+    print("eval case:", name, avg_loss, auroc)
+
+
 if __name__ == "__main__":
+    import sys as _sys
+
+    if len(_sys.argv) > 1 and _sys.argv[1] == "eval":
+        eval_case("c1", num_users=700, num_items=900, D=32, B=256, layers=[32, 16], n_batches=5, seed=21)
+        eval_case("limit", num_users=300, num_items=400, D=64, B=128, layers=[128, 64], n_batches=6, seed=22,
+                  limit_batches=4)
+        _sys.exit(0)
     kjt_cases()
     # config-1 shape family (plumbing), shrunk to keep fixtures small
     train_case("c1", num_users=1000, num_items=1200, D=16, B=256, layers=[16, 8], steps=3, seed=0)
