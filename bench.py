@@ -256,12 +256,38 @@ def run_single(args):
     ms = dt / steps_run * 1e3
     value = steps_run * B / dt
     loss = float(step.loss)
-    # ---- per-launch device time: K more steps of the same launch sequence, eager, with a HIP
-    # event pair around every launch on the stream it runs on
+    # ---- per-launch device time inside the replayed graphs: the same graphs re-captured with
+    # event-record nodes around every kernel node (graph_timing.py), replayed for K steps;
+    # eager steps with HIP events around each launch if the graph cannot be instrumented
     nnz, uniq = lookup_stats(step, batches)
     kern = launch_bytes(step, nnz, uniq)
-    timed = step.timed_steps(batches, args.steps)
+    timed, timing_how = None, None
+    if step.gather and step.dedup_single and step.combined_bwd:
+        try:
+            from two_tower_recommender_model_amd.graph_timing import GraphLaunchTimer
+
+            step.capture_pool(batches, steps_per_graph=k, keep_graph=True)
+            names = ["t1", "k2", "t3"]
+            timers = [GraphLaunchTimer(g, list(range(3 * k))) for g in step.pool_graphs]
+            acc = {n: [] for n in names}
+            n_done, j = 0, 0
+            while n_done < args.steps:
+                step.pool_graphs[j % len(step.pool_graphs)].replay()
+                torch.cuda.synchronize()
+                for i, t_ms in enumerate(timers[j % len(timers)].elapsed()):
+                    acc[names[i % 3]].append(t_ms)
+                n_done, j = n_done + k, j + 1
+            timed = {n: sum(v) / len(v) for n, v in acc.items()}
+            timing_how = "HIP event-record nodes around each kernel node of the replayed step graphs (K steps)"
+            for t in timers:
+                t.close()
+        except Exception as e:  # noqa: BLE001
+            print(f"graph instrumentation unavailable ({e}); eager per-launch events", file=sys.stderr)
+    if timed is None:
+        timed = step.timed_steps(batches, args.steps)
+        timing_how = "HIP events around each launch on its stream over K eager steps of the same sequence"
     roofline = roofline_report(kern, timed, nnz, uniq, step, B)
+    roofline["timing"] = timing_how
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(args, num_users, num_items, D, B, layers)

@@ -324,12 +324,12 @@ class FusedTwoTowerStep:
             self.towers.update(self.params, do_adam=False)
 
     # ------------------------------------------------------------------------------------------
-    def capture(self, batches: Optional[Sequence] = None) -> None:
+    def capture(self, batches: Optional[Sequence] = None, keep_graph: bool = False) -> None:
         """Record ``step()`` into a HIP graph (replayed by ``replay()``). With ``batches`` (a list of
         resident (cols, labels) device batches) the graph holds one full step per batch, in order."""
         self.sync_weights()
         torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=keep_graph)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         keep_cols, keep_labels = self.cols, self.labels
@@ -374,7 +374,7 @@ class FusedTwoTowerStep:
             self.cols, self.labels = keep
         return {k: sum(v) / len(v) for k, v in acc.items()}
 
-    def capture_pool(self, batches: Sequence, steps_per_graph: int = 1) -> None:
+    def capture_pool(self, batches: Sequence, steps_per_graph: int = 1, keep_graph: bool = False) -> None:
         """Graphs over resident input batches ((cols, labels) device tensors), read in place so a
         replay needs no input copy. Graph j runs full steps on batches j*k .. j*k+k-1 (k =
         ``steps_per_graph``, len(batches) % k == 0): k > 1 amortises the host cost of a graph
@@ -391,6 +391,6 @@ class FusedTwoTowerStep:
         self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]  # alive as long as any graph
         self.pool_graphs = []
         for j in range(0, len(staged), k):
-            self.capture(staged[j:j + k])
+            self.capture(staged[j:j + k], keep_graph=keep_graph)
             self.pool_graphs.append(self.graph)
         self.steps_per_graph = k
