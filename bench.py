@@ -311,6 +311,8 @@ def run_multi(args, world, rank, local_rank):
     torch.cuda.synchronize()
     k = args.steps_per_graph
     mode = "hipgraph"
+    ok = torch.ones(1, device=dev)
+    big = small = None
     try:
         step.capture_pool(batches, steps_per_graph=k)
         big = step.pool_graphs
@@ -318,8 +320,13 @@ def run_multi(args, world, rank, local_rank):
         small = step.pool_graphs
     except Exception as e:  # noqa: BLE001 - fall back to eager launches, same work per step
         print(f"rank {rank}: graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
+        ok.zero_()
+    torch.cuda.synchronize()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
+    if float(ok) < 1:
         mode = "eager"
-        torch.cuda.synchronize()
+        big = small = None
+        step.release_graphs()
         dist.barrier()
 
     def run(n, i=0):

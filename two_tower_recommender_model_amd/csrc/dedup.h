@@ -19,6 +19,7 @@ constexpr int DD_TABLE_SHIFT = 40;  // key = table << 40 | row (table < 64, rows
 constexpr int DD_CNT_BITS = 18;     // slot word = key << 18 | count; a step has < 2^18 lookups
 constexpr uint64_t DD_CNT_MASK = (1ull << DD_CNT_BITS) - 1;
 constexpr int DD_INL = 14;          // lookups stored inline per slot
+constexpr int DD_SPH = 2;           // slots per half-wave in the update launch
 
 struct __attribute__((aligned(64))) DSlot {
   uint64_t word;  // DD_EMPTY when free, else key << 18 | lookups of this key in the step
@@ -264,53 +265,86 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) 
   }
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31, hb = lane & 32;
-  const int64_t h = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
-  // the grid covers exactly cap slots (cap is a multiple of 1024): every half-wave has a slot
-  DSlot* sp = ws.slots + h;
-  const int dw = hl < 16 ? reinterpret_cast<const int32_t*>(sp)[hl] : 0;
-  const uint64_t word = ((uint64_t)(uint32_t)__shfl(dw, hb + 1, 64) << 32) | (uint32_t)__shfl(dw, hb, 64);
-  const uint64_t key = word >> DD_CNT_BITS;
-  const int cnt = (int)(word & DD_CNT_MASK);
-  const int item = __shfl(dw, hb + 2 + (hl < DD_INL ? hl : 0), 64);
-  // hot slots (reset by the hot role, one 8-B store) are never taken here
-  const bool active = word != DD_EMPTY && cnt <= DD_INL;
-  const int t = active ? (int)(key >> DD_TABLE_SHIFT) : 0;
-  const int64_t r = active ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
-  const tt_table_meta_t tm = m.tables[t];
-  const int D = tm.dim;
-  const bool col_ok = active && hl * 4 < D;
-  float* wrow = weights + tm.weight_offset + r * D;
-  float* srow = state + tm.state_offset + r;
-  f32x4v wv = col_ok ? *reinterpret_cast<const f32x4v*>(wrow + hl * 4) : (f32x4v)(0.f);
-  const float s_old = active ? *srow : 0.f;
-  const int c = active ? cnt : 0;
-  const int cmax = max(c, __shfl_xor(c, 32, 64));
-  int mine = hl < c ? item : 0x7fffffff;
-  if (cmax > 1) mine = dd_bitonic<32>(mine);
-  f32x4v g = (f32x4v)(0.f);
-  for (int i = 0; i < cmax; i += 2) {
-    const int b0 = __shfl(mine, hb + i, 64);
-    const int b1 = __shfl(mine, hb + min(i + 1, 31), 64);
-    f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
-    if (col_ok && i < c) x0 = *reinterpret_cast<const f32x4v*>(gm.row(b0) + hl * 4);
-    if (col_ok && i + 1 < c) x1 = *reinterpret_cast<const f32x4v*>(gm.row(b1) + hl * 4);
-    if (i < c) g += x0;
-    if (i + 1 < c) g += x1;
+  // DD_SPH slots per half-wave (h and h + cap / DD_SPH), their dependent loads interleaved: the
+  // grid covers exactly cap slots (cap is a multiple of 1024) in one round of resident waves
+  const int64_t hw = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
+  const int64_t nhw = ws.cap / DD_SPH;
+  DSlot* sp[DD_SPH];
+  int dw[DD_SPH];
+#pragma unroll
+  for (int q = 0; q < DD_SPH; ++q) {
+    sp[q] = ws.slots + hw + q * nhw;
+    dw[q] = hl < 16 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : 0;
   }
-  float sq = g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
+  bool active[DD_SPH], col_ok[DD_SPH];
+  int c[DD_SPH], cmax[DD_SPH], mine[DD_SPH], D[DD_SPH];
+  float* wrow[DD_SPH];
+  float* srow[DD_SPH];
+  f32x4v wv[DD_SPH], g[DD_SPH];
+  float s_old[DD_SPH];
 #pragma unroll
-  for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
-  if (active) {
-    const float snew = s_old + sq / (float)D;
-    const float stdv = sqrtf(snew) + eps;
-    if (col_ok) {
+  for (int q = 0; q < DD_SPH; ++q) {
+    const uint64_t word = ((uint64_t)(uint32_t)__shfl(dw[q], hb + 1, 64) << 32) | (uint32_t)__shfl(dw[q], hb, 64);
+    const uint64_t key = word >> DD_CNT_BITS;
+    const int cnt = (int)(word & DD_CNT_MASK);
+    const int item = __shfl(dw[q], hb + 2 + (hl < DD_INL ? hl : 0), 64);
+    // hot slots (reset by the hot role, one 8-B store) are never taken here
+    active[q] = word != DD_EMPTY && cnt <= DD_INL;
+    const int t = active[q] ? (int)(key >> DD_TABLE_SHIFT) : 0;
+    const int64_t r = active[q] ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
+    const tt_table_meta_t tm = m.tables[t];
+    D[q] = tm.dim;
+    col_ok[q] = active[q] && hl * 4 < D[q];
+    wrow[q] = weights + tm.weight_offset + r * D[q];
+    srow[q] = state + tm.state_offset + r;
+    wv[q] = col_ok[q] ? *reinterpret_cast<const f32x4v*>(wrow[q] + hl * 4) : (f32x4v)(0.f);
+    s_old[q] = active[q] ? *srow[q] : 0.f;
+    c[q] = active[q] ? cnt : 0;
+    cmax[q] = max(c[q], __shfl_xor(c[q], 32, 64));
+    mine[q] = hl < c[q] ? item : 0x7fffffff;
+    g[q] = (f32x4v)(0.f);
+  }
+  bool single = true;  // wave-uniform: every slot of the wave has at most one lookup
 #pragma unroll
-      for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
-      *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
+  for (int q = 0; q < DD_SPH; ++q) single = single && cmax[q] <= 1;
+  if (single) {
+    // the common case (uniform ids): one gradient row per slot, all loads in flight together
+#pragma unroll
+    for (int q = 0; q < DD_SPH; ++q)
+      if (col_ok[q] && c[q] == 1) g[q] += *reinterpret_cast<const f32x4v*>(gm.row(mine[q]) + hl * 4);
+  } else {
+#pragma unroll
+    for (int q = 0; q < DD_SPH; ++q) {
+      if (cmax[q] > 1) mine[q] = dd_bitonic<32>(mine[q]);
+      for (int i = 0; i < cmax[q]; i += 2) {
+        const int b0 = __shfl(mine[q], hb + i, 64);
+        const int b1 = __shfl(mine[q], hb + min(i + 1, 31), 64);
+        f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
+        if (col_ok[q] && i < c[q]) x0 = *reinterpret_cast<const f32x4v*>(gm.row(b0) + hl * 4);
+        if (col_ok[q] && i + 1 < c[q]) x1 = *reinterpret_cast<const f32x4v*>(gm.row(b1) + hl * 4);
+        if (i < c[q]) g[q] += x0;
+        if (i + 1 < c[q]) g[q] += x1;
+      }
     }
-    if (hl == 0) {
-      *srow = snew;
-      sp->word = DD_EMPTY;
+  }
+#pragma unroll
+  for (int q = 0; q < DD_SPH; ++q) {
+    float sq = g[q][0] * g[q][0] + g[q][1] * g[q][1] + g[q][2] * g[q][2] + g[q][3] * g[q][3];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (active[q]) {
+      const float snew = s_old[q] + sq / (float)D[q];
+      const float stdv = sqrtf(snew) + eps;
+      if (col_ok[q]) {
+        f32x4v w = wv[q];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[q][v]) / stdv;
+        *reinterpret_cast<f32x4v*>(wrow[q] + hl * 4) = w;
+      }
+      if (hl == 0) {
+        *srow[q] = snew;
+        sp[q]->word = DD_EMPTY;
+      }
     }
   }
 }

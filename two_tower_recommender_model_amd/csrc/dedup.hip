@@ -122,7 +122,7 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
   a.lr = lr;
   a.eps = eps;
   a.hot_wgs = (int)std::min<int64_t>(64, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
-  *grid = a.hot_wgs + a.ws.cap / 8;
+  *grid = a.hot_wgs + a.ws.cap / (8 * DD_SPH);
   return TT_OK;
 }
 

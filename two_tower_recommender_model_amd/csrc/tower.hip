@@ -46,6 +46,8 @@ struct TowerArgs {
   const float* params;  // flat fp32 (bias read from here)
   const __bf16* wb;     // bf16 W  [out][in] per (t,l), flat like params' W blocks
   const __bf16* wtb;    // bf16 W^T [in][out]
+  const __bf16* wbf;    // the same two copies in MFMA B-fragment order (frag_off): every fragment
+  const __bf16* wtbf;   //   load of a wave is 1 KB contiguous (full 128-B lines, one request each)
   int64_t woff[2][MAXL];  // element offset of W_(t,l) in params
   int64_t boff[2][MAXL];  // element offset of b_(t,l) in params
   int64_t wcoff[2][MAXL]; // element offset of W_(t,l) in the bf16 copies
@@ -78,7 +80,11 @@ struct TowerArgs {
   const int32_t* gpos[2];
   const float* gsrc[2];
   float* gdst[2];
+  int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
+  int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
 };
+#define T1_STAMP(k) \
+  do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 
 __device__ __forceinline__ float lbl(const void* p, int dt, int64_t i) {
   if (dt == TT_I32) return (float)reinterpret_cast<const int32_t*>(p)[i];
@@ -364,9 +370,15 @@ struct Frags {
   bf16x8 f[4][2];
 };
 
-__device__ __forceinline__ void load_frags(Frags& fr, const __bf16* Wg, int ld, int K, int N, int w4) {
+// B-fragment order of a [N][K] matrix (K % 32 == 0): the 16 x 32 fragment (n-tile nt, k-step s) is
+// 64 lanes x 8 contiguous elements, lane q * 16 + r holding row nt * 16 + r, columns s * 32 + q * 8 ..
+__host__ __device__ __forceinline__ int64_t frag_off(int n, int k, int K) {
+  return ((int64_t)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + ((k & 31) >> 3) * 16 + (n & 15)) * 8 + (k & 7);
+}
+
+// fragments of W (fragment-major copy, see frag_off): one 1-KB contiguous load per (tile, k-step)
+__device__ __forceinline__ void load_frags(Frags& fr, const __bf16* Wf, int ld, int K, int N, int w4) {
   const int lane = threadIdx.x & 63;
-  const int r = lane & 15, q = lane >> 4;
   const int nk = K >> 5, nt = N >> 4;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -374,7 +386,7 @@ __device__ __forceinline__ void load_frags(Frags& fr, const __bf16* Wg, int ld, 
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       if (tile < nt && s < nk)
-        fr.f[s][j] = *reinterpret_cast<const bf16x8*>(Wg + (int64_t)(tile * 16 + r) * ld + s * 32 + q * 8);
+        fr.f[s][j] = *reinterpret_cast<const bf16x8*>(Wf + ((int64_t)(tile * nk + s) * 64 + lane) * 8);
   }
 }
 
@@ -449,6 +461,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     return;
   }
   const int t = wid >> 2, w4 = wid & 3;
+  T1_STAMP(0);
   const int tt = threadIdx.x & 255;  // thread index inside the tower group
   const int r16 = lane & 15, q4 = lane >> 4;
   const int64_t B = a.B;
@@ -483,8 +496,8 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
             rpos[i] = a.gpos[t][gm];
             if (rpos[i] >= 0) src[i] = a.gsrc[t] + (int64_t)rpos[i] * in + c4;
           } else {
-            const int64_t id = load_id(a.gcol[t], a.gid_dtype, gm);
-            if (id != 0) src[i] = a.gtab[t] + py_mod64(id, a.gmod[t]) * in + c4;
+            const int64_t id = (a.dbg & 32) ? 1 : load_id(a.gcol[t], a.gid_dtype, gm);
+            if (id != 0) src[i] = a.gtab[t] + ((a.dbg & 4) ? 0 : py_mod64(id, a.gmod[t])) * in + c4;
           }
         }
       }
@@ -504,10 +517,14 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     }
   }
   Frags f0, f1, g1, g0;
-  load_frags(f0, a.wb + a.wcoff[t][0], in, in, W0, w4);      // W0 [W0][in]
-  load_frags(f1, a.wb + a.wcoff[t][1], W0, W0, W1, w4);      // W1 [W1][W0]
-  load_frags(g1, a.wtb + a.wcoff[t][1], W1, W1, W0, w4);     // W1^T [W0][W1]
-  load_frags(g0, a.wtb + a.wcoff[t][0], W0, W0, in, w4);     // W0^T [in][W0]
+  if (a.dbg & 16) {
+    for (int s_ = 0; s_ < 4; ++s_) for (int j_ = 0; j_ < 2; ++j_) { f0.f[s_][j_] = (bf16x8)(__bf16)0.f; f1.f[s_][j_] = f0.f[s_][j_]; g1.f[s_][j_] = f0.f[s_][j_]; g0.f[s_][j_] = f0.f[s_][j_]; }
+  } else {
+  load_frags(f0, a.wbf + a.wcoff[t][0], in, in, W0, w4);      // W0 [W0][in]
+  load_frags(f1, a.wbf + a.wcoff[t][1], W0, W0, W1, w4);      // W1 [W1][W0]
+  load_frags(g1, a.wtbf + a.wcoff[t][1], W1, W1, W0, w4);     // W1^T [W0][W1]
+  load_frags(g0, a.wtbf + a.wcoff[t][0], W0, W0, in, w4);     // W0^T [in][W0]
+  }
   float bias0[2], bias1[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -533,8 +550,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     }
   }
   __syncthreads();
+  T1_STAMP(1);
   // X^T for T2's dW0 (fire-and-forget stores)
-  for (int e = tt; e < in * (TR / 8); e += 256) {
+  for (int e = tt; e < ((a.dbg & 1) ? 0 : in * (TR / 8)); e += 256) {
     const int k = e / (TR / 8), rb = (e % (TR / 8)) * 8;
     bf16x8 v;
     for (int j = 0; j < 8; ++j) v[j] = xs[t][(rb + j) * LSTR + k];
@@ -565,10 +583,11 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         hs[t][row * LSTR + col] = pk[rr];
       }
       const int64_t gm = m0 + i * 16 + q4 * 4;
-      store_t4(a.act + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
+      if (!(a.dbg & 1)) store_t4(a.act + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
     }
   }
   __syncthreads();
+  T1_STAMP(2);
   // ---- 2. layer 1: out = relu(h W1^T + b1) (fp32)
   mma_frags(acc, hs[t], f1, W0, W1, w4);
 #pragma unroll
@@ -584,6 +603,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       }
   }
   __syncthreads();
+  T1_STAMP(3);
   // ---- 3. logits, BCE, dlogit: 16 threads per row
   {
     const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
@@ -606,6 +626,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     }
   }
   __syncthreads();
+  T1_STAMP(4);
   // ---- 4. dZ1 = dlogit * other * (self > 0): thread -> (column, 8 consecutive rows)
   for (int c = tt >> 2; c < W1; c += 64) {
     const int rb = (tt & 3) * 8;
@@ -624,7 +645,8 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     if ((tt & 3) == 0) a.dbpart[(((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW + c] = s;
     const int64_t gm = m0 + rb;
     __bf16* dst = a.dzt + (((int64_t)t * MAXL + 1) * MAXW + c) * B + gm;
-    if (gm + 8 <= B) {
+    if (a.dbg & 1) {
+    } else if (gm + 8 <= B) {
       *reinterpret_cast<bf16x8*>(dst) = v;
     } else {
       for (int j = 0; j < 8; ++j)
@@ -632,6 +654,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     }
   }
   __syncthreads();
+  T1_STAMP(5);
   // ---- 5. dZ0 = (dZ1 W1) * (h > 0)  -> xs (X is no longer needed)
   mma_frags(acc, dzs[t], g1, W1, W0, w4);
 #pragma unroll
@@ -652,13 +675,14 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         xs[t][row * LSTR + col] = pk[rr];
       }
       const int64_t gm = m0 + i * 16 + q4 * 4;
-      store_t4(a.dzt + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
+      if (!(a.dbg & 1)) store_t4(a.dzt + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
     }
     s += __shfl_xor(s, 16, 64);
     s += __shfl_xor(s, 32, 64);
     if (q4 == 0) a.dbpart[(((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW + col] = s;
   }
   __syncthreads();
+  T1_STAMP(6);
   // ---- 6. dX = dZ0 W0 -> LDS (outf is free since phase 4) -> pooled gradient, whole rows
   mma_frags(acc, xs[t], g0, W0, in, w4);
 #pragma unroll
@@ -677,6 +701,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     a.loss_part[blockIdx.x] = p;
   }
   __syncthreads();
+  T1_STAMP(7);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i < nxv) {
@@ -690,9 +715,10 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         else
           dst = a.gpooled + gm * a.ldp + incol + c4;
       }
-      if (dst) *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
+      if (dst && !(a.dbg & 2)) *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
     }
   }
+  T1_STAMP(15);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -776,8 +802,13 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
       }
     return;
   }
-  const int s = (int)(bid / a.ntiles);
-  const WgradTile tl = tiles[bid % a.ntiles];
+  // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs (bid % 8), so logical
+  // tile-workgroup (bid % 8) * n / 8 + bid / 8 puts a contiguous 1/8 of the (slice, tile) list —
+  // whole slices, whose tiles re-read the same operand strips — on one XCD and its L2
+  int lb = bid;
+  if (nwg_tiles % 8 == 0) lb = (int)((bid % 8) * (nwg_tiles / 8) + bid / 8);
+  const int s = (int)(lb / a.ntiles);
+  const WgradTile tl = tiles[lb % a.ntiles];
   const int64_t B = a.B;
   const __bf16* Z = a.dzt + ((int64_t)tl.t * MAXL + tl.l) * MAXW * B;  // [n][B]
   const __bf16* A = tl.l == 0 ? a.xt + (int64_t)tl.t * a.in_max * B
@@ -906,6 +937,8 @@ struct UpdateArgs {
   int64_t seg_wc[2 * 2 * MAXL];  // bf16 copy offset for W segments
   __bf16* wb;
   __bf16* wtb;
+  __bf16* wbf;
+  __bf16* wtbf;
   float lr, beta1, beta2, eps, wd;
   int64_t* step_state;
   int do_adam;
@@ -962,6 +995,8 @@ __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
       const int64_t n = e / K, k = e - n * K;
       a.wb[a.seg_wc[sg] + e] = (__bf16)p;
       a.wtb[a.seg_wc[sg] + k * N + n] = (__bf16)p;
+      a.wbf[a.seg_wc[sg] + frag_off((int)n, (int)k, K)] = (__bf16)p;   // W as [N][K]
+      a.wtbf[a.seg_wc[sg] + frag_off((int)k, (int)n, N)] = (__bf16)p;  // W^T as [K][N]
     }
   }
   if (a.do_adam && !a.adam_pre) {
@@ -991,7 +1026,7 @@ struct TowerLayout {
   int64_t mslice;
   int ntiles;
   // workspace carve (bytes)
-  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_tiles, total;
+  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_tiles, o_dbg, total;
 };
 
 static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) {
@@ -1051,7 +1086,10 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.o_counter = take(64);
   L.o_wb = take((size_t)L.PW * 2);
   L.o_wtb = take((size_t)L.PW * 2);
+  L.o_wbf = take((size_t)L.PW * 2);
+  L.o_wtbf = take((size_t)L.PW * 2);
   L.o_tiles = take((size_t)nt * sizeof(WgradTile));
+  L.o_dbg = take((size_t)L.nwg * 16 * sizeof(int64_t));
   L.total = off;
   *lay = L;
   return TT_OK;
@@ -1125,6 +1163,8 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   a.params = params;
   a.wb = reinterpret_cast<const __bf16*>(ws + L.o_wb);
   a.wtb = reinterpret_cast<const __bf16*>(ws + L.o_wtb);
+  a.wbf = reinterpret_cast<const __bf16*>(ws + L.o_wbf);
+  a.wtbf = reinterpret_cast<const __bf16*>(ws + L.o_wtbf);
   for (int t = 0; t < 2; ++t)
     for (int l = 0; l < MAXL; ++l) {
       a.woff[t][l] = L.woff[t][l];
@@ -1142,6 +1182,8 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   a.loss_part = reinterpret_cast<float*>(ws + L.o_losspart);
   a.in_max = L.in_max;
   a.nwg = L.nwg;
+  if (const char* e = getenv("TT_T1_DEBUG")) a.dbg = atoi(e);
+  if (a.dbg & 8) a.stamps = reinterpret_cast<int64_t*>(ws + L.o_dbg);
   const int i0 = shape->in_dim[0], i1 = shape->in_dim[1], w0 = shape->width[0], w1 = shape->width[1];
   const dim3 g(L.nwg), b512(T1_THREADS);
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
@@ -1343,6 +1385,8 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
   a.seg_off[sg] = L.P;
   a.wb = reinterpret_cast<__bf16*>(ws + L.o_wb);
   a.wtb = reinterpret_cast<__bf16*>(ws + L.o_wtb);
+  a.wbf = reinterpret_cast<__bf16*>(ws + L.o_wbf);
+  a.wtbf = reinterpret_cast<__bf16*>(ws + L.o_wtbf);
   a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.wd = weight_decay;
   a.step_state = step_state;
   a.do_adam = do_adam;
