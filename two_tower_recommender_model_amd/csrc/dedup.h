@@ -310,8 +310,10 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) 
   if (single) {
     // the common case (uniform ids): one gradient row per slot, all loads in flight together
 #pragma unroll
-    for (int q = 0; q < DD_SPH; ++q)
-      if (col_ok[q] && c[q] == 1) g[q] += *reinterpret_cast<const f32x4v*>(gm.row(mine[q]) + hl * 4);
+    for (int q = 0; q < DD_SPH; ++q) {
+      const int b0 = __shfl(mine[q], hb, 64);  // the slot's one lookup, held by lane 0 of the half
+      if (col_ok[q] && c[q] == 1) g[q] += *reinterpret_cast<const f32x4v*>(gm.row(b0) + hl * 4);
+    }
   } else {
 #pragma unroll
     for (int q = 0; q < DD_SPH; ++q) {
