@@ -146,26 +146,29 @@ def lookup_stats(step, batches):
 
 def launch_bytes(step, nnz: int, uniq: int):
     """Algorithmic HBM bytes (and MFMA flops) per launch of the one-stream step:
-    t1 = gather + towers fwd/bwd + dedup insert; k2 = T2 weight gradients + fused row-wise Adagrad;
-    t3 = Adam. The embedding-path total follows SURVEY.md 8(d)."""
+    t1 = gather + towers fwd/bwd + dedup insert; t2 = tower weight gradients (+ Adam scalars);
+    k3 = T3 (slab reduction + Adam + bf16 copies) + the fused row-wise Adagrad. The embedding-path
+    total follows SURVEY.md 8(d)."""
     D, B, F = step.dims[0], step.B, step.F
     L = step.layer_sizes
     idb = 8 if step.id_dtype == torch.int64 else 4
-    ins = [step.in_q, step.in_c]
     macs = sum(i * o for i, o in zip([D] + L[:-1], L))
     opnd = 2 * B * 2 * (D + L[0] + (L[0] + L[1]))  # bf16 X^T, act^T, dZ^T of both towers (T1 -> T2)
     P = step.params.numel()
-    S = max(1, min(400 // max(1, sum((w // 32) * (k // 32) for w, k in zip(L, [D] + L[:-1])) * 2), -(-B // 512), 64))
+    cdiv = lambda a, b: -(-a // b)  # noqa: E731
+    S = min(64, cdiv(B, 256))  # staged T2 slices of whole 256-row passes (tower.hip tower_layout)
+    S = cdiv(B, cdiv(cdiv(B, S), 256) * 256)
     t1 = (F * B * idb + B * 4 + nnz * 4 * D + B * 4 + F * B * 4 * D + opnd + nnz * 20)
     emb_upd = uniq * (64 + 8 * D + 8) + nnz * 4 * D
-    k2 = emb_upd + opnd + S * P * 4
-    t3 = S * P * 4 + 6 * P * 4 + 4 * P
+    t2 = opnd + S * P * 4
+    k3 = emb_upd + S * P * 4 + 6 * P * 4 + 4 * P
     emb_path = F * B * (1 * (8 + 8 + 4 * D) + 4 + 4 * D + 4 * D) + uniq * (8 * D + 8)  # 8(d), L = 1
     return {"t1": {"bytes": t1, "flop": 8 * B * macs, "what": "tower_l2_kernel: EBC gather + both towers fwd/bwd "
                                                               "+ dedup insert"},
-            "k2": {"bytes": k2, "flop": 4 * B * macs, "emb_bytes": emb_upd,
-                   "what": "tower_wgrad_dedup_kernel: T2 weight gradients + fused row-wise Adagrad"},
-            "t3": {"bytes": t3, "flop": 0, "what": "tower_update_kernel: slab reduction + Adam + bf16 copies"},
+            "t2": {"bytes": t2, "flop": 4 * B * macs, "what": "tower_wgrad_kernel: tower weight gradients (staged "
+                                                              "operand strips) + Adam step scalars"},
+            "k3": {"bytes": k3, "flop": 0, "emb_bytes": emb_upd,
+                   "what": "tower_update_dedup_kernel: fused row-wise Adagrad + slab reduction + Adam + bf16 copies"},
             "_emb_path_bytes": emb_path}
 
 
@@ -184,7 +187,7 @@ def pmc_traffic(kernel_name: str):
     return None, None
 
 
-KERNEL_NAMES = {"t1": "tower_l2_kernel", "k2": "tower_wgrad_dedup_kernel", "t3": "tower_update_kernel"}
+KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_kernel", "k3": "tower_update_dedup_kernel"}
 
 
 def roofline_report(kern, timed, nnz, uniq, step, B):
@@ -206,7 +209,7 @@ def roofline_report(kern, timed, nnz, uniq, step, B):
                 "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq}
     dom = max((n for n in out if "ms" in out[n]), key=lambda n: out[n]["ms"])
     traffic, src = pmc_traffic(KERNEL_NAMES[dom])
-    emb_ms = timed.get("t1", 0.0) + timed.get("k2", 0.0)
+    emb_ms = timed.get("t1", 0.0) + timed.get("k3", 0.0)
     ach = out[dom]["GB/s"]
     return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
@@ -217,7 +220,7 @@ def roofline_report(kern, timed, nnz, uniq, step, B):
                                "GB/s": round(emb_path_bytes / emb_ms / 1e6, 1) if emb_ms else None,
                                "frac": round(emb_path_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4) if emb_ms else None,
                                "note": "SURVEY 8(d) bytes over the in-step time of the launches that carry the "
-                                       "embedding work (T1 gather+insert, K2 Adagrad); both also run tower work"}}
+                                       "embedding work (T1 gather+insert, K3 Adagrad); both also run tower work"}}
 
 
 def run_single(args):
@@ -267,7 +270,7 @@ def run_single(args):
             from two_tower_recommender_model_amd.graph_timing import GraphLaunchTimer
 
             step.capture_pool(batches, steps_per_graph=k, keep_graph=True)
-            names = ["t1", "k2", "t3"]
+            names = ["t1", "t2", "k3"]
             timers = [GraphLaunchTimer(g, list(range(3 * k))) for g in step.pool_graphs]
             acc = {n: [] for n in names}
             n_done, j = 0, 0

@@ -301,8 +301,26 @@ int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, flo
                                    int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
                                    size_t dedup_ws_bytes, int64_t dedup_max_lookups, int64_t* adam_step_state,
                                    float adam_lr, float adam_beta1, float adam_beta2, void* stream);
-/* T3 after tt_tower_wgrad_rowwise_adagrad(adam_step_state != NULL): reduction + Adam with the
- * precomputed scalars + bf16 copies. */
+/* T2 alone (tt_tower_wgrad) that also advances the Adam step and precomputes the step's
+ * bias-correction scalars for tt_tower_update_pre / tt_tower_update_pre_rowwise_adagrad (the fused
+ * single-GPU step: T1 -> this -> T3 + embedding update). Replaces the towers' autograd weight
+ * gradients (03_model_training.py:455) and the step-count part of Adam (:826-829). */
+int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                       int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2, void* stream);
+/* T3 (as tt_tower_update_pre) and the embedding backward + row-wise Adagrad (as
+ * tt_dedup_rowwise_adagrad, emb_eps its eps) in ONE launch after tt_tower_wgrad_pre: the update's
+ * slot workgroups and T3's parameter workgroups share one round of resident waves. Replaces Adam's
+ * parameter update (03_model_training.py:826-829) and the fused TBE backward with RowWiseAdagrad
+ * (:791-795). */
+int tt_tower_update_pre_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
+                                        float* exp_avg_sq, float eps, float beta1, float beta2, float weight_decay,
+                                        float* grads_out, void* workspace, size_t ws_bytes,
+                                        const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
+                                        int64_t emb_B, const float* grad, int64_t ldg, float* weights, float* state,
+                                        float lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                        int64_t dedup_max_lookups, void* stream);
+/* T3 after tt_tower_wgrad_rowwise_adagrad / tt_tower_wgrad_pre (adam_step_state != NULL): reduction
+ * + Adam with the precomputed scalars + bf16 copies. */
 int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
                         size_t ws_bytes, void* stream);

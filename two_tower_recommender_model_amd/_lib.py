@@ -140,6 +140,12 @@ SIGNATURES = {
          _vp, _f32, _f32, _f32, _vp],
     ),
     "tt_tower_update_pre": (_int, [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp]),
+    "tt_tower_wgrad_pre": (_int, [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _vp]),
+    "tt_tower_update_pre_rowwise_adagrad": (
+        _int,
+        [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64,
+         _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
+    ),
     "tt_shard_route_workspace_bytes": (_sz, [_int, _i64]),
     "tt_shard_route_cols": (
         _int,
@@ -189,6 +195,8 @@ COMPUTE_ENTRY_POINTS = [
     "tt_dedup_rowwise_adagrad",
     "tt_tower_fwd_bwd_indexed",
     "tt_tower_wgrad_rowwise_adagrad",
+    "tt_tower_wgrad_pre",
+    "tt_tower_update_pre_rowwise_adagrad",
     "tt_shard_route_cols",
     "tt_shard_gather_rows",
     "tt_tower_adam_grads",

@@ -19,7 +19,7 @@ constexpr int DD_TABLE_SHIFT = 40;  // key = table << 40 | row (table < 64, rows
 constexpr int DD_CNT_BITS = 18;     // slot word = key << 18 | count; a step has < 2^18 lookups
 constexpr uint64_t DD_CNT_MASK = (1ull << DD_CNT_BITS) - 1;
 constexpr int DD_INL = 14;          // lookups stored inline per slot
-constexpr int DD_SPH = 2;           // slots per half-wave in the update launch
+constexpr int DD_SPH = 4;           // slots per half-wave in the update launch
 
 struct __attribute__((aligned(64))) DSlot {
   uint64_t word;  // DD_EMPTY when free, else key << 18 | lookups of this key in the step
@@ -34,7 +34,10 @@ struct DedupWs {
   int64_t cap;
   int64_t L;
   int32_t hot_cap;  // entries of `hot` (a step inserts <= L lookups: <= L / 14 hot rows)
+  int64_t* stamps;  // EXPERIMENT (TT_DD_STAMPS): [update workgroups][8] s_memrealtime per phase
 };
+#define DD_STAMP(k) \
+  do { if (ws.stamps && threadIdx.x == 0) ws.stamps[(int64_t)bid * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 
 __device__ __forceinline__ uint64_t dd_mix64(uint64_t x) {
   x ^= x >> 33;
@@ -116,15 +119,39 @@ struct DdUpdateArgs {
   int hot_wgs;         // workgroups of the hot role; the slot role has ws.cap / 8 more
 };
 
+// Per-lane table / feature meta from LDS: indexing the kernel-argument arrays by a per-lane value
+// compiles to a vector load from the kernarg segment — one more dependent memory hop (and an
+// in-order vmcnt wait) in front of every row access. The update workgroup copies the meta of its
+// T tables and F features into LDS once (overlapping its first slot load) and reads it per lane.
+struct DdMeta {
+  int64_t woff[TT_MAX_TABLES];
+  int64_t soff[TT_MAX_TABLES];
+  int64_t frow[TT_MAX_FEATURES];
+  int64_t foff[TT_MAX_FEATURES];
+  int32_t dim[TT_MAX_TABLES];
+};
+
+__device__ __forceinline__ void dd_meta_fill(const EmbMeta& m, DdMeta* lm) {
+  for (int u = threadIdx.x; u < m.T; u += blockDim.x) {
+    lm->woff[u] = m.tables[u].weight_offset;
+    lm->soff[u] = m.tables[u].state_offset;
+    lm->dim[u] = m.tables[u].dim;
+  }
+  for (int u = threadIdx.x; u < m.F; u += blockDim.x) {
+    lm->frow[u] = m.features[u].out_row;
+    lm->foff[u] = m.features[u].out_offset;
+  }
+}
+
+// lookup i = f * B + b -> its gradient row (features[f].out_row + b), column features[f].out_offset
 struct GradMap {
   const float* g;
   int64_t ldg;
-  int64_t B;
-  const tt_feature_meta_t* feats;
+  uint32_t B;  // lookups < 2^18 (DD_CNT_BITS): 32-bit division
+  const DdMeta* lm;
   __device__ __forceinline__ const float* row(int i) const {
-    const int f = (int)(i / B);
-    const int64_t b = i - (int64_t)f * B;
-    return g + (feats[f].out_row + b) * ldg + feats[f].out_offset;
+    const uint32_t f = (uint32_t)i / B;
+    return g + (lm->frow[f] + (int64_t)((uint32_t)i - f * B)) * ldg + lm->foff[f];
   }
 };
 
@@ -147,13 +174,17 @@ __device__ __forceinline__ int dd_bitonic(int v) {
 
 constexpr int DD_HOT_PT = 4;                 // lookups per thread per scan pass
 constexpr int DD_HOT_CH = 256 * DD_HOT_PT;  // lookups scanned per pass of a hot workgroup (LDS list)
+// LDS of the hot role (list + wave totals + group partials), provided by the launching kernel so a
+// combined launch can overlay it on its other roles' LDS
+constexpr int DD_SMEM_HOT = DD_HOT_CH * 4 + 16 + 8 * 32 * 16;
+constexpr int DD_SMEM = DD_SMEM_HOT + (int)sizeof(DdMeta);  // + the per-workgroup meta copy
 
-__device__ __forceinline__ void dd_hot_role(const EmbMeta& m, const GradMap& gm, int64_t n,
+__device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
                                             float* __restrict__ weights, float* __restrict__ state, float lr,
-                                            float eps, const DedupWs& ws, int hot_wgs, int bid) {
-  __shared__ int list[DD_HOT_CH];
-  __shared__ int wtot[4];
-  __shared__ f32x4v part[8][32];
+                                            float eps, const DedupWs& ws, int hot_wgs, int bid, char* smem) {
+  f32x4v (*part)[32] = reinterpret_cast<f32x4v (*)[32]>(smem);       // [8][32], 16-B aligned
+  int* list = reinterpret_cast<int*>(smem + 8 * 32 * 16);             // [DD_HOT_CH]
+  int* wtot = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4);  // [4]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = tid >> 5, hl = tid & 31;
   const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
@@ -162,8 +193,7 @@ __device__ __forceinline__ void dd_hot_role(const EmbMeta& m, const GradMap& gm,
     const uint64_t key = ws.slots[h].word >> DD_CNT_BITS;
     const int t = (int)(key >> DD_TABLE_SHIFT);
     const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
-    const tt_table_meta_t tm = m.tables[t];
-    const int D = tm.dim;
+    const int D = gm.lm->dim[t];
     const bool col_ok = hl * 4 < D;
     f32x4v acc = (f32x4v)(0.f);
     int seen = 0;  // matches before this pass (global position of list[0])
@@ -218,8 +248,8 @@ __device__ __forceinline__ void dd_hot_role(const EmbMeta& m, const GradMap& gm,
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
       if (lane < 32) {
-        float* wrow = weights + tm.weight_offset + r * D;
-        float* srow = state + tm.state_offset + r;
+        float* wrow = weights + gm.lm->woff[t] + r * D;
+        float* srow = state + gm.lm->soff[t] + r;
         const float snew = *srow + sq / (float)D;
         const float stdv = sqrtf(snew) + eps;
         if (col_ok) {
@@ -252,15 +282,20 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
                       void* workspace, size_t ws_bytes, int64_t max_lookups, DdUpdateArgs& a, int64_t* grid);
 
 // One workgroup (256 threads) of the update launch: bid < hot_wgs -> hot role, else 8 slots.
-__device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) {
+// smem: DD_SMEM bytes of 16-B aligned LDS.
+__device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, char* smem) {
   const EmbMeta& m = a.m;
   const DedupWs& ws = a.ws;
   float* __restrict__ weights = a.weights;
   float* __restrict__ state = a.state;
   const float lr = a.lr, eps = a.eps;
-  const GradMap gm{a.grad, a.ldg, m.B, m.features};
+  DD_STAMP(0);
+  DdMeta* lm = reinterpret_cast<DdMeta*>(smem + DD_SMEM_HOT);
+  const GradMap gm{a.grad, a.ldg, (uint32_t)m.B, lm};
   if (bid < a.hot_wgs) {
-    dd_hot_role(m, gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid);
+    dd_meta_fill(m, lm);
+    __syncthreads();
+    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem);
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -276,6 +311,9 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) 
     sp[q] = ws.slots + hw + q * nhw;
     dw[q] = hl < 16 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : 0;
   }
+  dd_meta_fill(m, lm);  // beside the slot loads
+  __syncthreads();
+  DD_STAMP(1);
   bool active[DD_SPH], col_ok[DD_SPH];
   int c[DD_SPH], cmax[DD_SPH], mine[DD_SPH], D[DD_SPH];
   float* wrow[DD_SPH];
@@ -292,11 +330,10 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) 
     active[q] = word != DD_EMPTY && cnt <= DD_INL;
     const int t = active[q] ? (int)(key >> DD_TABLE_SHIFT) : 0;
     const int64_t r = active[q] ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
-    const tt_table_meta_t tm = m.tables[t];
-    D[q] = tm.dim;
+    D[q] = lm->dim[t];
     col_ok[q] = active[q] && hl * 4 < D[q];
-    wrow[q] = weights + tm.weight_offset + r * D[q];
-    srow[q] = state + tm.state_offset + r;
+    wrow[q] = weights + lm->woff[t] + r * D[q];
+    srow[q] = state + lm->soff[t] + r;
     wv[q] = col_ok[q] ? *reinterpret_cast<const f32x4v*>(wrow[q] + hl * 4) : (f32x4v)(0.f);
     s_old[q] = active[q] ? *srow[q] : 0.f;
     c[q] = active[q] ? cnt : 0;
@@ -329,6 +366,7 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) 
       }
     }
   }
+  DD_STAMP(2);
 #pragma unroll
   for (int q = 0; q < DD_SPH; ++q) {
     float sq = g[q][0] * g[q][0] + g[q][1] * g[q][1] + g[q][2] * g[q][2] + g[q][3] * g[q][3];
@@ -349,6 +387,7 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid) 
       }
     }
   }
+  DD_STAMP(3);
 }
 
 

@@ -49,6 +49,8 @@ size_t dedup_layout(void* base, int64_t L, DedupWs* w) {
   t.lkey = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * L));
   t.hot = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (L / (DD_INL + 1) + 1)));
   t.ctr = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
+  int64_t* dbg = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * 8 * (cap / (8 * DD_SPH) + 64)));
+  t.stamps = getenv("TT_DD_STAMPS") ? dbg : nullptr;
   t.cap = cap;
   t.L = L;
   t.hot_cap = (int32_t)(L / (DD_INL + 1) + 1);
@@ -84,7 +86,10 @@ __global__ void __launch_bounds__(64) dd_insert_segments_kernel(const int64_t* _
 }
 
 // ---- update: dd_update_block (dedup.h) ----------------------------------------------------------
-__global__ void __launch_bounds__(256) dd_adagrad_kernel(DdUpdateArgs a) { dd_update_block(a, (int)blockIdx.x); }
+__global__ void __launch_bounds__(256) dd_adagrad_kernel(DdUpdateArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[DD_SMEM];
+  dd_update_block(a, (int)blockIdx.x, smem);
+}
 
 static int check_dd_ws(void* workspace, size_t ws_bytes, int64_t max_lookups, const char* what) {
   if (max_lookups < 1 || max_lookups >= (int64_t)DD_CNT_MASK)
@@ -121,7 +126,7 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
   a.state = state;
   a.lr = lr;
   a.eps = eps;
-  a.hot_wgs = (int)std::min<int64_t>(64, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
+  a.hot_wgs = (int)std::min<int64_t>(32, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
   *grid = a.hot_wgs + a.ws.cap / (8 * DD_SPH);
   return TT_OK;
 }

@@ -439,7 +439,10 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __shared__ float dlog[TR];
   __shared__ float lpart[TR];
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid via readfirstlane: the compiler then knows t (below) is wave-uniform and reads a.gcol[t],
+  // a.gtab[t], ... with scalar loads (a per-lane index into the kernarg arrays is a vector load from
+  // the kernarg segment: one more dependent memory hop in front of the row gather)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wid == 8) {
     // ---- the dedup wave: files this workgroup's 2 x TR lookups (gather + dedup) into the hash
     // table; its CAS round trips count only in ITS vmcnt, so the 8 compute waves never wait on
@@ -449,15 +452,18 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     const bool own = a.dd_on && gm < a.B;
     DdPend p;
     if (own) {
-      const int64_t id = load_id(a.gcol[tq], a.gid_dtype, gm);
-      const uint64_t key = id != 0 ? (((uint64_t)a.dd_table[tq] << DD_TABLE_SHIFT) |
-                                      (uint64_t)py_mod64(id, a.gmod[tq]))
-                                   : DD_EMPTY;
+      // per-lane tower: select between the two towers' kernel arguments (no dynamic kernarg index)
+      const int64_t id = load_id(tq ? a.gcol[1] : a.gcol[0], a.gid_dtype, gm);
+      const int64_t mod = tq ? a.gmod[1] : a.gmod[0];
+      const uint64_t tab = (uint64_t)(tq ? a.dd_table[1] : a.dd_table[0]);
+      const uint64_t key = id != 0 ? ((tab << DD_TABLE_SHIFT) | (uint64_t)py_mod64(id, mod)) : DD_EMPTY;
       dd_insert_begin(a.dd, key, (int32_t)(tq * a.B + gm), p);
     }
 #pragma unroll 1
     for (int k = 0; k < T1_BARRIERS; ++k) __syncthreads();
+    if (a.stamps && lane == 0) a.stamps[(int64_t)blockIdx.x * 16 + 9] = (int64_t)__builtin_amdgcn_s_memrealtime();
     if (own) dd_insert_finish(a.dd, p, (int32_t)(tq * a.B + gm));
+    if (a.stamps && lane == 0) a.stamps[(int64_t)blockIdx.x * 16 + 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
     return;
   }
   const int t = wid >> 2, w4 = wid & 3;
@@ -758,24 +764,140 @@ struct WgradArgs {
   int64_t* step_state;
   float* adam_pre;
   float lr, beta1, beta2;
+  // staged path (every K <= 128): tiles of T2_NT dW rows x the whole K, (t, l, n0) per tile
+  int lds;
+  int32_t t2_code[16];  // t | l << 4 | n0 << 8
+  int64_t* stamps;      // EXPERIMENT (TT_T2_STAMPS): [workgroups][8] s_memrealtime per phase
 };
+#define T2_STAMP(k) \
+  do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 
-__device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile* __restrict__ tiles, int bid) {
+// staged T2 (wgrad_lds_block): a workgroup owns T2_NT rows x all K columns of one dW over a batch
+// slice. The slice is read in passes of T2_PF chunks of T2_MB rows; ALL loads of a pass are issued
+// up front (T2_PF x 3 x 16 B per thread in flight: one memory latency per pass, not one per chunk),
+// then each chunk (T2_NT rows of dZ^T + K rows of A^T, bf16) goes through LDS (double-buffered, one
+// barrier per chunk) where the 4 waves share it
+constexpr int T2_NT = 64;
+constexpr int T2_MB = 32;                              // batch rows per staged chunk (one k-step)
+constexpr int T2_PF = 8;                               // chunks per pass (256 rows)
+constexpr int T2_STR = T2_MB + 8;                      // bf16 LDS row stride (80 B: conflict-free b128)
+constexpr int T2_ROWS = T2_NT + MAXW;                  // Z rows [0, 64) + A rows [64, 64 + K)
+constexpr int T2_LDS = 2 * T2_ROWS * T2_STR * 2;       // bytes (30,720)
+constexpr int T2_RED = 3 * 64 * 16 * 4;                // bytes of the register-path reduction
+constexpr int T2_SMEM0 = T2_LDS > T2_RED ? T2_LDS : T2_RED;
+constexpr int T2_SMEM = T2_SMEM0 > DD_SMEM ? T2_SMEM0 : DD_SMEM;  // the combined launch shares it with dedup.h
+
+// workgroups are dealt round-robin over the 8 XCDs (bid % 8): logical index of workgroup bid
+// among n so that each XCD runs one contiguous 1/8 of [0, n) (any n)
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int x = bid & 7, loc = bid >> 3, q = n >> 3, r = n & 7;
+  return x * q + min(x, r) + loc;
+}
+
+__device__ __forceinline__ void wgrad_lds_block(const WgradArgs& a, int lb, char* smem) {
+  __bf16* buf = reinterpret_cast<__bf16*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  // lb is workgroup-uniform: readfirstlane keeps the tile lookup a scalar kernarg load (a VGPR index
+  // would be a vector load from the kernarg segment, a dependent hop before the first operand load)
+  const int s = __builtin_amdgcn_readfirstlane(lb / a.ntiles), ti = __builtin_amdgcn_readfirstlane(lb % a.ntiles);
+  T2_STAMP(0);
+  const int code = a.t2_code[ti];
+  const int t = code & 15, l = (code >> 4) & 15, n0 = code >> 8;
+  const int K = a.K[t][l];
+  const int NT = min(T2_NT, a.width[l] - n0);  // 64, or 32 for the last tile of a width % 64 layer
+  const int64_t B = a.B;
+  const __bf16* Z = a.dzt + (((int64_t)t * MAXL + l) * MAXW + n0) * B;
+  const __bf16* A = l == 0 ? a.xt + (int64_t)t * a.in_max * B : a.act + ((int64_t)t * MAXL + l - 1) * MAXW * B;
+  const int64_t mb = (int64_t)s * a.mslice;
+  const int64_t me = min(mb + a.mslice, B);
+  // loader: 4 threads per 64-B operand row segment (32 batch rows), 64 rows per pass
+  const int seg = (tid & 3) * 8, frow = tid >> 2;
+  const __bf16* src[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int f = frow + 64 * i;
+    src[i] = f < T2_NT ? (f < NT ? Z + (int64_t)f * B : nullptr) : (f - T2_NT < K ? A + (int64_t)(f - T2_NT) * B : nullptr);
+  }
+  const int nh = wid >> 1, kh = wid & 1;  // wave: dW rows [32 nh, +32) x columns [64 kh, +64)
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)(0.f);
+  for (int64_t p0 = mb; p0 < me; p0 += T2_PF * T2_MB) {
+    bf16x8 ld[T2_PF][3];
+#pragma unroll
+    for (int c = 0; c < T2_PF; ++c) {
+      const int64_t m = p0 + c * T2_MB + seg;  // B % 8 == 0: a segment is wholly in or out
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        ld[c][i] = (src[i] && m < me) ? *reinterpret_cast<const bf16x8*>(src[i] + m) : (bf16x8)(__bf16)0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < T2_PF; ++c) {
+      if (p0 + c * T2_MB >= me) break;  // uniform: the slice's tail
+      __bf16* d = buf + (c & 1) * T2_ROWS * T2_STR;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (src[i]) *reinterpret_cast<bf16x8*>(d + (frow + 64 * i) * T2_STR + seg) = ld[c][i];
+      __syncthreads();  // one barrier per chunk: buffer c & 1 was last read two chunks ago
+      if (c == 0 && p0 == mb) T2_STAMP(1);
+      bf16x8 fa[2], fb[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(d + (nh * 32 + i * 16 + r) * T2_STR + q * 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(d + (T2_NT + kh * 64 + j * 16 + r) * T2_STR + q * 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  T2_STAMP(2);
+  // C[n][k]: row n = 4q + rr, column k = r of each 16 x 16 block
+  float* dst = a.slab + (int64_t)s * a.P + a.woff[t][l];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int n = n0 + nh * 32 + i * 16 + q * 4 + rr;
+          const int k = kh * 64 + j * 16 + r;
+          dst[(int64_t)n * K + k] = acc[i][j][rr];
+        }
+  T2_STAMP(3);
+}
+
+__device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile* __restrict__ tiles, int bid,
+                                            char* smem) {
   // workgroups [0, ntiles * S): one (32x32 tile of dW, batch slice) each, its 4 waves on 4
   // consecutive quarters of the slice, reduced through LDS in wave order -> one slab row.
   // Workgroups beyond: one wave per bias output (+ one for the loss).
-  __shared__ float red[3][64 * 16];
+  float (*red)[64 * 16] = reinterpret_cast<float (*)[64 * 16]>(smem);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int64_t nwg_tiles = (int64_t)a.ntiles * a.S;
   if ((int64_t)bid >= nwg_tiles) {
+    T2_STAMP(0);
     // bias gradient of one output n of (t, l): sum of the T1 workgroups' partials, lanes strided
     // over workgroups, then a fixed butterfly -> slab[0]
     int64_t b = ((int64_t)bid - nwg_tiles) * 4 + wid;
     if (b == a.nbias) {  // the scalar loss: T1's per-workgroup partials in a fixed order
       if (a.loss) {
         float s = 0.f;
-        for (int w = lane; w < a.nwg; w += 64) s += a.loss_part[w];
+        for (int w0 = 0; w0 < a.nwg; w0 += 512) {
+          float v[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = w0 + k * 64 + lane < a.nwg ? a.loss_part[w0 + k * 64 + lane] : 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) s += v[k];
+        }
         s = wave_sum(s);
         if (lane == 0) a.loss[0] = s / (float)a.B;
       }
@@ -793,20 +915,33 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
       for (int l = 0; l < a.L; ++l) {
         if (b >= 0 && b < a.width[l]) {
           const float* dbp = a.dbpart + ((int64_t)t * MAXL + l) * a.nwg * MAXW + b;
+          // 8 independent loads per lane in flight per round (not one dependent load per add)
           float s = 0.f;
-          for (int w = lane; w < a.nwg; w += 64) s += dbp[(int64_t)w * MAXW];
+          for (int w0 = 0; w0 < a.nwg; w0 += 512) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int w = w0 + k * 64 + lane;
+              v[k] = w < a.nwg ? dbp[(int64_t)w * MAXW] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += v[k];
+          }
           s = wave_sum(s);
           if (lane == 0) a.slab[a.boff[t][l] + b] = s;
         }
         b -= a.width[l];
       }
+    T2_STAMP(3);
     return;
   }
-  // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs (bid % 8), so logical
-  // tile-workgroup (bid % 8) * n / 8 + bid / 8 puts a contiguous 1/8 of the (slice, tile) list —
-  // whole slices, whose tiles re-read the same operand strips — on one XCD and its L2
-  int lb = bid;
-  if (nwg_tiles % 8 == 0) lb = (int)((bid % 8) * (nwg_tiles / 8) + bid / 8);
+  // XCD-aware placement: a contiguous 1/8 of the (slice, tile) list — whole slices, whose tiles
+  // re-read the same operand strips — on one XCD and its L2
+  const int lb = xcd_remap(bid, (int)nwg_tiles);
+  if (a.lds) {
+    wgrad_lds_block(a, lb, smem);
+    return;
+  }
   const int s = (int)(lb / a.ntiles);
   const WgradTile tl = tiles[lb % a.ntiles];
   const int64_t B = a.B;
@@ -903,7 +1038,8 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
 }
 
 __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const WgradTile* __restrict__ tiles) {
-  wgrad_block(a, tiles, (int)blockIdx.x);
+  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
+  wgrad_block(a, tiles, (int)blockIdx.x, smem);
 }
 
 // T2 + the embedding path's fused row-wise Adagrad (dedup.h) in ONE launch: workgroups
@@ -912,10 +1048,11 @@ __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const Wgr
 // the HBM-bound row updates on the same CUs.
 __global__ void __launch_bounds__(256) tower_wgrad_dedup_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
                                                                 DdUpdateArgs d, int n_t2) {
+  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
   if ((int)blockIdx.x < n_t2)
-    wgrad_block(a, tiles, (int)blockIdx.x);
+    wgrad_block(a, tiles, (int)blockIdx.x, smem);
   else
-    dd_update_block(d, (int)blockIdx.x - n_t2);
+    dd_update_block(d, (int)blockIdx.x - n_t2, smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -948,8 +1085,8 @@ struct UpdateArgs {
                           // also advanced step_state): no pow() and no arrival ticket here
 };
 
-__global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
+  const int64_t i = (int64_t)bid * 256 + threadIdx.x;
   int64_t t_step = 0;
   float step_size = 0.f, bc2_sqrt = 1.f;
   if (a.do_adam && a.adam_pre) {
@@ -1004,13 +1141,26 @@ __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) {
     if (threadIdx.x == 0) {
       unsigned* counter = reinterpret_cast<unsigned*>(a.step_state + 1);
       const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == gridDim.x - 1) {
+      if (prev == (unsigned)nblocks - 1) {
         __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.step_state), (unsigned long long)t_step,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
+}
+
+__global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) { update_block(a, (int)blockIdx.x, (int)gridDim.x); }
+
+// T3 + the embedding path's fused row-wise Adagrad (dedup.h) in ONE launch: workgroups [0, n_dd)
+// run dd_update_block (its slot workgroups fit one round of resident waves), the rest T3 (Adam with
+// T2's precomputed scalars). T2 runs alone before it with the registers and LDS it needs.
+__global__ void __launch_bounds__(256) tower_update_dedup_kernel(UpdateArgs a, DdUpdateArgs d, int n_dd) {
+  __shared__ __attribute__((aligned(16))) char smem[DD_SMEM];
+  if ((int)blockIdx.x < n_dd)
+    dd_update_block(d, (int)blockIdx.x, smem);
+  else
+    update_block(a, (int)blockIdx.x - n_dd, (int)gridDim.x - n_dd);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1025,6 +1175,8 @@ struct TowerLayout {
   int S;
   int64_t mslice;
   int ntiles;
+  int lds;  // staged T2 (wgrad_lds_block)
+  int32_t t2_code[16];
   // workspace carve (bytes)
   size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_tiles, o_dbg, total;
 };
@@ -1061,16 +1213,32 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.in_max = std::max(s->in_dim[0], s->in_dim[1]);
   L.nwg = (int)ceil_div(B, TR);
   int nt = 0;
-  for (int t = 0; t < 2; ++t)
-    for (int l = 0; l < s->L; ++l) nt += (s->width[l] / 32) * (L.K[t][l] / 32);
+  L.lds = L.in_max <= MAXW;
+  if (L.lds) {
+    // staged T2: tiles of 64 dW rows x all K
+    for (int t = 0; t < 2; ++t)
+      for (int l = 0; l < s->L; ++l)
+        for (int n0 = 0; n0 < s->width[l]; n0 += T2_NT) {
+          L.t2_code[nt] = t | l << 4 | n0 << 8;
+          ++nt;
+        }
+    // slices of whole passes (256 rows), at most 64 (the slab depth T3 reduces over)
+    const int64_t pass = T2_PF * T2_MB;
+    const int64_t S = std::min<int64_t>(64, ceil_div(B, pass));
+    L.mslice = ceil_div(ceil_div(B, S), pass) * pass;
+    L.S = (int)ceil_div(B, L.mslice);
+  } else {
+    for (int t = 0; t < 2; ++t)
+      for (int l = 0; l < s->L; ++l) nt += (s->width[l] / 32) * (L.K[t][l] / 32);
+    // slices (one T2 workgroup each per tile, 4 waves of mslice/4 rows): aim for ~400 workgroups,
+    // >= 512 rows per slice; the slice count is also the slab depth T3 reduces over
+    int64_t S = std::max<int64_t>(1, 400 / std::max(1, nt));
+    S = std::min<int64_t>(S, std::max<int64_t>(1, ceil_div(B, 512)));
+    S = std::min<int64_t>(S, 64);
+    L.S = (int)S;
+    L.mslice = ceil_div(ceil_div(B, S), 128) * 128;
+  }
   L.ntiles = nt;
-  // slices (one T2 workgroup each per tile, 4 waves of mslice/4 rows): aim for ~400 workgroups,
-  // >= 512 rows per slice; the slice count is also the slab depth T3 reduces over
-  int64_t S = std::max<int64_t>(1, 400 / std::max(1, nt));
-  S = std::min<int64_t>(S, std::max<int64_t>(1, ceil_div(B, 512)));
-  S = std::min<int64_t>(S, 64);
-  L.S = (int)S;
-  L.mslice = ceil_div(ceil_div(B, S), 128) * 128;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t r = off;
@@ -1089,7 +1257,7 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.o_wbf = take((size_t)L.PW * 2);
   L.o_wtbf = take((size_t)L.PW * 2);
   L.o_tiles = take((size_t)nt * sizeof(WgradTile));
-  L.o_dbg = take((size_t)L.nwg * 16 * sizeof(int64_t));
+  L.o_dbg = take((size_t)std::max<int64_t>(L.nwg * 2, 1024) * 8 * sizeof(int64_t));
   L.total = off;
   *lay = L;
   return TT_OK;
@@ -1122,7 +1290,8 @@ int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* work
   hipStream_t st = as_stream(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   if (hipMemsetAsync(ws, 0, L.total, st) != hipSuccess) return fail(TT_EINVAL, "tower: memset failed");
-  // the tile list of T2 (host-built, copied once)
+  if (L.lds) return hipStreamSynchronize(st) == hipSuccess ? TT_OK : fail(TT_EINVAL, "tower: init sync failed");
+  // the tile list of the register-path T2 (host-built, copied once)
   std::vector<WgradTile> tiles;
   for (int t = 0; t < 2; ++t)
     for (int l = 0; l < shape->L; ++l)
@@ -1236,7 +1405,12 @@ static int wgrad_args(const tt_tower_shape_t* shape, int64_t B, float* loss, voi
   a.loss = loss;
   a.nbias = nbias;
   a.tiles_off = (int64_t)L.o_tiles;
-  *wgs = (int64_t)L.ntiles * L.S + ceil_div(nbias + 1, 4);
+  if (getenv("TT_T2_STAMPS")) a.stamps = reinterpret_cast<int64_t*>(ws + L.o_dbg);
+  a.lds = L.lds;
+  for (int i = 0; i < 16; ++i) {
+    a.t2_code[i] = L.t2_code[i];
+  }
+  *wgs =(int64_t)L.ntiles * L.S + ceil_div(nbias + 1, 4);
   return TT_OK;
 }
 }  // namespace tt
@@ -1317,6 +1491,25 @@ int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* 
   return check_launch("tower_wgrad");
 }
 
+int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                       int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2, void* stream) {
+  if (!adam_step_state) return fail(TT_EINVAL, "tower_wgrad_pre: null Adam step state");
+  WgradArgs a{};
+  int64_t wgs = 0;
+  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
+  if (rc) return rc;
+  TowerLayout L;
+  tower_layout(shape, B, &L);
+  a.step_state = adam_step_state;
+  a.adam_pre = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + L.o_counter);
+  a.lr = adam_lr;
+  a.beta1 = adam_beta1;
+  a.beta2 = adam_beta2;
+  tower_wgrad_kernel<<<dim3((unsigned)wgs), dim3(256), 0, as_stream(stream)>>>(
+      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off));
+  return check_launch("tower_wgrad_pre");
+}
+
 int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
                                    size_t ws_bytes, const tt_table_meta_t* tables, int T,
                                    const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
@@ -1350,7 +1543,8 @@ int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, flo
 static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
                      float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
                      int do_adam, float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes,
-                     void* stream, const float* adam_pre = nullptr) {
+                     void* stream, const float* adam_pre = nullptr, const DdUpdateArgs* dd = nullptr,
+                     int64_t dd_grid = 0) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
@@ -1393,7 +1587,13 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
   a.grads_out = grads_out;
   a.grads_in = grads_in;
   a.adam_pre = adam_pre;
-  tower_update_kernel<<<dim3((unsigned)ceil_div(L.P, 256)), dim3(256), 0, as_stream(stream)>>>(a);
+  const int64_t g3 = ceil_div(L.P, 256);
+  if (dd) {
+    if (dd_grid + g3 > INT32_MAX) return fail(TT_EINVAL, "tower_update_rowwise_adagrad: grid too large");
+    tower_update_dedup_kernel<<<dim3((unsigned)(dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(a, *dd, (int)dd_grid);
+    return check_launch("tower_update_rowwise_adagrad");
+  }
+  tower_update_kernel<<<dim3((unsigned)g3), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_update");
 }
 
@@ -1414,6 +1614,27 @@ int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params,
   const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
   return launch_t3(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
                    nullptr, workspace, ws_bytes, stream, pre);
+}
+
+int tt_tower_update_pre_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
+                                        float* exp_avg_sq, float eps, float beta1, float beta2, float weight_decay,
+                                        float* grads_out, void* workspace, size_t ws_bytes,
+                                        const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
+                                        int64_t emb_B, const float* grad, int64_t ldg, float* weights, float* state,
+                                        float lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                        int64_t dedup_max_lookups, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  DdUpdateArgs d{};
+  int64_t dd_grid = 0;
+  rc = dedup_update_args(tables, T, features, F, emb_B, grad, ldg, weights, state, lr, emb_eps, dedup_ws,
+                         dedup_ws_bytes, dedup_max_lookups, d, &dd_grid);
+  if (rc) return rc;
+  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
+  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
+                   nullptr, workspace, ws_bytes, stream, pre, &d, dd_grid);
 }
 
 int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,

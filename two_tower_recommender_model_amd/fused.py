@@ -248,15 +248,15 @@ class FusedTwoTowerStep:
         else:
             self.tables.pooled_fwd_cols(self.cols, self.num_embeddings, out=self.pooled)
         if self.towers is not None and self.gather and self.dedup_single and self.combined_bwd:
-            # one stream: T1 -> [T2 + fused row-wise Adagrad] -> T3
+            # one stream: T1 -> T2 -> [T3 + fused row-wise Adagrad]
             self._mark("t1", 1)
-            self._mark("k2", 0)
-            self.towers.wgrad_rowwise_adagrad(self.loss, self.tables, self.gpooled, B, self.lr_emb, self.eps,
-                                              adam_step_state=self.adam_state, adam_lr=self.lr_dense)
-            self._mark("k2", 1)
-            self._mark("t3", 0)
-            self.towers.update_pre(self.params, self.exp_avg, self.exp_avg_sq, grads_out=self.grads)
-            self._mark("t3", 1)
+            self._mark("t2", 0)
+            self.towers.wgrad_pre(self.loss, self.adam_state, adam_lr=self.lr_dense)
+            self._mark("t2", 1)
+            self._mark("k3", 0)
+            self.towers.update_pre_rowwise_adagrad(self.params, self.exp_avg, self.exp_avg_sq, self.tables,
+                                                   self.gpooled, B, self.lr_emb, self.eps, grads_out=self.grads)
+            self._mark("k3", 1)
             return
         if self.towers is not None:
             # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update

@@ -602,6 +602,34 @@ class FusedTowers:
                                                      float(adam_beta1), float(adam_beta2), stream_handle(self.device)),
               "tower_wgrad_rowwise_adagrad")
 
+    def wgrad_pre(self, loss, adam_step_state, adam_lr: float = 0.01, adam_beta1: float = 0.9,
+                  adam_beta2: float = 0.999) -> None:
+        """T2 alone; also advances the Adam step and precomputes its scalars for ``update_pre`` /
+        ``update_pre_rowwise_adagrad``."""
+        check(_lib_().tt_tower_wgrad_pre(C.byref(self.shape), self.B, ptr(loss), ptr(self.ws), self.nbytes,
+                                         ptr(adam_step_state), float(adam_lr), float(adam_beta1), float(adam_beta2),
+                                         stream_handle(self.device)), "tower_wgrad_pre")
+
+    def update_pre_rowwise_adagrad(self, params, exp_avg, exp_avg_sq, tables: "TableSet", grad: torch.Tensor,
+                                   emb_B: int, lr: float, emb_eps: float, flat: bool = False, beta1: float = 0.9,
+                                   beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0,
+                                   grads_out=None) -> None:
+        """``update_pre`` and ``tables.dedup_rowwise_adagrad(grad, emb_B, lr, emb_eps, flat)`` in one launch
+        (after ``wgrad_pre``)."""
+        _dev(grad)
+        if flat:
+            fm = (FeatureMeta * 1)()
+            fm[0].table, fm[0].out_offset, fm[0].out_row = 0, 0, 0
+            F = 1
+        else:
+            fm, F = tables._fm, tables.F
+        check(_lib_().tt_tower_update_pre_rowwise_adagrad(
+            C.byref(self.shape), self.B, ptr(params), ptr(exp_avg), ptr(exp_avg_sq), float(eps), float(beta1),
+            float(beta2), float(weight_decay), ptr(grads_out), ptr(self.ws), self.nbytes, tables._tm, tables.T, fm, F,
+            int(emb_B), ptr(grad), grad.stride(0), ptr(tables.weights), ptr(tables.state), float(lr), float(emb_eps),
+            ptr(tables._dd_ws), tables._dd_ws.numel(), tables._dd_cap, stream_handle(self.device)),
+            "tower_update_pre_rowwise_adagrad")
+
     def update_pre(self, params, exp_avg, exp_avg_sq, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,
                    weight_decay: float = 0.0, grads_out=None) -> None:
         """T3 with the Adam scalars the preceding wgrad_rowwise_adagrad(adam_step_state=...) computed."""
