@@ -303,10 +303,12 @@ int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, flo
                                    float adam_lr, float adam_beta1, float adam_beta2, void* stream);
 /* T2 alone (tt_tower_wgrad) that also advances the Adam step and precomputes the step's
  * bias-correction scalars for tt_tower_update_pre / tt_tower_update_pre_rowwise_adagrad (the fused
- * single-GPU step: T1 -> this -> T3 + embedding update). Replaces the towers' autograd weight
- * gradients (03_model_training.py:455) and the step-count part of Adam (:826-829). */
+ * single-GPU step: T1 -> this -> T3 + embedding update). With dedup_ws (nullable) the same launch
+ * finishes the dedup inserts T1 deferred (as tt_dedup_resolve). Replaces the towers' autograd
+ * weight gradients (03_model_training.py:455) and the step-count part of Adam (:826-829). */
 int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
-                       int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2, void* stream);
+                       int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2, void* dedup_ws,
+                       size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 /* T3 (as tt_tower_update_pre) and the embedding backward + row-wise Adagrad (as
  * tt_dedup_rowwise_adagrad, emb_eps its eps) in ONE launch after tt_tower_wgrad_pre: the update's
  * slot workgroups and T3's parameter workgroups share one round of resident waves. Replaces Adam's
@@ -341,6 +343,10 @@ int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, flo
  * once with tt_dedup_workspace_init (synchronises `stream`). 64-B aligned. */
 size_t tt_dedup_workspace_bytes(int64_t max_lookups);
 int tt_dedup_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
+/* Finishes the inserts that tt_tower_fwd_bwd_gather (dedup on) deferred: a lookup whose first CAS
+ * did not claim a free slot is listed by T1 and filed here (probe / count). Run it between T1 and
+ * the update (tt_tower_wgrad_pre with the dedup workspace does the same inside its launch). */
+int tt_dedup_resolve(void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
 /* lookups i = f * B + b: key (table of feature f, cols[f][b] mod num_embeddings[f]); id 0 dropped */
 int tt_dedup_insert_cols(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F, int64_t B,
                          const void* const* cols, int id_dtype, const int64_t* num_embeddings, void* workspace,

@@ -16,7 +16,7 @@ st.load_batch([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
 tabs = [st.tables.table_view(0), st.tables.table_view(1)]
 L = 2 * B
 cap = 1024
-while cap < L + L // 2:
+while cap < 4 * L:
     cap <<= 1
 al = lambda x: (x + 255) // 256 * 256  # noqa: E731
 off = al(cap * 64) + al(L * 8) + al((L // 15 + 1) * 4) + al(16)
@@ -28,6 +28,7 @@ for it in range(6):
         st.towers.fwd_bwd_gather(st.cols, st.num_embeddings, tabs, st.gpooled, st.params, st.labels, st.logits,
                                  dedup=st.tables, dedup_tables=(0, 1))
         st.towers.wgrad(st.loss)
+        st.tables.dedup_resolve()
         st.tables.dedup_rowwise_adagrad(st.gpooled, B, st.lr_emb, st.eps)
     else:
         st.step()

@@ -17,6 +17,7 @@ for _ in range(20):
     st.towers.fwd_bwd_gather(st.cols, st.num_embeddings, tabs, st.gpooled, st.params, st.labels, st.logits,
                              dedup=st.tables, dedup_tables=(0, 1))
     st.towers.wgrad(st.loss)
+    st.tables.dedup_resolve()
     st.tables.dedup_rowwise_adagrad(st.gpooled, B, st.lr_emb, st.eps)
     st.towers.update(st.params, st.exp_avg, st.exp_avg_sq, st.adam_state, lr=st.lr_dense)
 for _ in range(20):

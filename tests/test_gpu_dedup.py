@@ -75,16 +75,22 @@ def test_dedup_cols_vs_oracle(ops, device, B, dims, zipf):
 
 
 def _assert_clean(ts):
-    """After every update the workspace is clean: every slot free, hot-row counters zero."""
+    """After every update the workspace is clean: every slot free, hot-row counters zero, no
+    deferred insert pending (dedup.hip dedup_layout: slots, keys, hot list, counters, claims,
+    overflow entries)."""
     L = ts._dd_cap
     cap = 1024
-    while cap < L + L // 2:
+    while cap < 4 * L:
         cap <<= 1
     al = lambda x: (x + 255) // 256 * 256  # noqa: E731
     sl = ts._dd_ws[:cap * 64].view(torch.int64).view(cap, 8).cpu()
     assert bool((sl[:, 0] == -1).all())
     o = cap * 64 + al(8 * L) + al(4 * (L // 15 + 1))
     assert ts._dd_ws[o:o + 16].view(torch.int32).cpu().tolist() == [0, 0, 0, 0]
+    o_ovf = o + 256 + al(4 * L)
+    G = (L + 63) // 64
+    ovf = ts._dd_ws[o_ovf:o_ovf + 16 * 64 * G].view(torch.int64).view(G * 64, 2).cpu()
+    assert bool((ovf[:, 0] == -1).all())
 
 
 def test_dedup_cols_equals_kjt_path_when_not_hot(ops, device):

@@ -140,7 +140,8 @@ SIGNATURES = {
          _vp, _f32, _f32, _f32, _vp],
     ),
     "tt_tower_update_pre": (_int, [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp]),
-    "tt_tower_wgrad_pre": (_int, [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _vp]),
+    "tt_tower_wgrad_pre": (_int, [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _vp, _sz, _i64, _vp]),
+    "tt_dedup_resolve": (_int, [_vp, _sz, _i64, _vp]),
     "tt_tower_update_pre_rowwise_adagrad": (
         _int,
         [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64,
@@ -196,6 +197,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_indexed",
     "tt_tower_wgrad_rowwise_adagrad",
     "tt_tower_wgrad_pre",
+    "tt_dedup_resolve",
     "tt_tower_update_pre_rowwise_adagrad",
     "tt_shard_route_cols",
     "tt_shard_gather_rows",

@@ -34,6 +34,17 @@ struct DedupWs {
   int64_t cap;
   int64_t L;
   int32_t hot_cap;  // entries of `hot` (a step inserts <= L lookups: <= L / 14 hot rows)
+  // deferred inserts (dd_insert_defer): lookups whose first CAS did not claim a free slot, per
+  // group of 64 (one T1 workgroup), finished later by dd_resolve_block
+  struct Ovf {
+    uint64_t key;
+    int32_t i;
+    int32_t pad;
+  };
+  int32_t* claim;    // [L] slot claimed by lookup i (position 0 of its key), else -1: the update
+                     // walks the claimers instead of all cap slots
+  Ovf* ovf;          // [groups][64], key EMPTY between steps (the resolver clears what it filed)
+  int32_t ovf_groups;
   int64_t* stamps;  // EXPERIMENT (TT_DD_STAMPS): [update workgroups][8] s_memrealtime per phase
 };
 #define DD_STAMP(k) \
@@ -63,7 +74,10 @@ __device__ __forceinline__ void dd_insert_begin(const DedupWs& ws, uint64_t key,
   p.key = key;
   p.prev = 0;
   p.h = 0;
-  if (key == DD_EMPTY) return;
+  if (key == DD_EMPTY) {
+    ws.claim[i] = -1;
+    return;
+  }
   p.h = dd_mix64(key) & ((uint64_t)ws.cap - 1);
   p.prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.slots[p.h].word), (unsigned long long)DD_EMPTY,
                      (unsigned long long)((key << DD_CNT_BITS) | 1ull));
@@ -89,6 +103,7 @@ __device__ __forceinline__ void dd_insert_finish(const DedupWs& ws, const DdPend
     prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.slots[h].word), (unsigned long long)DD_EMPTY,
                      (unsigned long long)mine);
   }
+  ws.claim[i] = k == 0 ? (int32_t)h : -1;
   if (k < DD_INL) {
     ws.slots[h].item[k] = i;
   } else if (k == DD_INL) {
@@ -104,6 +119,42 @@ __device__ __forceinline__ void dd_insert(const DedupWs& ws, uint64_t key, int32
   dd_insert_finish(ws, p, i);
 }
 
+// Deferred finish, for a whole wave (group `group` of <= 64 lookups, lane l holding entry l): a
+// lookup whose first CAS claimed a free slot files itself (position 0: no further round trip);
+// every other one (home slot held by its key or by another key) leaves its key in the group's
+// overflow entry for dd_resolve_block, which runs in a later launch. Every lane writes its entry
+// (EMPTY when there is nothing to resolve): no counts, no compaction. The wave's tail is then ONE
+// atomic round trip, not a probe chain (the slowest of 64 lanes decides when a wave ends).
+__device__ __forceinline__ void dd_insert_defer_finish(const DedupWs& ws, const DdPend& p, int32_t i, int group) {
+  const int lane = threadIdx.x & 63;
+  const bool live = p.key != DD_EMPTY;
+  const bool claimed = live && p.prev == DD_EMPTY;
+  if (claimed) ws.slots[p.h].item[0] = i;
+  if (live) ws.claim[i] = claimed ? (int32_t)p.h : -1;  // deferred: the resolver rewrites it
+  DedupWs::Ovf o;
+  o.key = live && !claimed ? p.key : DD_EMPTY;
+  o.i = i;
+  o.pad = 0;
+  ws.ovf[(int64_t)group * 64 + lane] = o;
+}
+
+// finishes the deferred inserts of groups [rb * gpw, (rb + 1) * gpw), gpw = ceil(groups / nres):
+// one thread per overflow entry; the entry is cleared for the next step
+__device__ __forceinline__ void dd_resolve_block(const DedupWs& ws, int rb, int nres) {
+  const int G = ws.ovf_groups;
+  const int gpw = (G + nres - 1) / nres;
+  for (int e = threadIdx.x; e < gpw * 64; e += blockDim.x) {
+    const int64_t g = (int64_t)rb * gpw + e / 64;
+    if (g >= G) break;
+    DedupWs::Ovf* op = ws.ovf + g * 64 + e % 64;
+    const DedupWs::Ovf o = *op;
+    if (o.key != DD_EMPTY) {
+      op->key = DD_EMPTY;
+      dd_insert(ws, o.key, o.i);
+    }
+  }
+}
+
 size_t dedup_layout(void* base, int64_t L, DedupWs* w);
 
 // arguments of the update launch (dd_adagrad_kernel, or a role of a combined launch)
@@ -116,7 +167,8 @@ struct DdUpdateArgs {
   float* state;
   float lr, eps;
   DedupWs ws;
-  int hot_wgs;         // workgroups of the hot role; the slot role has ws.cap / 8 more
+  int hot_wgs;         // workgroups of the hot role; the slot role has slot_hw / 8 more
+  int64_t slot_hw;     // half-waves of the slot role: ceil(L / DD_SPH), a multiple of 8
 };
 
 // Per-lane table / feature meta from LDS: indexing the kernel-argument arrays by a per-lane value
@@ -300,16 +352,24 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   }
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31, hb = lane & 32;
-  // DD_SPH slots per half-wave (h and h + cap / DD_SPH), their dependent loads interleaved: the
-  // grid covers exactly cap slots (cap is a multiple of 1024) in one round of resident waves
+  // DD_SPH claiming lookups per half-wave (i and i + nhw, ...), their dependent loads interleaved:
+  // the slot a lookup claimed (claim[i] >= 0) is updated by that lookup's half-wave; the grid covers
+  // the step's lookups (not the cap slots) in one round of resident waves
   const int64_t hw = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
-  const int64_t nhw = ws.cap / DD_SPH;
+  const int64_t nhw = a.slot_hw;
+  int hq[DD_SPH];
+#pragma unroll
+  for (int q = 0; q < DD_SPH; ++q) {
+    const int64_t i = hw + q * nhw;
+    hq[q] = i < a.n ? ws.claim[i] : -1;
+  }
   DSlot* sp[DD_SPH];
   int dw[DD_SPH];
 #pragma unroll
   for (int q = 0; q < DD_SPH; ++q) {
-    sp[q] = ws.slots + hw + q * nhw;
-    dw[q] = hl < 16 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : 0;
+    sp[q] = ws.slots + (hq[q] >= 0 ? hq[q] : 0);
+    // an idle half-wave reads nothing and sees an EMPTY word
+    dw[q] = hq[q] >= 0 ? (hl < 16 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : 0) : (hl < 2 ? -1 : 0);
   }
   dd_meta_fill(m, lm);  // beside the slot loads
   __syncthreads();

@@ -28,10 +28,12 @@ struct ColArgsD {
   int64_t num_emb[TT_MAX_FEATURES];
 };
 
-// slots: a power of two >= 1.5 x the lookups (load factor <= 2/3 even if every lookup is unique)
+// slots: a power of two >= 4 x the lookups (load factor <= 1/4 even if every lookup is unique): a
+// first CAS rarely collides and probe chains stay short; the update walks the claiming lookups,
+// so the table's size costs only memory (64 B a slot)
 static int64_t dedup_cap(int64_t L) {
   int64_t c = 1024;
-  while (c < L + L / 2) c <<= 1;
+  while (c < 4 * L) c <<= 1;
   return c;
 }
 
@@ -49,7 +51,10 @@ size_t dedup_layout(void* base, int64_t L, DedupWs* w) {
   t.lkey = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * L));
   t.hot = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (L / (DD_INL + 1) + 1)));
   t.ctr = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
-  int64_t* dbg = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * 8 * (cap / (8 * DD_SPH) + 64)));
+  t.claim = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
+  t.ovf_groups = (int32_t)((L + 63) / 64);
+  t.ovf = reinterpret_cast<DedupWs::Ovf*>(take(sizeof(DedupWs::Ovf) * 64 * (size_t)t.ovf_groups));
+  int64_t* dbg = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * 8 * (L / (8 * DD_SPH) + 64)));
   t.stamps = getenv("TT_DD_STAMPS") ? dbg : nullptr;
   t.cap = cap;
   t.L = L;
@@ -84,6 +89,10 @@ __global__ void __launch_bounds__(64) dd_insert_segments_kernel(const int64_t* _
     dd_insert(ws, key, (int32_t)i);
   }
 }
+
+// ---- deferred inserts: dd_resolve_block (dedup.h) ------------------------------------------------
+constexpr int DD_RES_WGS = 64;
+__global__ void __launch_bounds__(256) dd_resolve_kernel(DedupWs ws) { dd_resolve_block(ws, (int)blockIdx.x, DD_RES_WGS); }
 
 // ---- update: dd_update_block (dedup.h) ----------------------------------------------------------
 __global__ void __launch_bounds__(256) dd_adagrad_kernel(DdUpdateArgs a) {
@@ -127,7 +136,8 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
   a.lr = lr;
   a.eps = eps;
   a.hot_wgs = (int)std::min<int64_t>(32, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
-  *grid = a.hot_wgs + a.ws.cap / (8 * DD_SPH);
+  a.slot_hw = ceil_div(ceil_div(max_lookups, DD_SPH), 8) * 8;
+  *grid = a.hot_wgs + a.slot_hw / 8;
   return TT_OK;
 }
 
@@ -149,10 +159,20 @@ int tt_dedup_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookup
   hipStream_t st = as_stream(stream);
   // every slot word EMPTY (all ones; items unused), counters 0
   if (hipMemsetAsync(w.slots, 0xff, sizeof(DSlot) * w.cap, st) != hipSuccess ||
-      hipMemsetAsync(w.ctr, 0, sizeof(int32_t) * 4, st) != hipSuccess)
+      hipMemsetAsync(w.ctr, 0, sizeof(int32_t) * 4, st) != hipSuccess ||
+      hipMemsetAsync(w.ovf, 0xff, sizeof(DedupWs::Ovf) * 64 * w.ovf_groups, st) != hipSuccess)
     return fail(TT_EINVAL, "dedup_workspace_init: memset failed");
   if (hipStreamSynchronize(st) != hipSuccess) return fail(TT_EINVAL, "dedup_workspace_init: sync failed");
   return TT_OK;
+}
+
+int tt_dedup_resolve(void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream) {
+  int rc = check_dd_ws(workspace, ws_bytes, max_lookups, "dedup_resolve");
+  if (rc) return rc;
+  DedupWs w;
+  dedup_layout(workspace, max_lookups, &w);
+  dd_resolve_kernel<<<dim3(DD_RES_WGS), dim3(256), 0, as_stream(stream)>>>(w);
+  return check_launch("dedup_resolve");
 }
 
 int tt_dedup_insert_cols(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F, int64_t B,

@@ -458,12 +458,18 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       const uint64_t tab = (uint64_t)(tq ? a.dd_table[1] : a.dd_table[0]);
       const uint64_t key = id != 0 ? ((tab << DD_TABLE_SHIFT) | (uint64_t)py_mod64(id, mod)) : DD_EMPTY;
       dd_insert_begin(a.dd, key, (int32_t)(tq * a.B + gm), p);
+    } else {
+      p.key = DD_EMPTY;
     }
-#pragma unroll 1
-    for (int k = 0; k < T1_BARRIERS; ++k) __syncthreads();
-    if (a.stamps && lane == 0) a.stamps[(int64_t)blockIdx.x * 16 + 9] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    if (own) dd_insert_finish(a.dd, p, (int32_t)(tq * a.B + gm));
+    // the CAS results are needed only after two barriers (about half the compute chain later); a
+    // lookup that did not claim a free slot is deferred to the next launch's resolver instead of
+    // probing here (dd_insert_defer_finish): this wave's tail is one atomic round trip
+    __syncthreads();
+    __syncthreads();
+    if (a.dd_on) dd_insert_defer_finish(a.dd, p, (int32_t)(tq * a.B + gm), (int)blockIdx.x);
     if (a.stamps && lane == 0) a.stamps[(int64_t)blockIdx.x * 16 + 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+    for (int k = 2; k < T1_BARRIERS; ++k) __syncthreads();
     return;
   }
   const int t = wid >> 2, w4 = wid & 3;
@@ -768,6 +774,8 @@ struct WgradArgs {
   int lds;
   int32_t t2_code[16];  // t | l << 4 | n0 << 8
   int64_t* stamps;      // EXPERIMENT (TT_T2_STAMPS): [workgroups][8] s_memrealtime per phase
+  DedupWs dd;           // tt_tower_wgrad_pre with a dedup workspace: the first n_res workgroups
+  int n_res;            //   finish T1's deferred inserts (dd_resolve_block)
 };
 #define T2_STAMP(k) \
   do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
@@ -1039,7 +1047,12 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
 
 __global__ void __launch_bounds__(256) tower_wgrad_kernel(WgradArgs a, const WgradTile* __restrict__ tiles) {
   __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
-  wgrad_block(a, tiles, (int)blockIdx.x, smem);
+  // resolver workgroups first (their probe chains are the longest dependent work of the launch);
+  // n_res % 8 == 0 keeps the tiles' XCD placement
+  if ((int)blockIdx.x < a.n_res)
+    dd_resolve_block(a.dd, (int)blockIdx.x, a.n_res);
+  else
+    wgrad_block(a, tiles, (int)blockIdx.x - a.n_res, smem);
 }
 
 // T2 + the embedding path's fused row-wise Adagrad (dedup.h) in ONE launch: workgroups
@@ -1492,12 +1505,22 @@ int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* 
 }
 
 int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
-                       int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2, void* stream) {
+                       int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2, void* dedup_ws,
+                       size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
   if (!adam_step_state) return fail(TT_EINVAL, "tower_wgrad_pre: null Adam step state");
   WgradArgs a{};
   int64_t wgs = 0;
   int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
   if (rc) return rc;
+  if (dedup_ws) {
+    if (dedup_max_lookups < 1 || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+        dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
+        (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
+      return fail(TT_ECAPACITY, "tower_wgrad_pre: dedup workspace too small / misaligned");
+    dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
+    a.n_res = 64;
+    wgs += a.n_res;
+  }
   TowerLayout L;
   tower_layout(shape, B, &L);
   a.step_state = adam_step_state;

@@ -251,7 +251,7 @@ class FusedTwoTowerStep:
             # one stream: T1 -> T2 -> [T3 + fused row-wise Adagrad]
             self._mark("t1", 1)
             self._mark("t2", 0)
-            self.towers.wgrad_pre(self.loss, self.adam_state, adam_lr=self.lr_dense)
+            self.towers.wgrad_pre(self.loss, self.adam_state, adam_lr=self.lr_dense, dedup=self.tables)
             self._mark("t2", 1)
             self._mark("k3", 0)
             self.towers.update_pre_rowwise_adagrad(self.params, self.exp_avg, self.exp_avg_sq, self.tables,
@@ -297,6 +297,8 @@ class FusedTwoTowerStep:
     def _emb_update(self) -> None:
         """EBC backward + in-backward RowWiseAdagrad (03_model_training.py:791-795) on the pooled
         gradient of this step."""
+        if self.dedup_single and self.gather:
+            self.tables.dedup_resolve()  # the inserts T1 deferred
         if self.dedup_single:
             self.tables.dedup_rowwise_adagrad(self.gpooled, self.B, self.lr_emb, self.eps)
         else:

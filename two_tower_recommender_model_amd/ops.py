@@ -319,6 +319,11 @@ class TableSet:
                                                self._dd_ws.numel(), self._dd_cap, stream_handle(self.device)),
               "dedup_insert_segments")
 
+    def dedup_resolve(self) -> None:
+        """Finish the dedup inserts a fused T1 (``FusedTowers.fwd_bwd_gather(dedup=...)``) deferred."""
+        check(_lib_().tt_dedup_resolve(ptr(self._dd_ws), self._dd_ws.numel(), self._dd_cap,
+                                       stream_handle(self.device)), "dedup_resolve")
+
     def dedup_rowwise_adagrad(self, grad: torch.Tensor, B: int, lr: float, eps: float, flat: bool = False) -> None:
         """Fused row-wise Adagrad over the rows inserted since the last call. Gradient row of lookup
         i: the KeyedTensor row of (feature i // B, bag i % B) — or, with ``flat``, row i of ``grad``."""
@@ -603,12 +608,14 @@ class FusedTowers:
               "tower_wgrad_rowwise_adagrad")
 
     def wgrad_pre(self, loss, adam_step_state, adam_lr: float = 0.01, adam_beta1: float = 0.9,
-                  adam_beta2: float = 0.999) -> None:
+                  adam_beta2: float = 0.999, dedup: Optional["TableSet"] = None) -> None:
         """T2 alone; also advances the Adam step and precomputes its scalars for ``update_pre`` /
-        ``update_pre_rowwise_adagrad``."""
+        ``update_pre_rowwise_adagrad``. With ``dedup`` (the TableSet whose dedup workspace T1 filled)
+        the same launch finishes T1's deferred inserts."""
+        dws, dnb, dcap = (None, 0, 0) if dedup is None else (dedup._dd_ws, dedup._dd_ws.numel(), dedup._dd_cap)
         check(_lib_().tt_tower_wgrad_pre(C.byref(self.shape), self.B, ptr(loss), ptr(self.ws), self.nbytes,
                                          ptr(adam_step_state), float(adam_lr), float(adam_beta1), float(adam_beta2),
-                                         stream_handle(self.device)), "tower_wgrad_pre")
+                                         ptr(dws), dnb, dcap, stream_handle(self.device)), "tower_wgrad_pre")
 
     def update_pre_rowwise_adagrad(self, params, exp_avg, exp_avg_sq, tables: "TableSet", grad: torch.Tensor,
                                    emb_B: int, lr: float, emb_eps: float, flat: bool = False, beta1: float = 0.9,
