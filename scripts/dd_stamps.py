@@ -19,8 +19,9 @@ cap = 1024
 while cap < 4 * L:
     cap <<= 1
 al = lambda x: (x + 255) // 256 * 256  # noqa: E731
-off = al(cap * 64) + al(L * 8) + al((L // 15 + 1) * 4) + al(16)
-nwg = cap // 32 + 32
+G = (L + 63) // 64
+off = al(cap * 64) + al(L * 8) + al((L // 15 + 1) * 4) + al(16) + al(4 * L) + al(16 * 64 * G)
+nwg = L // 32 + 32
 ws = st.tables._dd_ws
 mode = os.environ.get("MODE", "step")
 for it in range(6):

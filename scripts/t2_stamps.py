@@ -13,9 +13,10 @@ st = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, dev)
 g = torch.Generator(device=dev).manual_seed(1)
 st.load_batch([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
               torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32))
+nres = 64  # resolver workgroups first (they do not stamp)
 ntile = 6 * 32
 nbias = (2 * (128 + 64) + 1 + 3) // 4
-nwg = ntile + nbias
+nwg = nres + ntile + nbias
 off = st.towers.nbytes - ((max(2 * (B // 32), 1024) * 64 + 255) // 256 * 256)
 for it in range(6):
     st.step()
@@ -23,6 +24,7 @@ for it in range(6):
     stm = st.towers.ws[off:off + nwg * 64].view(torch.int64).view(nwg, 8).cpu().double()
     if it < 2:
         continue
+    stm = stm[nres:]
     t0 = stm[:, 0].min()
     rel = (stm[:, :4] - t0) * 10 / 1000
     tl, bs = rel[:ntile], rel[ntile:]
