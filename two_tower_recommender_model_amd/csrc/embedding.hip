@@ -78,6 +78,43 @@ __device__ __forceinline__ void pool_bag_cols(const float* __restrict__ w, const
   }
 }
 
+// Fast path (float4 columns, the whole row in one pass of the group: D <= 4 G): the group's lanes
+// load up to G ids of the bag at once (one coalesced read), broadcast them by lane shuffles, and
+// keep FWD_INFLIGHT rows in flight per lane; rows are still added in bag order.
+constexpr int FWD_INFLIGHT = 8;
+
+__device__ __forceinline__ void pool_bag_row4(const float* __restrict__ w, const void* __restrict__ values,
+                                              int id_dtype, int64_t s, int64_t e, int64_t rows, int D,
+                                              int lane_g, int G, float scale, float* __restrict__ out,
+                                              int bounds_check, int32_t* err) {
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  const bool col_ok = lane_g * 4 < D;
+  f32x4v acc = (f32x4v)(0.f);
+  for (int64_t j0 = s; j0 < e; j0 += G) {
+    const int cnt = (int)min((int64_t)G, e - j0);
+    int64_t myid = 0;
+    if (lane_g < cnt) {
+      myid = load_id(values, id_dtype, j0 + lane_g);
+      if (bounds_check && (uint64_t)myid >= (uint64_t)rows) {
+        atomicAdd(err, 1);
+        myid = 0;
+      }
+    }
+    for (int k = 0; k < cnt; k += FWD_INFLIGHT) {
+      f32x4v r[FWD_INFLIGHT];
+#pragma unroll
+      for (int u = 0; u < FWD_INFLIGHT; ++u) {
+        const int64_t id = __shfl(myid, gbase + min(k + u, G - 1), 64);
+        r[u] = (col_ok && k + u < cnt) ? *reinterpret_cast<const f32x4v*>(w + id * D + lane_g * 4) : (f32x4v)(0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < FWD_INFLIGHT; ++u)
+        if (k + u < cnt) acc += r[u];
+    }
+  }
+  if (col_ok) *reinterpret_cast<f32x4v*>(out + lane_g * 4) = acc * scale;
+}
+
 __device__ __forceinline__ int feature_of_block(const FwdArgs& a) {
   int f = 0;
   while (f + 1 < a.m.F && (int)blockIdx.x >= a.block_start[f + 1]) ++f;
@@ -103,7 +140,9 @@ __global__ void __launch_bounds__(256) pooled_fwd_kernel(const float* __restrict
   const float scale = (pooling == TT_POOL_MEAN && e > s) ? 1.0f / (float)(e - s) : 1.0f;
   const float* w = weights + tm.weight_offset;
   float* o = out + (fm.out_row + b) * ldo + fm.out_offset;
-  if (a.vec[f] == 4)
+  if (a.vec[f] == 4 && tm.dim <= 4 * G)
+    pool_bag_row4(w, values, id_dtype, s, e, tm.num_rows, tm.dim, lane_g, G, scale, o, bounds_check, err);
+  else if (a.vec[f] == 4)
     pool_bag_cols<4>(w, values, id_dtype, s, e, tm.num_rows, tm.dim, lane_g, G, scale, o, bounds_check, err);
   else
     pool_bag_cols<1>(w, values, id_dtype, s, e, tm.num_rows, tm.dim, lane_g, G, scale, o, bounds_check, err);
@@ -144,6 +183,17 @@ __global__ void __launch_bounds__(256) pooled_fwd_cols_kernel(const float* __res
 
 constexpr uint64_t EMPTY_KEY = ~0ull;
 constexpr int KEY_TABLE_SHIFT = 40;  // key = table << 40 | row  (rows < 2^40 per shard)
+// Global hash slot word of the KJT-form grouping: (table << 34 | row) << 24 | lookup count, so ONE
+// CAS claims a free slot with its count and a repeat key adds to the same word (rows < 2^34 - 1,
+// < 2^24 lookups per step; checked on the host).
+constexpr int PK_CNT_BITS = 24;
+constexpr int PK_ROW_BITS = 34;
+constexpr uint64_t PK_CNT_MASK = (1ull << PK_CNT_BITS) - 1;
+__device__ __forceinline__ uint64_t pk_key(int t, uint64_t row) { return ((uint64_t)t << PK_ROW_BITS) | row; }
+__device__ __forceinline__ uint64_t pk_to_key(uint64_t word) {  // slot word -> table << 40 | row
+  const uint64_t k = word >> PK_CNT_BITS;
+  return ((k >> PK_ROW_BITS) << KEY_TABLE_SHIFT) | (k & ((1ull << PK_ROW_BITS) - 1));
+}
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33;
@@ -154,42 +204,78 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// Rows looked up more than HOT_MIN - 1 times in a step are "hot": the per-row kernels (which sort
+// a segment of <= 32 bag ids in registers) skip them; bwd_hot_partial_kernel / bwd_hot_final_kernel
+// sum them in a canonical order (bag-id ranges, ascending bag id inside a range, see below).
+constexpr int HOT_MIN = 33;
+// A hot row is split into NR bag-id ranges summed by separate workgroups (NR = 1 up to HOT_SPLIT
+// lookups, at most HOT_NR_MAX); range r of NB bags is [r*NB/NR, (r+1)*NB/NR), so the split depends
+// on the lookup count and the batch shape only.
+constexpr int HOT_SPLIT = 512;
+constexpr int HOT_NR_MAX = 64;
+constexpr int HOT_WIN = 8192;   // bags counted per LDS pass of bwd_hot_partial_kernel
+constexpr int HOT_DMAX = 1024;  // partial row stride (floats)
+// Tiled grouping of KJT lookups (bwd_tile_hash_kernel / bwd_tile_scatter_kernel): a workgroup owns
+// TILE_BAGS bags and walks their lookups in chunks of TILE_CH; a chunk's duplicate ids are merged in
+// an LDS hash first, so the global hash and the segment cursors see one atomic per (chunk, row)
+// instead of one per lookup (a Zipf-hot row costs a few hundred same-address atomics, not 10^5).
+constexpr int TILE_BAGS = 32;
+constexpr int TILE_CH = 2048;
+constexpr int TILE_HS = 4096;  // LDS hash slots per chunk (load <= 1/2)
+
 struct URec {
   uint64_t key;
-  int32_t seg;
+  int32_t seg;  // first position of the row's bag ids in perm; the bag id itself when len == 1
   int32_t len;
 };
 
-// Rows looked up more than HOT_MIN - 1 times in a step are "hot": the per-row kernels (which sort
-// a segment of <= 32 bag ids in registers) skip them and bwd_adagrad_hot_kernel sums them in
-// ascending bag order through LDS, so every row's gradient is summed in one canonical order.
-constexpr int HOT_MIN = 33;
-constexpr int HOT_CAP = 4096;  // bag ids sorted in LDS per pass of the hot kernel
+struct HotRec {
+  int32_t u;      // unique-row index
+  int32_t pbase;  // first work item (bwd_hot_partial_kernel) / partial row of this hot row
+  int32_t nr;     // bag-id ranges
+  int32_t pad;
+};
 
 struct BwdWs {
   uint64_t* keys;   // [cap] hash keys (EMPTY when free; cleaned by k2b)
-  int32_t* cnt;     // [cap] lookups per slot (cleaned by k2b)
+  int32_t* cnt;     // [cap] lookups of the slot's row this step (written by k2b)
   int32_t* cur;     // [cap] scatter cursor per slot (set by k2b)
-  int32_t* slot_of; // [L]   slot of each lookup (-1: none)
+  int32_t* slot_of; // [L]   slot of each lookup (-1: none; column form)
   int32_t* perm;    // [L]   bag ids grouped by unique row
   URec* urec;       // [L]   per unique row
+  int32_t* lk;      // [L]   tiled form: chunk entry | rank in entry << 16, per lookup
+  int32_t* ent_h;   // [L]   tiled form: global slot of chunk entry d, at [chunk start + d]
+  int32_t* ent_c;   // [L]   tiled form: lookups of chunk entry d
+  int32_t* ent_n;   // [L]   tiled form: entries of the chunk starting at this lookup
   int32_t* bsum_u;  // [nb]  scan partials (unique count)
   int32_t* bsum_c;  // [nb]  scan partials (lookup count)
-  int32_t* hot;     // [L/HOT_MIN] unique indices whose segment is longer than HOT_MIN - 1
-  int32_t* U;       // [4]   {unique rows, -, hot rows, -}
+  HotRec* hot;      // [L/HOT_MIN + 1] hot rows
+  float* hotp;      // [hot items][HOT_DMAX] partial sums of split hot rows
+  int32_t* U;       // [4]   {unique rows, -, hot work items, hot rows} (U[2..3]: one 64-bit word)
   int64_t cap;
   int64_t L;
 };
 
+constexpr int SCAN_TILE = 4096;  // hash slots per workgroup of k2b
+
 static int64_t bwd_cap(int64_t L) {
-  int64_t c = 1024;
+  int64_t c = SCAN_TILE;
   while (c < 2 * L) c <<= 1;
   return c;
 }
 
+// hot work items <= hot rows + sum over split rows of ceil(c / HOT_SPLIT) <= L/HOT_MIN + 2L/HOT_SPLIT
+static int64_t hot_items_max(int64_t L) { return L / HOT_MIN + 2 * ceil_div(L, HOT_SPLIT) + 1; }
+
+__host__ __device__ __forceinline__ int hot_nr(int c) {
+  if (c <= HOT_SPLIT) return 1;
+  const int n = (c + HOT_SPLIT - 1) / HOT_SPLIT;
+  return n < HOT_NR_MAX ? n : HOT_NR_MAX;
+}
+
 static size_t bwd_layout(void* base, int64_t L, BwdWs* w) {
   const int64_t cap = bwd_cap(L);
-  const int64_t nb = ceil_div(cap, 1024);
+  const int64_t nb = ceil_div(cap, SCAN_TILE);
   char* p = reinterpret_cast<char*>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -204,46 +290,257 @@ static size_t bwd_layout(void* base, int64_t L, BwdWs* w) {
   t.slot_of = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
   t.perm = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
   t.urec = reinterpret_cast<URec*>(take(sizeof(URec) * L));
+  t.lk = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
+  t.ent_h = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
+  t.ent_c = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
+  t.ent_n = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
   t.bsum_u = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
   t.bsum_c = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
-  t.hot = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (L / HOT_MIN + 1)));
-  t.U =reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
+  t.hot = reinterpret_cast<HotRec*>(take(sizeof(HotRec) * (L / HOT_MIN + 1)));
+  t.hotp = reinterpret_cast<float*>(take(sizeof(float) * HOT_DMAX * hot_items_max(L)));
+  t.U = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
   t.cap = cap;
   t.L = L;
   if (w) *w = t;
   return off;
 }
 
-__device__ __forceinline__ int32_t hash_insert(BwdWs& ws, uint64_t key) {
-  // one returning CAS per probe: it claims an empty slot or reports who holds it
+__device__ __forceinline__ int32_t hash_insert(BwdWs& ws, uint64_t pk) {
+  // one returning CAS per probe: it claims an empty slot (count 1) or reports who holds it
   const uint64_t mask = (uint64_t)ws.cap - 1;
-  uint64_t h = mix64(key) & mask;
+  uint64_t h = mix64(pk) & mask;
   while (true) {
     const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.keys[h]),
-                                    (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-    if (prev == EMPTY_KEY || prev == key) break;
+                                    (unsigned long long)EMPTY_KEY, (unsigned long long)((pk << PK_CNT_BITS) | 1));
+    if (prev == EMPTY_KEY) break;
+    if ((prev >> PK_CNT_BITS) == pk) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&ws.keys[h]), 1ull);
+      break;
+    }
     h = (h + 1) & mask;
   }
-  atomicAdd(&ws.cnt[h], 1);
   return (int32_t)h;
 }
 
-// k2a: thread per bag: hash-insert every lookup's (table,row), count per slot
-__global__ void __launch_bounds__(256) bwd_hash_kernel(EmbMeta m, const void* __restrict__ values, int id_dtype,
-                                                       const int32_t* __restrict__ offsets, int bounds_check,
-                                                       BwdWs ws) {
-  const int64_t nbag = (int64_t)m.F * m.B;
-  for (int64_t bag = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; bag < nbag;
-       bag += (int64_t)gridDim.x * blockDim.x) {
-    const int f = (int)(bag / m.B);
-    const int t = m.features[f].table;
-    const int64_t rows = m.tables[t].num_rows;
-    const int64_t s = offsets[bag], e = offsets[bag + 1];
-    for (int64_t j = s; j < e; ++j) {
-      int64_t id = load_id(values, id_dtype, j);
-      if (bounds_check && (uint64_t)id >= (uint64_t)rows) id = 0;
-      ws.slot_of[j] = hash_insert(ws, ((uint64_t)t << KEY_TABLE_SHIFT) | (uint64_t)id);
+// Block-wide exclusive scan of one int per thread (256 threads); *total = the block's sum.
+__device__ __forceinline__ int block_excl_scan(int v, int* red, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();
+  if (lane == 63) red[wid] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    base += w < wid ? red[w] : 0;
+    tot += red[w];
+  }
+  *total = tot;
+  return base + inc - v;
+}
+
+// local bag of lookup j: the largest i < nb with off[i] <= j (off[0] <= j < off[nb])
+__device__ __forceinline__ int lds_bag_of(const int32_t* off, int nb, int64_t j) {
+  int lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)off[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// k2a (KJT form): workgroup per TILE_BAGS bags, their lookups in chunks of TILE_CH. Per chunk:
+// (1) every lookup joins its (table,row) entry of an LDS hash (rank = its LDS count ticket);
+// (2) the entries are compacted (dense index d, ascending LDS slot) and each is inserted ONCE into
+//     the global hash with its count: all of a thread's first-probe CASes are issued together,
+//     collisions retried in rounds;
+// (3) per lookup lk = d | rank << 16; per entry ent_h / ent_c at [chunk start + d], ent_n at the
+//     chunk start. k2c turns (entry base + rank) into the lookup's position in its row's segment.
+constexpr int TILE_EPT = TILE_CH / 256;  // lookups (and at most entries) per thread
+constexpr int TILE_SPT = TILE_HS / 256;  // LDS hash slots per thread in the compaction
+
+__global__ void __launch_bounds__(256) bwd_tile_hash_kernel(EmbMeta m, const void* __restrict__ values, int id_dtype,
+                                                            const int32_t* __restrict__ offsets, int bounds_check,
+                                                            BwdWs ws) {
+  __shared__ unsigned long long hkey[TILE_HS];
+  __shared__ int hcnt[TILE_HS];
+  __shared__ int16_t hmap[TILE_HS];
+  __shared__ int32_t off[TILE_BAGS + 1];
+  __shared__ int red[4];
+  const int tid = threadIdx.x;
+  const int64_t NB = (int64_t)m.F * m.B;
+  const int64_t b0 = (int64_t)blockIdx.x * TILE_BAGS;
+  const int nb = (int)min((int64_t)TILE_BAGS, NB - b0);
+  if (tid <= nb) off[tid] = offsets[b0 + tid];
+  for (int i = tid; i < TILE_HS; i += 256) {
+    hkey[i] = EMPTY_KEY;
+    hcnt[i] = 0;
+  }
+  __syncthreads();
+  const int64_t s0 = off[0], e0 = off[nb];
+  const uint64_t gmask = (uint64_t)ws.cap - 1;
+  for (int64_t j0 = s0; j0 < e0; j0 += TILE_CH) {
+    const int n = (int)min((int64_t)TILE_CH, e0 - j0);
+    int pos[TILE_EPT], rk[TILE_EPT];
+    int64_t idv[TILE_EPT];
+    int tv[TILE_EPT];
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q) {  // all id loads first
+      const int i = q * 256 + tid;
+      tv[q] = -1;
+      if (i < n) {
+        const int64_t j = j0 + i;
+        const int f = (int)((b0 + lds_bag_of(off, nb, j)) / m.B);
+        tv[q] = m.features[f].table;
+        idv[q] = load_id(values, id_dtype, j);
+      }
     }
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q) {
+      pos[q] = -1;
+      if (tv[q] >= 0) {
+        int64_t id = idv[q];
+        if (bounds_check && (uint64_t)id >= (uint64_t)m.tables[tv[q]].num_rows) id = 0;
+        const unsigned long long key = pk_key(tv[q], (uint64_t)id);
+        unsigned h = (unsigned)mix64(key) & (TILE_HS - 1);
+        while (true) {
+          const unsigned long long prev = atomicCAS(&hkey[h], (unsigned long long)EMPTY_KEY, key);
+          if (prev == EMPTY_KEY || prev == key) break;
+          h = (h + 1) & (TILE_HS - 1);
+        }
+        pos[q] = (int)h;
+        rk[q] = atomicAdd(&hcnt[h], 1);
+      }
+    }
+    __syncthreads();
+    // (2) compaction: thread owns slots [tid*SPT, tid*SPT+SPT)
+    unsigned long long ck[TILE_SPT];
+    int cc[TILE_SPT], k = 0;
+#pragma unroll
+    for (int v = 0; v < TILE_SPT; ++v) {
+      cc[v] = hcnt[tid * TILE_SPT + v];
+      ck[v] = hkey[tid * TILE_SPT + v];
+      k += cc[v] > 0;
+    }
+    int tot;
+    int d = block_excl_scan(k, red, &tot);  // its barriers order the reads above before the writes below
+#pragma unroll
+    for (int v = 0; v < TILE_SPT; ++v) {
+      if (cc[v] > 0) {
+        hmap[tid * TILE_SPT + v] = (int16_t)d;
+        hkey[d] = ck[v];  // compacted in place (d <= slot index)
+        hcnt[d] = cc[v];
+        ++d;
+      }
+    }
+    __syncthreads();
+    // global insert: entries tid, tid+256, ... (<= TILE_EPT per thread); first probes issued together
+    unsigned long long ekey[TILE_EPT];
+    uint32_t eh[TILE_EPT];
+    bool todo[TILE_EPT];
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q) {
+      const int e = q * 256 + tid;
+      todo[q] = e < tot;
+      ekey[q] = todo[q] ? hkey[e] : 0ull;
+      eh[q] = (uint32_t)(mix64(ekey[q]) & gmask);
+    }
+    int ecnt[TILE_EPT];
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q) ecnt[q] = todo[q] ? hcnt[q * 256 + tid] : 0;
+    bool any = true;
+    while (any) {
+      unsigned long long prev[TILE_EPT];
+#pragma unroll
+      for (int q = 0; q < TILE_EPT; ++q)
+        if (todo[q])
+          prev[q] = atomicCAS(reinterpret_cast<unsigned long long*>(&ws.keys[eh[q]]), (unsigned long long)EMPTY_KEY,
+                              (ekey[q] << PK_CNT_BITS) | (unsigned long long)ecnt[q]);
+      any = false;
+#pragma unroll
+      for (int q = 0; q < TILE_EPT; ++q) {
+        if (!todo[q]) continue;
+        const bool mine = prev[q] == EMPTY_KEY;
+        if (mine || (prev[q] >> PK_CNT_BITS) == ekey[q]) {
+          const int e = q * 256 + tid;
+          const int c = ecnt[q];
+          if (!mine) atomicAdd(reinterpret_cast<unsigned long long*>(&ws.keys[eh[q]]), (unsigned long long)c);
+          ws.ent_h[j0 + e] = (int32_t)eh[q];
+          ws.ent_c[j0 + e] = c;
+          todo[q] = false;
+        } else {
+          eh[q] = (uint32_t)((eh[q] + 1) & gmask);
+          any = true;
+        }
+      }
+    }
+    if (tid == 0) ws.ent_n[j0] = tot;
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q)
+      if (pos[q] >= 0) ws.lk[j0 + q * 256 + tid] = (int32_t)hmap[pos[q]] | (rk[q] << 16);
+    __syncthreads();
+    if (j0 + TILE_CH < e0) {
+      for (int i = tid; i < TILE_HS; i += 256) {
+        hkey[i] = EMPTY_KEY;
+        hcnt[i] = 0;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// k2c (KJT form): per chunk, one cursor atomic per entry reserves its run in the row's segment,
+// then every lookup writes its bag id at (run base + rank).
+__global__ void __launch_bounds__(256) bwd_tile_scatter_kernel(EmbMeta m, const int32_t* __restrict__ offsets,
+                                                               BwdWs ws) {
+  __shared__ int32_t off[TILE_BAGS + 1];
+  __shared__ int lbase[TILE_CH];
+  const int tid = threadIdx.x;
+  const int64_t NB = (int64_t)m.F * m.B;
+  const int64_t b0 = (int64_t)blockIdx.x * TILE_BAGS;
+  const int nb = (int)min((int64_t)TILE_BAGS, NB - b0);
+  if (tid <= nb) off[tid] = offsets[b0 + tid];
+  __syncthreads();
+  const int64_t s0 = off[0], e0 = off[nb];
+  for (int64_t j0 = s0; j0 < e0; j0 += TILE_CH) {
+    const int n = (int)min((int64_t)TILE_CH, e0 - j0);
+    const int ne = ws.ent_n[j0];
+    int hb[TILE_EPT], cb[TILE_EPT];
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q) {
+      const int e = q * 256 + tid;
+      hb[q] = e < ne ? ws.ent_h[j0 + e] : -1;
+      cb[q] = e < ne ? ws.ent_c[j0 + e] : 0;
+    }
+    int ln[TILE_EPT];
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q) ln[q] = hb[q] >= 0 ? ws.cnt[hb[q]] : 0;
+    // a row whose lookups all sit in this chunk owns its whole segment: no cursor atomic; a row
+    // looked up once keeps its bag in its record (cur = its unique index, stored as ~u here)
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q)
+      if (hb[q] >= 0)
+        lbase[q * 256 + tid] = ln[q] == cb[q] ? (ln[q] == 1 ? ~ws.cur[hb[q]] : ws.cur[hb[q]])
+                                              : atomicAdd(&ws.cur[hb[q]], cb[q]);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < TILE_EPT; ++q) {
+      const int i = q * 256 + tid;
+      if (i < n) {
+        const int v = ws.lk[j0 + i];
+        const int lb = lbase[v & 0xffff];
+        const int32_t bag = (int32_t)(b0 + lds_bag_of(off, nb, j0 + i));
+        if (lb < 0) ws.urec[~lb].seg = bag;
+        else ws.perm[lb + (v >> 16)] = bag;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -258,20 +555,22 @@ __global__ void __launch_bounds__(256) bwd_hash_cols_kernel(EmbMeta m, ColArgs c
     int32_t h = -1;
     if (id != 0) {
       const int t = m.features[f].table;
-      h = hash_insert(ws, ((uint64_t)t << KEY_TABLE_SHIFT) | (uint64_t)py_mod64(id, ca.num_emb[f]));
+      h = hash_insert(ws, pk_key(t, (uint64_t)py_mod64(id, ca.num_emb[f])));
     }
     ws.slot_of[bag] = h;
   }
 }
 
-// k2b-1: per 1024-slot tile: number of occupied slots and of lookups
+__device__ __forceinline__ int slot_count(uint64_t w) { return w == EMPTY_KEY ? 0 : (int)(w & PK_CNT_MASK); }
+
+// k2b-1: per SCAN_TILE-slot tile: number of occupied slots and of lookups
 __global__ void __launch_bounds__(256) bwd_scan_reduce_kernel(BwdWs ws) {
   __shared__ int lu[4], lc[4];
-  const int64_t base = (int64_t)blockIdx.x * 1024;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
   int su = 0, sc = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = ws.cnt[base + j * 256 + threadIdx.x];
+  for (int j = 0; j < SCAN_TILE / 256; ++j) {
+    const int c = slot_count(ws.keys[base + j * 256 + threadIdx.x]);
     su += c > 0;
     sc += c;
   }
@@ -285,7 +584,7 @@ __global__ void __launch_bounds__(256) bwd_scan_reduce_kernel(BwdWs ws) {
   if (threadIdx.x == 0) {
     ws.bsum_u[blockIdx.x] = lu[0] + lu[1] + lu[2] + lu[3];
     ws.bsum_c[blockIdx.x] = lc[0] + lc[1] + lc[2] + lc[3];
-    if (blockIdx.x == 0) ws.U[2] = 0;  // hot list, filled by k2b-2
+    if (blockIdx.x == 0) *reinterpret_cast<unsigned long long*>(ws.U + 2) = 0ull;  // hot list, filled by k2b-2
   }
 }
 
@@ -309,11 +608,14 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
   pu = lds[0] + lds[1] + lds[2] + lds[3];
   pc = lds[4] + lds[5] + lds[6] + lds[7];
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x * 4;
-  int c[4], lu = 0, lcnt = 0;
+  constexpr int SPT = SCAN_TILE / 256;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SPT;
+  int c[SPT], lu = 0, lcnt = 0;
+  uint64_t wd[SPT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    c[j] = ws.cnt[base + j];
+  for (int j = 0; j < SPT; ++j) {
+    wd[j] = ws.keys[base + j];
+    c[j] = slot_count(wd[j]);
     lu += c[j] > 0;
     lcnt += c[j];
   }
@@ -342,18 +644,23 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
   }
   int eu = pu + wu + iu - lu, ec = pc + wc + ic - lcnt;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < SPT; ++j) {
     if (c[j] > 0) {
       const int64_t h = base + j;
       URec rec;
-      rec.key = ws.keys[h];
+      rec.key = pk_to_key(wd[j]);
       rec.seg = ec;
       rec.len = c[j];
       ws.urec[eu] = rec;
-      if (c[j] >= HOT_MIN) ws.hot[atomicAdd(&ws.U[2], 1)] = eu;
-      ws.cur[h] = ec;
+      if (c[j] >= HOT_MIN) {  // one 64-bit atomic: hot-row index (high word) and first work item (low)
+        const int nr = hot_nr(c[j]);
+        const unsigned long long pk =
+            atomicAdd(reinterpret_cast<unsigned long long*>(ws.U + 2), (1ull << 32) | (unsigned long long)nr);
+        ws.hot[(int)(pk >> 32)] = HotRec{eu, (int32_t)(pk & 0xffffffffull), nr, 0};
+      }
+      ws.cur[h] = c[j] == 1 ? eu : ec;  // a single lookup's bag goes into its record (k2c)
+      ws.cnt[h] = c[j];
       ws.keys[h] = EMPTY_KEY;
-      ws.cnt[h] = 0;
       eu += 1;
       ec += c[j];
     }
@@ -370,8 +677,12 @@ __global__ void __launch_bounds__(256) bwd_scatter_kernel(EmbMeta m, const int32
     for (int64_t j = s; j < e; ++j) {
       const int h = ws.slot_of[j];
       if (h < 0) continue;
-      const int pos = atomicAdd(&ws.cur[h], 1);
-      ws.perm[pos] = (int32_t)bag;
+      if (ws.cnt[h] == 1) {
+        ws.urec[ws.cur[h]].seg = (int32_t)bag;
+      } else {
+        const int pos = atomicAdd(&ws.cur[h], 1);
+        ws.perm[pos] = (int32_t)bag;
+      }
     }
   }
 }
@@ -407,65 +718,104 @@ struct BagRow {
 };
 
 // ---- k2d narrow: half-wave per unique row, D <= 128, D % 4 == 0 ----------------------------
+// Each half-wave takes NARROW_ROWS unique rows per pass and issues their loads together (record ->
+// {weight row, state, segment} -> gradient rows), so a wave keeps 8 independent row chains in
+// flight. Segments of <= 32 lookups are summed in ascending bag order (bitonic over the half-wave;
+// skipped when every segment of that row slot has one lookup): bitwise reproducible.
+constexpr int NARROW_ROWS = 4;
+
 __global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, const float* __restrict__ grad_out,
                                                                  int64_t ldg, const int32_t* __restrict__ offsets,
                                                                  int pooling, float* __restrict__ weights,
                                                                  float* __restrict__ state, float lr, float eps,
                                                                  BwdWs ws) {
+  constexpr int R = NARROW_ROWS;
   const int U = ws.U[0];
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31, half = lane >> 5;
   const BagRow br{grad_out, m.B, ldg, m.features};
-  const int64_t nhalf = (int64_t)gridDim.x * 8;
-  for (int64_t u = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half; u - half < U; u += nhalf) {
-    URec rec{0, 0, 0};
-    if (u < U) rec = ws.urec[u];
-    const bool active = u < U && rec.len < HOT_MIN;  // hot rows: bwd_adagrad_hot_kernel
-    if (!active) rec = URec{0, 0, 0};
-    const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
-    const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
-    const tt_table_meta_t tm = m.tables[active ? t : 0];
-    const int D = tm.dim;
-    const bool col_ok = active && hl * 4 < D;
-    // independent of the gradient: fetch the row and its state early
-    float* wrow = weights + tm.weight_offset + r * D;
-    float* srow = state + tm.state_offset + r;
-    f32x4v wv = col_ok ? *reinterpret_cast<const f32x4v*>(wrow + hl * 4) : (f32x4v)(0.f);
-    const float s_old = active ? *srow : 0.f;
-    const int n = rec.len;
-    f32x4v g = (f32x4v)(0.f);
-    // ascending bag order (bitonic over the half-wave), fp32: bitwise reproducible
-    const int nmax = max(n, __shfl_xor(n, 32, 64));
-    int mine = (active && hl < n) ? ws.perm[rec.seg + hl] : 0x7fffffff;
-    mine = bitonic_sort<32>(mine);
-    for (int i = 0; i < nmax; i += 2) {
-      const int b0 = __shfl(mine, (lane & 32) + i, 64);
-      const int b1 = __shfl(mine, (lane & 32) + min(i + 1, 31), 64);
-      const bool v0 = i < n, v1 = i + 1 < n;
-      f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
-      if (col_ok && v0) x0 = *reinterpret_cast<const f32x4v*>(br.row(b0) + hl * 4);
-      if (col_ok && v1) x1 = *reinterpret_cast<const f32x4v*>(br.row(b1) + hl * 4);
-      if (pooling == TT_POOL_MEAN) {
-        if (v0) x0 *= 1.f / (float)max(1, offsets[b0 + 1] - offsets[b0]);
-        if (v1) x1 *= 1.f / (float)max(1, offsets[b1 + 1] - offsets[b1]);
+  const int64_t wstep = (int64_t)gridDim.x * 4 * 64;
+  for (int64_t wbase = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; wbase < U; wbase += wstep) {
+  // the wave's 64 records in one coalesced read, handed out by lane shuffles
+  const URec myrec = wbase + lane < U ? ws.urec[wbase + lane] : URec{0, 0, 0};
+  for (int64_t base = wbase; base < min((int64_t)U, wbase + 64); base += 2 * R) {
+    URec rec[R];
+    bool act[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int src = (int)(base - wbase) + half * R + r;
+      const int64_t u = base + half * R + r;
+      rec[r].key = __shfl(myrec.key, src, 64);
+      rec[r].seg = __shfl(myrec.seg, src, 64);
+      rec[r].len = __shfl(myrec.len, src, 64);
+      act[r] = u < U && rec[r].len < HOT_MIN;  // hot rows: bwd_hot_partial_kernel
+      if (!act[r]) rec[r] = URec{0, 0, 0};
+    }
+    f32x4v wv[R];
+    float s_old[R];
+    int mine[R], n[R], D[R];
+    bool col_ok[R];
+    float* wrow[R];
+    float* srow[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {  // independent of the gradient: rows, state and segments first
+      const int t = (int)(rec[r].key >> KEY_TABLE_SHIFT);
+      const int64_t row = (int64_t)(rec[r].key & ((1ull << KEY_TABLE_SHIFT) - 1));
+      const tt_table_meta_t tm = m.tables[act[r] ? t : 0];
+      D[r] = tm.dim;
+      col_ok[r] = act[r] && hl * 4 < D[r];
+      wrow[r] = weights + tm.weight_offset + row * D[r];
+      srow[r] = state + tm.state_offset + row;
+      wv[r] = col_ok[r] ? *reinterpret_cast<const f32x4v*>(wrow[r] + hl * 4) : (f32x4v)(0.f);
+      s_old[r] = act[r] ? *srow[r] : 0.f;
+      n[r] = rec[r].len;
+      mine[r] = (act[r] && hl < n[r]) ? (n[r] == 1 ? rec[r].seg : ws.perm[rec[r].seg + hl]) : 0x7fffffff;
+    }
+    int nall = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int nm = max(n[r], __shfl_xor(n[r], 32, 64));
+      if (nm > 1) mine[r] = bitonic_sort<32>(mine[r]);
+      nall = max(nall, nm);
+    }
+    f32x4v g[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) g[r] = (f32x4v)(0.f);
+    for (int i = 0; i < nall; ++i) {
+      f32x4v x[R];
+      int b[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        b[r] = __shfl(mine[r], (lane & 32) + i, 64);
+        x[r] = (col_ok[r] && i < n[r]) ? *reinterpret_cast<const f32x4v*>(br.row(b[r]) + hl * 4) : (f32x4v)(0.f);
       }
-      if (v0) g += x0;
-      if (v1) g += x1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (i < n[r]) {
+          if (pooling == TT_POOL_MEAN) x[r] *= 1.f / (float)max(1, offsets[b[r] + 1] - offsets[b[r]]);
+          g[r] += x[r];
+        }
+      }
     }
     // row-wise Adagrad: s += mean(G^2); w += (-lr * G) / (sqrt(s) + eps)
-    float sq = g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
-    if (active) {
-      const float snew = s_old + sq / (float)D;
-      const float stdv = sqrtf(snew) + eps;
-      if (col_ok) {
+    for (int r = 0; r < R; ++r) {
+      float sq = g[r][0] * g[r][0] + g[r][1] * g[r][1] + g[r][2] * g[r][2] + g[r][3] * g[r][3];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
-        *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
+      for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+      if (act[r]) {
+        const float snew = s_old[r] + sq / (float)D[r];
+        const float stdv = sqrtf(snew) + eps;
+        if (col_ok[r]) {
+          f32x4v w = wv[r];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[r][v]) / stdv;
+          *reinterpret_cast<f32x4v*>(wrow[r] + hl * 4) = w;
+        }
+        if (hl == 0) *srow[r] = snew;
       }
-      if (hl == 0) *srow = snew;
     }
+  }
   }
 }
 
@@ -486,7 +836,7 @@ __device__ __forceinline__ void adagrad_row(const EmbMeta& m, const BagRow& br, 
   float sq = 0.f;
   float gsave[ADA_KMAX][VEC];
   // n < HOT_MIN (hot rows go to bwd_adagrad_hot_kernel): ascending bag order, fp32
-  int sorted = lane < n ? ws.perm[s + lane] : 0x7fffffff;
+  int sorted = lane < n ? (n == 1 ? s : ws.perm[s + lane]) : 0x7fffffff;  // n == 1: s is the bag
   sorted = bitonic_sort<64>(sorted);
 #pragma unroll
   for (int k = 0; k < ADA_KMAX; ++k) {
@@ -547,151 +897,242 @@ __global__ void __launch_bounds__(256) bwd_adagrad_kernel(EmbMeta m, const float
   }
 }
 
-// ---- k2d hot rows: a workgroup per row looked up >= HOT_MIN times --------------------------
-// The segment's bag ids are summed in ascending order whatever order the scatter left them in:
-// passes over bag-id ranges [lo, hi) holding <= HOT_CAP ids each (hi found by halving, so the
-// ranges depend on the id multiset only), each range sorted in LDS; inside a range, group g of
-// HOT_G sums sorted positions g, g + HOT_G, ..., and the group partials are added in group order.
-// Every step of that is a function of the multiset of bag ids: bitwise reproducible.
-constexpr int HOT_TPR = 64;                 // threads per gradient row (columns strided by 64)
-constexpr int HOT_G = 256 / HOT_TPR;        // row groups
-constexpr int HOT_KC = 1024 / HOT_TPR;      // columns per thread at D = 1024
-
-__device__ __forceinline__ int block_sum_i(int v, int* red) {
-  v = wave_sum_i(v);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+// ---- k2d hot rows (looked up >= HOT_MIN times) -----------------------------------------------
+// A hot row with c lookups is split into NR = hot_nr(c) bag-id ranges (one work item each; bwd_
+// hot_partial_kernel, persistent grid). An item counts its row's lookups per bag of its range in LDS
+// (HOT_WIN bags per pass; passes start at the smallest bag not yet counted, so empty windows cost
+// nothing), compacts the non-zero bags in ascending order, and 8 half-wave groups sum
+// count x grad_out[bag] over positions g, g+8, ...; the group partials are added in group order.
+// NR = 1: the item applies row-wise Adagrad itself; NR > 1: it writes a partial row and
+// bwd_hot_final_kernel adds the NR partials in range order and applies Adagrad. Every step is a
+// function of the multiset of (row, bag) lookups: bitwise reproducible, no sort, no same-address
+// atomics beyond LDS, and the hottest row is spread over up to HOT_NR_MAX workgroups.
+__device__ __forceinline__ int block_min_i(int v, int* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
   __syncthreads();
-  if (lane == 0) red[wid] = v;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  return red[0] + red[1] + red[2] + red[3];
+  return min(min(red[0], red[1]), min(red[2], red[3]));
 }
 
-__global__ void __launch_bounds__(256) bwd_adagrad_hot_kernel(EmbMeta m, const float* __restrict__ grad_out,
-                                                              int64_t ldg, const int32_t* __restrict__ offsets,
-                                                              int pooling, float* __restrict__ weights,
-                                                              float* __restrict__ state, float lr, float eps,
-                                                              BwdWs ws) {
-  __shared__ int ids[HOT_CAP];
-  __shared__ float part[HOT_G][1024];
-  __shared__ int redi[4];
-  __shared__ float redf[4];
-  __shared__ int fill;
-  const int tid = threadIdx.x;
-  const int cg = tid % HOT_TPR, gi = tid / HOT_TPR;
-  const int nhot = ws.U[2];
-  const BagRow br{grad_out, m.B, ldg, m.features};
-  for (int h = blockIdx.x; h < nhot; h += gridDim.x) {
-    const URec rec = ws.urec[ws.hot[h]];
-    const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
-    const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
-    const tt_table_meta_t tm = m.tables[t];
-    const int D = tm.dim;
-    const int32_t* seg = ws.perm + rec.seg;
-    const int n = rec.len;
-    float tot[4] = {0.f, 0.f, 0.f, 0.f};  // column tid + 256 k (D <= 1024)
-    const int64_t NB = (int64_t)m.F * m.B;  // bag ids are < F * B
-    int64_t lo = 0, width = 1;
-    while (width < NB) width <<= 1;
-    while (lo < NB) {
-      int64_t hi;
-      int c;
-      while (true) {  // shrink [lo, hi) until it holds <= HOT_CAP ids (or a single bag id)
-        hi = lo + width < NB ? lo + width : NB;
-        int k = 0;
-        for (int i = tid; i < n; i += 256) {
-          const int b = seg[i];
-          k += (b >= lo && b < hi);
-        }
-        c = block_sum_i(k, redi);
-        if (c <= HOT_CAP || hi - lo == 1) break;
-        width >>= 1;
-      }
-      if (c == 0) {
-        lo = hi;
-        width <<= 1;
-        continue;
-      }
-      const bool single = c > HOT_CAP;  // one bag id repeated c times: every position holds lo
-      if (!single) {
-        if (tid == 0) fill = 0;
-        __syncthreads();
-        for (int i = tid; i < n; i += 256) {
-          const int b = seg[i];
-          if (b >= lo && b < hi) ids[atomicAdd(&fill, 1)] = b;
-        }
-        int P = 1;
-        while (P < c) P <<= 1;
-        for (int i = c + tid; i < P; i += 256) ids[i] = 0x7fffffff;
-        __syncthreads();
-        for (int k = 2; k <= P; k <<= 1)
-          for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < P; i += 256) {
-              const int x = i ^ j;
-              if (x > i) {
-                const int a = ids[i], b = ids[x];
-                if ((a > b) == ((i & k) == 0)) {
-                  ids[i] = b;
-                  ids[x] = a;
-                }
-              }
-            }
-            __syncthreads();
-          }
-      }
-      float acc[HOT_KC];
+template <int VEC, int KC>
+__device__ __forceinline__ void hot_accumulate(const BagRow& br, const int32_t* __restrict__ offsets, int pooling,
+                                               int D, const int* wcnt, const int16_t* wb, int64_t wlo, int mtot,
+                                               float (&acc)[KC][VEC]) {
+  typedef __attribute__((ext_vector_type(VEC))) float vf;
+  const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
+  constexpr int U4 = KC == 1 ? 4 : 1;  // rows in flight per group (KC loads each)
+  for (int e0 = g; e0 < mtot; e0 += 8 * U4) {
+    vf x[U4][KC];
+    float sc[U4];
 #pragma unroll
-      for (int k = 0; k < HOT_KC; ++k) acc[k] = 0.f;
-      for (int i = gi; i < c; i += HOT_G) {
-        const int b = single ? (int)lo : ids[i];
-        const float* g = br.row(b);
-        const float sc = pooling == TT_POOL_MEAN ? 1.f / (float)max(1, offsets[b + 1] - offsets[b]) : 1.f;
+    for (int u = 0; u < U4; ++u) {
+      const int e = e0 + 8 * u;
+      sc[u] = 0.f;
+      if (e < mtot) {
+        const int b = (int)(wlo + wb[e]);
+        float s = (float)wcnt[e];
+        if (pooling == TT_POOL_MEAN) s *= 1.f / (float)max(1, offsets[b + 1] - offsets[b]);
+        sc[u] = s;
+        const float* row = br.row(b);
 #pragma unroll
-        for (int k = 0; k < HOT_KC; ++k) {
-          const int col = cg + k * HOT_TPR;
-          if (col < D) acc[k] += g[col] * sc;
+        for (int k = 0; k < KC; ++k) {
+          const int c = l + 32 * k;
+          x[u][k] = c * VEC < D ? *reinterpret_cast<const vf*>(row + c * VEC) : (vf)(0.f);
         }
       }
-#pragma unroll
-      for (int k = 0; k < HOT_KC; ++k) {
-        const int col = cg + k * HOT_TPR;
-        if (col < D) part[gi][col] = acc[k];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int col = tid + 256 * k;
-        if (col < D) {
-          float s = 0.f;
-#pragma unroll
-          for (int g = 0; g < HOT_G; ++g) s += part[g][col];
-          tot[k] += s;
-        }
-      }
-      __syncthreads();
-      lo = hi;
-      width <<= 1;  // the next range starts wider (still a function of the id multiset only)
     }
-    // row-wise Adagrad on the summed row
-    float sq = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (tid + 256 * k < D) sq += tot[k] * tot[k];
-    sq = wave_sum(sq);
+    for (int u = 0; u < U4; ++u) {
+      if (e0 + 8 * u < mtot) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[k][v] += sc[u] == 1.f ? x[u][k][v] : x[u][k][v] * sc[u];
+      }
+    }
+  }
+}
+
+template <int VEC, int KC>
+__device__ __forceinline__ void hot_item(const EmbMeta& m, const BagRow& br, const int32_t* __restrict__ offsets,
+                                         int pooling, float* __restrict__ weights, float* __restrict__ state,
+                                         float lr, float eps, const BwdWs& ws, const HotRec& hr, int item,
+                                         int* wcnt, int16_t* wb, int* red, float* redf) {
+  const int tid = threadIdx.x;
+  const URec rec = ws.urec[hr.u];
+  const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
+  const int64_t row = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
+  const tt_table_meta_t tm = m.tables[t];
+  const int D = tm.dim;
+  const int32_t* seg = ws.perm + rec.seg;
+  const int n = rec.len;
+  const int64_t NB = (int64_t)m.F * m.B;
+  const int r = item - hr.pbase;
+  const int64_t rlo = r * NB / hr.nr, rhi = (r + 1) * NB / hr.nr;
+  float acc[KC][VEC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[k][v] = 0.f;
+  int64_t wlo = rlo;
+  while (wlo < rhi) {
+    int mn = 0x7fffffff;
+    for (int i = tid; i < n; i += 256) {
+      const int b = seg[i];
+      if (b >= wlo && b < rhi) mn = min(mn, b);
+    }
+    mn = block_min_i(mn, red);
+    if (mn == 0x7fffffff) break;
+    wlo = mn;
+    const int64_t whi = min(rhi, wlo + HOT_WIN);
+    for (int i = tid; i < HOT_WIN; i += 256) wcnt[i] = 0;
     __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+      const int b = seg[i];
+      if (b >= wlo && b < whi) atomicAdd(&wcnt[b - wlo], 1);
+    }
+    __syncthreads();
+    constexpr int BPT = HOT_WIN / 256;
+    int cc[BPT], k = 0;
+#pragma unroll
+    for (int v = 0; v < BPT; ++v) {
+      cc[v] = wcnt[tid * BPT + v];
+      k += cc[v] > 0;
+    }
+    int mtot;
+    int d = block_excl_scan(k, red, &mtot);
+#pragma unroll
+    for (int v = 0; v < BPT; ++v)
+      if (cc[v] > 0) {
+        wcnt[d] = cc[v];
+        wb[d] = (int16_t)(tid * BPT + v);
+        ++d;
+      }
+    __syncthreads();
+    hot_accumulate<VEC, KC>(br, offsets, pooling, D, wcnt, wb, wlo, mtot, acc);
+    __syncthreads();
+    wlo = whi;
+  }
+  // group partials -> LDS (wcnt reused as float[8][HOT_DMAX]) -> summed in group order
+  float* part = reinterpret_cast<float*>(wcnt);
+  const int g = tid >> 5, l = tid & 31;
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const int c = (l + 32 * k) * VEC + v;
+      if (c < D) part[g * HOT_DMAX + c] = acc[k][v];
+    }
+  __syncthreads();
+  float tot[HOT_DMAX / 256];
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < HOT_DMAX / 256; ++k) {
+    const int c = tid + 256 * k;
+    float s = 0.f;
+    if (c < D) {
+#pragma unroll
+      for (int gg = 0; gg < 8; ++gg) s += part[gg * HOT_DMAX + c];
+    }
+    tot[k] = s;
+    sq += s * s;
+  }
+  if (hr.nr == 1) {
+    sq = wave_sum(sq);
     if ((tid & 63) == 0) redf[tid >> 6] = sq;
     __syncthreads();
     sq = (redf[0] + redf[1]) + (redf[2] + redf[3]);
-    float* srow = state + tm.state_offset + r;
+    float* srow = state + tm.state_offset + row;
     const float snew = *srow + sq / (float)D;
     const float stdv = sqrtf(snew) + eps;
-    float* wrow = weights + tm.weight_offset + r * D;
+    float* wrow = weights + tm.weight_offset + row * D;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int col = tid + 256 * k;
-      if (col < D) wrow[col] = wrow[col] + (-lr * tot[k]) / stdv;
+    for (int k = 0; k < HOT_DMAX / 256; ++k) {
+      const int c = tid + 256 * k;
+      if (c < D) wrow[c] = wrow[c] + (-lr * tot[k]) / stdv;
     }
     __syncthreads();
     if (tid == 0) *srow = snew;
+  } else {
+    float* p = ws.hotp + (int64_t)item * HOT_DMAX;
+#pragma unroll
+    for (int k = 0; k < HOT_DMAX / 256; ++k) {
+      const int c = tid + 256 * k;
+      if (c < D) p[c] = tot[k];
+    }
+  }
+  __syncthreads();  // LDS reuse by the next item
+}
+
+__global__ void __launch_bounds__(256) bwd_hot_partial_kernel(EmbMeta m, const float* __restrict__ grad_out,
+                                                              int64_t ldg, const int32_t* __restrict__ offsets,
+                                                              int pooling, float* __restrict__ weights,
+                                                              float* __restrict__ state, float lr, float eps,
+                                                              BwdWs ws, int vec4_ok) {
+  __shared__ int wcnt[HOT_WIN];  // per-bag counts of a window / compacted counts / group partials
+  __shared__ int16_t wb[HOT_WIN];
+  __shared__ int red[4];
+  __shared__ float redf[4];
+  const unsigned long long hw = *reinterpret_cast<const unsigned long long*>(ws.U + 2);
+  const int items = (int)(hw & 0xffffffffull), nhot = (int)(hw >> 32);
+  const BagRow br{grad_out, m.B, ldg, m.features};
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    int lo = 0, hi = nhot;  // hot row of the item: the largest h with pbase <= it (pbase ascends with h)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (ws.hot[mid].pbase <= it) lo = mid;
+      else hi = mid;
+    }
+    const HotRec hr = ws.hot[lo];
+    const int D = m.tables[(int)(ws.urec[hr.u].key >> KEY_TABLE_SHIFT)].dim;
+    if (vec4_ok && (D & 3) == 0 && D <= 128)
+      hot_item<4, 1>(m, br, offsets, pooling, weights, state, lr, eps, ws, hr, it, wcnt, wb, red, redf);
+    else if (vec4_ok && (D & 3) == 0)
+      hot_item<4, 8>(m, br, offsets, pooling, weights, state, lr, eps, ws, hr, it, wcnt, wb, red, redf);
+    else
+      hot_item<1, 32>(m, br, offsets, pooling, weights, state, lr, eps, ws, hr, it, wcnt, wb, red, redf);
+  }
+}
+
+// rows split over NR > 1 ranges: a wave per row adds the partials in range order, then Adagrad
+__global__ void __launch_bounds__(256) bwd_hot_final_kernel(EmbMeta m, float* __restrict__ weights,
+                                                            float* __restrict__ state, float lr, float eps,
+                                                            BwdWs ws) {
+  const int nhot = ws.U[3];
+  const int lane = threadIdx.x & 63;
+  for (int h = blockIdx.x * 4 + (threadIdx.x >> 6); h < nhot; h += gridDim.x * 4) {
+    const HotRec hr = ws.hot[h];
+    if (hr.nr == 1) continue;
+    const URec rec = ws.urec[hr.u];
+    const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
+    const int64_t row = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
+    const tt_table_meta_t tm = m.tables[t];
+    const int D = tm.dim;
+    const float* p = ws.hotp + (int64_t)hr.pbase * HOT_DMAX;
+    float tot[HOT_DMAX / 64];
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < HOT_DMAX / 64; ++k) {
+      const int c = lane + 64 * k;
+      float s = 0.f;
+      if (c < D)
+        for (int r = 0; r < hr.nr; ++r) s += p[(int64_t)r * HOT_DMAX + c];
+      tot[k] = s;
+      sq += s * s;
+    }
+    sq = wave_sum(sq);
+    float* srow = state + tm.state_offset + row;
+    const float snew = *srow + sq / (float)D;
+    const float stdv = sqrtf(snew) + eps;
+    float* wrow = weights + tm.weight_offset + row * D;
+#pragma unroll
+    for (int k = 0; k < HOT_DMAX / 64; ++k) {
+      const int c = lane + 64 * k;
+      if (c < D) wrow[c] = wrow[c] + (-lr * tot[k]) / stdv;
+    }
+    if (lane == 0) *srow = snew;
   }
 }
 
@@ -822,7 +1263,7 @@ int tt_bwd_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookups,
 }
 
 static int launch_scan_scatter(const EmbMeta& m, const int32_t* offsets, BwdWs& w, hipStream_t st, int gb) {
-  const int nb = (int)ceil_div(w.cap, 1024);
+  const int nb = (int)ceil_div(w.cap, SCAN_TILE);
   bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
   bwd_scan_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
   if ((int64_t)m.F * m.B > 0) bwd_scatter_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, offsets, w);
@@ -842,14 +1283,20 @@ int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t
   if (rc) return rc;
   if (!offsets) return fail(TT_EINVAL, "bwd_prepare: null offsets");
   for (int t = 0; t < T; ++t)
-    if (tables[t].num_rows >= (1ll << KEY_TABLE_SHIFT)) return fail(TT_EINVAL, "bwd_prepare: table rows >= 2^40");
+    if (tables[t].num_rows >= (1ll << PK_ROW_BITS) - 1) return fail(TT_EINVAL, "bwd_prepare: table rows >= 2^34 - 1");
   BwdWs w;
   bwd_layout(workspace, max_lookups, &w);
   hipStream_t st = as_stream(stream);
   const int64_t nbag = (int64_t)F * B;
-  const int gb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(nbag, 256)));
-  if (nbag > 0) bwd_hash_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, values, id_dtype, offsets, bounds_check, w);
-  return launch_scan_scatter(m, offsets, w, st, gb);
+  const int64_t tiles = ceil_div(nbag, TILE_BAGS);
+  if (tiles > INT32_MAX) return fail(TT_EINVAL, "bwd_prepare: too many bags");
+  if (nbag > 0)
+    bwd_tile_hash_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, values, id_dtype, offsets, bounds_check, w);
+  const int nb = (int)ceil_div(w.cap, SCAN_TILE);
+  bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
+  bwd_scan_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
+  if (nbag > 0) bwd_tile_scatter_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, offsets, w);
+  return check_launch("bwd_prepare");
 }
 
 int tt_bwd_prepare_cols(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F, int64_t B,
@@ -867,6 +1314,8 @@ int tt_bwd_prepare_cols(const tt_table_meta_t* tables, int T, const tt_feature_m
   for (int f = 0; f < F; ++f)
     if (num_embeddings[f] > tables[features[f].table].num_rows)
       return fail(TT_EINVAL, "bwd_prepare_cols: num_embeddings exceeds the table's rows");
+  for (int t = 0; t < T; ++t)
+    if (tables[t].num_rows >= (1ll << PK_ROW_BITS) - 1) return fail(TT_EINVAL, "bwd_prepare_cols: table rows >= 2^34 - 1");
   BwdWs w;
   bwd_layout(workspace, max_lookups, &w);
   hipStream_t st = as_stream(stream);
@@ -913,7 +1362,7 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
   bwd_layout(workspace, max_lookups, &w);
   hipStream_t st = as_stream(stream);
   if (narrow) {
-    const int grid = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(max_lookups, 8)));
+    const int grid = (int)std::min<int64_t>(4096, std::max<int64_t>(1, ceil_div(max_lookups, 4 * 64)));
     bwd_adagrad_narrow_kernel<<<dim3(grid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
                                                                 lr, eps, w);
   } else {
@@ -922,9 +1371,11 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
                                                          w, vec_ok ? 1 : 0);
   }
   if (max_lookups >= HOT_MIN) {
-    const int hgrid = (int)std::min<int64_t>(512, max_lookups / HOT_MIN);
-    bwd_adagrad_hot_kernel<<<dim3(hgrid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
-                                                              lr, eps, w);
+    const int hgrid = (int)std::min<int64_t>(2048, hot_items_max(max_lookups));
+    bwd_hot_partial_kernel<<<dim3(hgrid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
+                                                              lr, eps, w, vec_ok ? 1 : 0);
+    const int fgrid = (int)std::min<int64_t>(1024, max_lookups / HOT_SPLIT / 4 + 1);
+    bwd_hot_final_kernel<<<dim3(fgrid), dim3(256), 0, st>>>(m, weights, state, lr, eps, w);
   }
   return check_launch("bwd_rowwise_adagrad");
 }
@@ -949,7 +1400,7 @@ int tt_pooled_bwd_dense(const tt_table_meta_t* tables, int T, const tt_feature_m
 
 namespace tt {
 static int check_ws(void* workspace, size_t ws_bytes, int64_t max_lookups, const char* what) {
-  if (max_lookups > INT32_MAX / 2) return fail(TT_EINVAL, std::string(what) + ": max_lookups too large");
+  if (max_lookups >= (1ll << PK_CNT_BITS)) return fail(TT_EINVAL, std::string(what) + ": max_lookups >= 2^24");
   if (!workspace || ws_bytes < tt_bwd_workspace_bytes(max_lookups))
     return fail(TT_ECAPACITY, std::string(what) + ": workspace too small");
   return TT_OK;
