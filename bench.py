@@ -38,7 +38,10 @@ WORKLOADS = {
     # name: (num_users, num_items, dim, batch, layer_sizes)
     "northstar": (50_000_000, 100_000_000, 128, 8192, [128, 64]),
     "config2": (5_000_000, 10_000_000, 64, 4096, [128, 64]),
+    # SURVEY 8(d) config 5 on one GPU (both tables fit in 288 GB): multi-hot bags, lengths U{1..39}
+    "config5": (50_000_000, 100_000_000, 128, 16384, [128, 64]),
 }
+MULTIHOT = {"config5": 39}  # workload -> max bag length (KJT input, bags of 1..max ids)
 
 
 def parse():
@@ -188,6 +191,139 @@ def pmc_traffic(kernel_name: str):
 
 
 KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_kernel", "k3": "tower_update_dedup_kernel"}
+
+
+def synth_kjt_batches(num_users, num_items, B, maxlen, n, device, ids, seed):
+    """Multi-hot KJT batches (keys user, item; key-major bags of Uniform{1..maxlen} ids in range)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    out = []
+    for _ in range(n):
+        lengths = torch.randint(1, maxlen + 1, (2 * B,), generator=g, device=device, dtype=torch.int32)
+        offsets = torch.zeros(2 * B + 1, dtype=torch.int32, device=device)
+        offsets[1:] = torch.cumsum(lengths, 0)
+        vals = []
+        for f, N in enumerate((num_users, num_items)):
+            k = int(lengths[f * B:(f + 1) * B].sum())
+            if ids == "uniform":
+                vals.append(torch.randint(0, N, (k,), generator=g, device=device, dtype=torch.int64))
+            else:
+                u01 = torch.rand(k, generator=g, device=device, dtype=torch.float64)
+                r = torch.floor(torch.exp(u01 * torch.log(torch.tensor(float(N), device=device, dtype=torch.float64))))
+                vals.append((r.to(torch.int64) * 2654435761) % N)
+        lab = torch.randint(0, 2, (B,), generator=g, device=device, dtype=torch.int32)
+        out.append((torch.cat(vals), offsets, lab))
+    return out
+
+
+def run_multihot(args):
+    """SURVEY 8(d) config 5 shape at N = 1: the fused step on multi-hot KJT input (tt_pooled_fwd ->
+    fused towers T1 -> tiled tt_bwd_prepare (side stream) -> T2/T3 (side stream) ->
+    tt_bwd_rowwise_adagrad), one HIP graph per resident batch."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    maxlen = MULTIHOT[args.workload]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    batches = synth_kjt_batches(num_users, num_items, B, maxlen, 4, dev, args.ids, seed=4)
+    cap = max(v.numel() for v, _, _ in batches)
+    step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01, lr_dense=0.01,
+                             id_dtype=torch.int64, seed=0, max_lookups=cap)
+    step.capture_pool_kjt(batches)
+
+    def run(n, i=0):
+        for j in range(n):
+            step.pool_graphs[(i + j) % len(step.pool_graphs)].replay()
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms = dt / args.steps * 1e3
+    value = args.steps * B / dt
+    loss = float(step.loss)
+    # per-launch device time: eager steps with HIP events around each launch on its stream
+    keep = step.values, step.offsets, step.labels
+    step._timing = []
+    try:
+        for i in range(min(args.steps, 20)):
+            step.values, step.offsets, step.labels = batches[i % len(batches)]
+            step._timing.append({})
+            step.step()
+        torch.cuda.synchronize()
+        acc = {}
+        for mk in step._timing:
+            for name, (a, b) in mk.items():
+                acc.setdefault(name, []).append(a.elapsed_time(b))
+    finally:
+        step._timing = None
+        step.values, step.offsets, step.labels = keep
+    timed = {k: sum(v) / len(v) for k, v in acc.items()}
+    nnz = sum(v.numel() for v, _, _ in batches) // len(batches)
+    uniq = 0
+    for v, o, _ in batches:
+        nb = int(o[B])
+        uniq += int(torch.unique(torch.cat([v[:nb], v[nb:] + (1 << 40)])).numel())
+    uniq //= len(batches)
+    FB = 2 * B
+    kern = {
+        "fwd": {"bytes": nnz * (8 + 4 * D) + FB * (4 + 4 * D), "kernel": "pooled_fwd_kernel",
+                "what": "tt_pooled_fwd: segmented gather + sum pool (8 B id + 4D row per lookup, 4D per bag)"},
+        "prep": {"bytes": nnz * (8 + 4 + 4) + FB * 4, "kernel": "bwd_tile_hash + scan + bwd_tile_scatter",
+                 "what": "tt_bwd_prepare: ids read, per-lookup entry word, segment scatter"},
+        "upd": {"bytes": nnz * (4 * D + 4) + uniq * (8 * D + 8), "kernel": "bwd_adagrad_narrow_kernel (+ hot-row launches)",
+                "what": "tt_bwd_rowwise_adagrad: grad rows per lookup, weight row + state read+write per unique row"},
+        "t1": {"bytes": None, "kernel": "tower_fwd_bwd_kernel", "what": "fused towers fwd/bwd + dot/BCE"},
+        "t2t3": {"bytes": None, "kernel": "tower_wgrad + tower_update", "what": "tower weight grads + Adam (side stream)"},
+    }
+    for name, k in kern.items():
+        if name in timed:
+            k["ms"] = round(timed[name], 5)
+            if k["bytes"]:
+                k["GB/s"] = round(k["bytes"] / timed[name] / 1e6, 1)
+    emb_bytes = nnz * (16 + 4 * D) + FB * (4 + 8 * D) + uniq * (8 * D + 8)  # SURVEY 8(d)
+    emb_ms = sum(timed.get(n, 0.0) for n in ("fwd", "prep", "upd"))
+    dom = max(("fwd", "upd"), key=lambda n: timed.get(n, 0.0))
+    traffic, src = pmc_traffic(kern[dom]["kernel"].split()[0])
+    ach = kern[dom].get("GB/s")
+    roofline = {"bound": "hbm", "kernel": kern[dom]["kernel"], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic, "traffic_source": src,
+                "bytes_per_launch": kern[dom]["bytes"], "ms_per_launch": kern[dom].get("ms"),
+                "timing": "HIP events around each launch on its stream over eager steps of the same sequence",
+                "kernels": kern, "lookups": nnz, "unique_rows": uniq,
+                "embedding_path": {"bytes_per_step": emb_bytes, "ms": round(emb_ms, 5),
+                                   "GB/s": round(emb_bytes / emb_ms / 1e6, 1) if emb_ms else None,
+                                   "frac": round(emb_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4) if emb_ms else None,
+                                   "note": "SURVEY 8(d) bytes over the summed time of the three embedding "
+                                           "launches (fwd, prepare, fused Adagrad)"}}
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen)
+    return value, ms, loss, roofline, cpu, args.steps
+
+
+def cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen):
+    """The oracle train_step on multi-hot bags of the same shape (tables scaled to --cpu-rows)."""
+    from oracle import ref
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    rows = min(args.cpu_rows, num_users), min(args.cpu_rows, num_items)
+    st = ref.init_state(list(rows), [D, D], [0, 1], [0], [1], layers, seed=0)
+    bs = synth_kjt_batches(rows[0], rows[1], B, maxlen, 2, torch.device("cpu"), "uniform", seed=0)
+    ref.train_step(st, bs[0][0], bs[0][1], B, bs[0][2], 0.01, 0.01)
+    n = min(args.cpu_steps, 5)
+    t0 = time.perf_counter()
+    for i in range(n):
+        v, o, lab = bs[i % 2]
+        ref.train_step(st, v, o, B, lab, 0.01, 0.01)
+    dt = time.perf_counter() - t0
+    return {"value": round(n * B / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} steps of the oracle train_step on multi-hot bags (lengths U{{1..{maxlen}}}) at B={B}, "
+                      f"D={D}, towers {layers}, tables scaled to {rows[0]}x{D} / {rows[1]}x{D}; host CPU "
+                      f"{platform.processor() or platform.machine()}"}
 
 
 def roofline_report(kern, timed, nnz, uniq, step, B):
@@ -382,12 +518,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    hot = f"multi-hot (bags of 1..{MULTIHOT[args.workload]})" if args.workload in MULTIHOT else "single-hot"
     config = {"workload": f"{args.workload}: {num_items // 1_000_000}M items x {num_users // 1_000_000}M users, "
-                          f"emb_dim {D}, towers {layers}, single-hot {args.ids} ids",
+                          f"emb_dim {D}, towers {layers}, {hot} {args.ids} ids",
               "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D, "tower_dtype": "bf16 (MFMA, fp32 acc)",
               "parallelism": "single-gpu hipgraph"}
     sharded_info = None
-    if world == 1 and not args.sharded:
+    if args.workload in MULTIHOT:
+        if world != 1 or args.sharded:
+            raise SystemExit(f"{args.workload}: the multi-hot workload runs at N = 1 (unsharded tables)")
+        value, ms, loss, roofline, cpu, steps_run = run_multihot(args)
+        config["parallelism"] = "single-gpu hipgraph, KJT input"
+    elif world == 1 and not args.sharded:
         value, ms, loss, roofline, cpu, steps_run = run_single(args)
     else:
         torch.cuda.set_device(local_rank)
@@ -402,7 +544,7 @@ def main():
                                  f"{sharded_info['mode']}")
         config["sharded"] = sharded_info
     if rank == 0:
-        out = {"metric": "training pairs/sec at batch 8192 (per GPU)", "value": round(value, 1), "unit": "pairs/s",
+        out = {"metric": f"training pairs/sec at batch {B} (per GPU)", "value": round(value, 1), "unit": "pairs/s",
                "n_gpus": world, "steps": steps_run, "warmup": args.warmup, "ms_per_step": round(ms, 5),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (uniform ids, Bernoulli labels), random-init weights", "config": config,

@@ -29,13 +29,17 @@ __global__ void k_rmw(float* __restrict__ tab, const int64_t* __restrict__ rows,
   }
 }
 
-int main() {
-  const int n = 16384;
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 16384;  // rows per launch (654342: config 5 multi-hot scale)
   const int64_t sizes_rows[] = {1ll << 17, 1ll << 21, 1ll << 24, 1ll << 26, 150000000ll};  // 64 MB .. 76.8 GB
   float* out;
   int64_t* rows;
   hipMalloc(&out, (size_t)n * 512);
   hipMalloc(&rows, (size_t)n * 8);
+  hipEvent_t e0, e1, e2;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventCreate(&e2);
   std::mt19937_64 rng(1);
   for (int64_t R : sizes_rows) {
     float* tab = nullptr;
@@ -46,13 +50,28 @@ int main() {
     hipMemset(tab, 0, (size_t)R * 512);
     std::vector<int64_t> h(n);
     for (auto& x : h) x = (int64_t)(rng() % (uint64_t)R);
-    hipMemcpy(rows, h.data(), n * 8, hipMemcpyHostToDevice);
-    for (int rep = 0; rep < 20; ++rep) {
-      hipLaunchKernelGGL(k_gather, dim3(n * 32 / 256), dim3(256), 0, 0, tab, rows, out, n);
-      hipLaunchKernelGGL(k_rmw, dim3(n * 32 / 256), dim3(256), 0, 0, tab, rows, out, n);
+    hipMemcpy(rows, h.data(), (size_t)n * 8, hipMemcpyHostToDevice);
+    float tg = 0.f, tr = 0.f;
+    const int reps = 20;
+    for (int rep = 0; rep < reps + 2; ++rep) {
+      hipEventRecord(e0, 0);
+      hipLaunchKernelGGL(k_gather, dim3((unsigned)((int64_t)n * 32 / 256)), dim3(256), 0, 0, tab, rows, out, n);
+      hipEventRecord(e1, 0);
+      hipLaunchKernelGGL(k_rmw, dim3((unsigned)((int64_t)n * 32 / 256)), dim3(256), 0, 0, tab, rows, out, n);
+      hipEventRecord(e2, 0);
+      hipEventSynchronize(e2);
+      float a = 0.f, b = 0.f;
+      hipEventElapsedTime(&a, e0, e1);
+      hipEventElapsedTime(&b, e1, e2);
+      if (rep >= 2) {
+        tg += a;
+        tr += b;
+      }
     }
-    hipDeviceSynchronize();
-    printf("rows %lld done\n", (long long)R);
+    tg /= reps;
+    tr /= reps;
+    printf("rows %lld n %d: gather %.1f us (%.0f GB/s of rows), rmw %.1f us (%.0f GB/s of rows r+w)\n", (long long)R, n,
+           tg * 1e3, (double)n * 512 / tg / 1e6, tr * 1e3, (double)n * 1024 / tr / 1e6);
     hipFree(tab);
   }
   return 0;

@@ -1,0 +1,96 @@
+"""The fused step on multi-hot KJT input (FusedTwoTowerStep(max_lookups=...), SURVEY 8(d) config 5
+shape at test size) against the oracle's train_step (torch CPU fp32 embedding_bag sum, towers, BCE,
+row-wise Adagrad on touched rows, Adam): bags of 0..9 ids (empty bags included), ids in range as a
+KJT carries them (03_model_training.py:367-371, :417).
+
+Tolerances: pooled embeddings (fp32 sums; torch CPU embedding_bag adds in its own order) rtol 1e-5, atol 1e-6 x max bag length; fp32 parity mode loss/logits
+rtol 1e-4 and updated tables atol 1e-5 over 3 steps; bf16 towers: pooled exact-order sums as above,
+loss rtol 2e-2 on the first step."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _kjt(rng, B, N, maxlen, hot=False):
+    lengths = rng.integers(0, maxlen + 1, 2 * B).astype(np.int32)
+    vals = []
+    for i in range(2 * B):
+        n = N[i // B]
+        v = (rng.zipf(1.5, lengths[i]) - 1) % n if hot else rng.integers(0, n, lengths[i])
+        vals.extend(v.tolist())
+    return np.asarray(vals, np.int64), ref.complete_cumsum(lengths)
+
+
+def _state(st, N, D):
+    return ref.TwoTowerState(
+        tables=[st.tables.table_view(0).cpu().clone(), st.tables.table_view(1).cpu().clone()],
+        states=[torch.zeros(n) for n in N], feature_table=[0, 1], query_features=[0], cand_features=[1],
+        dims=[D, D], query_layers=[(w.cpu().clone(), b.cpu().clone()) for w, b in zip(st.qW, st.qb)],
+        cand_layers=[(w.cpu().clone(), b.cpu().clone()) for w, b in zip(st.cW, st.cb)])
+
+
+@pytest.mark.parametrize("hot", [False, True], ids=["uniform", "zipf"])
+def test_multihot_step_fp32_vs_oracle(device, hot):
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    rng = np.random.default_rng(21 if hot else 20)
+    B, D, layers, N = 128, 64, [64, 32], [300, 500]
+    batches = [_kjt(rng, B, N, 9, hot) for _ in range(3)]
+    cap = max(v.size for v, _ in batches)
+    st = FusedTwoTowerStep(N, [D, D], [0], [1], layers, B, device, lr_emb=0.02, lr_dense=0.01, precision="fp32",
+                           seed=4, max_lookups=cap)
+    s0 = _state(st, N, D)
+    g = torch.Generator().manual_seed(9)
+    for v, o in batches:
+        labels = torch.randint(0, 2, (B,), generator=g).to(torch.int32)
+        st.load_kjt(torch.from_numpy(v).to(device), torch.from_numpy(o).to(device), labels.to(device))
+        st.step()
+        torch.cuda.synchronize()
+        loss, logits, pooled, _ = ref.train_step(s0, torch.from_numpy(v), torch.from_numpy(o), B, labels, 0.02, 0.01)
+        np.testing.assert_allclose(st.pooled.cpu().numpy(), pooled.numpy(), rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(st.logits.cpu().numpy(), logits.numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(float(st.loss), float(loss), rtol=1e-4)
+    for t in range(2):
+        np.testing.assert_allclose(st.tables.table_view(t).cpu().numpy(), s0.tables[t].numpy(), rtol=0, atol=1e-5)
+        np.testing.assert_allclose(st.tables.state_view(t).cpu().numpy(), s0.states[t].numpy(), rtol=1e-4, atol=1e-9)
+
+
+def test_multihot_step_bf16_graph(device):
+    """bf16 fused towers, one HIP graph per resident batch (capture_pool_kjt), first step vs the
+    oracle; a replay of the same graph sequence from the same state is bitwise reproducible."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    rng = np.random.default_rng(22)
+    B, D, layers, N = 256, 128, [128, 64], [2000, 3000]
+    host = [_kjt(rng, B, N, 9) for _ in range(2)]
+    g = torch.Generator().manual_seed(2)
+    labels = [torch.randint(0, 2, (B,), generator=g).to(torch.int32) for _ in host]
+    batches = [(torch.from_numpy(v).to(device), torch.from_numpy(o).to(device), lab.to(device))
+               for (v, o), lab in zip(host, labels)]
+    cap = max(v.size for v, _ in host)
+
+    def run():
+        st = FusedTwoTowerStep(N, [D, D], [0], [1], layers, B, device, lr_emb=0.02, lr_dense=0.01, seed=5,
+                               max_lookups=cap)
+        assert st.towers is not None  # the fused bf16 tower kernels
+        s0 = _state(st, N, D)
+        st.capture_pool_kjt(batches)
+        st.pool_graphs[0].replay()
+        torch.cuda.synchronize()
+        first = (st.pooled.cpu().clone(), float(st.loss))
+        st.pool_graphs[1].replay()
+        torch.cuda.synchronize()
+        return st, s0, first
+
+    st, s0, (pooled, loss) = run()
+    v, o = host[0]
+    want_loss, _, want_pooled, _ = ref.train_step(s0, torch.from_numpy(v), torch.from_numpy(o), B, labels[0], 0.02,
+                                                  0.01)
+    np.testing.assert_allclose(pooled.numpy(), want_pooled.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(loss, float(want_loss), rtol=2e-2)
+    st2, _, _ = run()
+    assert torch.equal(st.tables.weights, st2.tables.weights) and torch.equal(st.params, st2.params)

@@ -214,4 +214,5 @@ def test_sharded_rccl_world1_graph_equals_eager(device):
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, os.path.join(here, "rccl_graph_check.py")], capture_output=True, text=True,
                        timeout=300, cwd=os.path.dirname(here))
-    assert r.returncode == 0 and "RCCL-GRAPH-OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    assert r.returncode == 0 and "RCCL-GRAPH-OK" in r.stdout, (r.returncode, r.stdout[-1500:], r.stderr[:3000],
+                                                               r.stderr[-1500:])

@@ -718,104 +718,73 @@ struct BagRow {
 };
 
 // ---- k2d narrow: half-wave per unique row, D <= 128, D % 4 == 0 ----------------------------
-// Each half-wave takes NARROW_ROWS unique rows per pass and issues their loads together (record ->
-// {weight row, state, segment} -> gradient rows), so a wave keeps 8 independent row chains in
-// flight. Segments of <= 32 lookups are summed in ascending bag order (bitonic over the half-wave;
-// skipped when every segment of that row slot has one lookup): bitwise reproducible.
-constexpr int NARROW_ROWS = 4;
-
+// 32 lanes x float4 = one 512-B row; two rows per wave, many waves (the update is bound by the
+// number of independent row chains in flight: measured, a deeper per-wave pipeline with fewer
+// waves was slower). A row looked up once has its bag in its record (no perm hop); segments of
+// 2..32 lookups are summed in ascending bag order (bitonic over the half-wave): bitwise reproducible.
 __global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, const float* __restrict__ grad_out,
                                                                  int64_t ldg, const int32_t* __restrict__ offsets,
                                                                  int pooling, float* __restrict__ weights,
                                                                  float* __restrict__ state, float lr, float eps,
                                                                  BwdWs ws) {
-  constexpr int R = NARROW_ROWS;
   const int U = ws.U[0];
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31, half = lane >> 5;
   const BagRow br{grad_out, m.B, ldg, m.features};
-  const int64_t wstep = (int64_t)gridDim.x * 4 * 64;
-  for (int64_t wbase = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; wbase < U; wbase += wstep) {
-  // the wave's 64 records in one coalesced read, handed out by lane shuffles
-  const URec myrec = wbase + lane < U ? ws.urec[wbase + lane] : URec{0, 0, 0};
-  for (int64_t base = wbase; base < min((int64_t)U, wbase + 64); base += 2 * R) {
-    URec rec[R];
-    bool act[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int src = (int)(base - wbase) + half * R + r;
-      const int64_t u = base + half * R + r;
-      rec[r].key = __shfl(myrec.key, src, 64);
-      rec[r].seg = __shfl(myrec.seg, src, 64);
-      rec[r].len = __shfl(myrec.len, src, 64);
-      act[r] = u < U && rec[r].len < HOT_MIN;  // hot rows: bwd_hot_partial_kernel
-      if (!act[r]) rec[r] = URec{0, 0, 0};
-    }
-    f32x4v wv[R];
-    float s_old[R];
-    int mine[R], n[R], D[R];
-    bool col_ok[R];
-    float* wrow[R];
-    float* srow[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {  // independent of the gradient: rows, state and segments first
-      const int t = (int)(rec[r].key >> KEY_TABLE_SHIFT);
-      const int64_t row = (int64_t)(rec[r].key & ((1ull << KEY_TABLE_SHIFT) - 1));
-      const tt_table_meta_t tm = m.tables[act[r] ? t : 0];
-      D[r] = tm.dim;
-      col_ok[r] = act[r] && hl * 4 < D[r];
-      wrow[r] = weights + tm.weight_offset + row * D[r];
-      srow[r] = state + tm.state_offset + row;
-      wv[r] = col_ok[r] ? *reinterpret_cast<const f32x4v*>(wrow[r] + hl * 4) : (f32x4v)(0.f);
-      s_old[r] = act[r] ? *srow[r] : 0.f;
-      n[r] = rec[r].len;
-      mine[r] = (act[r] && hl < n[r]) ? (n[r] == 1 ? rec[r].seg : ws.perm[rec[r].seg + hl]) : 0x7fffffff;
-    }
-    int nall = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int nm = max(n[r], __shfl_xor(n[r], 32, 64));
-      if (nm > 1) mine[r] = bitonic_sort<32>(mine[r]);
-      nall = max(nall, nm);
-    }
-    f32x4v g[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) g[r] = (f32x4v)(0.f);
-    for (int i = 0; i < nall; ++i) {
-      f32x4v x[R];
-      int b[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        b[r] = __shfl(mine[r], (lane & 32) + i, 64);
-        x[r] = (col_ok[r] && i < n[r]) ? *reinterpret_cast<const f32x4v*>(br.row(b[r]) + hl * 4) : (f32x4v)(0.f);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (i < n[r]) {
-          if (pooling == TT_POOL_MEAN) x[r] *= 1.f / (float)max(1, offsets[b[r] + 1] - offsets[b[r]]);
-          g[r] += x[r];
+  const int64_t nhalf = (int64_t)gridDim.x * 8;
+  for (int64_t u = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half; u - half < U; u += nhalf) {
+    URec rec{0, 0, 0};
+    if (u < U) rec = ws.urec[u];
+    const bool active = u < U && rec.len < HOT_MIN;  // hot rows: bwd_hot_partial_kernel
+    if (!active) rec = URec{0, 0, 0};
+    const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
+    const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
+    const tt_table_meta_t tm = m.tables[active ? t : 0];
+    const int D = tm.dim;
+    const bool col_ok = active && hl * 4 < D;
+    float* wrow = weights + tm.weight_offset + r * D;
+    float* srow = state + tm.state_offset + r;
+    const int n = rec.len;
+    // once-looked-up row: its gradient row is known now, fetched with the weight row and state
+    const int b1 = n == 1 ? rec.seg : 0;
+    f32x4v g = (col_ok && n == 1) ? *reinterpret_cast<const f32x4v*>(br.row(b1) + hl * 4) : (f32x4v)(0.f);
+    f32x4v wv = col_ok ? *reinterpret_cast<const f32x4v*>(wrow + hl * 4) : (f32x4v)(0.f);
+    const float s_old = active ? *srow : 0.f;
+    if (pooling == TT_POOL_MEAN && n == 1) g *= 1.f / (float)max(1, offsets[b1 + 1] - offsets[b1]);
+    const int nmax = max(n, __shfl_xor(n, 32, 64));
+    if (nmax > 1) {  // ascending bag order (bitonic over the half-wave), fp32: bitwise reproducible
+      const bool many = n > 1;
+      int mine = (many && hl < n) ? ws.perm[rec.seg + hl] : 0x7fffffff;
+      mine = bitonic_sort<32>(mine);
+      for (int i = 0; i < nmax; i += 2) {
+        const int b0 = __shfl(mine, (lane & 32) + i, 64);
+        const int bb = __shfl(mine, (lane & 32) + min(i + 1, 31), 64);
+        const bool v0 = many && i < n, v1 = many && i + 1 < n;
+        f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
+        if (col_ok && v0) x0 = *reinterpret_cast<const f32x4v*>(br.row(b0) + hl * 4);
+        if (col_ok && v1) x1 = *reinterpret_cast<const f32x4v*>(br.row(bb) + hl * 4);
+        if (pooling == TT_POOL_MEAN) {
+          if (v0) x0 *= 1.f / (float)max(1, offsets[b0 + 1] - offsets[b0]);
+          if (v1) x1 *= 1.f / (float)max(1, offsets[bb + 1] - offsets[bb]);
         }
+        if (v0) g += x0;
+        if (v1) g += x1;
       }
     }
     // row-wise Adagrad: s += mean(G^2); w += (-lr * G) / (sqrt(s) + eps)
+    float sq = g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float sq = g[r][0] * g[r][0] + g[r][1] * g[r][1] + g[r][2] * g[r][2] + g[r][3] * g[r][3];
+    for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (active) {
+      const float snew = s_old + sq / (float)D;
+      const float stdv = sqrtf(snew) + eps;
+      if (col_ok) {
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
-      if (act[r]) {
-        const float snew = s_old[r] + sq / (float)D[r];
-        const float stdv = sqrtf(snew) + eps;
-        if (col_ok[r]) {
-          f32x4v w = wv[r];
-#pragma unroll
-          for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[r][v]) / stdv;
-          *reinterpret_cast<f32x4v*>(wrow[r] + hl * 4) = w;
-        }
-        if (hl == 0) *srow[r] = snew;
+        for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
+        *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
       }
+      if (hl == 0) *srow = snew;
     }
-  }
   }
 }
 
@@ -1362,7 +1331,7 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
   bwd_layout(workspace, max_lookups, &w);
   hipStream_t st = as_stream(stream);
   if (narrow) {
-    const int grid = (int)std::min<int64_t>(4096, std::max<int64_t>(1, ceil_div(max_lookups, 4 * 64)));
+    const int grid = (int)std::min<int64_t>(65536, std::max<int64_t>(1, ceil_div(max_lookups, 8)));
     bwd_adagrad_narrow_kernel<<<dim3(grid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
                                                                 lr, eps, w);
   } else {

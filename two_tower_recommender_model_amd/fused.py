@@ -31,7 +31,8 @@ class FusedTwoTowerStep:
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
                  overlap_prepare: bool = True, precision: str = "bf16", fused_towers: bool = True,
                  kjt_mode: str = "cols", overlap_towers: bool = True, fuse_gather: bool = True,
-                 materialize_pooled: bool = False, dedup: str = "single", combined_bwd: bool = True):
+                 materialize_pooled: bool = False, dedup: str = "single", combined_bwd: bool = True,
+                 max_lookups: Optional[int] = None):
         """One table per feature (feature f -> table f), features ordered as the KJT keys.
         precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode).
         overlap_prepare / overlap_towers: run the dedup prepare / the towers' weight-gradient and
@@ -45,11 +46,18 @@ class FusedTwoTowerStep:
         combined_bwd: with the fused gather and the single-hot dedup, run the whole step on ONE
         stream as three launches — T1 (gather + towers + dedup insert), T2 + row-wise Adagrad in
         one launch, T3 (Adam) — instead of side streams (cross-stream joins inside a HIP graph
-        cost several microseconds each)."""
+        cost several microseconds each).
+        max_lookups: multi-hot KJT input (config 5 bags): the step takes a KeyedJaggedTensor's
+        values / offsets through ``load_kjt`` (ids already in range, as TorchRec's EBC takes them) with
+        up to ``max_lookups`` ids per step, and runs the KJT-form kernels (tt_pooled_fwd, tiled
+        tt_bwd_prepare, tt_bwd_rowwise_adagrad) around the fused towers."""
         self.device = torch.device(device)
         self.precision = precision
         if kjt_mode not in ("cols", "kjt"):
             raise _lib.TTError("kjt_mode must be 'cols' or 'kjt'")
+        self.kjt_input = max_lookups is not None
+        if self.kjt_input:
+            kjt_mode = "kjt"
         self.kjt_mode = kjt_mode
         self.offsets_used = None
         self.F = len(num_embeddings)
@@ -119,9 +127,10 @@ class FusedTwoTowerStep:
         B, F = self.B, self.F
         self.cols = [torch.zeros(B, dtype=id_dtype, device=dev) for _ in range(F)]
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.values = torch.empty(F * B, dtype=id_dtype, device=dev)
-        self.lengths = torch.empty(F * B, dtype=torch.int32, device=dev)
-        self.offsets = torch.empty(F * B + 1, dtype=torch.int32, device=dev)
+        self.max_lookups = int(max_lookups) if self.kjt_input else F * B
+        self.values = torch.zeros(max(1, self.max_lookups), dtype=id_dtype, device=dev)
+        self.lengths = torch.zeros(F * B, dtype=torch.int32, device=dev)
+        self.offsets = torch.zeros(F * B + 1, dtype=torch.int32, device=dev)
         self.lpk = torch.empty(F, dtype=torch.int64, device=dev)
         self.pooled = torch.empty(B, self.out_dim, dtype=torch.float32, device=dev)
         self.gpooled = torch.empty(B, self.out_dim, dtype=torch.float32, device=dev)
@@ -132,7 +141,7 @@ class FusedTwoTowerStep:
         self.logits = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
         self.dot_bce = ops.DotBCE(dev, B)
-        self.tables.ensure_bwd_workspace(F * B)
+        self.tables.ensure_bwd_workspace(self.max_lookups)
         self.side = torch.cuda.Stream(device=dev) if overlap_prepare else None
         # bf16 towers on the three fused kernels when the shape allows (else per-layer GEMMs)
         self.towers = None
@@ -177,6 +186,39 @@ class FusedTwoTowerStep:
             dst.copy_(src, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
 
+    def load_kjt(self, values: torch.Tensor, offsets: torch.Tensor, labels: torch.Tensor) -> None:
+        """Multi-hot input (``max_lookups`` set): a KJT's values (keys in step order, key-major bags)
+        and its complete offsets [F*B + 1] (int32), plus labels. Copied into the step's static
+        buffers (graph-capturable)."""
+        if not self.kjt_input:
+            raise _lib.TTError("load_kjt: construct the step with max_lookups")
+        n = values.numel()
+        if n > self.max_lookups or offsets.numel() != self.F * self.B + 1:
+            raise _lib.TTError("load_kjt: more ids than max_lookups, or offsets not [F*B + 1]")
+        self.values[:n].copy_(values, non_blocking=True)
+        self.offsets.copy_(offsets.to(torch.int32), non_blocking=True)
+        self.labels.copy_(labels, non_blocking=True)
+
+    def capture_pool_kjt(self, batches: Sequence, keep_graph: bool = False) -> None:
+        """One graph per resident multi-hot batch (values, offsets int32, labels), read in place."""
+        staged = []
+        for values, offsets, labels in batches:
+            if values.dtype != self.id_dtype or offsets.dtype != torch.int32 or values.numel() > self.max_lookups \
+                    or offsets.numel() != self.F * self.B + 1:
+                raise _lib.TTError("capture_pool_kjt: batch does not match the step's dtype / capacity")
+            staged.append((values.contiguous(), offsets.contiguous(), labels.to(torch.int32).contiguous()))
+        self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]
+        keep = self.values, self.offsets, self.labels
+        self.pool_graphs = []
+        try:
+            for v, o, lab in staged:
+                self.values, self.offsets, self.labels = v, o, lab
+                self.capture(None, keep_graph=keep_graph)
+                self.pool_graphs.append(self.graph)
+        finally:
+            self.values, self.offsets, self.labels = keep
+        self.steps_per_graph = 1
+
     def _towers_fwd(self):
         L = len(self.layer_sizes)
         pr = self.precision
@@ -215,10 +257,13 @@ class FusedTwoTowerStep:
         B, F = self.B, self.F
         main = torch.cuda.current_stream(self.device)
         if self.kjt_mode == "kjt":
-            # materialise the KJT (values / lengths / offsets), then the KJT-form kernels
-            ops.kjt_build_mod_dropzero(self.cols, self.num_embeddings, self.values, self.lengths, self.offsets,
-                                       self.lpk)
-            prepare = lambda: self.tables.bwd_prepare(self.values, self.offsets, B, max_lookups=F * B)  # noqa: E731
+            # materialise the KJT (values / lengths / offsets) from the single-hot columns, or take
+            # the multi-hot KJT as loaded; then the KJT-form kernels
+            if not self.kjt_input:
+                ops.kjt_build_mod_dropzero(self.cols, self.num_embeddings, self.values, self.lengths, self.offsets,
+                                           self.lpk)
+            prepare = lambda: self.tables.bwd_prepare(self.values, self.offsets, B,  # noqa: E731
+                                                      max_lookups=self.max_lookups)
             self.offsets_used = self.offsets
         elif self.dedup_single:
             # single-hot columns, two-launch dedup: the insert runs inside T1 (gather) or here
@@ -232,9 +277,13 @@ class FusedTwoTowerStep:
             if self.side is not None:
                 self.side.wait_stream(main)
                 with torch.cuda.stream(self.side):
+                    self._mark("prep", 0)
                     prepare()
+                    self._mark("prep", 1)
             else:
+                self._mark("prep", 0)
                 prepare()
+                self._mark("prep", 1)
         if self.gather:
             # EBC forward (and, with the single-hot dedup, its insert) fused into T1
             self._mark("t1", 0)
@@ -244,7 +293,9 @@ class FusedTwoTowerStep:
                                        pooled_out=self.pooled if self.materialize_pooled else None,
                                        dedup=self.tables if self.dedup_single else None, dedup_tables=(0, 1))
         elif self.kjt_mode == "kjt":
+            self._mark("fwd", 0)
             self.tables.pooled_fwd(self.values, self.offsets, B, out=self.pooled)
+            self._mark("fwd", 1)
         else:
             self.tables.pooled_fwd_cols(self.cols, self.num_embeddings, out=self.pooled)
         if self.towers is not None and self.gather and self.dedup_single and self.combined_bwd:
@@ -261,17 +312,23 @@ class FusedTwoTowerStep:
         if self.towers is not None:
             # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update
             if not self.gather:
+                self._mark("t1", 0)
                 self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
+                self._mark("t1", 1)
             s2 = self.side2 if self.side2 is not None else main
             if self.side2 is not None:
                 self.side2.wait_stream(main)
             with torch.cuda.stream(s2):
+                self._mark("t2t3", 0)
                 self.towers.wgrad(self.loss)
                 self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
                                    grads_out=self.grads)
+                self._mark("t2t3", 1)
             if self.side is not None and prepare is not None:
                 main.wait_stream(self.side)
+            self._mark("upd", 0)
             self._emb_update()
+            self._mark("upd", 1)
             if self.side2 is not None:
                 main.wait_stream(self.side2)
             return
