@@ -219,9 +219,9 @@ constexpr int HOT_DMAX = 1024;  // partial row stride (floats)
 // TILE_BAGS bags and walks their lookups in chunks of TILE_CH; a chunk's duplicate ids are merged in
 // an LDS hash first, so the global hash and the segment cursors see one atomic per (chunk, row)
 // instead of one per lookup (a Zipf-hot row costs a few hundred same-address atomics, not 10^5).
-constexpr int TILE_BAGS = 32;
-constexpr int TILE_CH = 2048;
-constexpr int TILE_HS = 4096;  // LDS hash slots per chunk (load <= 1/2)
+constexpr int TILE_BAGS = 16;
+constexpr int TILE_CH = 1024;
+constexpr int TILE_HS = 2048;  // LDS hash slots per chunk (load <= 1/2)
 
 struct URec {
   uint64_t key;
@@ -592,6 +592,7 @@ __global__ void __launch_bounds__(256) bwd_scan_reduce_kernel(BwdWs ws) {
 // the slot's key and count are reset here, so the table is clean for the next step's k2a.
 __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
   __shared__ int lds[8];
+  __shared__ uint64_t tile[SCAN_TILE + SCAN_TILE / 16];  // the block's slot words (padded: no bank conflicts)
   int pu = 0, pc = 0;
   for (int i = threadIdx.x; i < (int)blockIdx.x; i += 256) {
     pu += ws.bsum_u[i];
@@ -609,12 +610,20 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
   pc = lds[4] + lds[5] + lds[6] + lds[7];
   __syncthreads();
   constexpr int SPT = SCAN_TILE / 256;
-  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SPT;
+  const int64_t tbase = (int64_t)blockIdx.x * SCAN_TILE;
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int idx = j * 256 + threadIdx.x;
+    tile[idx + idx / 16] = ws.keys[tbase + idx];
+    ws.keys[tbase + j * 256 + threadIdx.x] = EMPTY_KEY;  // clean for the next step's k2a
+  }
+  __syncthreads();
+  const int64_t base = tbase + threadIdx.x * SPT;
   int c[SPT], lu = 0, lcnt = 0;
   uint64_t wd[SPT];
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
-    wd[j] = ws.keys[base + j];
+    wd[j] = tile[threadIdx.x * (SPT + 1) + j];
     c[j] = slot_count(wd[j]);
     lu += c[j] > 0;
     lcnt += c[j];
@@ -660,7 +669,6 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
       }
       ws.cur[h] = c[j] == 1 ? eu : ec;  // a single lookup's bag goes into its record (k2c)
       ws.cnt[h] = c[j];
-      ws.keys[h] = EMPTY_KEY;
       eu += 1;
       ec += c[j];
     }
