@@ -179,14 +179,13 @@ def pmc_traffic(kernel_name: str):
     """HBM bytes per launch of `kernel_name` from the newest committed PMC summary (profiles/*pmc*.json,
     FETCH_SIZE/WRITE_SIZE passes of scripts/pmc_traffic.sh, gfx950-corrected), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    for k, v in d.get("kernels", {}).items():
-        if kernel_name in k:
-            return v.get("hbm_bytes"), os.path.relpath(files[-1], ROOT)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=os.path.getmtime)
+    for fn in reversed(files):  # newest summary that holds the kernel
+        with open(fn) as f:
+            d = json.load(f)
+        for k, v in d.get("kernels", {}).items():
+            if kernel_name in k:
+                return v.get("hbm_bytes"), os.path.relpath(fn, ROOT)
     return None, None
 
 

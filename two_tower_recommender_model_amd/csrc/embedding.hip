@@ -249,9 +249,12 @@ struct BwdWs {
   int32_t* ent_n;   // [L]   tiled form: entries of the chunk starting at this lookup
   int32_t* bsum_u;  // [nb]  scan partials (unique count)
   int32_t* bsum_c;  // [nb]  scan partials (lookup count)
+  int32_t* bsum_m;  // [nb]  scan partials (rows looked up more than once)
   HotRec* hot;      // [L/HOT_MIN + 1] hot rows
   float* hotp;      // [hot items][HOT_DMAX] partial sums of split hot rows
-  int32_t* U;       // [4]   {unique rows, -, hot work items, hot rows} (U[2..3]: one 64-bit word)
+  int32_t* U;       // [8]   {unique rows, KJT-form flag, hot work items, hot rows (U[2..3]: one 64-bit word),
+                    //        rows looked up more than once (their records come first), -, -, -}
+  int64_t* vmeta;   // [2]   KJT form: the step's values pointer and id dtype (for the direct update)
   int64_t cap;
   int64_t L;
 };
@@ -296,9 +299,11 @@ static size_t bwd_layout(void* base, int64_t L, BwdWs* w) {
   t.ent_n = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * L));
   t.bsum_u = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
   t.bsum_c = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
+  t.bsum_m = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * nb));
   t.hot = reinterpret_cast<HotRec*>(take(sizeof(HotRec) * (L / HOT_MIN + 1)));
   t.hotp = reinterpret_cast<float*>(take(sizeof(float) * HOT_DMAX * hot_items_max(L)));
-  t.U = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
+  t.U = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 8));
+  t.vmeta = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * 2));
   t.cap = cap;
   t.L = L;
   if (w) *w = t;
@@ -385,6 +390,10 @@ __global__ void __launch_bounds__(256) bwd_tile_hash_kernel(EmbMeta m, const voi
   __syncthreads();
   const int64_t s0 = off[0], e0 = off[nb];
   const uint64_t gmask = (uint64_t)ws.cap - 1;
+  if (blockIdx.x == 0 && tid == 0) {
+    ws.vmeta[0] = reinterpret_cast<int64_t>(values);
+    ws.vmeta[1] = id_dtype;
+  }
   for (int64_t j0 = s0; j0 < e0; j0 += TILE_CH) {
     const int n = (int)min((int64_t)TILE_CH, e0 - j0);
     int pos[TILE_EPT], rk[TILE_EPT];
@@ -495,6 +504,8 @@ __global__ void __launch_bounds__(256) bwd_tile_hash_kernel(EmbMeta m, const voi
   }
 }
 
+constexpr int SINGLE_MARK = (int)0x80000000;  // lk sign bit: the lookup's row is looked up once
+
 // k2c (KJT form): per chunk, one cursor atomic per entry reserves its run in the row's segment,
 // then every lookup writes its bag id at (run base + rank).
 __global__ void __launch_bounds__(256) bwd_tile_scatter_kernel(EmbMeta m, const int32_t* __restrict__ offsets,
@@ -522,11 +533,12 @@ __global__ void __launch_bounds__(256) bwd_tile_scatter_kernel(EmbMeta m, const 
 #pragma unroll
     for (int q = 0; q < TILE_EPT; ++q) ln[q] = hb[q] >= 0 ? ws.cnt[hb[q]] : 0;
     // a row whose lookups all sit in this chunk owns its whole segment: no cursor atomic; a row
-    // looked up once keeps its bag in its record (cur = its unique index, stored as ~u here)
+    // looked up once gets no segment at all: its lookup is marked (lk sign bit) and updated in
+    // lookup order by bwd_adagrad_direct_kernel
 #pragma unroll
     for (int q = 0; q < TILE_EPT; ++q)
       if (hb[q] >= 0)
-        lbase[q * 256 + tid] = ln[q] == cb[q] ? (ln[q] == 1 ? ~ws.cur[hb[q]] : ws.cur[hb[q]])
+        lbase[q * 256 + tid] = ln[q] == cb[q] ? (ln[q] == 1 ? SINGLE_MARK : ws.cur[hb[q]])
                                               : atomicAdd(&ws.cur[hb[q]], cb[q]);
     __syncthreads();
 #pragma unroll
@@ -535,9 +547,8 @@ __global__ void __launch_bounds__(256) bwd_tile_scatter_kernel(EmbMeta m, const 
       if (i < n) {
         const int v = ws.lk[j0 + i];
         const int lb = lbase[v & 0xffff];
-        const int32_t bag = (int32_t)(b0 + lds_bag_of(off, nb, j0 + i));
-        if (lb < 0) ws.urec[~lb].seg = bag;
-        else ws.perm[lb + (v >> 16)] = bag;
+        if (lb == SINGLE_MARK) ws.lk[j0 + i] = v | SINGLE_MARK;
+        else ws.perm[lb + (v >> 16)] = (int32_t)(b0 + lds_bag_of(off, nb, j0 + i));
       }
     }
     __syncthreads();
@@ -564,50 +575,73 @@ __global__ void __launch_bounds__(256) bwd_hash_cols_kernel(EmbMeta m, ColArgs c
 __device__ __forceinline__ int slot_count(uint64_t w) { return w == EMPTY_KEY ? 0 : (int)(w & PK_CNT_MASK); }
 
 // k2b-1: per SCAN_TILE-slot tile: number of occupied slots and of lookups
-__global__ void __launch_bounds__(256) bwd_scan_reduce_kernel(BwdWs ws) {
-  __shared__ int lu[4], lc[4];
+__global__ void __launch_bounds__(256) bwd_scan_reduce_kernel(BwdWs ws, int tiled) {
+  __shared__ int lu[4], lc[4], lm[4];
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
-  int su = 0, sc = 0;
+  int su = 0, sc = 0, sm = 0;
 #pragma unroll
   for (int j = 0; j < SCAN_TILE / 256; ++j) {
     const int c = slot_count(ws.keys[base + j * 256 + threadIdx.x]);
     su += c > 0;
     sc += c;
+    sm += c > 1;
   }
   su = wave_sum_i(su);
   sc = wave_sum_i(sc);
+  sm = wave_sum_i(sm);
   if ((threadIdx.x & 63) == 0) {
     lu[threadIdx.x >> 6] = su;
     lc[threadIdx.x >> 6] = sc;
+    lm[threadIdx.x >> 6] = sm;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     ws.bsum_u[blockIdx.x] = lu[0] + lu[1] + lu[2] + lu[3];
     ws.bsum_c[blockIdx.x] = lc[0] + lc[1] + lc[2] + lc[3];
-    if (blockIdx.x == 0) *reinterpret_cast<unsigned long long*>(ws.U + 2) = 0ull;  // hot list, filled by k2b-2
+    ws.bsum_m[blockIdx.x] = lm[0] + lm[1] + lm[2] + lm[3];
+    if (blockIdx.x == 0) {
+      *reinterpret_cast<unsigned long long*>(ws.U + 2) = 0ull;  // hot list, filled by k2b-2
+      ws.U[1] = tiled;  // 1: KJT-form grouping (once-looked-up lookups marked in lk, see k2c)
+    }
   }
 }
 
 // k2b-2: exclusive scans -> record {key, segment start, count} per unique row; cursor per slot;
 // the slot's key and count are reset here, so the table is clean for the next step's k2a.
 __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
-  __shared__ int lds[8];
+  __shared__ int lds[20];
   __shared__ uint64_t tile[SCAN_TILE + SCAN_TILE / 16];  // the block's slot words (padded: no bank conflicts)
-  int pu = 0, pc = 0;
-  for (int i = threadIdx.x; i < (int)blockIdx.x; i += 256) {
-    pu += ws.bsum_u[i];
-    pc += ws.bsum_c[i];
+  // prefixes over the previous blocks (unique rows, lookups, multi rows) and the totals (U, M)
+  int pu = 0, pc = 0, pm = 0, tU = 0, tM = 0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
+    const int bu = ws.bsum_u[i], bm = ws.bsum_m[i];
+    if (i < (int)blockIdx.x) {
+      pu += bu;
+      pc += ws.bsum_c[i];
+      pm += bm;
+    }
+    tU += bu;
+    tM += bm;
   }
   pu = wave_sum_i(pu);
   pc = wave_sum_i(pc);
+  pm = wave_sum_i(pm);
+  tU = wave_sum_i(tU);
+  tM = wave_sum_i(tM);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (lane == 0) {
     lds[wid] = pu;
     lds[4 + wid] = pc;
+    lds[8 + wid] = pm;
+    lds[12 + wid] = tU;
+    lds[16 + wid] = tM;
   }
   __syncthreads();
   pu = lds[0] + lds[1] + lds[2] + lds[3];
   pc = lds[4] + lds[5] + lds[6] + lds[7];
+  pm = lds[8] + lds[9] + lds[10] + lds[11];
+  tU = lds[12] + lds[13] + lds[14] + lds[15];
+  tM = lds[16] + lds[17] + lds[18] + lds[19];
   __syncthreads();
   constexpr int SPT = SCAN_TILE / 256;
   const int64_t tbase = (int64_t)blockIdx.x * SCAN_TILE;
@@ -628,34 +662,45 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
     lu += c[j] > 0;
     lcnt += c[j];
   }
-  int iu = lu, ic = lcnt;
+  int lmul = 0;
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) lmul += c[j] > 1;
+  int iu = lu, ic = lcnt, im = lmul;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    int yu = __shfl_up(iu, o, 64), yc = __shfl_up(ic, o, 64);
+    int yu = __shfl_up(iu, o, 64), yc = __shfl_up(ic, o, 64), ym = __shfl_up(im, o, 64);
     if (lane >= o) {
       iu += yu;
       ic += yc;
+      im += ym;
     }
   }
   if (lane == 63) {
     lds[wid] = iu;
     lds[4 + wid] = ic;
+    lds[8 + wid] = im;
   }
   __syncthreads();
-  int wu = 0, wc = 0, tu = 0;
+  int wu = 0, wc = 0, wm = 0;
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
     if (w < wid) {
       wu += lds[w];
       wc += lds[4 + w];
+      wm += lds[8 + w];
     }
-    tu += lds[w];
   }
-  int eu = pu + wu + iu - lu, ec = pc + wc + ic - lcnt;
+  // records: rows looked up more than once first (in slot order), then the once-looked-up rows
+  // from the end of the record array (in reverse slot order), so the per-row kernels of the KJT
+  // form visit only the first M records
+  int em = pm + wm + im - lmul;                                   // multi rows before this thread's
+  int es = (pu - pm) + (wu - wm) + (iu - lu) - (im - lmul);      // single rows before this thread's
+  int ec = pc + wc + ic - lcnt;
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     if (c[j] > 0) {
       const int64_t h = base + j;
+      const int eu = c[j] > 1 ? em++ : tU - 1 - es++;
       URec rec;
       rec.key = pk_to_key(wd[j]);
       rec.seg = ec;
@@ -669,11 +714,13 @@ __global__ void __launch_bounds__(256) bwd_scan_kernel(BwdWs ws) {
       }
       ws.cur[h] = c[j] == 1 ? eu : ec;  // a single lookup's bag goes into its record (k2c)
       ws.cnt[h] = c[j];
-      eu += 1;
       ec += c[j];
     }
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) ws.U[0] = pu + tu;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    ws.U[0] = tU;
+    ws.U[4] = tM;
+  }
 }
 
 // k2c: thread per bag: scatter bag ids into their unique row's segment
@@ -713,13 +760,26 @@ __device__ __forceinline__ int bitonic_sort(int v) {
   return v;
 }
 
+// Table / feature metadata staged in LDS at block start: indexing the kernel-argument copy with a
+// per-lane index is a vector load from the kernarg segment (one more dependent hop per row).
+struct LdsMeta {
+  tt_table_meta_t tab[TT_MAX_TABLES];
+  tt_feature_meta_t feat[TT_MAX_FEATURES];
+};
+
+__device__ __forceinline__ void stage_meta(const EmbMeta& m, LdsMeta& lm) {
+  for (int i = threadIdx.x; i < m.T; i += blockDim.x) lm.tab[i] = m.tables[i];
+  for (int i = threadIdx.x; i < m.F; i += blockDim.x) lm.feat[i] = m.features[i];
+  __syncthreads();
+}
+
 struct BagRow {
   const float* g;
   int64_t B;
   int64_t ldg;
   const tt_feature_meta_t* feats;
   __device__ __forceinline__ const float* row(int bag) const {
-    const int f = (int)(bag / B);
+    const int f = (int)((uint32_t)bag / (uint32_t)B);  // bag ids < F * B < 2^31: 32-bit division
     const int64_t b = bag - (int64_t)f * B;
     return g + (feats[f].out_row + b) * ldg + feats[f].out_offset;
   }
@@ -735,19 +795,23 @@ __global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, cons
                                                                  int pooling, float* __restrict__ weights,
                                                                  float* __restrict__ state, float lr, float eps,
                                                                  BwdWs ws) {
-  const int U = ws.U[0];
+  __shared__ LdsMeta lm;
+  stage_meta(m, lm);
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31, half = lane >> 5;
-  const BagRow br{grad_out, m.B, ldg, m.features};
+  const BagRow br{grad_out, m.B, ldg, lm.feat};
+  const bool direct = ws.U[1] != 0;
+  const int U = direct ? ws.U[4] : ws.U[0];  // direct: the once-looked-up rows are not visited at all
   const int64_t nhalf = (int64_t)gridDim.x * 8;
   for (int64_t u = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half; u - half < U; u += nhalf) {
     URec rec{0, 0, 0};
     if (u < U) rec = ws.urec[u];
-    const bool active = u < U && rec.len < HOT_MIN;  // hot rows: bwd_hot_partial_kernel
+    // hot rows: bwd_hot_partial_kernel; once-looked-up rows of the KJT form: bwd_adagrad_direct_kernel
+    const bool active = u < U && rec.len < HOT_MIN && !(direct && rec.len == 1);
     if (!active) rec = URec{0, 0, 0};
     const int t = (int)(rec.key >> KEY_TABLE_SHIFT);
     const int64_t r = (int64_t)(rec.key & ((1ull << KEY_TABLE_SHIFT) - 1));
-    const tt_table_meta_t tm = m.tables[active ? t : 0];
+    const tt_table_meta_t tm = lm.tab[active ? t : 0];
     const int D = tm.dim;
     const bool col_ok = active && hl * 4 < D;
     float* wrow = weights + tm.weight_offset + r * D;
@@ -794,6 +858,102 @@ __global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, cons
       if (hl == 0) *srow = snew;
     }
   }
+}
+
+// ---- k2d direct (KJT form, D <= 128): once-looked-up rows in lookup order --------------------
+// Most rows of a uniform multi-hot batch are looked up once. Their lookups (marked by k2c) are
+// updated straight from the bag walk: half-wave per lookup, consecutive lookups share their bag's
+// gradient row (cache hits instead of a random gradient-row read per row), no record / segment
+// indirection. Four lookups per half-wave in flight. The row is the hash's row: ids >= rows -> 0.
+__global__ void __launch_bounds__(256) bwd_adagrad_direct_kernel(EmbMeta m, const float* __restrict__ grad_out,
+                                                                 int64_t ldg, const int32_t* __restrict__ offsets,
+                                                                 int pooling, float* __restrict__ weights,
+                                                                 float* __restrict__ state, float lr, float eps,
+                                                                 BwdWs ws) {
+  if (ws.U[1] == 0) return;
+  __shared__ int32_t off[TILE_BAGS + 1];
+  __shared__ LdsMeta lm;
+  const int tid = threadIdx.x;
+  const int64_t NB = (int64_t)m.F * m.B;
+  const int64_t b0 = (int64_t)blockIdx.x * TILE_BAGS;
+  const int nb = (int)min((int64_t)TILE_BAGS, NB - b0);
+  if (tid <= nb) off[tid] = offsets[b0 + tid];
+  stage_meta(m, lm);
+  const void* values = reinterpret_cast<const void*>(ws.vmeta[0]);
+  const int id_dtype = (int)ws.vmeta[1];
+  __syncthreads();
+  const int64_t s0 = off[0], e0 = off[nb];
+  const int hw = tid >> 5, hl = tid & 31;
+  const BagRow br{grad_out, m.B, ldg, lm.feat};
+  constexpr int UN = 4;
+  for (int64_t j0 = s0 + hw; j0 < e0; j0 += 8 * UN) {
+    bool on[UN];
+    int lb[UN];
+    int64_t id[UN];
+    f32x4v wv[UN], g[UN];
+    float s_old[UN];
+    float* wrow[UN];
+    float* srow[UN];
+    int D[UN];
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int64_t j = j0 + 8 * k;
+      on[k] = j < e0 && ws.lk[j] < 0;
+      id[k] = j < e0 ? load_id(values, id_dtype, j) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int64_t j = j0 + 8 * k;
+      lb[k] = on[k] ? lds_bag_of(off, nb, j) : 0;
+      const int64_t bag = b0 + lb[k];
+      const tt_table_meta_t tm = lm.tab[lm.feat[on[k] ? (int)((uint32_t)bag / (uint32_t)m.B) : 0].table];
+      if ((uint64_t)id[k] >= (uint64_t)tm.num_rows) id[k] = 0;
+      D[k] = tm.dim;
+      const bool col = on[k] && hl * 4 < D[k];
+      wrow[k] = weights + tm.weight_offset + id[k] * D[k];
+      srow[k] = state + tm.state_offset + id[k];
+      wv[k] = col ? *reinterpret_cast<const f32x4v*>(wrow[k] + hl * 4) : (f32x4v)(0.f);
+      s_old[k] = on[k] ? *srow[k] : 0.f;
+      g[k] = col ? *reinterpret_cast<const f32x4v*>(br.row((int)bag) + hl * 4) : (f32x4v)(0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      if (pooling == TT_POOL_MEAN && on[k]) g[k] *= 1.f / (float)max(1, off[lb[k] + 1] - off[lb[k]]);
+      float sq = g[k][0] * g[k][0] + g[k][1] * g[k][1] + g[k][2] * g[k][2] + g[k][3] * g[k][3];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+      if (on[k]) {
+        const float snew = s_old[k] + sq / (float)D[k];
+        const float stdv = sqrtf(snew) + eps;
+        if (hl * 4 < D[k]) {
+          f32x4v w = wv[k];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[k][v]) / stdv;
+          *reinterpret_cast<f32x4v*>(wrow[k] + hl * 4) = w;
+        }
+        if (hl == 0) *srow[k] = snew;
+      }
+    }
+  }
+}
+
+// generic-width tables (no direct kernel): the once-looked-up rows of the KJT form get their bag
+// written into their record (seg), as the per-row kernels expect
+__global__ void __launch_bounds__(256) bwd_single_fix_kernel(EmbMeta m, const int32_t* __restrict__ offsets, BwdWs ws) {
+  if (ws.U[1] == 0) return;
+  __shared__ int32_t off[TILE_BAGS + 1];
+  const int tid = threadIdx.x;
+  const int64_t NB = (int64_t)m.F * m.B;
+  const int64_t b0 = (int64_t)blockIdx.x * TILE_BAGS;
+  const int nb = (int)min((int64_t)TILE_BAGS, NB - b0);
+  if (tid <= nb) off[tid] = offsets[b0 + tid];
+  __syncthreads();
+  const int64_t s0 = off[0], e0 = off[nb];
+  for (int64_t j0 = s0; j0 < e0; j0 += TILE_CH)
+    for (int i = tid; i < (int)min((int64_t)TILE_CH, e0 - j0); i += 256) {
+      const int v = ws.lk[j0 + i];
+      if (v < 0) ws.urec[ws.cur[ws.ent_h[j0 + (v & 0xffff)]]].seg = (int32_t)(b0 + lds_bag_of(off, nb, j0 + i));
+    }
 }
 
 // ---- k2d generic: a wave per unique row, any D <= 1024 ------------------------------------
@@ -1234,14 +1394,14 @@ int tt_bwd_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookups,
   hipStream_t st = as_stream(stream);
   if (hipMemsetAsync(w.keys, 0xff, sizeof(uint64_t) * w.cap, st) != hipSuccess ||
       hipMemsetAsync(w.cnt, 0, sizeof(int32_t) * w.cap, st) != hipSuccess ||
-      hipMemsetAsync(w.U, 0, sizeof(int32_t) * 4, st) != hipSuccess)
+      hipMemsetAsync(w.U, 0, sizeof(int32_t) * 8, st) != hipSuccess)
     return fail(TT_EINVAL, "bwd_workspace_init: memset failed");
   return TT_OK;
 }
 
 static int launch_scan_scatter(const EmbMeta& m, const int32_t* offsets, BwdWs& w, hipStream_t st, int gb) {
   const int nb = (int)ceil_div(w.cap, SCAN_TILE);
-  bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
+  bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w, 0);
   bwd_scan_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
   if ((int64_t)m.F * m.B > 0) bwd_scatter_kernel<<<dim3(gb), dim3(256), 0, st>>>(m, offsets, w);
   return check_launch("bwd_prepare");
@@ -1270,7 +1430,7 @@ int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t
   if (nbag > 0)
     bwd_tile_hash_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, values, id_dtype, offsets, bounds_check, w);
   const int nb = (int)ceil_div(w.cap, SCAN_TILE);
-  bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
+  bwd_scan_reduce_kernel<<<dim3(nb), dim3(256), 0, st>>>(w, 1);
   bwd_scan_kernel<<<dim3(nb), dim3(256), 0, st>>>(w);
   if (nbag > 0) bwd_tile_scatter_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, offsets, w);
   return check_launch("bwd_prepare");
@@ -1338,8 +1498,16 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
   BwdWs w;
   bwd_layout(workspace, max_lookups, &w);
   hipStream_t st = as_stream(stream);
+  const int64_t tiles = ceil_div((int64_t)F * B, TILE_BAGS);
+  if (offsets && F * B > 0 && tiles <= INT32_MAX) {  // once-looked-up rows of a KJT-form prepare (device flag)
+    if (narrow)
+      bwd_adagrad_direct_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights,
+                                                                            state, lr, eps, w);
+    else
+      bwd_single_fix_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, offsets, w);
+  }
   if (narrow) {
-    const int grid = (int)std::min<int64_t>(65536, std::max<int64_t>(1, ceil_div(max_lookups, 8)));
+    const int grid = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(max_lookups, 8)));
     bwd_adagrad_narrow_kernel<<<dim3(grid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
                                                                 lr, eps, w);
   } else {
