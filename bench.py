@@ -272,8 +272,9 @@ def run_multihot(args):
                 "what": "tt_pooled_fwd: segmented gather + sum pool (8 B id + 4D row per lookup, 4D per bag)"},
         "prep": {"bytes": nnz * (8 + 4 + 4) + FB * 4, "kernel": "bwd_tile_hash + scan + bwd_tile_scatter",
                  "what": "tt_bwd_prepare: ids read, per-lookup entry word, segment scatter"},
-        "upd": {"bytes": nnz * (4 * D + 4) + uniq * (8 * D + 8), "kernel": "bwd_adagrad_narrow_kernel (+ hot-row launches)",
-                "what": "tt_bwd_rowwise_adagrad: grad rows per lookup, weight row + state read+write per unique row"},
+        "upd": {"bytes": nnz * (4 * D + 4) + uniq * (8 * D + 8), "kernel": "bwd_adagrad_direct_kernel (+ narrow and hot-row launches)",
+                "what": "tt_bwd_rowwise_adagrad: grad rows per lookup, weight row + state read+write per unique row "
+                        "(once-looked-up rows in lookup order, the others per row)"},
         "t1": {"bytes": None, "kernel": "tower_fwd_bwd_kernel", "what": "fused towers fwd/bwd + dot/BCE"},
         "t2t3": {"bytes": None, "kernel": "tower_wgrad + tower_update", "what": "tower weight grads + Adam (side stream)"},
     }

@@ -158,13 +158,20 @@ int tt_pooled_fwd_cols(const float* weights, const tt_table_meta_t* tables, int 
 
 /* ---- a8: deduplicated backward + fused exact row-wise Adagrad -------------------------------- */
 
-/* Workspace for up to max_lookups ids per step. Must be zeroed once by tt_bwd_workspace_init;
- * tt_bwd_rowwise_adagrad leaves it clean again for the next step. */
+/* Workspace for up to max_lookups ids per step (max_lookups < 2^24; table rows < 2^34 - 1). Must be
+ * initialised once by tt_bwd_workspace_init; every prepare leaves the hash clean again for the next
+ * step. */
 size_t tt_bwd_workspace_bytes(int64_t max_lookups);
 int tt_bwd_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
 
-/* Group the step's lookups by unique (table,row): hash insert, count, scan, scatter. Depends only
- * on the ids, so it may run concurrently with the forward and the towers. */
+/* Group the step's lookups by unique (table,row) (FBGEMM's linearize + radix sort + run-length
+ * encode, done as a hash): per chunk of 1024 lookups the duplicates are merged in an LDS hash, each
+ * (chunk, row) pair pays ONE global CAS (key and count share a 64-bit slot word), a scan assigns
+ * segments (rows looked up more than once first), and a chunk scatter fills them (one cursor
+ * atomic per (chunk, row), none for a row whose lookups sit in one chunk); a row looked up once
+ * gets no segment, its lookup is marked for the direct update. Depends only on the ids, so it may
+ * run concurrently with the forward and the towers. values must stay valid until the matching
+ * tt_bwd_rowwise_adagrad, which must be given the same offsets. */
 int tt_bwd_prepare(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
                    int64_t B, const void* values, int id_dtype, const int32_t* offsets,
                    int bounds_check, void* workspace, size_t ws_bytes, int64_t max_lookups,
@@ -182,8 +189,9 @@ int tt_bwd_prepare_cols(const tt_table_meta_t* tables, int T, const tt_feature_m
  *   G[r]   = sum over its lookups of grad_out[b, out_offset(f) : +D]  (x 1/len for MEAN pooling)
  *   s[r]  += mean_d G[r,d]^2
  *   W[r,d] = W[r,d] + (-lr * G[r,d]) / (sqrt(s[r]) + eps)
- * (torchrec RowWiseAdagrad, lr_decay = weight_decay = 0). deterministic: 1 = segments of <= 64
- * lookups are summed in sorted-bag order (bitwise reproducible), longer ones in fp64. */
+ * (torchrec RowWiseAdagrad, lr_decay = weight_decay = 0). Bitwise reproducible: rows of 2..32
+ * lookups are summed in ascending bag order, hotter rows over fixed bag-id ranges (ascending inside
+ * a range, ranges in order); rows looked up once (KJT form) are updated in lookup order. */
 int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
                            int F, int64_t B, const float* grad_out, int64_t ldg,
                            const int32_t* offsets, int pooling, float* weights, float* state,
