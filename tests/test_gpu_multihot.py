@@ -94,3 +94,44 @@ def test_multihot_step_bf16_graph(device):
     np.testing.assert_allclose(loss, float(want_loss), rtol=2e-2)
     st2, _, _ = run()
     assert torch.equal(st.tables.weights, st2.tables.weights) and torch.equal(st.params, st2.params)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_config3_shape_step_vs_oracle(device, precision):
+    """SURVEY 8(d) config 3 shape at test size: 8 single-hot features per tower (16 tables), towers
+    over the concatenation (in_size = 8 x D = 512), ids through the reference transform (id 0
+    dropped, id mod N). fp32 parity mode: 2 steps vs the oracle (pooled rows exact on the first step,
+    then atol 1e-5; loss rtol 1e-4, tables atol 1e-5); bf16 fused towers: the first step's pooled rows
+    exactly and its loss rtol 2e-2."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    F, B, D, layers = 16, 64, 64, [64, 32]
+    N = [200 + 37 * f for f in range(F)]
+    st = FusedTwoTowerStep(N, [D] * F, list(range(8)), list(range(8, 16)), layers, B, device, lr_emb=0.02,
+                           lr_dense=0.01, precision=precision, seed=7, materialize_pooled=True)
+    if precision == "bf16":
+        assert st.towers is not None
+    s0 = ref.TwoTowerState(
+        tables=[st.tables.table_view(f).cpu().clone() for f in range(F)], states=[torch.zeros(n) for n in N],
+        feature_table=list(range(F)), query_features=list(range(8)), cand_features=list(range(8, 16)),
+        dims=[D] * F, query_layers=[(w.cpu().clone(), b.cpu().clone()) for w, b in zip(st.qW, st.qb)],
+        cand_layers=[(w.cpu().clone(), b.cpu().clone()) for w, b in zip(st.cW, st.cb)])
+    g = torch.Generator().manual_seed(3)
+    for step in range(2 if precision == "fp32" else 1):
+        cols = [torch.randint(0, 2 * n, (B,), generator=g) for n in N]
+        for c in cols:
+            c[:3] = 0  # dropped ids: empty bags
+        labels = torch.randint(0, 2, (B,), generator=g).to(torch.int32)
+        st.load_batch([c.to(device) for c in cols], labels.to(device))
+        st.step()
+        torch.cuda.synchronize()
+        v, _, o = ref.kjt_build([c.numpy() for c in cols], N)
+        loss, logits, pooled, _ = ref.train_step(s0, torch.from_numpy(v), torch.from_numpy(o), B, labels, 0.02, 0.01)
+        if step == 0:  # a gather of identical tables: exact; later steps gather updated rows (atol 1e-5)
+            np.testing.assert_array_equal(st.pooled.cpu().numpy(), pooled.numpy())
+        else:
+            np.testing.assert_allclose(st.pooled.cpu().numpy(), pooled.numpy(), rtol=0, atol=1e-5)
+        np.testing.assert_allclose(float(st.loss), float(loss), rtol=1e-4 if precision == "fp32" else 2e-2)
+    if precision == "fp32":
+        for f in range(F):
+            np.testing.assert_allclose(st.tables.table_view(f).cpu().numpy(), s0.tables[f].numpy(), rtol=0, atol=1e-5)
