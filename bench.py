@@ -459,6 +459,7 @@ def run_multi(args, world, rank, local_rank):
     step.load_batch(*batches[0])
     step.step()  # creates the RCCL communicators before any capture
     torch.cuda.synchronize()
+    time.sleep(0.5)  # let the process group's watchdog retire the eager collectives before capture
     k = args.steps_per_graph
     mode = "hipgraph"
     ok = torch.ones(1, device=dev)
@@ -533,6 +534,9 @@ def main():
         value, ms, loss, roofline, cpu, steps_run = run_single(args)
     else:
         torch.cuda.set_device(local_rank)
+        from two_tower_recommender_model_amd.sharded import graph_safe_nccl_env
+
+        graph_safe_nccl_env()  # RCCL collectives inside HIP graphs (before the process group exists)
         if "RANK" in os.environ:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:  # --sharded without a launcher (e.g. under rocprofv3): a one-rank group

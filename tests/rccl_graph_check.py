@@ -1,6 +1,7 @@
 """Child process of tests/test_gpu_sharded.py::test_sharded_rccl_world1_graph_equals_eager."""
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -8,12 +9,14 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, ThreadComm, TorchComm  # noqa: E402
+from two_tower_recommender_model_amd.sharded import (FusedShardedTwoTowerStep, ThreadComm, TorchComm,  # noqa: E402
+                                                     graph_safe_nccl_env)
 
 
 def main():
     device = torch.device("cuda:0")
     torch.cuda.set_device(device)
+    graph_safe_nccl_env()
     dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=device)
     B, D, N = 1024, 128, [30_000, 50_000]
     g = torch.Generator().manual_seed(5)
@@ -28,6 +31,8 @@ def main():
     a.step()  # communicator init; the same first step on b
     b.load_batch(*batches[0])
     b.step()
+    torch.cuda.synchronize()
+    time.sleep(0.5)  # the watchdog retires the eager collectives before the capture
     a.capture_pool(batches, steps_per_graph=2)
     for j in range(2):
         a.pool_graphs[j].replay()

@@ -44,6 +44,19 @@ class _Done:
         return None
 
 
+def graph_safe_nccl_env() -> None:
+    """Environment for a "nccl" (RCCL) process group whose collectives are captured into HIP graphs;
+    call BEFORE dist.init_process_group. ProcessGroupNCCL's watchdog queries the end events of the
+    works it tracks; with its event cache on, an event of an eager collective can come back recorded
+    in a capturing stream, and the query then fails (hipErrorCapturedEvent), which the watchdog
+    turned into an abort of the process (seen on MI355X after a run of the graphed sharded step).
+    The cache is turned off, and such a query error is logged instead of rethrown."""
+    import os
+
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
+
+
 class TorchComm:
     """torch.distributed collectives on the current stream (backend "nccl" = RCCL over xGMI)."""
 
