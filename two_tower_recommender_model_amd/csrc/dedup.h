@@ -224,7 +224,7 @@ __device__ __forceinline__ int dd_bitonic(int v) {
   return v;
 }
 
-constexpr int DD_HOT_PT = 4;                 // lookups per thread per scan pass
+constexpr int DD_HOT_PT = 16;                // lookups per thread per scan pass (4096 a pass)
 constexpr int DD_HOT_CH = 256 * DD_HOT_PT;  // lookups scanned per pass of a hot workgroup (LDS list)
 // LDS of the hot role (list + wave totals + group partials), provided by the launching kernel so a
 // combined launch can overlay it on its other roles' LDS

@@ -135,7 +135,7 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
   a.state = state;
   a.lr = lr;
   a.eps = eps;
-  a.hot_wgs = (int)std::min<int64_t>(32, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
+  a.hot_wgs = (int)std::min<int64_t>(64, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
   a.slot_hw = ceil_div(ceil_div(max_lookups, DD_SPH), 8) * 8;
   *grid = a.hot_wgs + a.slot_hw / 8;
   return TT_OK;
