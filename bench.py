@@ -175,11 +175,19 @@ def launch_bytes(step, nnz: int, uniq: int):
             "_emb_path_bytes": emb_path}
 
 
-def pmc_traffic(kernel_name: str):
-    """HBM bytes per launch of `kernel_name` from the newest committed PMC summary (profiles/*pmc*.json,
-    FETCH_SIZE/WRITE_SIZE passes of scripts/pmc_traffic.sh, gfx950-corrected), or None."""
+def pmc_traffic(kernel_name: str, workload: str = "northstar"):
+    """HBM bytes per launch of `kernel_name` from the newest committed PMC summary of this workload
+    (profiles/*pmc*.json; a non-default workload's summaries carry its name, e.g.
+    r01_pmc_traffic_config5.json; FETCH_SIZE/WRITE_SIZE passes of scripts/pmc_traffic.sh,
+    gfx950-corrected), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=os.path.getmtime)
+    files = glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))
+    others = [w for w in WORKLOADS if w != "northstar"]
+    if workload == "northstar":
+        files = [f for f in files if not any(w in os.path.basename(f) for w in others)]
+    else:
+        files = [f for f in files if workload in os.path.basename(f)]
+    files = sorted(files, key=os.path.basename)
     for fn in reversed(files):  # newest summary that holds the kernel
         with open(fn) as f:
             d = json.load(f)
@@ -286,7 +294,7 @@ def run_multihot(args):
     emb_bytes = nnz * (16 + 4 * D) + FB * (4 + 8 * D) + uniq * (8 * D + 8)
     emb_ms = sum(timed.get(n, 0.0) for n in ("fwd", "prep", "upd"))
     dom = max(("fwd", "upd"), key=lambda n: timed.get(n, 0.0))
-    traffic, src = pmc_traffic(kern[dom]["kernel"].split()[0])
+    traffic, src = pmc_traffic(kern[dom]["kernel"].split()[0], args.workload)
     ach = kern[dom].get("GB/s")
     roofline = {"bound": "hbm", "kernel": kern[dom]["kernel"], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic, "traffic_source": src,
@@ -326,7 +334,7 @@ def cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen):
                       f"{platform.processor() or platform.machine()}"}
 
 
-def roofline_report(kern, timed, nnz, uniq, step, B):
+def roofline_report(kern, timed, nnz, uniq, step, B, workload="northstar"):
     emb_path_bytes = kern.pop("_emb_path_bytes")
     out = {}
     for name, k in kern.items():
@@ -344,7 +352,7 @@ def roofline_report(kern, timed, nnz, uniq, step, B):
         return {"bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq}
     dom = max((n for n in out if "ms" in out[n]), key=lambda n: out[n]["ms"])
-    traffic, src = pmc_traffic(KERNEL_NAMES[dom])
+    traffic, src = pmc_traffic(KERNEL_NAMES[dom], workload)
     emb_ms = timed.get("t1", 0.0) + timed.get("k3", 0.0)
     ach = out[dom]["GB/s"]
     return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -435,7 +443,7 @@ def run_single(args):
         timed = {n: v * ms / tot for n, v in raw.items()}
         timing_how += ("; each span scaled by (step time without event nodes) / (sum of the spans) = "
                        f"{ms / tot:.3f}")
-    roofline = roofline_report(kern, timed, nnz, uniq, step, B)
+    roofline = roofline_report(kern, timed, nnz, uniq, step, B, args.workload)
     roofline["timing"] = timing_how
     roofline["event_span_ms"] = {n: round(v, 5) for n, v in raw.items()}
     cpu = None
