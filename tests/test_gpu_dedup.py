@@ -80,7 +80,7 @@ def _assert_clean(ts):
     overflow entries)."""
     L = ts._dd_cap
     cap = 1024
-    while cap < 4 * L:
+    while cap < 16 * L:
         cap <<= 1
     al = lambda x: (x + 255) // 256 * 256  # noqa: E731
     sl = ts._dd_ws[:cap * 64].view(torch.int64).view(cap, 8).cpu()

@@ -33,7 +33,7 @@ struct ColArgsD {
 // so the table's size costs only memory (64 B a slot)
 static int64_t dedup_cap(int64_t L) {
   int64_t c = 1024;
-  while (c < 4 * L) c <<= 1;
+  while (c < 16 * L) c <<= 1;
   return c;
 }
 
