@@ -28,7 +28,7 @@ struct ColArgsD {
   int64_t num_emb[TT_MAX_FEATURES];
 };
 
-// slots: a power of two >= 4 x the lookups (load factor <= 1/4 even if every lookup is unique): a
+// slots: a power of two >= 16 x the lookups (load factor <= 1/16 even if every lookup is unique): a
 // first CAS rarely collides and probe chains stay short; the update walks the claiming lookups,
 // so the table's size costs only memory (64 B a slot)
 static int64_t dedup_cap(int64_t L) {
