@@ -276,17 +276,18 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
         if (mask & (1u << q)) list[pos++] = (int)(i0 + q);
       __syncthreads();
       // group grp takes global positions == grp (mod 8), ascending
+      // (4 rows in flight per group; added in ascending position order as before)
       int p = (grp - (seen & 7) + 8) & 7;
-      for (; p + 8 < total; p += 16) {
-        f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
-        if (col_ok) {
-          x0 = *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
-          x1 = *reinterpret_cast<const f32x4v*>(gm.row(list[p + 8]) + hl * 4);
-        }
-        acc += x0;
-        acc += x1;
+      for (; p + 24 < total; p += 32) {
+        f32x4v x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          x[u] = col_ok ? *reinterpret_cast<const f32x4v*>(gm.row(list[p + 8 * u]) + hl * 4) : (f32x4v)(0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += x[u];
       }
-      if (p < total && col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
+      for (; p < total; p += 8)
+        if (col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
       seen += total;
       __syncthreads();
     }
