@@ -362,7 +362,7 @@ int tt_dedup_insert_cols(const tt_table_meta_t* tables, int T, const tt_feature_
 /* lookups i = s * seg_capacity + k, k < counts[s]: keys[i] = local table << 40 | local row */
 int tt_dedup_insert_segments(const int64_t* keys, const int32_t* counts, int64_t num_segments, int64_t seg_capacity,
                              void* workspace, size_t ws_bytes, int64_t max_lookups, void* stream);
-/* sum every unique row's gradient rows (ascending lookup order; rows with > 14 lookups: fixed
+/* sum every unique row's gradient rows (ascending lookup order; rows with > 30 lookups: fixed
  * 8-way interleave), then s += mean(G^2), w -= lr * G / (sqrt(s) + eps). D % 4 == 0, D <= 128. */
 int tt_dedup_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
                              int64_t B, const float* grad, int64_t ldg, float* weights, float* state, float lr,

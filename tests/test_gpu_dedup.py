@@ -83,9 +83,9 @@ def _assert_clean(ts):
     while cap < 16 * L:
         cap <<= 1
     al = lambda x: (x + 255) // 256 * 256  # noqa: E731
-    sl = ts._dd_ws[:cap * 64].view(torch.int64).view(cap, 8).cpu()
+    sl = ts._dd_ws[:cap * 128].view(torch.int64).view(cap, 16).cpu()  # 128-B slots
     assert bool((sl[:, 0] == -1).all())
-    o = cap * 64 + al(8 * L) + al(4 * (L // 15 + 1))
+    o = cap * 128 + al(8 * L) + al(4 * (L // 31 + 1))
     assert ts._dd_ws[o:o + 16].view(torch.int32).cpu().tolist() == [0, 0, 0, 0]
     o_ovf = o + 256 + al(4 * L)
     G = (L + 63) // 64

@@ -1,12 +1,12 @@
 // Single-pass dedup of single-hot lookups for the fused row-wise Adagrad (gfx950).
 //
-// A lookup i (one id of a single-hot bag) is inserted into an open-addressing table of 64-B slots
-// {word = key << 18 | count, items[14]}: a first-time key claims a free slot with ONE returning
+// A lookup i (one id of a single-hot bag) is inserted into an open-addressing table of 128-B slots
+// (one cache line) {word = key << 18 | count, items[30]}: a first-time key claims a free slot with ONE returning
 // 64-bit CAS that also sets its count to 1 (the common case: a single atomic round trip); a
 // repeated key finds its slot and takes a position with one atomicAdd on the same word. Positions
-// < 14 store the lookup index inline, so after the insert pass every unique (table, row) owns ONE
-// cache line holding everything its update needs, read in one hop. Rows looked up more than 14
-// times in a step ("hot") are listed by the lookup that takes position 14 and are summed by a
+// < 30 store the lookup index inline, so after the insert pass every unique (table, row) owns ONE
+// cache line holding everything its update needs, read in one hop by a half-wave. Rows looked up
+// more than 30 times in a step ("hot") are listed by the lookup that takes position 30 and are summed by a
 // workgroup that finds their lookups by scanning the per-lookup key array in index order.
 #pragma once
 
@@ -18,10 +18,10 @@ constexpr uint64_t DD_EMPTY = ~0ull;
 constexpr int DD_TABLE_SHIFT = 40;  // key = table << 40 | row (table < 64, rows < 2^40 per shard)
 constexpr int DD_CNT_BITS = 18;     // slot word = key << 18 | count; a step has < 2^18 lookups
 constexpr uint64_t DD_CNT_MASK = (1ull << DD_CNT_BITS) - 1;
-constexpr int DD_INL = 14;          // lookups stored inline per slot
+constexpr int DD_INL = 30;          // lookups stored inline per slot (128-B slot: word + 30 items)
 constexpr int DD_SPH = 4;           // slots per half-wave in the update launch
 
-struct __attribute__((aligned(64))) DSlot {
+struct __attribute__((aligned(128))) DSlot {
   uint64_t word;  // DD_EMPTY when free, else key << 18 | lookups of this key in the step
   int32_t item[DD_INL];
 };
@@ -370,7 +370,7 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   for (int q = 0; q < DD_SPH; ++q) {
     sp[q] = ws.slots + (hq[q] >= 0 ? hq[q] : 0);
     // an idle half-wave reads nothing and sees an EMPTY word
-    dw[q] = hq[q] >= 0 ? (hl < 16 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : 0) : (hl < 2 ? -1 : 0);
+    dw[q] = hq[q] >= 0 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : (hl < 2 ? -1 : 0);  // 32 lanes: 128 B
   }
   dd_meta_fill(m, lm);  // beside the slot loads
   __syncthreads();

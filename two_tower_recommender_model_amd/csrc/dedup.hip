@@ -30,7 +30,7 @@ struct ColArgsD {
 
 // slots: a power of two >= 16 x the lookups (load factor <= 1/16 even if every lookup is unique): a
 // first CAS rarely collides and probe chains stay short; the update walks the claiming lookups,
-// so the table's size costs only memory (64 B a slot)
+// so the table's size costs only memory (128 B a slot)
 static int64_t dedup_cap(int64_t L) {
   int64_t c = 1024;
   while (c < 16 * L) c <<= 1;
