@@ -182,7 +182,7 @@ def pmc_traffic(kernel_name: str, workload: str = "northstar"):
     gfx950-corrected), or None."""
     import glob
     files = glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))
-    others = [w for w in WORKLOADS if w != "northstar"]
+    others = [w for w in WORKLOADS if w != "northstar"] + ["zipf"]
     if workload == "northstar":
         files = [f for f in files if not any(w in os.path.basename(f) for w in others)]
     else:
@@ -294,7 +294,8 @@ def run_multihot(args):
     emb_bytes = nnz * (16 + 4 * D) + FB * (4 + 8 * D) + uniq * (8 * D + 8)
     emb_ms = sum(timed.get(n, 0.0) for n in ("fwd", "prep", "upd"))
     dom = max(("fwd", "upd"), key=lambda n: timed.get(n, 0.0))
-    traffic, src = pmc_traffic(kern[dom]["kernel"].split()[0], args.workload)
+    traffic, src = pmc_traffic(kern[dom]["kernel"].split()[0],
+                               args.workload if args.ids == "uniform" else f"{args.workload}_{args.ids}")
     ach = kern[dom].get("GB/s")
     roofline = {"bound": "hbm", "kernel": kern[dom]["kernel"], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic, "traffic_source": src,
@@ -443,7 +444,8 @@ def run_single(args):
         timed = {n: v * ms / tot for n, v in raw.items()}
         timing_how += ("; each span scaled by (step time without event nodes) / (sum of the spans) = "
                        f"{ms / tot:.3f}")
-    roofline = roofline_report(kern, timed, nnz, uniq, step, B, args.workload)
+    roofline = roofline_report(kern, timed, nnz, uniq, step, B,
+                               args.workload if args.ids == "uniform" else f"{args.workload}_{args.ids}")
     roofline["timing"] = timing_how
     roofline["event_span_ms"] = {n: round(v, 5) for n, v in raw.items()}
     cpu = None
