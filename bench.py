@@ -518,7 +518,7 @@ def run_multi(args, world, rank, local_rank):
     loss = float(step.loss)
     big = small = None
     step.release_graphs()  # before the process group is destroyed
-    info = {"capacity": step.C, "exchange_bytes_per_step": 2 * 4 * step.nslots * D + 8 * step.send.numel(),
+    info = {"capacity": step.C, "exchange_bytes_per_step": (2 + 4) * step.nslots * D + 8 * step.send.numel(),  # bf16 rows, fp32 grads
             "mode": mode}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info
 

@@ -294,6 +294,12 @@ int tt_tower_fwd_bwd_indexed(const tt_tower_shape_t* shape, int64_t B, const int
                              const float* const* rows_in, float* const* grad_rows_out, const float* params,
                              const void* labels, int label_dtype, float grad_scale, float* logits,
                              void* workspace, size_t ws_bytes, void* stream);
+/* The same with bf16 rows_in (from tt_shard_gather_rows_bf16): T1 computes on bf16 inputs anyway,
+ * so the result is bit-identical to the fp32-row form, and the rows all-to-all moves half the bytes. */
+int tt_tower_fwd_bwd_indexed_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos,
+                                  const void* const* rows_in, float* const* grad_rows_out, const float* params,
+                                  const void* labels, int label_dtype, float grad_scale, float* logits,
+                                  void* workspace, size_t ws_bytes, void* stream);
 /* T2: weight/bias gradients of every layer into the workspace (fixed-order partial slabs), and
  * the mean BCE of the preceding T1 into loss[0] (nullable; fixed-order sum of T1's partials). */
 int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
@@ -391,6 +397,10 @@ int tt_shard_route_cols(int F, int64_t B, const void* const* cols, int id_dtype,
 int tt_shard_gather_rows(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
                          int64_t seg_capacity, const int64_t* recv, float* rows_out, int32_t* bad, void* dedup_ws,
                          size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
+/* The same with rows_out in bf16 (round to nearest even), for tt_tower_fwd_bwd_indexed_bf16. */
+int tt_shard_gather_rows_bf16(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                              int64_t seg_capacity, const int64_t* recv, void* rows_out, int32_t* bad, void* dedup_ws,
+                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 
 /* T3 with the gradient taken from `grads` (data-parallel towers: the all-reduced gradient) instead
  * of T2's partials: Adam + the bf16 weight copies. */

@@ -153,12 +153,12 @@ def test_sharded_threads_vs_oracle(device, W, sharding):
                 kept = p >= 0
                 ids = np.mod(cols[f].numpy()[kept], N[f])
                 assert np.array_equal(kept, cols[f].numpy() != 0)
-                got = rin[torch.from_numpy(p[kept]).long()]
-                want = full[f][torch.from_numpy(ids)]
-                if s == 0:  # initial tables: bit for bit
+                got = rin[torch.from_numpy(p[kept]).long()]  # bf16 rows (the all-to-all carries bf16)
+                want = full[f][torch.from_numpy(ids)].to(torch.bfloat16)
+                if s == 0:  # initial tables: bit for bit (after the same bf16 rounding)
                     assert torch.equal(got, want), (r, f)
-                else:  # updated rows: the row-wise mean of G^2 is reduced in another order
-                    np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-5, atol=1e-7)
+                else:  # updated rows: the row-wise mean of G^2 is reduced in another order -> one bf16 ulp
+                    np.testing.assert_allclose(got.float().numpy(), want.float().numpy(), rtol=1e-2, atol=1e-7)
                 rows_all[f].append(torch.from_numpy(ids))
                 grads_all[f].append(gout[torch.from_numpy(p[kept]).long()])
         # (b) oracle update from the union of the gradient rows, rank-major

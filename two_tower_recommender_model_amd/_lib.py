@@ -153,11 +153,16 @@ SIGNATURES = {
         [_int, _i64, _pvp, _int, _pi64, _pi64, _pi32, _int, _i64, _vp, _vp, _vp, _vp, _sz, _vp],
     ),
     "tt_shard_gather_rows": (_int, [_vp, _ptm, _int, _int, _int, _i64, _vp, _vp, _vp, _vp, _sz, _i64, _vp]),
+    "tt_shard_gather_rows_bf16": (_int, [_vp, _ptm, _int, _int, _int, _i64, _vp, _vp, _vp, _vp, _sz, _i64, _vp]),
     "tt_tower_adam_grads": (
         _int,
         [_psh, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp],
     ),
     "tt_tower_fwd_bwd_indexed": (
+        _int,
+        [_psh, _i64, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
+    ),
+    "tt_tower_fwd_bwd_indexed_bf16": (
         _int,
         [_psh, _i64, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
     ),
@@ -201,6 +206,8 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_update_pre_rowwise_adagrad",
     "tt_shard_route_cols",
     "tt_shard_gather_rows",
+    "tt_shard_gather_rows_bf16",
+    "tt_tower_fwd_bwd_indexed_bf16",
     "tt_tower_adam_grads",
     "tt_tower_update_pre",
 ]

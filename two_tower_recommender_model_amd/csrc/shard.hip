@@ -143,7 +143,8 @@ struct GatherArgs {
   int64_t C;
   int D;
   const int64_t* recv;  // [W][F + F * C]
-  float* rows_out;      // [W * F * C][D]
+  float* rows_out;      // [W * F * C][D] fp32, or bf16 when out_bf16
+  int out_bf16;
   DedupWs dd;
   int dd_on;
   int32_t* bad;         // sticky: a received key outside the local shard
@@ -174,8 +175,20 @@ __global__ void __launch_bounds__(256) shard_gather_rows_kernel(GatherArgs a) {
   }
   DdPend pend;
   if (a.dd_on && hl == 0) dd_insert_begin(a.dd, key, (int32_t)i, pend);
-  float* dst = a.rows_out + i * a.D;
-  if (src) {
+  if (src && a.out_bf16) {  // the rows T1 rounds to bf16 anyway: half the all-to-all bytes
+    __bf16* dst = reinterpret_cast<__bf16*>(a.rows_out) + i * a.D;
+    for (int c = hl * 4; c < a.D; c += 128) {
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(src + c);
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
+      bf16x4v o;
+      o[0] = (__bf16)v[0];
+      o[1] = (__bf16)v[1];
+      o[2] = (__bf16)v[2];
+      o[3] = (__bf16)v[3];
+      *reinterpret_cast<bf16x4v*>(dst + c) = o;
+    }
+  } else if (src) {
+    float* dst = a.rows_out + i * a.D;
     for (int c = hl * 4; c < a.D; c += 128)
       *reinterpret_cast<f32x4v*>(dst + c) = *reinterpret_cast<const f32x4v*>(src + c);
   }
@@ -240,9 +253,9 @@ int tt_shard_route_cols(int F, int64_t B, const void* const* cols, int id_dtype,
   return check_launch("shard_route");
 }
 
-int tt_shard_gather_rows(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
-                         int64_t seg_capacity, const int64_t* recv, float* rows_out, int32_t* bad, void* dedup_ws,
-                         size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+static int gather_rows(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                       int64_t seg_capacity, const int64_t* recv, float* rows_out, int32_t* bad, void* dedup_ws,
+                       size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream, int out_bf16) {
   if (T < 1 || T > TT_MAX_TABLES || F < 1 || F > TT_MAX_FEATURES || W < 1 || seg_capacity < 1)
     return fail(TT_EINVAL, "shard_gather_rows: bad sizes");
   if (!weights || !tables || !recv || !rows_out || !bad) return fail(TT_EINVAL, "shard_gather_rows: null pointer");
@@ -264,6 +277,7 @@ int tt_shard_gather_rows(const float* weights, const tt_table_meta_t* tables, in
   a.C = seg_capacity;
   a.recv = recv;
   a.rows_out = rows_out;
+  a.out_bf16 = out_bf16;
   a.bad = bad;
   if (dedup_ws) {
     if (dedup_max_lookups < n || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
@@ -276,6 +290,20 @@ int tt_shard_gather_rows(const float* weights, const tt_table_meta_t* tables, in
   const int64_t grid = ceil_div(n, 8);
   shard_gather_rows_kernel<<<dim3((unsigned)grid), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("shard_gather_rows");
+}
+
+int tt_shard_gather_rows(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                         int64_t seg_capacity, const int64_t* recv, float* rows_out, int32_t* bad, void* dedup_ws,
+                         size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+  return gather_rows(weights, tables, T, F, W, seg_capacity, recv, rows_out, bad, dedup_ws, dedup_ws_bytes,
+                     dedup_max_lookups, stream, 0);
+}
+
+int tt_shard_gather_rows_bf16(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                              int64_t seg_capacity, const int64_t* recv, void* rows_out, int32_t* bad, void* dedup_ws,
+                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+  return gather_rows(weights, tables, T, F, W, seg_capacity, recv, reinterpret_cast<float*>(rows_out), bad, dedup_ws,
+                     dedup_ws_bytes, dedup_max_lookups, stream, 1);
 }
 
 }  // extern "C"

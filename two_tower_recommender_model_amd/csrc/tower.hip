@@ -78,8 +78,9 @@ struct TowerArgs {
   // gpos[t][m] of gsrc[t] ([*][in_dim[t]] fp32; -1 -> zeros) and its dX row goes to row gpos[t][m]
   // of gdst[t] instead of gpooled
   const int32_t* gpos[2];
-  const float* gsrc[2];
+  const float* gsrc[2];  // fp32 rows, or bf16 rows when gsrc_bf16 (the same bf16 values T1 computes on)
   float* gdst[2];
+  int gsrc_bf16;
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
 };
@@ -430,7 +431,9 @@ __device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int64_t 
 constexpr int T1_THREADS = 576;
 constexpr int T1_BARRIERS = 7;
 
-template <int IN_, int W0_, int W1_>
+// R16: indexed rows arrive as bf16 (sharded step, tt_tower_fwd_bwd_indexed_bf16); its own
+// instantiation, so the other modes' code and registers are untouched
+template <int IN_, int W0_, int W1_, bool R16 = false>
 __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][TR * LSTR];   // X, later dZ0
   __shared__ __attribute__((aligned(16))) __bf16 hs[2][TR * LSTR];   // hidden activation (bf16)
@@ -493,8 +496,10 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) rpos[i] = -1;
   if (gather || indexed) {
-    // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros
-    const float* src[4];
+    // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros.
+    // Indexed rows may be bf16 (tt_tower_fwd_bwd_indexed_bf16): byte offsets with the element size
+    const bool r16 = R16;
+    const char* src[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       src[i] = nullptr;
@@ -506,16 +511,29 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         if (gm < B) {
           if (indexed) {
             rpos[i] = a.gpos[t][gm];
-            if (rpos[i] >= 0) src[i] = a.gsrc[t] + (int64_t)rpos[i] * in + c4;
+            if (rpos[i] >= 0)
+              src[i] = reinterpret_cast<const char*>(a.gsrc[t]) + ((int64_t)rpos[i] * in + c4) * (r16 ? 2 : 4);
           } else {
             const int64_t id = (a.dbg & 32) ? 1 : load_id(a.gcol[t], a.gid_dtype, gm);
-            if (id != 0) src[i] = a.gtab[t] + ((a.dbg & 4) ? 0 : py_mod64(id, a.gmod[t])) * in + c4;
+            if (id != 0)
+              src[i] = reinterpret_cast<const char*>(a.gtab[t] + ((a.dbg & 4) ? 0 : py_mod64(id, a.gmod[t])) * in + c4);
           }
         }
       }
     }
+    if (r16) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xv[i] = src[i] ? *reinterpret_cast<const f32x4*>(src[i]) : (f32x4)(0.f);
+      for (int i = 0; i < 4; ++i) {
+        xv[i] = (f32x4)(0.f);
+        if (src[i]) {
+          const bf16x4 v = *reinterpret_cast<const bf16x4*>(src[i]);
+          xv[i] = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xv[i] = src[i] ? *reinterpret_cast<const f32x4*>(src[i]) : (f32x4)(0.f);
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1371,7 +1389,11 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
   if ((a.gcol[0] || a.gpos[0]) && !two)
     return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
-  if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
+  if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64 && a.gsrc_bf16)
+    tower_l2_kernel<128, 128, 64, true><<<g, b512, 0, as_stream(stream)>>>(a);
+  else if (two && a.gsrc_bf16)
+    tower_l2_kernel<0, 0, 0, true><<<g, b512, 0, as_stream(stream)>>>(a);
+  else if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
     tower_l2_kernel<128, 128, 64><<<g, b512, 0, as_stream(stream)>>>(a);
   else if (two && i0 == 64 && i1 == 64 && w0 == 128 && w1 == 64)
     tower_l2_kernel<64, 128, 64><<<g, b512, 0, as_stream(stream)>>>(a);
@@ -1474,12 +1496,13 @@ int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void
                    ws_bytes, stream);
 }
 
-int tt_tower_fwd_bwd_indexed(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos,
-                             const float* const* rows_in, float* const* grad_rows_out, const float* params,
-                             const void* labels, int label_dtype, float grad_scale, float* logits, void* workspace,
-                             size_t ws_bytes, void* stream) {
+static int tower_indexed(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos,
+                         const float* const* rows_in, float* const* grad_rows_out, const float* params,
+                         const void* labels, int label_dtype, float grad_scale, float* logits, void* workspace,
+                         size_t ws_bytes, void* stream, int bf16_rows) {
   if (!pos || !rows_in || !grad_rows_out) return fail(TT_EINVAL, "tower_indexed: null pointer");
   TowerArgs a{};
+  a.gsrc_bf16 = bf16_rows;
   for (int t = 0; t < 2; ++t) {
     if (!pos[t] || !rows_in[t] || !grad_rows_out[t]) return fail(TT_EINVAL, "tower_indexed: null pointer");
     if ((reinterpret_cast<uintptr_t>(rows_in[t]) & 15) || (reinterpret_cast<uintptr_t>(grad_rows_out[t]) & 15))
@@ -1491,6 +1514,22 @@ int tt_tower_fwd_bwd_indexed(const tt_tower_shape_t* shape, int64_t B, const int
   return launch_t1(shape, B, a, nullptr,
                    std::max(shape->in_col[0] + shape->in_dim[0], shape->in_col[1] + shape->in_dim[1]), nullptr, params, labels, label_dtype,
                    grad_scale, logits, workspace, ws_bytes, stream);
+}
+
+int tt_tower_fwd_bwd_indexed(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos,
+                             const float* const* rows_in, float* const* grad_rows_out, const float* params,
+                             const void* labels, int label_dtype, float grad_scale, float* logits, void* workspace,
+                             size_t ws_bytes, void* stream) {
+  return tower_indexed(shape, B, pos, rows_in, grad_rows_out, params, labels, label_dtype, grad_scale, logits,
+                       workspace, ws_bytes, stream, 0);
+}
+
+int tt_tower_fwd_bwd_indexed_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos,
+                                  const void* const* rows_in, float* const* grad_rows_out, const float* params,
+                                  const void* labels, int label_dtype, float grad_scale, float* logits,
+                                  void* workspace, size_t ws_bytes, void* stream) {
+  return tower_indexed(shape, B, pos, reinterpret_cast<const float* const*>(rows_in), grad_rows_out, params, labels,
+                       label_dtype, grad_scale, logits, workspace, ws_bytes, stream, 1);
 }
 
 int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,

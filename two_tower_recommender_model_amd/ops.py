@@ -571,13 +571,16 @@ class FusedTowers:
         """T1 of the sharded step: tower t's input row m is ``rows_in[t][pos[t][m]]`` (-1: zeros) and
         its input gradient goes to ``grad_rows_out[t][pos[t][m]]``."""
         ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}[labels.dtype]
+        bf16 = rows_in[0].dtype == torch.bfloat16  # rows from tt_shard_gather_rows_bf16
         for t in range(2):
             if pos[t].dtype != torch.int32 or pos[t].numel() < self.B:
                 raise _lib.TTError("fwd_bwd_indexed: pos must be int32 [B]")
-            for x in (rows_in[t], grad_rows_out[t]):
-                if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != self.shape.in_dim[t] or not x.is_contiguous():
-                    raise _lib.TTError("fwd_bwd_indexed: row buffers must be contiguous fp32 [*, in_dim]")
-        check(_lib_().tt_tower_fwd_bwd_indexed(C.byref(self.shape), self.B, ptr_array(list(pos)),
+            for x, want in ((rows_in[t], torch.bfloat16 if bf16 else torch.float32), (grad_rows_out[t], torch.float32)):
+                if x.dtype != want or x.dim() != 2 or x.shape[1] != self.shape.in_dim[t] or not x.is_contiguous():
+                    raise _lib.TTError("fwd_bwd_indexed: row buffers must be contiguous [*, in_dim] (rows fp32 or "
+                                       "bf16, gradient rows fp32)")
+        fn = _lib_().tt_tower_fwd_bwd_indexed_bf16 if bf16 else _lib_().tt_tower_fwd_bwd_indexed
+        check(fn(C.byref(self.shape), self.B, ptr_array(list(pos)),
                                                ptr_array(list(rows_in)), ptr_array(list(grad_rows_out)), ptr(params),
                                                ptr(labels), ldt, float(grad_scale), ptr(logits), ptr(self.ws),
                                                self.nbytes, stream_handle(self.device)), "tower_fwd_bwd_indexed")

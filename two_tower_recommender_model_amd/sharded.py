@@ -246,10 +246,12 @@ class FusedShardedTwoTowerStep:
         self.send = torch.zeros(W, F + F * C_, dtype=torch.int64, device=dev)
         self.recv = torch.zeros_like(self.send)
         self.pos = torch.full((F * B,), -1, dtype=torch.int32, device=dev)
-        self.rows_out = torch.zeros(self.nslots, D, dtype=torch.float32, device=dev)
+        # gathered rows travel as bf16 (T1 computes on bf16 inputs, so nothing changes but the bytes:
+        # half the rows all-to-all); gradient rows stay fp32 (the fp32 row-wise Adagrad)
+        self.rows_out = torch.zeros(self.nslots, D, dtype=torch.bfloat16, device=dev)
         self.rows_in = torch.zeros_like(self.rows_out)
-        self.grad_out = torch.zeros_like(self.rows_out)
-        self.grad_in = torch.zeros_like(self.rows_out)
+        self.grad_out = torch.zeros(self.nslots, D, dtype=torch.float32, device=dev)
+        self.grad_in = torch.zeros_like(self.grad_out)
         self.flags = torch.zeros(2, dtype=torch.int32, device=dev)  # {overflow, bad key}
         self.route_ws = torch.empty(_lib.load().tt_shard_route_workspace_bytes(F, B), dtype=torch.uint8, device=dev)
         self.tables.ensure_dedup_workspace(self.nslots)
@@ -318,8 +320,9 @@ class FusedShardedTwoTowerStep:
               "shard_route_cols")
         self.comm.all_to_all(self.recv, self.send)
         # owner lookup (+ dedup insert), rows back
-        check(lib.tt_shard_gather_rows(ptr(ts.weights), ts._tm, ts.T, F, W, C_, ptr(self.recv), ptr(self.rows_out),
-                                       ptr(self.flags[1:]), ptr(ts._dd_ws), ts._dd_ws.numel(), ts._dd_cap, st),
+        check(lib.tt_shard_gather_rows_bf16(ptr(ts.weights), ts._tm, ts.T, F, W, C_, ptr(self.recv),
+                                            ptr(self.rows_out), ptr(self.flags[1:]), ptr(ts._dd_ws), ts._dd_ws.numel(),
+                                            ts._dd_cap, st),
               "shard_gather_rows")
         self.comm.all_to_all(self.rows_in, self.rows_out)
         # towers (dX straight into the gradient rows the owners receive)
