@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--steps-per-graph", type=int, default=8, choices=[1, 2, 4, 8])
+    ap.add_argument("--overlap-comm", action="store_true",
+                    help="sharded step: gradient all-to-all and tower all-reduce on RCCL's stream (async)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
     return ap.parse_args()
@@ -464,7 +466,7 @@ def run_multi(args, world, rank, local_rank):
     dev = torch.device("cuda", local_rank)
     comm = TorchComm(always_collective=True)
     step = FusedShardedTwoTowerStep(comm, [num_users, num_items], D, layers, B, dev, lr_emb=0.01, lr_dense=0.01,
-                                    seed=0)
+                                    seed=0, overlap_comm=args.overlap_comm)
     batches = synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1 + rank)
     step.load_batch(*batches[0])
     step.step()  # creates the RCCL communicators before any capture
@@ -555,7 +557,8 @@ def main():
         value, ms, loss, sharded_info = run_multi(args, world, rank, local_rank)
         roofline, cpu, steps_run = None, None, args.steps
         config["parallelism"] = (f"row-wise sharded tables (id all-to-all over RCCL) + data-parallel towers x{world}, "
-                                 f"{sharded_info['mode']}")
+                                 f"{sharded_info['mode']}, collectives "
+                                 f"{'overlapped (RCCL stream)' if args.overlap_comm else 'in-stream'}")
         config["sharded"] = sharded_info
     if rank == 0:
         out = {"metric": f"training pairs/sec at batch {B} (per GPU)", "value": round(value, 1), "unit": "pairs/s",

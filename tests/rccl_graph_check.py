@@ -25,7 +25,8 @@ def main():
         cols = [torch.randint(0, n, (B,), generator=g).to(device) for n in N]
         batches.append((cols, torch.randint(0, 2, (B,), generator=g).to(torch.int32).to(device)))
     full = [torch.empty(n, D).uniform_(-0.01, 0.01, generator=g) for n in N]
-    a = FusedShardedTwoTowerStep(TorchComm(always_collective=True), N, D, [128, 64], B, device, full_tables=full)
+    a = FusedShardedTwoTowerStep(TorchComm(always_collective=True), N, D, [128, 64], B, device, full_tables=full,
+                                 overlap_comm="--overlap" in sys.argv)
     b = FusedShardedTwoTowerStep(ThreadComm.group(1)[0], N, D, [128, 64], B, device, full_tables=full)
     a.load_batch(*batches[0])
     a.step()  # communicator init; the same first step on b

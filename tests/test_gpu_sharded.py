@@ -203,16 +203,19 @@ def test_sharded_overflow_raises(device):
         steps[0].check()
 
 
-def test_sharded_rccl_world1_graph_equals_eager(device):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_sharded_rccl_world1_graph_equals_eager(device, overlap):
     """The production comm (torch.distributed "nccl" = RCCL) with its collectives captured into
     HIP graphs, at world size 1 with the collectives forced on: identical to eager ThreadComm. Run
-    in a child process (a process group and RCCL-in-graph state stay out of this test process)."""
+    in a child process (a process group and RCCL-in-graph state stay out of this test process).
+    overlap: the gradient all-to-all and tower all-reduce on RCCL's stream (overlap_comm=True)."""
     import os
     import subprocess
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, os.path.join(here, "rccl_graph_check.py")], capture_output=True, text=True,
+    r = subprocess.run([sys.executable, os.path.join(here, "rccl_graph_check.py")] + (["--overlap"] if overlap else []),
+                       capture_output=True, text=True,
                        timeout=300, cwd=os.path.dirname(here))
     assert r.returncode == 0 and "RCCL-GRAPH-OK" in r.stdout, (r.returncode, r.stdout[-1500:], r.stderr[:3000],
                                                                r.stderr[-1500:])

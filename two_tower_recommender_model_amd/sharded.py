@@ -187,13 +187,18 @@ class FusedShardedTwoTowerStep:
                  batch_size: int, device: torch.device, sharding: Optional[Sequence[str]] = None,
                  tw_owners: Optional[Sequence[int]] = None, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
-                 capacity: Optional[int] = None, full_tables: Optional[Sequence[torch.Tensor]] = None):
+                 capacity: Optional[int] = None, full_tables: Optional[Sequence[torch.Tensor]] = None,
+                 overlap_comm: bool = False):
         """Two features (query, candidate), one table each, single-hot. ``sharding[f]`` is
         "row_wise" (default) or "table_wise" (owner ``tw_owners[f]``). ``full_tables`` (CPU,
         optional) give the initial weights; otherwise each rank draws its shard from
         U(-sqrt(1/N), sqrt(1/N)) (torchrec EBC init). Tower parameters are initialised from
-        ``seed`` identically on every rank (what DDP's initial broadcast guarantees)."""
+        ``seed`` identically on every rank (what DDP's initial broadcast guarantees).
+        ``overlap_comm``: run the gradient all-to-all beside T2 and the tower all-reduce beside the
+        owner's Adagrad on RCCL's stream; off by default, since each cross-stream join inside the
+        step graph costs more than the overlap wins at world 1."""
         self.comm = comm
+        self.overlap_comm = bool(overlap_comm)
         self.W, self.rank = comm.world, comm.rank
         self.device = torch.device(device)
         dev = self.device
@@ -328,12 +333,12 @@ class FusedShardedTwoTowerStep:
         # towers (dX straight into the gradient rows the owners receive)
         tw.fwd_bwd_indexed([self.pos[:B], self.pos[B:]], [self.rows_in, self.rows_in],
                            [self.grad_out, self.grad_out], self.params, self.labels, self.logits)
-        # gradient rows to the owners, overlapped with the towers' weight gradients (T2) and their
-        # reduction; the towers' all-reduce overlaps the owner's row-wise Adagrad
-        h_rows = self.comm.all_to_all(self.grad_in, self.grad_out, async_op=True)
+        # gradient rows to the owners (with overlap_comm: beside the towers' weight gradients (T2)
+        # and their reduction, and the towers' all-reduce beside the owner's row-wise Adagrad)
+        h_rows = self.comm.all_to_all(self.grad_in, self.grad_out, async_op=self.overlap_comm)
         tw.wgrad(self.loss)
         tw.update(self.params, do_adam=False, grads_out=self.grads)
-        h_dense = self.comm.all_reduce_mean(self.grads, async_op=True)
+        h_dense = self.comm.all_reduce_mean(self.grads, async_op=self.overlap_comm)
         h_rows.wait()
         ts.dedup_rowwise_adagrad(self.grad_in, self.nslots, self.lr_emb, self.eps, flat=True)
         h_dense.wait()
