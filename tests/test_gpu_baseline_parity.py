@@ -1,0 +1,226 @@
+"""Parity of the PRODUCTION step at the BASELINE.json sizes.
+
+The step under test is exactly what bench.py times: ``FusedTwoTowerStep`` with its defaults (T1 =
+EBC gather + bf16-MFMA towers fwd/bwd-data + dot/BCE + dedup insert, T2 = weight gradients +
+deferred inserts, K3 = fused row-wise Adagrad + slab reduction + Adam) replayed from HIP graphs over
+resident batches; for config 5 the multi-hot KJT path (tt_pooled_fwd -> towers -> tiled
+tt_bwd_prepare -> tt_bwd_rowwise_adagrad). Shapes:
+
+  north star  100M items x 50M users, D 128, B 8192 (tables of 1.28e10 / 6.4e9 fp32 elements: far
+              past 2^31, so every 64-bit row offset is exercised); uniform and Zipf ids
+  config 2    10M items x 5M users, D 64, B 4096
+  config 5    100M x 50M, D 128, B 16384, multi-hot bags of Uniform{1..39} ids (mean 20)
+
+Two steps run; the second is checked, from a state the first one changed (non-zero Adagrad state,
+Adam step 2). Each check feeds the oracle the kernels' OWN intermediate where the comparison would
+otherwise be a bf16-tower comparison (the gradient rows dX that T1 writes):
+
+* gathered rows (``materialize_pooled``): bit-exact against the table rows the transform selects
+  (id 0 -> an empty bag, id % N, 03_model_training.py:356-365); multi-hot: the oracle's
+  ``F.embedding_bag`` sum over the same rows, rtol 1e-6;
+* towers: logits, dX and the tower gradients against the fp64 emulation of the kernels' rounding
+  points (tests/tower_emul.py), relative Frobenius error < 2e-3; loss rtol 1e-4;
+* K3 (tables + row-wise state of every touched row): ``oracle.rowwise_adagrad_from_lookups`` fed
+  T1's dX, rtol 1e-5 (weights atol 1e-5 x lr, state atol 1e-12) — eps 1e-10, lr 0.01 (03:791-795);
+* Adam: the oracle's torch.optim.Adam restatement fed the kernels' own tower gradient, rtol 1e-5
+  (absolute floors: 1e-6 x max|g| on the moments, 1e-5 x lr on the parameters, where m = 0.9 m0 +
+  0.1 g cancels).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref
+from tower_emul import emulate, rel_err, split_params
+
+pytestmark = pytest.mark.gpu
+
+LAYERS = [128, 64]
+LR = 0.01
+CASES = {
+    "northstar": dict(N=[50_000_000, 100_000_000], D=128, B=8192),
+    "config2": dict(N=[5_000_000, 10_000_000], D=64, B=4096),
+}
+
+
+def _zipf(g, n, N, device):
+    u01 = torch.rand(n, generator=g, device=device, dtype=torch.float64)
+    r = torch.floor(torch.exp(u01 * np.log(float(N))))
+    return (r.to(torch.int64) * 2654435761) % N
+
+
+def _single_hot_batches(N, B, ids, device, seed, n=2):
+    g = torch.Generator(device=device).manual_seed(seed)
+    out = []
+    for _ in range(n):
+        cols = []
+        for n_ in N:
+            if ids == "uniform":  # ids past N exercise the reference's id % N, zeros its drop
+                c = torch.randint(0, 2 * n_, (B,), generator=g, device=device, dtype=torch.int64)
+            else:
+                c = _zipf(g, B, n_, device)
+            c[torch.randint(0, B, (B // 64,), generator=g, device=device)] = 0
+            cols.append(c)
+        lab = torch.randint(0, 2, (B,), generator=g, device=device, dtype=torch.int32)
+        out.append((cols, lab))
+    return out
+
+
+def _free():
+    import gc
+
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def _check_towers(xq, xc, params_before, st, labels, logits, gq, gc_, grads, B):
+    D_q, D_c = xq.shape[1], xc.shape[1]
+    prm = split_params(params_before, [D_q, D_c], LAYERS)
+    lg, loss, dxs, gw = emulate(xq, xc, prm, LAYERS, labels.cpu())
+    assert rel_err(logits, lg) < 2e-3
+    np.testing.assert_allclose(float(st.loss), float(loss), rtol=1e-4)
+    assert rel_err(gq, dxs[0]) < 2e-3 and rel_err(gc_, dxs[1]) < 2e-3
+    o = 0
+    for want in gw:
+        n = want.numel()
+        assert rel_err(grads[o:o + n].reshape(want.shape), want) < 2e-3
+        o += n
+    return prm
+
+
+def _check_adam(prm_before, grads, m0, v0, step0, params_after, exp_avg_after, exp_avg_sq_after):
+    """torch.optim.Adam (03_model_training.py:826-829) fed the kernels' tower gradient."""
+    shapes = [p.shape for p in prm_before]
+    ps, gs, ms, vs, o = [], [], [], [], 0
+    for s in shapes:
+        n = int(np.prod(s))
+        ps.append(torch.cat([p.reshape(-1) for p in prm_before])[o:o + n].clone())
+        gs.append(grads[o:o + n].clone())
+        ms.append(m0[o:o + n].clone())
+        vs.append(v0[o:o + n].clone())
+        o += n
+    ref.adam(ps, gs, ms, vs, step0 + 1, LR)
+    # the moments and the step may cancel (m = 0.9 m0 + 0.1 g): absolute floors relative to the
+    # gradient scale and to the step size lr (an Adam step moves a parameter by at most ~lr)
+    gmax = float(grads.abs().max())
+    np.testing.assert_allclose(exp_avg_after.numpy(), torch.cat(ms).numpy(), rtol=1e-5, atol=1e-6 * gmax)
+    np.testing.assert_allclose(exp_avg_sq_after.numpy(), torch.cat(vs).numpy(), rtol=1e-5, atol=1e-6 * gmax ** 2)
+    np.testing.assert_allclose(params_after.numpy(), torch.cat(ps).numpy(), rtol=1e-5, atol=1e-5 * LR)
+
+
+def _check_rowwise_adagrad(table_view, state_view, u, w_before, s_before, lookup_rows, grad_rows):
+    """K3 against the oracle on the touched rows only: ``u`` (device) = unique rows, ``lookup_rows``
+    (CPU) = row of every kept lookup in lookup order, ``grad_rows`` = its gradient row."""
+    w_want, s_want = w_before.clone(), s_before.clone()
+    inv = torch.searchsorted(u.cpu(), lookup_rows)
+    ref.rowwise_adagrad_from_lookups(w_want, s_want, inv, grad_rows, LR, 1e-10)
+    w_got = table_view[u].cpu()
+    s_got = state_view[u].cpu()
+    np.testing.assert_allclose(s_got.numpy(), s_want.numpy(), rtol=1e-5, atol=1e-12)
+    # a row's update is lr * G / rms(G): summation-order differences of a hot row's G (Zipf rows are
+    # looked up hundreds of times) reach ~1e-6 of that step where the row's entry cancels to ~0
+    np.testing.assert_allclose(w_got.numpy(), w_want.numpy(), rtol=1e-5, atol=1e-5 * LR)
+    assert not torch.equal(w_got, w_before)  # the update happened
+
+
+@pytest.mark.parametrize("case,ids", [("northstar", "uniform"), ("northstar", "zipf"), ("config2", "uniform")])
+def test_production_step_at_baseline_size(device, case, ids):
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N, D, B = CASES[case]["N"], CASES[case]["D"], CASES[case]["B"]
+    st = FusedTwoTowerStep(N, [D, D], [0], [1], LAYERS, B, device, lr_emb=LR, lr_dense=LR, id_dtype=torch.int64,
+                           seed=0, materialize_pooled=True)
+    # the production configuration bench.py times: fused gather + single-hot dedup + 3 launches
+    assert st.towers is not None and st.gather and st.dedup_single and st.combined_bwd
+    if case == "northstar":
+        assert st.tables.rows[1] * D > 2 ** 31 and st.tables.weight_offsets[1] > 2 ** 31
+    batches = _single_hot_batches(N, B, ids, device, seed=11 if ids == "uniform" else 12)
+    st.capture_pool(batches, steps_per_graph=1)
+    st.pool_graphs[0].replay()
+    torch.cuda.synchronize()
+    cols, lab = batches[1]
+    # state before step 2 (touched rows only; the tables themselves stay on the GPU)
+    keep = [c != 0 for c in cols]
+    rows = [c[k] % n for c, k, n in zip(cols, keep, N)]
+    uniq = [torch.unique(r) for r in rows]
+    before = [(st.tables.table_view(t)[uniq[t]].cpu(), st.tables.state_view(t)[uniq[t]].cpu()) for t in range(2)]
+    params0, m0, v0 = st.params.cpu().clone(), st.exp_avg.cpu().clone(), st.exp_avg_sq.cpu().clone()
+    step0 = int(st.adam_state[0])
+    assert step0 == 1
+    st.pool_graphs[1].replay()
+    torch.cuda.synchronize()
+    # (1) gathered rows: bit-exact (id 0 -> zeros)
+    pooled = st.pooled.cpu()
+    for t in range(2):
+        want = torch.zeros(B, D)
+        want[keep[t].cpu()] = before[t][0][torch.searchsorted(uniq[t].cpu(), rows[t].cpu())]
+        assert torch.equal(pooled[:, t * D:(t + 1) * D], want), f"table {t}: gathered rows differ"
+    # (2) towers vs the fp64 emulation of the kernels' rounding points
+    gp = st.gpooled.cpu()
+    grads = st.grads.cpu()
+    prm = _check_towers(pooled[:, :D], pooled[:, D:], params0, st, lab, st.logits.cpu(), gp[:, :D], gp[:, D:],
+                        grads, B)
+    # (3) K3: fused row-wise Adagrad fed T1's own dX rows (lookup i = (feature, bag), kept lookups only)
+    for t in range(2):
+        k = keep[t].cpu()
+        _check_rowwise_adagrad(st.tables.table_view(t), st.tables.state_view(t), uniq[t], before[t][0], before[t][1],
+                               rows[t].cpu(), gp[k, t * D:(t + 1) * D].contiguous())
+    # (4) Adam on the towers, fed the kernels' tower gradient
+    _check_adam(prm, grads, m0, v0, step0, st.params.cpu(), st.exp_avg.cpu(), st.exp_avg_sq.cpu())
+    del st, batches
+    _free()
+
+
+def _kjt_batches(N, B, maxlen, device, seed, n=2):
+    g = torch.Generator(device=device).manual_seed(seed)
+    out = []
+    for _ in range(n):
+        lengths = torch.randint(1, maxlen + 1, (2 * B,), generator=g, device=device, dtype=torch.int32)
+        offsets = torch.zeros(2 * B + 1, dtype=torch.int32, device=device)
+        offsets[1:] = torch.cumsum(lengths, 0)
+        vals = [torch.randint(0, n_, (int(lengths[f * B:(f + 1) * B].sum()),), generator=g, device=device,
+                              dtype=torch.int64) for f, n_ in enumerate(N)]
+        lab = torch.randint(0, 2, (B,), generator=g, device=device, dtype=torch.int32)
+        out.append((torch.cat(vals), offsets, lab))
+    return out
+
+
+def test_production_multihot_step_config5(device):
+    """SURVEY §8(d) config 5 on one GPU: 100M x 50M, D 128, B 16384, bags U{1..39}."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N, D, B = [50_000_000, 100_000_000], 128, 16384
+    batches = _kjt_batches(N, B, 39, device, seed=4)
+    cap = max(v.numel() for v, _, _ in batches)
+    st = FusedTwoTowerStep(N, [D, D], [0], [1], LAYERS, B, device, lr_emb=LR, lr_dense=LR, id_dtype=torch.int64,
+                           seed=0, max_lookups=cap)
+    assert st.towers is not None and st.kjt_input
+    st.capture_pool_kjt(batches)
+    st.pool_graphs[0].replay()
+    torch.cuda.synchronize()
+    vals, offs, lab = batches[1]
+    o = offs.cpu().to(torch.int64)
+    seg = [(int(o[f * B]), int(o[(f + 1) * B])) for f in range(2)]
+    rows = [vals[s:e] for s, e in seg]
+    uniq = [torch.unique(r) for r in rows]
+    before = [(st.tables.table_view(t)[uniq[t]].cpu(), st.tables.state_view(t)[uniq[t]].cpu()) for t in range(2)]
+    params0, m0, v0 = st.params.cpu().clone(), st.exp_avg.cpu().clone(), st.exp_avg_sq.cpu().clone()
+    step0 = int(st.adam_state[0])
+    st.pool_graphs[1].replay()
+    torch.cuda.synchronize()
+    pooled, gp, grads = st.pooled.cpu(), st.gpooled.cpu(), st.grads.cpu()
+    inv = [torch.searchsorted(uniq[t].cpu(), rows[t].cpu()) for t in range(2)]
+    for t in range(2):
+        bag_off = (o[t * B:(t + 1) * B + 1] - o[t * B])
+        want = torch.nn.functional.embedding_bag(inv[t], before[t][0], bag_off, mode="sum", include_last_offset=True)
+        np.testing.assert_allclose(pooled[:, t * D:(t + 1) * D].numpy(), want.numpy(), rtol=1e-6, atol=1e-7)
+    prm = _check_towers(pooled[:, :D], pooled[:, D:], params0, st, lab, st.logits.cpu(), gp[:, :D], gp[:, D:],
+                        grads, B)
+    for t in range(2):
+        lens = o[t * B + 1:(t + 1) * B + 1] - o[t * B:(t + 1) * B]
+        bag = torch.repeat_interleave(torch.arange(B), lens)
+        _check_rowwise_adagrad(st.tables.table_view(t), st.tables.state_view(t), uniq[t], before[t][0], before[t][1],
+                               rows[t].cpu(), gp[bag, t * D:(t + 1) * D].contiguous())
+    _check_adam(prm, grads, m0, v0, step0, st.params.cpu(), st.exp_avg.cpu(), st.exp_avg_sq.cpu())
+    del st, batches
+    _free()
