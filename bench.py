@@ -52,12 +52,15 @@ def parse():
     ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
     ap.add_argument("--ids", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=2_000_000, help="table rows of the CPU sample")
-    ap.add_argument("--cpu-steps", type=int, default=20)
+    ap.add_argument("--cpu-rows", type=int, default=0,
+                    help="table rows of the CPU sample (0: the workload's full tables when host RAM allows)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: timed seconds of steps")
+    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--batches", type=int, default=64,
+                    help="resident synthetic batches cycled by the single-hot bench (64 x 16,384 rows x 512 B "
+                         "= 537 MB touched: past the 256 MiB Infinity Cache)")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--steps-per-graph", type=int, default=8, choices=[1, 2, 4, 8])
-    ap.add_argument("--overlap-comm", action="store_true",
-                    help="sharded step: gradient all-to-all and tower all-reduce on RCCL's stream (async)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
     return ap.parse_args()
@@ -105,15 +108,67 @@ def time_kernel(fn, iters):
     return a.elapsed_time(b) / iters  # ms
 
 
+def cpu_threads() -> int:
+    """Host threads of the CPU baseline: every core this process may run on, capped by the CPU share
+    the host grants one GPU (the box exports OMP_NUM_THREADS = its per-GPU share; nproc there shows
+    the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(share))) if share and share.isdigit() else n
+
+
+def cpu_tables(rows, D, threads, seed=0):
+    """The oracle's tables at the requested rows, filled U(-sqrt(1/N), sqrt(1/N)) (torchrec EBC init)
+    in parallel chunks (torch's CPU uniform_ runs on one thread: ~1.5 s/GB)."""
+    import concurrent.futures as cf
+
+    out = []
+    for t, n in enumerate(rows):
+        w = torch.empty(n, D)
+        a = (1.0 / n) ** 0.5
+        step = max(1, -(-n // (4 * threads)))
+
+        def fill(i, w=w, a=a, t=t):
+            w[i:i + step].uniform_(-a, a, generator=torch.Generator().manual_seed(seed * 7919 + t * 104729 + i))
+
+        with cf.ThreadPoolExecutor(threads) as ex:
+            list(ex.map(fill, range(0, n, step)))
+        out.append(w)
+    return out
+
+
+def cpu_rows(args, num_users, num_items, D):
+    """Full tables when this host can hold them, else scaled-down tables
+    (--cpu-rows, default 2M rows each when RAM is short). Returns (rows, description)."""
+    full = (num_users + num_items) * (4 * D + 4)
+    try:
+        import psutil
+
+        avail = psutil.virtual_memory().available
+    except Exception:  # noqa: BLE001
+        avail = 0
+    if args.cpu_rows == 0 and avail > 1.5 * full + (8 << 30):
+        return (num_users, num_items), "full tables"
+    n = args.cpu_rows or 2_000_000
+    rows = (min(n, num_users), min(n, num_items))
+    if args.cpu_rows:
+        return rows, "tables scaled down (--cpu-rows)"
+    return rows, (f"tables scaled down (host RAM available {avail / 2**30:.0f} GiB < 1.5 x "
+                  f"{full / 2**30:.0f} GiB + 8 GiB)")
+
+
 def cpu_baseline(args, num_users, num_items, D, B, layers):
     """The oracle (CPU restatement of TorchRec's unsharded CPU path, sparse touched-row update) on
-    this host's cores, bounded sample: full B, D, towers; tables scaled to --cpu-rows rows."""
+    this host's cores, bounded sample: full B, D, towers, full tables when RAM allows; steps until
+    --cpu-seconds of CPU work (at least 5)."""
     from oracle import ref
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
-    rows = min(args.cpu_rows, num_users), min(args.cpu_rows, num_items)
-    st = ref.init_state(list(rows), [D, D], [0, 1], [0], [1], layers, seed=0)
+    rows, how = cpu_rows(args, num_users, num_items, D)
+    st = ref.init_state([1, 1], [D, D], [0, 1], [0], [1], layers, seed=0)
+    st.tables = cpu_tables(rows, D, threads)
+    st.states = [torch.zeros(n) for n in rows]
     g = torch.Generator().manual_seed(0)
     batches = []
     for _ in range(4):
@@ -125,17 +180,30 @@ def cpu_baseline(args, num_users, num_items, D, B, layers):
         v, o, lab = batches[i % 4]
         ref.train_step(st, v, o, B, lab, 0.01, 0.01)
     t0 = time.perf_counter()
-    n = args.cpu_steps
-    for i in range(n):
-        v, o, lab = batches[i % 4]
+    n = 0
+    while n < args.cpu_steps or time.perf_counter() - t0 < args.cpu_seconds:
+        v, o, lab = batches[n % 4]
         ref.train_step(st, v, o, B, lab, 0.01, 0.01)
+        n += 1
     dt = time.perf_counter() - t0
     return {
         "value": round(n * B / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-        "sample": f"{n} steps of the oracle train_step (torch CPU fp32: embedding_bag sum, towers "
-                  f"{layers}, BCE, sparse row-wise Adagrad, Adam) at B={B}, D={D}, tables scaled to "
-                  f"{rows[0]}x{D} / {rows[1]}x{D} rows; host CPU {platform.processor() or platform.machine()}",
+        "sample": f"{n} steps ({dt:.1f} s) of the oracle train_step (torch CPU fp32: embedding_bag sum, towers "
+                  f"{layers}, BCE, sparse row-wise Adagrad, Adam) at B={B}, D={D}, {how} "
+                  f"({rows[0]}x{D} / {rows[1]}x{D}); {threads} threads of {len(os.sched_getaffinity(0))} in the "
+                  f"affinity mask; host CPU {cpu_model()}",
     }
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
 
 
 def lookup_stats(step, batches):
@@ -150,10 +218,16 @@ def lookup_stats(step, batches):
 
 
 def launch_bytes(step, nnz: int, uniq: int):
-    """Algorithmic HBM bytes (and MFMA flops) per launch of the one-stream step:
-    t1 = gather + towers fwd/bwd + dedup insert; t2 = tower weight gradients (+ Adam scalars);
-    k3 = T3 (slab reduction + Adam + bf16 copies) + the fused row-wise Adagrad. The embedding-path
-    total follows SURVEY.md 8(d)."""
+    """Per launch of the one-stream step: ``alg`` = the launch's share of the
+    SURVEY.md 8(d) algorithmic bytes (the FBGEMM convention: every lookup's id + row in the forward,
+    4 B length + 4D pooled write + 4D gradient read per bag, unique rows' weight + state read and
+    write in the backward); ``design`` = what the launch moves by design (incl. the T1 -> T2 bf16
+    operand strips, the split-K slabs and the dedup slots); ``flop`` = tower MFMA flops.
+      t1 = gather + towers fwd/bwd + dedup insert: 8(d) ids fwd + rows + lengths + pooled (the
+           pooled rows stay on chip; T1 writes the pooled gradient dX instead, same bytes);
+      t2 = tower weight gradients (+ Adam scalars): no 8(d) bytes;
+      k3 = T3 (slab reduction + Adam + bf16 copies) + the fused row-wise Adagrad: 8(d) ids bwd +
+           gradient rows + unique rows' weight and state read-modify-write."""
     D, B, F = step.dims[0], step.B, step.F
     L = step.layer_sizes
     idb = 8 if step.id_dtype == torch.int64 else 4
@@ -163,18 +237,19 @@ def launch_bytes(step, nnz: int, uniq: int):
     cdiv = lambda a, b: -(-a // b)  # noqa: E731
     S = min(64, cdiv(B, 256))  # staged T2 slices of whole 256-row passes (tower.hip tower_layout)
     S = cdiv(B, cdiv(cdiv(B, S), 256) * 256)
-    t1 = (F * B * idb + B * 4 + nnz * 4 * D + B * 4 + F * B * 4 * D + opnd + nnz * 20)
+    t1_design = (F * B * idb + B * 4 + nnz * 4 * D + B * 4 + F * B * 4 * D + opnd + nnz * 20)
     emb_upd = uniq * (64 + 8 * D + 8) + nnz * 4 * D
-    t2 = opnd + S * P * 4
-    k3 = emb_upd + S * P * 4 + 6 * P * 4 + 4 * P
-    emb_path = F * B * (1 * (8 + 8 + 4 * D) + 4 + 4 * D + 4 * D) + uniq * (8 * D + 8)  # 8(d), L = 1
-    return {"t1": {"bytes": t1, "flop": 8 * B * macs, "what": "tower_l2_kernel: EBC gather + both towers fwd/bwd "
-                                                              "+ dedup insert"},
-            "t2": {"bytes": t2, "flop": 4 * B * macs, "what": "tower_wgrad_kernel: tower weight gradients (staged "
-                                                              "operand strips) + Adam step scalars"},
-            "k3": {"bytes": k3, "flop": 0, "emb_bytes": emb_upd,
+    t2_design = opnd + S * P * 4
+    k3_design = emb_upd + S * P * 4 + 6 * P * 4 + 4 * P
+    t1_alg = nnz * (8 + 4 * D) + F * B * (4 + 4 * D)
+    k3_alg = nnz * 8 + F * B * 4 * D + uniq * (8 * D + 8)
+    return {"t1": {"alg_bytes": t1_alg, "design_bytes": t1_design, "flop": 8 * B * macs,
+                   "what": "tower_l2_kernel: EBC gather + both towers fwd/bwd + dedup insert"},
+            "t2": {"alg_bytes": 0, "design_bytes": t2_design, "flop": 4 * B * macs,
+                   "what": "tower_wgrad_kernel: tower weight gradients (staged operand strips) + Adam step scalars"},
+            "k3": {"alg_bytes": k3_alg, "design_bytes": k3_design, "flop": 0,
                    "what": "tower_update_dedup_kernel: fused row-wise Adagrad + slab reduction + Adam + bf16 copies"},
-            "_emb_path_bytes": emb_path}
+            "_emb_path_bytes": t1_alg + k3_alg}
 
 
 def pmc_traffic(kernel_name: str, workload: str = "northstar"):
@@ -277,38 +352,48 @@ def run_multihot(args):
         uniq += int(torch.unique(torch.cat([v[:nb], v[nb:] + (1 << 40)])).numel())
     uniq //= len(batches)
     FB = 2 * B
+    # alg = SURVEY 8(d) bytes (ids + rows per lookup in the forward, ids again in the backward, 4 B
+    # length + 4D pooled write + 4D gradient read per bag, unique rows' weight + state read and write);
+    # design = what the launches move (the update reads a gradient row per lookup, mostly cache hits)
     kern = {
-        "fwd": {"bytes": nnz * (8 + 4 * D) + FB * (4 + 4 * D), "kernel": "pooled_fwd_kernel",
+        "fwd": {"alg_bytes": nnz * (8 + 4 * D) + FB * (4 + 4 * D), "design_bytes": nnz * (8 + 4 * D) + FB * (4 + 4 * D),
+                "kernel": "pooled_fwd_kernel",
                 "what": "tt_pooled_fwd: segmented gather + sum pool (8 B id + 4D row per lookup, 4D per bag)"},
-        "prep": {"bytes": nnz * (8 + 4 + 4) + FB * 4, "kernel": "bwd_tile_hash + scan + bwd_tile_scatter",
+        "prep": {"alg_bytes": nnz * 8, "design_bytes": nnz * (8 + 4 + 4) + FB * 4,
+                 "kernel": "bwd_tile_hash + scan + bwd_tile_scatter",
                  "what": "tt_bwd_prepare: ids read, per-lookup entry word, segment scatter"},
-        "upd": {"bytes": nnz * (4 * D + 4) + uniq * (8 * D + 8), "kernel": "bwd_adagrad_direct_kernel (+ narrow and hot-row launches)",
-                "what": "tt_bwd_rowwise_adagrad: grad rows per lookup, weight row + state read+write per unique row "
-                        "(once-looked-up rows in lookup order, the others per row)"},
-        "t1": {"bytes": None, "kernel": "tower_fwd_bwd_kernel", "what": "fused towers fwd/bwd + dot/BCE"},
-        "t2t3": {"bytes": None, "kernel": "tower_wgrad + tower_update", "what": "tower weight grads + Adam (side stream)"},
+        "upd": {"alg_bytes": FB * 4 * D + uniq * (8 * D + 8), "design_bytes": nnz * (4 * D + 4) + uniq * (8 * D + 8),
+                "kernel": "bwd_adagrad_direct_kernel (+ narrow and hot-row launches)",
+                "what": "tt_bwd_rowwise_adagrad: weight row + state read+write per unique row (8(d)), gradient row "
+                        "per bag (8(d)); by design a gradient row per lookup (once-looked-up rows in lookup order)"},
+        "t1": {"alg_bytes": None, "kernel": "tower_fwd_bwd_kernel", "what": "fused towers fwd/bwd + dot/BCE"},
+        "t2t3": {"alg_bytes": None, "kernel": "tower_wgrad + tower_update", "what": "tower weight grads + Adam (side stream)"},
     }
     for name, k in kern.items():
         if name in timed:
             k["ms"] = round(timed[name], 5)
-            if k["bytes"]:
-                k["GB/s"] = round(k["bytes"] / timed[name] / 1e6, 1)
+            if k["alg_bytes"]:
+                k["alg_GB/s"] = round(k["alg_bytes"] / timed[name] / 1e6, 1)
+                k["design_GB/s"] = round(k["design_bytes"] / timed[name] / 1e6, 1)
     emb_bytes = nnz * (16 + 4 * D) + FB * (4 + 8 * D) + uniq * (8 * D + 8)
     emb_ms = sum(timed.get(n, 0.0) for n in ("fwd", "prep", "upd"))
     dom = max(("fwd", "upd"), key=lambda n: timed.get(n, 0.0))
     traffic, src = pmc_traffic(kern[dom]["kernel"].split()[0],
                                args.workload if args.ids == "uniform" else f"{args.workload}_{args.ids}")
-    ach = kern[dom].get("GB/s")
+    ach = kern[dom].get("alg_GB/s")
     roofline = {"bound": "hbm", "kernel": kern[dom]["kernel"], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic, "traffic_source": src,
-                "bytes_per_launch": kern[dom]["bytes"], "ms_per_launch": kern[dom].get("ms"),
+                "alg_bytes_per_launch": kern[dom]["alg_bytes"], "design_bytes_per_launch": kern[dom]["design_bytes"],
+                "ms_per_launch": kern[dom].get("ms"),
                 "timing": "HIP events around each launch on its stream over eager steps of the same sequence",
                 "kernels": kern, "lookups": nnz, "unique_rows": uniq,
                 "embedding_path": {"bytes_per_step": emb_bytes, "ms": round(emb_ms, 5),
                                    "GB/s": round(emb_bytes / emb_ms / 1e6, 1) if emb_ms else None,
                                    "frac": round(emb_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4) if emb_ms else None,
+                                   "GB/s_over_step": round(emb_bytes / ms / 1e6, 1),
+                                   "frac_over_step": round(emb_bytes / ms / 1e6 / HBM_PEAK_GBS, 4),
                                    "note": "SURVEY 8(d) bytes over the summed time of the three embedding "
-                                           "launches (fwd, prepare, fused Adagrad)"}}
+                                           "launches (fwd, prepare, fused Adagrad), and over the step"}}
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen)
@@ -316,28 +401,35 @@ def run_multihot(args):
 
 
 def cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen):
-    """The oracle train_step on multi-hot bags of the same shape (tables scaled to --cpu-rows)."""
+    """The oracle train_step on multi-hot bags of the same shape (full tables when RAM allows)."""
     from oracle import ref
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
-    rows = min(args.cpu_rows, num_users), min(args.cpu_rows, num_items)
-    st = ref.init_state(list(rows), [D, D], [0, 1], [0], [1], layers, seed=0)
+    rows, how = cpu_rows(args, num_users, num_items, D)
+    st = ref.init_state([1, 1], [D, D], [0, 1], [0], [1], layers, seed=0)
+    st.tables = cpu_tables(rows, D, threads)
+    st.states = [torch.zeros(n) for n in rows]
     bs = synth_kjt_batches(rows[0], rows[1], B, maxlen, 2, torch.device("cpu"), "uniform", seed=0)
     ref.train_step(st, bs[0][0], bs[0][1], B, bs[0][2], 0.01, 0.01)
-    n = min(args.cpu_steps, 5)
     t0 = time.perf_counter()
-    for i in range(n):
-        v, o, lab = bs[i % 2]
+    n = 0
+    while n < args.cpu_steps or time.perf_counter() - t0 < args.cpu_seconds:
+        v, o, lab = bs[n % 2]
         ref.train_step(st, v, o, B, lab, 0.01, 0.01)
+        n += 1
     dt = time.perf_counter() - t0
     return {"value": round(n * B / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} steps of the oracle train_step on multi-hot bags (lengths U{{1..{maxlen}}}) at B={B}, "
-                      f"D={D}, towers {layers}, tables scaled to {rows[0]}x{D} / {rows[1]}x{D}; host CPU "
-                      f"{platform.processor() or platform.machine()}"}
+            "sample": f"{n} steps ({dt:.1f} s) of the oracle train_step on multi-hot bags (lengths U{{1..{maxlen}}}) "
+                      f"at B={B}, D={D}, towers {layers}, {how} ({rows[0]}x{D} / {rows[1]}x{D}); {threads} threads; "
+                      f"host CPU {cpu_model()}"}
 
 
-def roofline_report(kern, timed, nnz, uniq, step, B, workload="northstar"):
+def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northstar"):
+    """``roofline`` of the dominant launch (T1): achieved = its SURVEY 8(d) bytes / its average
+    device time; ``traffic`` = its HBM bytes per launch from the committed PMC summary; per-launch
+    design bytes, flops and MFMA fractions beside it; the whole embedding path (8(d) bytes per step)
+    over the step time and over the time of the two launches that carry it."""
     emb_path_bytes = kern.pop("_emb_path_bytes")
     out = {}
     for name, k in kern.items():
@@ -346,28 +438,34 @@ def roofline_report(kern, timed, nnz, uniq, step, B, workload="northstar"):
         e["kernel"] = KERNEL_NAMES[name]
         if ms:
             e["ms"] = round(ms, 5)
-            e["GB/s"] = round(k["bytes"] / ms / 1e6, 1)
+            e["alg_GB/s"] = round(k["alg_bytes"] / ms / 1e6, 1)
+            e["design_GB/s"] = round(k["design_bytes"] / ms / 1e6, 1)
             if k["flop"]:
                 e["TFLOP/s"] = round(k["flop"] / ms / 1e9, 1)
                 e["frac_of_bf16_peak"] = round(k["flop"] / ms / 1e9 / MFMA_BF16_PEAK_TFS, 4)
+        t, src = pmc_traffic(KERNEL_NAMES[name], workload)
+        e["pmc_hbm_bytes"], e["pmc_source"] = t, src
         out[name] = e
+    path = {"bytes_per_step": emb_path_bytes,
+            "GB/s_over_step": round(emb_path_bytes / ms_step / 1e6, 1),
+            "frac_over_step": round(emb_path_bytes / ms_step / 1e6 / HBM_PEAK_GBS, 4)}
     if not timed:
         return {"bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq}
-    dom = max((n for n in out if "ms" in out[n]), key=lambda n: out[n]["ms"])
-    traffic, src = pmc_traffic(KERNEL_NAMES[dom], workload)
+                "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq, "embedding_path": path}
+    dom = "t1"  # the longest launch, and the one that carries the forward's row reads
     emb_ms = timed.get("t1", 0.0) + timed.get("k3", 0.0)
-    ach = out[dom]["GB/s"]
+    ach = out[dom]["alg_GB/s"]
+    path.update({"ms_t1_k3": round(emb_ms, 5), "GB/s_over_t1_k3": round(emb_path_bytes / emb_ms / 1e6, 1),
+                 "frac_over_t1_k3": round(emb_path_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4),
+                 "note": "SURVEY 8(d) bytes per step: over the whole step, and over T1 + K3 (the launches that "
+                         "carry the embedding work; both also run tower work)"})
     return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-            "bytes_per_launch": out[dom]["bytes"], "ms_per_launch": out[dom]["ms"],
-            "timing": "HIP events around each launch on its stream over K eager steps of the same sequence",
-            "kernels": out, "lookups": nnz, "unique_rows": uniq,
-            "embedding_path": {"bytes_per_step": emb_path_bytes, "ms": round(emb_ms, 5),
-                               "GB/s": round(emb_path_bytes / emb_ms / 1e6, 1) if emb_ms else None,
-                               "frac": round(emb_path_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4) if emb_ms else None,
-                               "note": "SURVEY 8(d) bytes over the in-step time of the launches that carry the "
-                                       "embedding work (T1 gather+insert, K3 Adagrad); both also run tower work"}}
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": out[dom]["pmc_hbm_bytes"],
+            "traffic_source": out[dom]["pmc_source"], "alg_bytes_per_launch": out[dom]["alg_bytes"],
+            "alg_bytes_rule": "SURVEY 8(d) share of T1 per kept lookup: 8 B id + 4D row; per bag: 4 B length + "
+                              "4D pooled row (T1 keeps the pooled rows on chip and writes dX, the same bytes)",
+            "design_bytes_per_launch": out[dom]["design_bytes"], "ms_per_launch": out[dom]["ms"],
+            "kernels": out, "lookups": nnz, "unique_rows": uniq, "embedding_path": path}
 
 
 def run_single(args):
@@ -378,8 +476,9 @@ def run_single(args):
     torch.cuda.set_device(dev)
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
-    batches = synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1)
-    # HIP graphs over the 8 resident batches, k full steps per graph (no input copies): a graph
+    nb = max(args.steps_per_graph, args.batches // args.steps_per_graph * args.steps_per_graph)
+    batches = synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1)
+    # HIP graphs over the resident batches, k full steps per graph (no input copies): a graph
     # launch costs the host ~35-55 us, more than a step's GPU time, so k > 1 keeps the GPU fed
     # (graphs of k steps, plus single-step graphs for a remainder, so exactly K steps are timed)
     k = args.steps_per_graph
@@ -446,7 +545,7 @@ def run_single(args):
         timed = {n: v * ms / tot for n, v in raw.items()}
         timing_how += ("; each span scaled by (step time without event nodes) / (sum of the spans) = "
                        f"{ms / tot:.3f}")
-    roofline = roofline_report(kern, timed, nnz, uniq, step, B,
+    roofline = roofline_report(kern, timed, nnz, uniq, step, B, ms,
                                args.workload if args.ids == "uniform" else f"{args.workload}_{args.ids}")
     roofline["timing"] = timing_how
     roofline["event_span_ms"] = {n: round(v, 5) for n, v in raw.items()}
@@ -457,30 +556,36 @@ def run_single(args):
 
 
 def run_multi(args, world, rank, local_rank):
-    """N >= 1 ranks, one per GPU: the sharded single-hot step (row-wise shards of both tables,
-    id-level all-to-alls over RCCL, data-parallel towers), replayed as HIP graphs with the
-    collectives inside (eager launches if capture is refused)."""
-    from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, TorchComm
+    """N >= 1 ranks, one per GPU: the pipelined sharded single-hot step (row-wise shards of both
+    tables; per step one all-to-all of [gradient rows | tower gradient | next batch's ids] and one of
+    the next batch's rows, over RCCL; data-parallel towers), replayed as HIP graphs with the
+    collectives inside (eager launches if capture is refused). Segment capacities are sized from the
+    resident batches (max over batches and ranks), so no timed step can overflow; the sticky
+    overflow / bad-key flags are all-reduced and checked before and after the timed region."""
+    from two_tower_recommender_model_amd.sharded import (FusedShardedTwoTowerStep, TorchComm, default_capacity,
+                                                         segment_counts)
 
     num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    N = [num_users, num_items]
     dev = torch.device("cuda", local_rank)
     comm = TorchComm(always_collective=True)
-    step = FusedShardedTwoTowerStep(comm, [num_users, num_items], D, layers, B, dev, lr_emb=0.01, lr_dense=0.01,
-                                    seed=0, overlap_comm=args.overlap_comm)
-    batches = synth_batches(num_users, num_items, B, 8, dev, args.ids, seed=1 + rank)
+    k = args.steps_per_graph
+    nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k
+    batches = synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1 + rank)
+    blocks = [-(-n // world) for n in N]
+    need = torch.zeros(1, dtype=torch.int64)
+    for cols, _ in batches:
+        need = torch.maximum(need, segment_counts(cols, N, blocks, [0, 0], world).max().reshape(1))
+    need = need.to(dev)
+    dist.all_reduce(need, op=dist.ReduceOp.MAX)
+    cap = max(default_capacity(B, world), -(-int(need) // 8) * 8)
+    step = FusedShardedTwoTowerStep(comm, N, D, layers, B, dev, lr_emb=0.01, lr_dense=0.01, seed=0, capacity=cap)
     step.load_batch(*batches[0])
     step.step()  # creates the RCCL communicators before any capture
-    torch.cuda.synchronize()
-    time.sleep(0.5)  # let the process group's watchdog retire the eager collectives before capture
-    k = args.steps_per_graph
     mode = "hipgraph"
     ok = torch.ones(1, device=dev)
-    big = small = None
     try:
         step.capture_pool(batches, steps_per_graph=k)
-        big = step.pool_graphs
-        step.capture_pool(batches, steps_per_graph=1)
-        small = step.pool_graphs
     except Exception as e:  # noqa: BLE001 - fall back to eager launches, same work per step
         print(f"rank {rank}: graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
         ok.zero_()
@@ -488,26 +593,19 @@ def run_multi(args, world, rank, local_rank):
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
     if float(ok) < 1:
         mode = "eager"
-        big = small = None
         step.release_graphs()
+        step.cursor = None
         dist.barrier()
 
-    def run(n, i=0):
+    def run(n):
         if mode == "eager":
-            for j in range(n):
-                cols, lab = batches[(i + j) % len(batches)]
-                step.cols, step.labels = cols, lab
-                step.step()
-            return
-        while n >= k:
-            big[(i // k) % len(big)].replay()
-            i, n = i + k, n - k
-        while n > 0:
-            small[i % len(small)].replay()
-            i, n = i + 1, n - 1
+            step.run_eager(batches, n)
+        else:
+            step.run(n)
 
     run(args.warmup)
     torch.cuda.synchronize()
+    step.check()  # all ranks: a segment over capacity would invalidate the timed steps
     dist.barrier()
     t0 = time.perf_counter()
     run(args.steps)
@@ -516,12 +614,14 @@ def run_multi(args, world, rank, local_rank):
     dt = torch.tensor([time.perf_counter() - t0], device=dev)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt)
-    step.check()  # a segment over capacity would have invalidated the run
+    step.check()
     loss = float(step.loss)
-    big = small = None
     step.release_graphs()  # before the process group is destroyed
-    info = {"capacity": step.C, "exchange_bytes_per_step": (2 + 4) * step.nslots * D + 8 * step.send.numel(),  # bf16 rows, fp32 grads
-            "mode": mode}
+    r = step.rank
+    info = {"capacity": cap, "capacity_needed": int(need), "resident_batches": nb,
+            "exchange_A_bytes_sent": 4 * step.A_total,
+            "exchange_B_bytes_sent": 2 * D * world * step.S[r],
+            "collectives_per_step": 2, "mode": mode}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info
 
 
@@ -556,9 +656,9 @@ def main():
                                     device_id=torch.device("cuda", local_rank))
         value, ms, loss, sharded_info = run_multi(args, world, rank, local_rank)
         roofline, cpu, steps_run = None, None, args.steps
-        config["parallelism"] = (f"row-wise sharded tables (id all-to-all over RCCL) + data-parallel towers x{world}, "
-                                 f"{sharded_info['mode']}, collectives "
-                                 f"{'overlapped (RCCL stream)' if args.overlap_comm else 'in-stream'}")
+        config["parallelism"] = (f"row-wise sharded tables + data-parallel towers x{world}: pipelined, 2 RCCL "
+                                 f"all-to-alls per step ([grad rows | tower grad | next ids], next rows), "
+                                 f"{sharded_info['mode']}")
         config["sharded"] = sharded_info
     if rank == 0:
         out = {"metric": f"training pairs/sec at batch {B} (per GPU)", "value": round(value, 1), "unit": "pairs/s",

@@ -402,6 +402,62 @@ int tt_shard_gather_rows_bf16(const float* weights, const tt_table_meta_t* table
                               int64_t seg_capacity, const int64_t* recv, void* rows_out, int32_t* bad, void* dedup_ws,
                               size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 
+/* ---- a10 (single-hot), pipelined: TWO collectives per step ------------------------------------
+ * Exchange A (requester -> owner, one all-to-all with fixed per-destination sizes) carries, in the
+ * block for destination d: [gradient rows of step i: S_d x D fp32 | tower gradient of step i: P fp32
+ * (padded to a multiple of D) | counts: F int64 | keys of step i+1: S_d int64 | pad], S_d = sum over f
+ * of the capacity of segment (d, f). Exchange B (owner -> requester) returns the rows (bf16) of the
+ * received keys. Replaces ShardedEmbeddingBagCollection's input_dist (KJT all-to-all), output_dist
+ * (pooled all-to-all / reduce-scatter) and their adjoints, and DDP's all-reduce of the towers'
+ * gradients (03_model_training.py:812-815): the next batch's ids travel with this batch's gradients.
+ * Segment (d, f) = the lookups of feature f owned by rank d, ascending bag order. */
+typedef struct {
+  int64_t cap;        /* slots of segment (d, f); 0 when rank d holds no rows of feature f */
+  int64_t key_index;  /* int64 index (send buffer viewed as int64) of slot 0's key */
+  int64_t cnt_index;  /* int64 index of the segment's count */
+  int32_t pos_in;     /* row of slot 0 in the requester's returned-rows buffer (exchange B output) */
+  int32_t pos_out;    /* row (units of D floats) of slot 0's gradient row in the send buffer */
+} tt_shard_seg_t;
+
+/* requester: every kept lookup (id 0 dropped, row = id mod N, 03_model_training.py:356-365) of
+ * feature f owned by d (row-wise: (row / block_sizes[f]); table-wise: owners[f]) takes slot k of
+ * segment (d, f): send[key_index + k] = f << 40 | local row, send[cnt_index] = count (<= cap),
+ * pos_in[f * B + b] = pos_in + k, pos_out[f * B + b] = pos_out + k (both -1 for id 0). segs: DEVICE
+ * array [W][F]. A segment over capacity sets *overflow (sticky; the step's results are invalid). */
+int tt_shard_route_segs(int F, int64_t B, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
+                        const int64_t* block_sizes, const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                        int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* workspace,
+                        size_t ws_bytes, void* stream);
+/* owner: source s's block of the received buffer starts at recv + s * block_i64 (int64 units), its
+ * counts at + counts_i64, feature f's keys at + counts_i64 + F + seg_off[f] (seg_off: host [F],
+ * ascending, slots = S). Slot j of source s: rows_out[s * S + j] = the local row (bf16, round to
+ * nearest even) and, with dedup_ws, lookup s * S + j inserted for tt_dedup_rowwise_adagrad (one
+ * pseudo-feature per source: B = S, out_row = the row of source s's gradient block). Tables: one
+ * per feature (table f = feature f), one dim. A key outside the shard sets *bad (sticky). */
+int tt_shard_gather_segs_bf16(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                              const int64_t* recv, int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
+                              int64_t slots, void* rows_out, int32_t* bad, void* dedup_ws, size_t dedup_ws_bytes,
+                              int64_t dedup_max_lookups, void* stream);
+/* T1 of the pipelined sharded step: tt_tower_fwd_bwd_indexed_bf16 with the dX row of (tower t,
+ * bag m) written at row pos_out[t][m] (units of in_dim floats) of grad_rows_out[t] — the gradient
+ * region of exchange A's send buffer — instead of at its input row. */
+int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
+                                   const int32_t* const* pos_out, const void* const* rows_in,
+                                   float* const* grad_rows_out, const float* params, const void* labels,
+                                   int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
+                                   void* stream);
+/* T3 without Adam: the reduced tower gradient, times `scale`, written at base + offsets[q] for
+ * q < copies <= 16 (offsets: host array, floats) — the tower region of every destination block of
+ * exchange A: DDP's mean all-reduce becomes a fixed-order sum on the receivers. */
+int tt_tower_grads_replicated(const tt_tower_shape_t* shape, int64_t B, float* params, float* base, int copies,
+                              const int64_t* offsets, float scale, void* workspace, size_t ws_bytes, void* stream);
+/* T3 with Adam on the gradient sum_{s < nsrc} grads[s * src_stride + i] (ascending s: identical on
+ * every rank) + the bf16 weight copies. */
+int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
+                            int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2,
+                            float eps, float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes,
+                            void* stream);
+
 /* T3 with the gradient taken from `grads` (data-parallel towers: the all-reduced gradient) instead
  * of T2's partials: Adam + the bf16 weight copies. */
 int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,

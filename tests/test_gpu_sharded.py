@@ -107,9 +107,18 @@ def test_sharded_w1_equals_fused_single_gpu_step(device):
 @pytest.mark.parametrize("W,sharding", [(2, ("row_wise", "row_wise")), (3, ("table_wise", "row_wise")),
                                         (4, ("row_wise", "table_wise")), (8, ("row_wise", "row_wise"))])
 def test_sharded_threads_vs_oracle(device, W, sharding):
+    """W ranks as threads: (a) the rows each rank's towers read are the oracle tables' rows; (b) each
+    rank's gradient rows dX and its tower gradient (sent x 1/W) match the fp64 emulation of the bf16
+    towers on ITS OWN batch and mean loss (the loss scale TorchRec's sharded EBC gives: the sum over
+    ranks of the per-rank mean-loss gradients); (c) every shard equals the oracle's row-wise Adagrad
+    over the union of the kernels' gradient rows (ascending (rank, bag) order); (d) the towers equal
+    the oracle's Adam fed the fixed-order sum of the ranks' tower gradients x 1/W (DDP's mean
+    all-reduce) and are identical on every rank."""
+    from tower_emul import emulate, rel_err, split_params
+
     from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, ThreadComm
 
-    B, D, N, lr = 1024, 64, [9_000, 12_345], 0.02
+    B, D, N, lr, layers = 1024, 64, [9_000, 12_345], 0.02, [128, 64]
     gen = torch.Generator().manual_seed(W)
     full = [torch.empty(n, D).uniform_(-0.05, 0.05, generator=gen) for n in N]
     states = [torch.zeros(n) for n in N]
@@ -118,12 +127,15 @@ def test_sharded_threads_vs_oracle(device, W, sharding):
 
     def build(r):
         torch.cuda.set_device(device)
-        steps[r] = FusedShardedTwoTowerStep(comms[r], N, D, [128, 64], B, device, sharding=sharding,
+        steps[r] = FusedShardedTwoTowerStep(comms[r], N, D, layers, B, device, sharding=sharding,
                                             tw_owners=[W - 1, 0], full_tables=full, lr_emb=lr, seed=3)
 
     _run_ranks([lambda r=r: build(r) for r in range(W)])
+    P = steps[0].towers.num_params
+    m_ref, v_ref = [torch.zeros(P)], [torch.zeros(P)]
     for s in range(3):
         batches = []
+        params0 = steps[0].params.cpu().clone()
         for r in range(W):
             cols = [torch.randint(0, 2 * n, (B,), generator=gen) for n in N]
             cols[0][torch.rand(B, generator=gen) < 0.05] = 0
@@ -139,29 +151,42 @@ def test_sharded_threads_vs_oracle(device, W, sharding):
             torch.cuda.synchronize()
 
         _run_ranks([lambda r=r: run(r) for r in range(W)])
-        # (a) every rank's tower inputs are the oracle rows (pre-update)
+        _run_ranks([lambda r=r: steps[r].check() for r in range(W)])
         rows_all, grads_all = [[] for _ in N], [[] for _ in N]
+        tower_sum = torch.zeros(P)
         for r in range(W):
             st = steps[r]
-            st.check()
-            pos = st.pos.cpu().numpy()
-            rin = st.rows_in.cpu()
-            gout = st.grad_out.cpu()
-            cols, _ = batches[r]
+            cols, lab = batches[r]
+            rin = st.rows_for(0).cpu()     # [F*B, D] bf16 rows T1 read
+            gout = st.grad_rows(0).cpu()   # [F*B, D] the dX rows it sent
+            pos = st.pos_in[0].cpu().numpy()
             for f in range(2):
-                p = pos[f * B:(f + 1) * B]
-                kept = p >= 0
-                ids = np.mod(cols[f].numpy()[kept], N[f])
+                kept = pos[f * B:(f + 1) * B] >= 0
                 assert np.array_equal(kept, cols[f].numpy() != 0)
-                got = rin[torch.from_numpy(p[kept]).long()]  # bf16 rows (the all-to-all carries bf16)
+                ids = np.mod(cols[f].numpy()[kept], N[f])
+                got = rin[f * B:(f + 1) * B][torch.from_numpy(kept)]
                 want = full[f][torch.from_numpy(ids)].to(torch.bfloat16)
-                if s == 0:  # initial tables: bit for bit (after the same bf16 rounding)
+                # (a) initial tables: bit for bit (after the same bf16 rounding); updated rows: the
+                # row-wise mean of G^2 is reduced in another order -> one bf16 ulp
+                if s == 0:
                     assert torch.equal(got, want), (r, f)
-                else:  # updated rows: the row-wise mean of G^2 is reduced in another order -> one bf16 ulp
+                else:
                     np.testing.assert_allclose(got.float().numpy(), want.float().numpy(), rtol=1e-2, atol=1e-7)
                 rows_all[f].append(torch.from_numpy(ids))
-                grads_all[f].append(gout[torch.from_numpy(p[kept]).long()])
-        # (b) oracle update from the union of the gradient rows, rank-major
+                grads_all[f].append(gout[f * B:(f + 1) * B][torch.from_numpy(kept)])
+            # (b) this rank's dX and tower gradient vs the emulation on its own batch
+            x = rin.float()
+            _, _, dxs, gw = emulate(x[:B], x[B:], split_params(params0, [D, D], layers), layers, lab)
+            for f in range(2):
+                assert rel_err(gout[f * B:(f + 1) * B], dxs[f] * (cols[f] != 0).double()[:, None]) < 2e-3
+            sent = st.tower_grad_sent().cpu()
+            o = 0
+            for want in gw:
+                n = want.numel()
+                assert rel_err(sent[o:o + n] * W, want.reshape(-1)) < 2e-3
+                o += n
+            tower_sum += sent  # fixed rank order, as the receivers sum
+        # (c) oracle update from the union of the gradient rows, rank-major
         for f in range(2):
             ref.rowwise_adagrad_from_lookups(full[f], states[f], torch.cat(rows_all[f]), torch.cat(grads_all[f]),
                                              lr, 1e-10)
@@ -174,12 +199,65 @@ def test_sharded_threads_vs_oracle(device, W, sharding):
                                            rtol=1e-5, atol=1e-7)
                 np.testing.assert_allclose(st.tables.state_view(f)[:n].cpu().numpy(), states[f][lo:lo + n].numpy(),
                                            rtol=1e-5, atol=1e-10)
-        # (c) data-parallel towers identical everywhere
+        # (d) Adam on the summed (mean) tower gradient; identical replicas
+        p_ref = [params0.clone()]
+        ref.adam(p_ref, [tower_sum], m_ref, v_ref, s + 1, 0.01)
+        np.testing.assert_allclose(steps[0].params.cpu().numpy(), p_ref[0].numpy(), rtol=1e-5, atol=1e-7)
         for r in range(1, W):
             assert torch.equal(steps[r].params, steps[0].params)
     # every row held exactly once
     for f in range(2):
         assert sum(steps[r].local_rows[f] for r in range(W)) == N[f]
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_sharded_pipelined_equals_synchronous(device, W):
+    """The pipelined schedule (two exchanges per step: the next batch's ids travel with this batch's
+    gradients) gives bit for bit the results of the synchronous step, over a cyclic batch pool."""
+    from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, ThreadComm
+
+    B, D, N = 512, 128, [7_000, 11_000]
+    gen = torch.Generator().manual_seed(40 + W)
+    full = [torch.empty(n, D).uniform_(-0.05, 0.05, generator=gen) for n in N]
+    pools = []
+    for r in range(W):
+        pool = []
+        for _ in range(4):
+            cols = [torch.randint(0, 2 * n, (B,), generator=gen).to(device) for n in N]
+            cols[1][:20] = 77  # a hot row
+            pool.append((cols, torch.randint(0, 2, (B,), generator=gen).to(torch.int32).to(device)))
+        pools.append(pool)
+    runs = {}
+    for mode in ("sync", "pipe"):
+        comms = ThreadComm.group(W)
+        steps = [None] * W
+
+        def build(r):
+            torch.cuda.set_device(device)
+            steps[r] = FusedShardedTwoTowerStep(comms[r], N, D, [128, 64], B, device, full_tables=full, seed=8,
+                                                sharding=("row_wise", "table_wise"), tw_owners=[0, W - 1])
+
+        _run_ranks([lambda r=r: build(r) for r in range(W)])
+
+        def go(r):
+            torch.cuda.set_device(device)
+            st = steps[r]
+            if mode == "sync":
+                for i in range(6):
+                    st.load_batch(*pools[r][i % 4])
+                    st.step()
+            else:
+                st.run_eager(pools[r], 6)
+            torch.cuda.synchronize()
+
+        _run_ranks([lambda r=r: go(r) for r in range(W)])
+        runs[mode] = steps
+    for r in range(W):
+        a, b = runs["sync"][r], runs["pipe"][r]
+        assert torch.equal(a.tables.weights, b.tables.weights)
+        assert torch.equal(a.tables.state, b.tables.state)
+        assert torch.equal(a.params, b.params) and torch.equal(a.exp_avg_sq, b.exp_avg_sq)
+        assert float(a.loss) == float(b.loss)
 
 
 def test_sharded_overflow_raises(device):
@@ -195,27 +273,99 @@ def test_sharded_overflow_raises(device):
 
     _run_ranks([lambda r=r: build(r) for r in range(W)])
     for r in range(W):
-        steps[r].load_batch([torch.full((B,), 7, device=device), torch.full((B,), 9, device=device)],
+        # rank 0 overflows (every id owned by rank 0), rank 1 does not: both must raise
+        ids = 7 if r == 0 else 999
+        steps[r].load_batch([torch.full((B,), ids, device=device), torch.full((B,), ids, device=device)],
                             torch.zeros(B, dtype=torch.int32, device=device))
     _run_ranks([lambda r=r: steps[r].step() for r in range(W)])
     torch.cuda.synchronize()
-    with pytest.raises(_lib.TTError, match="capacity"):
-        steps[0].check()
+    raised = [False] * W
+
+    def chk(r):
+        try:
+            steps[r].check()
+        except _lib.TTError as e:
+            assert "capacity" in str(e)
+            raised[r] = True
+
+    _run_ranks([lambda r=r: chk(r) for r in range(W)])
+    assert all(raised)
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_sharded_rccl_world1_graph_equals_eager(device, overlap):
+def test_sharded_optimizer_state_resume(device):
+    """gathered_state_dict(optimizer=True) + load_state_dict resumes bit-exactly (tables, row-wise
+    Adagrad state, towers and their Adam moments / step), also across a different rank count."""
+    from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, ThreadComm
+
+    B, D, N = 256, 64, [3_000, 5_000]
+    gen = torch.Generator().manual_seed(5)
+    batches = [([torch.randint(0, 2 * n, (B,), generator=gen).to(device) for n in N],
+                torch.randint(0, 2, (B,), generator=gen).to(torch.int32).to(device)) for _ in range(4)]
+
+    def make(W, seed):
+        comms = ThreadComm.group(W)
+        steps = [None] * W
+
+        def build(r):
+            torch.cuda.set_device(device)
+            steps[r] = FusedShardedTwoTowerStep(comms[r], N, D, [128, 64], B, device, seed=seed)
+
+        _run_ranks([lambda r=r: build(r) for r in range(W)])
+        return steps
+
+    def train(steps, bs):
+        def go(r):
+            torch.cuda.set_device(device)
+            for cols, lab in bs:
+                steps[r].load_batch(cols, lab)  # every rank the same batch (the check is resume only)
+                steps[r].step()
+            torch.cuda.synchronize()
+
+        _run_ranks([lambda r=r: go(r) for r in range(len(steps))])
+
+    def gathered(steps):
+        out = {}
+
+        def g(r):
+            out[r] = steps[r].gathered_state_dict(optimizer=True)
+
+        _run_ranks([lambda r=r: g(r) for r in range(len(steps))])
+        return out[0]
+
+    # 1 rank: 4 steps straight vs 2 steps, save, load into a fresh 1-rank step, 2 more
+    a = make(1, 1)
+    train(a, batches)
+    b = make(1, 1)
+    train(b, batches[:2])
+    sd = gathered(b)
+    c = make(1, 9)
+    c[0].load_state_dict(sd)
+    train(c, batches[2:])
+    assert torch.equal(a[0].tables.weights, c[0].tables.weights)
+    assert torch.equal(a[0].tables.state, c[0].tables.state)
+    assert torch.equal(a[0].params, c[0].params) and torch.equal(a[0].exp_avg, c[0].exp_avg)
+    # the state dict re-shards: 2 ranks take their rows of tables and Adagrad state
+    d = make(2, 9)
+    _run_ranks([lambda r=r: d[r].load_state_dict(sd) for r in range(2)])
+    for r in range(2):
+        for f, name in enumerate(("user_id", "product_id")):
+            lo, n = d[r].spans(f)[r]
+            assert torch.equal(d[r].tables.state_view(f)[:n].cpu(),
+                               sd[f"optim.ebc.t_{name}.rowwise_adagrad_state"][lo:lo + n].cpu())
+        assert int(d[r].adam_state[0]) == 2
+
+
+def test_sharded_rccl_world1_graph_equals_eager(device):
     """The production comm (torch.distributed "nccl" = RCCL) with its collectives captured into
-    HIP graphs, at world size 1 with the collectives forced on: identical to eager ThreadComm. Run
-    in a child process (a process group and RCCL-in-graph state stay out of this test process).
-    overlap: the gradient all-to-all and tower all-reduce on RCCL's stream (overlap_comm=True)."""
+    pipelined HIP graphs, at world size 1 with the collectives forced on: identical to eager
+    synchronous steps over ThreadComm. Run in a child process (a process group and RCCL-in-graph
+    state stay out of this test process)."""
     import os
     import subprocess
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, os.path.join(here, "rccl_graph_check.py")] + (["--overlap"] if overlap else []),
-                       capture_output=True, text=True,
+    r = subprocess.run([sys.executable, os.path.join(here, "rccl_graph_check.py")], capture_output=True, text=True,
                        timeout=300, cwd=os.path.dirname(here))
     assert r.returncode == 0 and "RCCL-GRAPH-OK" in r.stdout, (r.returncode, r.stdout[-1500:], r.stderr[:3000],
                                                                r.stderr[-1500:])

@@ -37,6 +37,11 @@ class FeatureMeta(C.Structure):
     _fields_ = [("table", C.c_int32), ("out_offset", C.c_int32), ("out_row", C.c_int64)]
 
 
+class ShardSeg(C.Structure):
+    _fields_ = [("cap", C.c_int64), ("key_index", C.c_int64), ("cnt_index", C.c_int64), ("pos_in", C.c_int32),
+                ("pos_out", C.c_int32)]
+
+
 class TowerShape(C.Structure):
     _fields_ = [
         ("L", C.c_int32),
@@ -170,6 +175,23 @@ SIGNATURES = {
         _int,
         [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _int, _vp, _vp, _sz, _vp],
     ),
+    "tt_shard_route_segs": (
+        _int,
+        [_int, _i64, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
+    ),
+    "tt_shard_gather_segs_bf16": (
+        _int,
+        [_vp, _ptm, _int, _int, _int, _vp, _i64, _i64, _pi64, _i64, _vp, _vp, _vp, _sz, _i64, _vp],
+    ),
+    "tt_tower_fwd_bwd_indexed2_bf16": (
+        _int,
+        [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
+    ),
+    "tt_tower_grads_replicated": (_int, [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _vp]),
+    "tt_tower_adam_grads_sum": (
+        _int,
+        [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp],
+    ),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -210,6 +232,11 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_indexed_bf16",
     "tt_tower_adam_grads",
     "tt_tower_update_pre",
+    "tt_shard_route_segs",
+    "tt_shard_gather_segs_bf16",
+    "tt_tower_fwd_bwd_indexed2_bf16",
+    "tt_tower_grads_replicated",
+    "tt_tower_adam_grads_sum",
 ]
 
 _lib = None

@@ -49,6 +49,8 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_dedup_workspace_init, tt_dedup_insert_cols, tt_dedup_insert_segments, tt_dedup_rowwise_adagrad
 // tt_tower_fwd_bwd_indexed, tt_tower_wgrad_rowwise_adagrad, tt_shard_route_cols, tt_shard_gather_rows,
 // tt_tower_adam_grads, tt_tower_update_pre
-int tt_num_entry_points(void) { return 37; }
+// tt_shard_route_segs, tt_shard_gather_segs_bf16, tt_tower_fwd_bwd_indexed2_bf16, tt_tower_grads_replicated,
+// tt_tower_adam_grads_sum
+int tt_num_entry_points(void) { return 42; }
 
 }  // extern "C"

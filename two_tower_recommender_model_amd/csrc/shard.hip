@@ -48,6 +48,10 @@ struct RouteArgs {
   int32_t* overflow;  // sticky flag
   int64_t* dl;        // [F][B] workspace: owner << 48 | local row, -1 = dropped
   int32_t* cnt;       // [F][nblk][RT_MAXW] workspace: lookups per (block, owner)
+  // segment-table form (tt_shard_route_segs): per (owner d, feature f) capacity and addresses in
+  // the packed send buffer; pos_out (nullable) = the lookup's gradient row in that buffer
+  const tt_shard_seg_t* segs;
+  int32_t* pos_out;
 };
 
 // route pass 1 (thread per bag, coalesced): owner + local row of every lookup, and per-workgroup
@@ -86,7 +90,10 @@ __global__ void __launch_bounds__(RT_BLOCK) shard_route_count_kernel(RouteArgs a
 }
 
 // route pass 2: slot k = (lookups of the same owner in earlier workgroups) + (earlier waves) +
-// (earlier lanes): ascending bag order inside each (owner, feature) segment
+// (earlier lanes): ascending bag order inside each (owner, feature) segment. SEGS: per-(owner,
+// feature) capacities and addresses from the segment table (tt_shard_route_segs), else the
+// uniform layout of tt_shard_route_cols.
+template <bool SEGS>
 __global__ void __launch_bounds__(RT_BLOCK) shard_route_place_kernel(RouteArgs a) {
   __shared__ int base[RT_MAXW];
   __shared__ int wc[RT_BLOCK / 64][RT_MAXW];
@@ -103,8 +110,14 @@ __global__ void __launch_bounds__(RT_BLOCK) shard_route_place_kernel(RouteArgs a
     }
     base[threadIdx.x] = t;
     if (blk == 0) {  // the segment header: lookups kept for this (owner, feature)
-      if (all > a.C) atomicOr(a.overflow, 1);
-      a.send[(int64_t)threadIdx.x * seg_stride + f] = all < a.C ? all : a.C;
+      if (SEGS) {
+        const tt_shard_seg_t sg = a.segs[(int64_t)threadIdx.x * a.F + f];
+        if (all > sg.cap) atomicOr(a.overflow, 1);
+        a.send[sg.cnt_index] = all < sg.cap ? all : sg.cap;
+      } else {
+        if (all > a.C) atomicOr(a.overflow, 1);
+        a.send[(int64_t)threadIdx.x * seg_stride + f] = all < a.C ? all : a.C;
+      }
     }
   }
   const int64_t b = (int64_t)blk * RT_BLOCK + threadIdx.x;
@@ -119,19 +132,29 @@ __global__ void __launch_bounds__(RT_BLOCK) shard_route_place_kernel(RouteArgs a
   }
   __syncthreads();
   if (b >= a.B) return;
-  int32_t p = -1;
+  int32_t p = -1, po = -1;
   if (d >= 0) {
     int k = base[d] + rank;
     for (int v2 = 0; v2 < wid; ++v2) k += wc[v2][d];
-    if (k < a.C) {
-      a.send[(int64_t)d * seg_stride + a.F + (int64_t)f * a.C + k] =
-          (int64_t)(((uint64_t)f << DD_TABLE_SHIFT) | ((uint64_t)v & ((1ull << 48) - 1)));
+    const int64_t key = (int64_t)(((uint64_t)f << DD_TABLE_SHIFT) | ((uint64_t)v & ((1ull << 48) - 1)));
+    if (SEGS) {
+      const tt_shard_seg_t sg = a.segs[(int64_t)d * a.F + f];
+      if (k < sg.cap) {
+        a.send[sg.key_index + k] = key;
+        p = sg.pos_in + k;
+        po = sg.pos_out + k;
+      } else {
+        atomicOr(a.overflow, 1);
+      }
+    } else if (k < a.C) {
+      a.send[(int64_t)d * seg_stride + a.F + (int64_t)f * a.C + k] = key;
       p = (int32_t)(((int64_t)d * a.F + f) * a.C + k);
     } else {
       atomicOr(a.overflow, 1);
     }
   }
   a.pos[(int64_t)f * a.B + b] = p;
+  if (SEGS) a.pos_out[(int64_t)f * a.B + b] = po;
 }
 
 struct GatherArgs {
@@ -195,6 +218,70 @@ __global__ void __launch_bounds__(256) shard_gather_rows_kernel(GatherArgs a) {
   if (a.dd_on && hl == 0) dd_insert_finish(a.dd, pend, (int32_t)i);
 }
 
+
+// owner side of the pipelined exchange (tt_shard_gather_segs_bf16): the keys of source s sit in
+// source block s of the received buffer (int64 view: block s at s * blk64, counts at + cnt64, the
+// slots of feature f at + cnt64 + F + seg_off[f]); slot j of source s (j < S) -> rows_out[s * S + j]
+// (bf16) and, with the dedup on, lookup s * S + j
+struct GatherSegArgs {
+  const float* weights;
+  tt_table_meta_t tables[TT_MAX_TABLES];
+  int T;
+  int F;
+  int W;
+  int D;
+  int64_t S;
+  int64_t blk64, cnt64;
+  int64_t seg_off[TT_MAX_FEATURES + 1];
+  const int64_t* recv;
+  __bf16* rows_out;
+  DedupWs dd;
+  int dd_on;
+  int32_t* bad;
+};
+
+__global__ void __launch_bounds__(256) shard_gather_segs_kernel(GatherSegArgs a) {
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t n = (int64_t)a.W * a.S;
+  const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (i >= n) return;
+  const int64_t s = i / a.S, j = i - s * a.S;
+  int f = 0;
+  while (f + 1 < a.F && j >= a.seg_off[f + 1]) ++f;
+  const int64_t k = j - a.seg_off[f];
+  const int64_t* blk = a.recv + s * a.blk64 + a.cnt64;
+  const int64_t cnt = blk[f];
+  uint64_t key = DD_EMPTY;
+  const float* src = nullptr;
+  if (k < cnt) {
+    key = (uint64_t)blk[a.F + j];
+    const int t = (int)(key >> DD_TABLE_SHIFT);
+    const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
+    if (t == f && t < a.T && r < a.tables[t].num_rows && a.tables[t].dim == a.D) {
+      src = a.weights + a.tables[t].weight_offset + r * a.D;
+    } else {
+      key = DD_EMPTY;
+      if (hl == 0) atomicOr(a.bad, 1);
+    }
+  }
+  DdPend pend;
+  if (a.dd_on && hl == 0) dd_insert_begin(a.dd, key, (int32_t)i, pend);
+  if (src) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
+    __bf16* dst = a.rows_out + i * a.D;
+    for (int c = hl * 4; c < a.D; c += 128) {
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(src + c);
+      bf16x4v o;
+      o[0] = (__bf16)v[0];
+      o[1] = (__bf16)v[1];
+      o[2] = (__bf16)v[2];
+      o[3] = (__bf16)v[3];
+      *reinterpret_cast<bf16x4v*>(dst + c) = o;
+    }
+  }
+  if (a.dd_on && hl == 0) dd_insert_finish(a.dd, pend, (int32_t)i);
+}
+
 }  // namespace tt
 
 using namespace tt;
@@ -249,7 +336,7 @@ int tt_shard_route_cols(int F, int64_t B, const void* const* cols, int id_dtype,
   a.cnt = reinterpret_cast<int32_t*>(ws + align_up(sizeof(int64_t) * (size_t)F * (size_t)B, 256));
   const dim3 grid(a.nblk, F);
   shard_route_count_kernel<<<grid, dim3(RT_BLOCK), 0, as_stream(stream)>>>(a);
-  shard_route_place_kernel<<<grid, dim3(RT_BLOCK), 0, as_stream(stream)>>>(a);
+  shard_route_place_kernel<false><<<grid, dim3(RT_BLOCK), 0, as_stream(stream)>>>(a);
   return check_launch("shard_route");
 }
 
@@ -304,6 +391,101 @@ int tt_shard_gather_rows_bf16(const float* weights, const tt_table_meta_t* table
                               size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
   return gather_rows(weights, tables, T, F, W, seg_capacity, recv, reinterpret_cast<float*>(rows_out), bad, dedup_ws,
                      dedup_ws_bytes, dedup_max_lookups, stream, 1);
+}
+
+int tt_shard_route_segs(int F, int64_t B, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
+                        const int64_t* block_sizes, const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                        int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* workspace,
+                        size_t ws_bytes, void* stream) {
+  if (F < 1 || F > TT_MAX_FEATURES) return fail(TT_EINVAL, "shard_route_segs: feature count out of range");
+  if (W < 1 || W > RT_MAXW) return fail(TT_EINVAL, "shard_route_segs: 1..16 ranks supported");
+  if (B < 0) return fail(TT_EINVAL, "shard_route_segs: negative batch");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "shard_route_segs: ids must be int32/int64");
+  if (!cols || !num_embeddings || !block_sizes || !owners || !segs || !send || !pos_in || !pos_out || !overflow)
+    return fail(TT_EINVAL, "shard_route_segs: null pointer");
+  if (!workspace || ws_bytes < tt_shard_route_workspace_bytes(F, B))
+    return fail(TT_ECAPACITY, "shard_route_segs: workspace too small");
+  RouteArgs a{};
+  for (int f = 0; f < F; ++f) {
+    if (!cols[f] || num_embeddings[f] < 1) return fail(TT_EINVAL, "shard_route_segs: bad column");
+    if (block_sizes[f] < 0 || (block_sizes[f] == 0 && (owners[f] < 0 || owners[f] >= W)))
+      return fail(TT_EINVAL, "shard_route_segs: bad sharding of a feature");
+    if (block_sizes[f] > 0 && (num_embeddings[f] + block_sizes[f] - 1) / block_sizes[f] > W)
+      return fail(TT_EINVAL, "shard_route_segs: row blocks exceed the rank count");
+    if ((block_sizes[f] > 0 ? block_sizes[f] : num_embeddings[f]) >= (1ll << DD_TABLE_SHIFT))
+      return fail(TT_EINVAL, "shard_route_segs: local rows >= 2^40");
+    a.col[f] = cols[f];
+    a.num_emb[f] = num_embeddings[f];
+    a.block[f] = block_sizes[f];
+    a.owner[f] = owners[f];
+  }
+  if (B == 0) return TT_OK;
+  a.id_dtype = id_dtype;
+  a.F = F;
+  a.W = W;
+  a.B = B;
+  a.C = 1;
+  a.nblk = (int)ceil_div(B, RT_BLOCK);
+  a.send = send;
+  a.pos = pos_in;
+  a.pos_out = pos_out;
+  a.segs = segs;
+  a.overflow = overflow;
+  char* ws = reinterpret_cast<char*>(workspace);
+  a.dl = reinterpret_cast<int64_t*>(ws);
+  a.cnt = reinterpret_cast<int32_t*>(ws + align_up(sizeof(int64_t) * (size_t)F * (size_t)B, 256));
+  const dim3 grid(a.nblk, F);
+  shard_route_count_kernel<<<grid, dim3(RT_BLOCK), 0, as_stream(stream)>>>(a);
+  shard_route_place_kernel<true><<<grid, dim3(RT_BLOCK), 0, as_stream(stream)>>>(a);
+  return check_launch("shard_route_segs");
+}
+
+int tt_shard_gather_segs_bf16(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
+                              const int64_t* recv, int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
+                              int64_t slots, void* rows_out, int32_t* bad, void* dedup_ws, size_t dedup_ws_bytes,
+                              int64_t dedup_max_lookups, void* stream) {
+  if (T < 1 || T > TT_MAX_TABLES || F < 1 || F > TT_MAX_FEATURES || F > T || W < 1 || slots < 0)
+    return fail(TT_EINVAL, "shard_gather_segs: bad sizes");
+  if (!weights || !tables || !recv || !rows_out || !bad || !seg_off)
+    return fail(TT_EINVAL, "shard_gather_segs: null pointer");
+  GatherSegArgs a{};
+  a.D = tables[0].dim;
+  for (int t = 0; t < T; ++t) {
+    if (tables[t].dim != a.D) return fail(TT_EINVAL, "shard_gather_segs: tables must share one dim");
+    if (tables[t].weight_offset % 4) return fail(TT_EINVAL, "shard_gather_segs: rows must be 16-B aligned");
+    a.tables[t] = tables[t];
+  }
+  if (a.D % 4 || (reinterpret_cast<uintptr_t>(weights) & 15) || (reinterpret_cast<uintptr_t>(rows_out) & 7))
+    return fail(TT_EINVAL, "shard_gather_segs: D % 4 == 0 and aligned buffers required");
+  for (int f = 0; f <= F; ++f) {
+    a.seg_off[f] = f < F ? seg_off[f] : slots;
+    if (a.seg_off[f] < 0 || a.seg_off[f] > slots || (f && a.seg_off[f] < a.seg_off[f - 1]))
+      return fail(TT_EINVAL, "shard_gather_segs: segment offsets must ascend within [0, slots]");
+  }
+  if (block_i64 < counts_i64 + F + slots || counts_i64 < 0) return fail(TT_EINVAL, "shard_gather_segs: bad block layout");
+  const int64_t n = (int64_t)W * slots;
+  if (n > INT32_MAX) return fail(TT_EINVAL, "shard_gather_segs: too many slots");
+  a.weights = weights;
+  a.T = T;
+  a.F = F;
+  a.W = W;
+  a.S = slots;
+  a.blk64 = block_i64;
+  a.cnt64 = counts_i64;
+  a.recv = recv;
+  a.rows_out = reinterpret_cast<__bf16*>(rows_out);
+  a.bad = bad;
+  if (dedup_ws) {
+    if (dedup_max_lookups < n || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+        dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
+        (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
+      return fail(TT_ECAPACITY, "shard_gather_segs: dedup workspace too small / misaligned");
+    dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
+    a.dd_on = 1;
+  }
+  if (n == 0) return TT_OK;
+  shard_gather_segs_kernel<<<dim3((unsigned)ceil_div(n, 8)), dim3(256), 0, as_stream(stream)>>>(a);
+  return check_launch("shard_gather_segs");
 }
 
 }  // extern "C"

@@ -80,6 +80,8 @@ struct TowerArgs {
   const int32_t* gpos[2];
   const float* gsrc[2];  // fp32 rows, or bf16 rows when gsrc_bf16 (the same bf16 values T1 computes on)
   float* gdst[2];
+  const int32_t* gpos_out[2];  // nullable: dX row index in gdst (units of in_dim floats) when it differs
+                               // from the input row (the pipelined sharded step's packed send buffer)
   int gsrc_bf16;
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
@@ -493,8 +495,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   const bool indexed = a.gpos[t] != nullptr;
   const int incol = a.s.in_col[t];  // read once, before any store (no vmcnt waits mid-chain)
   int32_t rpos[4];                   // indexed: the source/destination row of each xv
+  int32_t opos[4];                   // indexed: the dX row of each xv (gpos_out, else rpos)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) rpos[i] = -1;
+  for (int i = 0; i < 4; ++i) rpos[i] = opos[i] = -1;
   if (gather || indexed) {
     // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros.
     // Indexed rows may be bf16 (tt_tower_fwd_bwd_indexed_bf16): byte offsets with the element size
@@ -511,6 +514,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         if (gm < B) {
           if (indexed) {
             rpos[i] = a.gpos[t][gm];
+            opos[i] = a.gpos_out[t] ? a.gpos_out[t][gm] : rpos[i];
             if (rpos[i] >= 0)
               src[i] = reinterpret_cast<const char*>(a.gsrc[t]) + ((int64_t)rpos[i] * in + c4) * (r16 ? 2 : 4);
           } else {
@@ -741,7 +745,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       float* dst = nullptr;
       if (gm < B) {
         if (indexed)
-          dst = rpos[i] >= 0 ? a.gdst[t] + (int64_t)rpos[i] * in + c4 : nullptr;
+          dst = opos[i] >= 0 ? a.gdst[t] + (int64_t)opos[i] * in + c4 : nullptr;
         else
           dst = a.gpooled + gm * a.ldp + incol + c4;
       }
@@ -1114,6 +1118,15 @@ struct UpdateArgs {
   const float* grads_in;  // nullable: take the gradient from here (data-parallel: all-reduced)
   const float* adam_pre;  // nullable: step size / sqrt(bias correction 2) precomputed by T2 (which
                           // also advanced step_state): no pow() and no arrival ticket here
+  // data-parallel towers without an all-reduce launch (pipelined sharded step): grads_out is
+  // written out_copies times (stride out_stride, scaled by out_scale: one copy per destination
+  // rank of the exchange), and grads_in is the fixed-order sum of in_srcs vectors (stride in_stride)
+  int out_copies;
+  int64_t out_stride;
+  int64_t out_off[16];  // with out_copies > 1: element offset of copy q (explicit, out_stride unused)
+  float out_scale;
+  int in_srcs;
+  int64_t in_stride;
 };
 
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
@@ -1138,6 +1151,7 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
     float g = 0.f;
     if (a.grads_in) {
       g = a.grads_in[i];
+      for (int q = 1; q < a.in_srcs; ++q) g += a.grads_in[(int64_t)q * a.in_stride + i];
     } else if (a.do_adam || a.grads_out) {
       if (a.seg_isw[sg]) {
 #pragma unroll 8
@@ -1145,7 +1159,14 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
       } else {
         g = a.slab[i];  // bias gradient, reduced over the T1 workgroups by T2's bias waves
       }
-      if (a.grads_out) a.grads_out[i] = g;
+      if (a.grads_out) {
+        if (a.out_copies <= 1) {
+          a.grads_out[i] = g;
+        } else {
+          const float gs = g * a.out_scale;
+          for (int q = 0; q < a.out_copies; ++q) a.grads_out[a.out_off[q] + i] = gs;
+        }
+      }
     }
     if (a.do_adam) {
       if (a.wd != 0.f) g = g + a.wd * p;
@@ -1606,7 +1627,8 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
                      float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
                      int do_adam, float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes,
                      void* stream, const float* adam_pre = nullptr, const DdUpdateArgs* dd = nullptr,
-                     int64_t dd_grid = 0) {
+                     int64_t dd_grid = 0, int out_copies = 1, const int64_t* out_off = nullptr,
+                     float out_scale = 1.f, int in_srcs = 1, int64_t in_stride = 0) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
@@ -1649,6 +1671,12 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
   a.grads_out = grads_out;
   a.grads_in = grads_in;
   a.adam_pre = adam_pre;
+  a.out_copies = out_copies;
+  if (out_copies > 16) return fail(TT_EINVAL, "tower: at most 16 gradient copies");
+  for (int q = 0; q < out_copies && out_off; ++q) a.out_off[q] = out_off[q];
+  a.out_scale = out_scale;
+  a.in_srcs = in_srcs;
+  a.in_stride = in_stride;
   const int64_t g3 = ceil_div(L.P, 256);
   if (dd) {
     if (dd_grid + g3 > INT32_MAX) return fail(TT_EINVAL, "tower_update_rowwise_adagrad: grid too large");
@@ -1705,6 +1733,56 @@ int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params,
   if (!grads) return fail(TT_EINVAL, "tower_adam_grads: null gradient");
   return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, 1,
                    nullptr, grads, workspace, ws_bytes, stream);
+}
+
+int tt_tower_grads_replicated(const tt_tower_shape_t* shape, int64_t B, float* params, float* base, int copies,
+                              const int64_t* offsets, float scale, void* workspace, size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!base || !offsets || copies < 1 || copies > 16) return fail(TT_EINVAL, "tower_grads_replicated: bad output");
+  for (int q = 0; q < copies; ++q)
+    if (offsets[q] < 0) return fail(TT_EINVAL, "tower_grads_replicated: negative offset");
+  int64_t off[16];
+  for (int q = 0; q < copies; ++q) off[q] = offsets[q];
+  if (copies == 1) off[1] = off[0];
+  // copies == 1 takes the multi-copy path too (scale applied): give it two identical copies
+  return launch_t3(shape, B, params, nullptr, nullptr, 0.f, 0.9f, 0.999f, 1e-8f, 0.f, nullptr, 0, base, nullptr,
+                   workspace, ws_bytes, stream, nullptr, nullptr, 0, copies == 1 ? 2 : copies, off, scale);
+}
+
+int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
+                            int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2,
+                            float eps, float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes,
+                            void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!grads || nsrc < 1 || (nsrc > 1 && src_stride < L.P)) return fail(TT_EINVAL, "tower_adam_grads_sum: bad gradient");
+  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, 1,
+                   nullptr, grads, workspace, ws_bytes, stream, nullptr, nullptr, 0, 1, 0, 1.f, nsrc, src_stride);
+}
+
+int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
+                                   const int32_t* const* pos_out, const void* const* rows_in,
+                                   float* const* grad_rows_out, const float* params, const void* labels,
+                                   int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+  if (!pos_in || !pos_out || !rows_in || !grad_rows_out) return fail(TT_EINVAL, "tower_indexed2: null pointer");
+  TowerArgs a{};
+  a.gsrc_bf16 = 1;
+  for (int t = 0; t < 2; ++t) {
+    if (!pos_in[t] || !pos_out[t] || !rows_in[t] || !grad_rows_out[t]) return fail(TT_EINVAL, "tower_indexed2: null pointer");
+    if ((reinterpret_cast<uintptr_t>(rows_in[t]) & 15) || (reinterpret_cast<uintptr_t>(grad_rows_out[t]) & 15))
+      return fail(TT_EINVAL, "tower_indexed2: rows not 16-B aligned");
+    a.gpos[t] = pos_in[t];
+    a.gpos_out[t] = pos_out[t];
+    a.gsrc[t] = reinterpret_cast<const float*>(rows_in[t]);
+    a.gdst[t] = grad_rows_out[t];
+  }
+  return launch_t1(shape, B, a, nullptr,
+                   std::max(shape->in_col[0] + shape->in_dim[0], shape->in_col[1] + shape->in_dim[1]), nullptr, params,
+                   labels, label_dtype, grad_scale, logits, workspace, ws_bytes, stream);
 }
 
 }  // extern "C"

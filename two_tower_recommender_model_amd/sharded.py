@@ -3,37 +3,42 @@
 Semantics = DistributedModelParallel(TwoTowerTrainTask) + TrainPipelineSparseDist.progress of the
 reference (03_model_training.py:798-829, :618): every table row-wise (block ceil(N/W)) or
 table-wise sharded over the ranks, the towers data-parallel (DDP: gradients averaged over ranks),
-each rank training on its own local batch of B pairs. Per step and rank:
+each rank training on its own local batch of B pairs.
 
-  route           ids -> owners: segment (owner d, feature f) of fixed capacity C, pos[f][b]
-                  (tt_shard_route_cols; transform_to_torchrec_batch's id % N and drop-0 inline)
-  all-to-all      ids out                                   [W][F + F*C] int64
-  gather          owner copies the requested rows, files each slot in its dedup table
-  all-to-all      rows back                                 [W*F*C][D] fp32
-  T1 (indexed)    towers fwd/bwd reading rows_in[pos], dX -> grad_out[pos]
-  all-to-all      gradient rows to the owners               [W*F*C][D] fp32
-  T2, T3a         towers' weight gradients, reduced (beside the gradient all-to-all)
-  all-reduce      tower gradient mean over ranks (beside the owner's row-wise Adagrad)
-  Adagrad         owner's fused row-wise Adagrad over the received gradient rows
-  T3b             Adam from the all-reduced gradient
+Pipelined schedule: TWO collectives per step. Per rank, step i (batch i's rows already returned):
 
-Every exchange has a fixed size, so with RCCL (backend "nccl") the step is captured into HIP graphs
-like the single-GPU step. The embedding gradient a row receives is the sum over ranks of the
-per-rank mean-loss gradients (TorchRec's sharded EBC semantics); lookups of a row are summed in
-ascending (source rank, bag) order. A segment over capacity or a key outside a shard raises on
-``check()`` (sticky device flags).
+  T1 (indexed)    towers fwd/bwd reading rows_in[pos_in], dX -> exchange A's gradient region
+  T2, T3          towers' weight gradients, the reduced gradient x 1/W copied into the tower
+                  region of every destination block of exchange A
+  route(i+1)      next batch's ids -> owners (segment (d, f) of fixed capacity; transform_to_
+                  torchrec_batch's id % N and drop-0 inline) -> exchange A's key region
+  all-to-all A    [gradient rows(i) | tower gradient(i) | keys(i+1)]   requester -> owner
+  Adagrad(i)      owner's fused row-wise Adagrad over the received gradient rows
+  Adam(i)         fixed-order sum of the W received tower gradients (= DDP's mean all-reduce)
+  gather(i+1)     owner copies the rows the received keys name (bf16), files them for Adagrad(i+1)
+  all-to-all B    rows(i+1)                                            owner -> requester
+
+Every exchange has a fixed size (per-destination capacities), so with RCCL (backend "nccl") the
+step is captured into HIP graphs like the single-GPU step. Batch i+1's rows are gathered after
+Adagrad(i) has updated the owner's shard, so results are those of the synchronous loop. The
+embedding gradient a row receives is the sum over ranks of the per-rank mean-loss gradients
+(TorchRec's sharded EBC semantics); lookups of a row are summed in ascending (source rank, slot)
+order. ``step()`` (no next batch known) runs the same kernels in order with one extra exchange.
+A segment over capacity or a key outside a shard raises on ``check()`` (sticky device flags,
+all-reduced over the ranks).
 """
 from __future__ import annotations
 
 import ctypes as C
 import threading
+import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
 from . import _lib, ops
-from ._lib import check, id_dtype_code, ptr, ptr_array, stream_handle
+from ._lib import FeatureMeta, ShardSeg, check, id_dtype_code, ptr, ptr_array, stream_handle
 
 
 # ---- collectives --------------------------------------------------------------------------------
@@ -43,18 +48,21 @@ class _Done:
     def wait(self):
         return None
 
+    def is_completed(self):
+        return True
+
 
 def graph_safe_nccl_env() -> None:
     """Environment for a "nccl" (RCCL) process group whose collectives are captured into HIP graphs;
-    call BEFORE dist.init_process_group. ProcessGroupNCCL's watchdog queries the end events of the
-    works it tracks; with its event cache on, an event of an eager collective can come back recorded
-    in a capturing stream, and the query then fails (hipErrorCapturedEvent), which the watchdog
-    turned into an abort of the process (seen on MI355X after a run of the graphed sharded step).
-    The cache is turned off, and such a query error is logged instead of rethrown."""
+    call BEFORE dist.init_process_group. ProcessGroupNCCL's watchdog queries the end event of every
+    eager work it tracks; with its CUDA-event cache on, a finished work's event goes back to the
+    cache and is re-recorded by a collective issued during a later capture, and the watchdog's
+    query of the old work then fails with hipErrorCapturedEvent (seen on MI355X: the process
+    aborted at exit after a graphed run). With the cache off every work owns its event. Eager works
+    are also retired before any capture (``TorchComm.retire``)."""
     import os
 
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-    os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
 
 
 class TorchComm:
@@ -69,29 +77,53 @@ class TorchComm:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.always = bool(always_collective)
+        self._eager: List = []
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
-        """Equal-split all-to-all along dim 0. async_op: returns a handle whose wait() makes the
-        current stream wait for the collective (RCCL runs on its own stream meanwhile)."""
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Optional[List[int]] = None,
+                   in_splits: Optional[List[int]] = None):
+        """All-to-all along dim 0 (equal blocks, or the given fixed split sizes)."""
         if self.world == 1 and not self.always:
             out.copy_(inp)
-            return _Done()
-        w = dist.all_to_all_single(out, inp, group=self.group, async_op=async_op)
-        return w if async_op else _Done()
+            return
+        capturing = torch.cuda.is_current_stream_capturing()
+        w = dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                   group=self.group, async_op=not capturing)
+        if w is not None:
+            w.wait()  # the current stream waits for RCCL's; the handle is kept for retire()
+            if len(self._eager) >= 64:
+                self._eager = [h for h in self._eager if not h.is_completed()]
+            self._eager.append(w)
+
+    def retire(self, timeout_s: float = 60.0) -> None:
+        """Wait until every eager collective issued so far is complete (device and watchdog view)
+        — call before capturing collectives into a HIP graph."""
+        torch.cuda.synchronize()
+        t0 = time.monotonic()
+        for w in self._eager:
+            w.wait()
+            while not w.is_completed():
+                if time.monotonic() - t0 > timeout_s:
+                    raise _lib.TTError("an eager collective did not complete before graph capture")
+                time.sleep(0.001)
+        self._eager.clear()
+
+    def all_reduce_max_(self, t: torch.Tensor) -> None:
+        if self.world > 1 or self.always:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
 
     def gather_rows(self, local: torch.Tensor, spans: Sequence[Tuple[int, int]], full_rows: int):
         """Rank 0 receives every rank's row block (spans[r] = (first row, rows)) into one
-        [full_rows, D] tensor (returned on rank 0, None elsewhere); point-to-point, so no rank
+        [full_rows, *] tensor (returned on rank 0, None elsewhere); point-to-point, so no rank
         ever holds more than its own shard plus, on rank 0, the result."""
-        D = local.shape[1]
+        shape = tuple(local.shape[1:])
         if self.rank == 0:
-            full = torch.empty(full_rows, D, dtype=local.dtype, device=local.device)
+            full = torch.empty((full_rows,) + shape, dtype=local.dtype, device=local.device)
             lo, n = spans[0]
             full[lo:lo + n].copy_(local[:n])
             for r in range(1, self.world):
                 lo, n = spans[r]
                 if n:
-                    buf = torch.empty(n, D, dtype=local.dtype, device=local.device)
+                    buf = torch.empty((n,) + shape, dtype=local.dtype, device=local.device)
                     dist.recv(buf, src=r, group=self.group)
                     full[lo:lo + n].copy_(buf)
             return full
@@ -100,17 +132,14 @@ class TorchComm:
             dist.send(local[:n].contiguous(), dst=0, group=self.group)
         return None
 
-    def all_reduce_mean(self, t: torch.Tensor, async_op: bool = False):
-        if self.world == 1 and not self.always:
-            return _Done()
-        t.mul_(1.0 / self.world)  # DDP divides by the world size, then sums
-        w = dist.all_reduce(t, group=self.group, async_op=async_op)
-        return w if async_op else _Done()
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
+        if self.world > 1:
+            dist.broadcast(t, src=src, group=self.group)
 
 
 class ThreadComm:
     """W ranks as W threads of ONE process on one device (tests): each collective is a rendezvous
-    on a barrier; all-to-all copies the peers' blocks, all-reduce sums in rank order."""
+    on a barrier; all-to-all copies the peers' blocks."""
 
     capturable = False
 
@@ -135,21 +164,41 @@ class ThreadComm:
         self.shared.slots[self.rank] = t
         self.shared.barrier.wait()
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
-        self._exchange(inp)
-        n = out.shape[0] // self.world
-        for s in range(self.world):
-            src = self.shared.slots[s]
-            out[s * n:(s + 1) * n].copy_(src[self.rank * n:(self.rank + 1) * n])
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Optional[List[int]] = None,
+                   in_splits: Optional[List[int]] = None):
+        W = self.world
+        self._exchange((inp, in_splits))
+        o = 0
+        for s in range(W):
+            src, splits = self.shared.slots[s]
+            if splits is None:
+                n = src.shape[0] // W
+                lo, hi = self.rank * n, (self.rank + 1) * n
+            else:
+                lo = sum(splits[:self.rank])
+                hi = lo + splits[self.rank]
+            out[o:o + hi - lo].copy_(src[lo:hi])
+            o += hi - lo
         torch.cuda.current_stream().synchronize()
         self.shared.barrier.wait()
-        return _Done()
+
+    def retire(self, timeout_s: float = 60.0) -> None:
+        torch.cuda.synchronize()
+
+    def all_reduce_max_(self, t: torch.Tensor) -> None:
+        self._exchange(t.clone())
+        acc = self.shared.slots[0]
+        for s in range(1, self.world):
+            acc = torch.maximum(acc, self.shared.slots[s])
+        torch.cuda.current_stream().synchronize()
+        self.shared.barrier.wait()
+        t.copy_(acc)
 
     def gather_rows(self, local: torch.Tensor, spans: Sequence[Tuple[int, int]], full_rows: int):
         self._exchange(local)
         full = None
         if self.rank == 0:
-            full = torch.empty(full_rows, local.shape[1], dtype=local.dtype, device=local.device)
+            full = torch.empty((full_rows,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
             for r in range(self.world):
                 lo, n = spans[r]
                 full[lo:lo + n].copy_(self.shared.slots[r][:n])
@@ -157,29 +206,37 @@ class ThreadComm:
         self.shared.barrier.wait()
         return full
 
-    def all_reduce_mean(self, t: torch.Tensor, async_op: bool = False):
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
         self._exchange(t.clone())
-        acc = None
-        for s in range(self.world):
-            x = self.shared.slots[s] * (1.0 / self.world)
-            acc = x if acc is None else acc + x
+        v = self.shared.slots[src]
         torch.cuda.current_stream().synchronize()
         self.shared.barrier.wait()
-        t.copy_(acc)
-        torch.cuda.current_stream().synchronize()
-        return _Done()
+        t.copy_(v)
 
 
 # ---- the step -----------------------------------------------------------------------------------
 
 
 def default_capacity(B: int, W: int, factor: float = 1.25) -> int:
-    """Per-(owner, feature) segment capacity: the expected B/W lookups per owner with slack for
-    the binomial spread of uniformly spread ids (B/W + 6 sigma at B = 8192, W = 8 is ~1200)."""
+    """Per-(owner, feature) segment capacity of a row-wise feature: the expected B/W lookups per
+    owner with slack for the binomial spread of uniformly spread ids (B/W + 6 sigma at B = 8192,
+    W = 8 is ~1200)."""
     if W == 1:
         return B
     c = int(factor * B / W) + 64
     return min(B, (c + 7) // 8 * 8)
+
+
+def segment_counts(cols: Sequence[torch.Tensor], num_embeddings: Sequence[int], block_sizes: Sequence[int],
+                   owners: Sequence[int], W: int) -> torch.Tensor:
+    """[W, F] kept lookups per (owner, feature) of one batch (host check of a capacity)."""
+    out = torch.zeros(W, len(cols), dtype=torch.int64)
+    for f, c in enumerate(cols):
+        c = c.to(torch.int64)
+        row = torch.remainder(c[c != 0], int(num_embeddings[f]))
+        d = row // block_sizes[f] if block_sizes[f] > 0 else torch.full_like(row, int(owners[f]))
+        out[:, f] = torch.bincount(d.cpu(), minlength=W)[:W]
+    return out
 
 
 class FusedShardedTwoTowerStep:
@@ -187,18 +244,15 @@ class FusedShardedTwoTowerStep:
                  batch_size: int, device: torch.device, sharding: Optional[Sequence[str]] = None,
                  tw_owners: Optional[Sequence[int]] = None, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
-                 capacity: Optional[int] = None, full_tables: Optional[Sequence[torch.Tensor]] = None,
-                 overlap_comm: bool = False):
+                 capacity=None, full_tables: Optional[Sequence[torch.Tensor]] = None):
         """Two features (query, candidate), one table each, single-hot. ``sharding[f]`` is
-        "row_wise" (default) or "table_wise" (owner ``tw_owners[f]``). ``full_tables`` (CPU,
-        optional) give the initial weights; otherwise each rank draws its shard from
-        U(-sqrt(1/N), sqrt(1/N)) (torchrec EBC init). Tower parameters are initialised from
-        ``seed`` identically on every rank (what DDP's initial broadcast guarantees).
-        ``overlap_comm``: run the gradient all-to-all beside T2 and the tower all-reduce beside the
-        owner's Adagrad on RCCL's stream; off by default, since each cross-stream join inside the
-        step graph costs more than the overlap wins at world 1."""
+        "row_wise" (default) or "table_wise" (owner ``tw_owners[f]``). ``capacity``: slots per
+        (owner, row-wise feature) segment — an int, a per-feature list, or None (default_capacity);
+        a table-wise feature's owner segment holds B. ``full_tables`` (CPU, optional) give the
+        initial weights; otherwise each rank draws its shard from U(-sqrt(1/N), sqrt(1/N)) (torchrec
+        EBC init). Tower parameters are initialised from ``seed`` identically on every rank (what
+        DDP's initial broadcast guarantees)."""
         self.comm = comm
-        self.overlap_comm = bool(overlap_comm)
         self.W, self.rank = comm.world, comm.rank
         self.device = torch.device(device)
         dev = self.device
@@ -213,6 +267,8 @@ class FusedShardedTwoTowerStep:
         tw_owners = list(tw_owners or [f % self.W for f in range(self.F)])
         self.sharding = sharding
         W, r, F, B, D = self.W, self.rank, self.F, self.B, self.D
+        if D % 4 or D > 128:
+            raise _lib.TTError("sharded step: D % 4 == 0 and D <= 128")
         # ---- shards
         self.block, self.owner, local_rows, self.row_lo = [], [], [], []
         for f in range(F):
@@ -232,8 +288,11 @@ class FusedShardedTwoTowerStep:
                 raise _lib.TTError(f"sharding must be row_wise / table_wise, got {sharding[f]}")
         self.local_rows = local_rows
         self.tables = ops.TableSet([max(1, n) for n in local_rows], [D] * F, list(range(F)), dev)
+        self.tables.weights.zero_()  # a feature this rank holds no rows of keeps one zero dummy row
         for f in range(F):
             view = self.tables.table_view(f)
+            if local_rows[f] == 0:
+                continue
             if full_tables is not None:
                 if local_rows[f]:
                     lo = self.row_lo[f]
@@ -241,58 +300,110 @@ class FusedShardedTwoTowerStep:
             else:
                 a = (1.0 / self.N[f]) ** 0.5
                 view.uniform_(-a, a, generator=torch.Generator(device=dev).manual_seed(seed * 1000 + 17 * r + f))
-        # ---- exchange buffers (fixed sizes)
-        # a table-wise feature sends all B lookups to its owner: its segment needs capacity B
-        if capacity is None:
-            capacity = B if "table_wise" in sharding else default_capacity(B, W)
-        self.C = int(capacity)
-        C_ = self.C
-        self.nslots = W * F * C_
-        self.send = torch.zeros(W, F + F * C_, dtype=torch.int64, device=dev)
-        self.recv = torch.zeros_like(self.send)
-        self.pos = torch.full((F * B,), -1, dtype=torch.int32, device=dev)
-        # gathered rows travel as bf16 (T1 computes on bf16 inputs, so nothing changes but the bytes:
-        # half the rows all-to-all); gradient rows stay fp32 (the fp32 row-wise Adagrad)
-        self.rows_out = torch.zeros(self.nslots, D, dtype=torch.bfloat16, device=dev)
-        self.rows_in = torch.zeros_like(self.rows_out)
-        self.grad_out = torch.zeros(self.nslots, D, dtype=torch.float32, device=dev)
-        self.grad_in = torch.zeros_like(self.grad_out)
-        self.flags = torch.zeros(2, dtype=torch.int32, device=dev)  # {overflow, bad key}
-        self.route_ws = torch.empty(_lib.load().tt_shard_route_workspace_bytes(F, B), dtype=torch.uint8, device=dev)
-        self.tables.ensure_dedup_workspace(self.nslots)
         # ---- towers (data-parallel replicas)
-        if not ops.FusedTowers.supported([D, D], self.layer_sizes, [0, D], B) or len(self.layer_sizes) != 2 or D > 128:
-            raise _lib.TTError("sharded step: towers must be 2 layers with D <= 128 (fused T1 indexed mode)")
+        if not ops.FusedTowers.supported([D, D], self.layer_sizes, [0, D], B) or len(self.layer_sizes) != 2:
+            raise _lib.TTError("sharded step: towers must be 2 layers (fused T1 indexed mode)")
         self.towers = ops.FusedTowers([D, D], self.layer_sizes, [0, D], B, dev)
-        n = self.towers.num_params
-        self.params = torch.empty(n, dtype=torch.float32, device=dev)
-        self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        P = self.towers.num_params
+        self.params = torch.empty(P, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(P, dtype=torch.float32, device=dev)
         self.adam_state = torch.zeros(2, dtype=torch.int64, device=dev)
         g = torch.Generator().manual_seed(seed + 1)
-        chunks, o = [], 0
+        chunks = []
         for _ in range(2):
             i = D
             for out in self.layer_sizes:
                 bound = 1.0 / i ** 0.5
-                w = torch.empty(out, i).uniform_(-bound, bound, generator=g)
-                b = torch.empty(out).uniform_(-bound, bound, generator=g)
-                chunks += [w.flatten(), b]
+                chunks += [torch.empty(out, i).uniform_(-bound, bound, generator=g).flatten(),
+                           torch.empty(out).uniform_(-bound, bound, generator=g)]
                 i = out
         self.params.copy_(torch.cat(chunks))
         self.towers.update(self.params, do_adam=False)
+        # ---- exchange layout (fixed sizes, identical arithmetic on every rank)
+        if capacity is None:
+            caps_f = [default_capacity(B, W)] * F
+        elif isinstance(capacity, (list, tuple)):
+            caps_f = [int(c) for c in capacity]
+        else:
+            caps_f = [int(capacity)] * F
+        self.caps_f = caps_f
+        self.cap = [[(caps_f[f] if sharding[f] == "row_wise" else (B if self.owner[f] == d else 0))
+                     for f in range(F)] for d in range(W)]
+        self._layout()
+        # ---- buffers
+        self.sendA = torch.zeros(self.A_total, dtype=torch.float32, device=dev)
+        self.recvA = torch.zeros(W * self.Asz[r], dtype=torch.float32, device=dev)
+        self.rows_out = torch.zeros(max(1, W * self.S[r]), D, dtype=torch.bfloat16, device=dev)
+        self.rows_in = torch.zeros(max(1, sum(self.S)), D, dtype=torch.bfloat16, device=dev)
+        self.pos_in = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
+        self.pos_out = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
+        self.flags = torch.zeros(2, dtype=torch.int32, device=dev)  # {overflow, bad key}
+        self.route_ws = torch.empty(_lib.load().tt_shard_route_workspace_bytes(F, B), dtype=torch.uint8, device=dev)
+        segs = (ShardSeg * (W * F))()
+        for d in range(W):
+            for f in range(F):
+                e = segs[d * F + f]
+                ids64 = (self.A_off[d] + self.Ppad + self.S[d] * D) // 2
+                e.cap = self.cap[d][f]
+                e.key_index = ids64 + F + self.seg_off[d][f]
+                e.cnt_index = ids64 + f
+                e.pos_in = self.RB_off[d] + self.seg_off[d][f]
+                e.pos_out = (self.A_off[d] + self.Ppad) // D + self.seg_off[d][f]
+        raw = torch.frombuffer(bytearray(bytes(segs)), dtype=torch.uint8)
+        self.segs = raw.to(dev)
+        # dedup workspaces: batch i inserts at gather(i), Adagrad(i) consumes: two in flight
+        self.max_lookups = max(1, W * self.S[r])
+        nbytes = _lib.load().tt_dedup_workspace_bytes(self.max_lookups)
+        self.dd_ws = []
+        for _ in range(2):
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            check(_lib.load().tt_dedup_workspace_init(ptr(ws), nbytes, self.max_lookups, stream_handle(dev)),
+                  "dedup_workspace_init")
+            self.dd_ws.append(ws)
+        # Adagrad over the received gradient rows: one pseudo-feature per source block
+        self._fm_src = (FeatureMeta * W)()
+        for s in range(W):
+            self._fm_src[s].table = 0
+            self._fm_src[s].out_offset = 0
+            self._fm_src[s].out_row = (s * self.Asz[r] + self.Ppad) // D
+        self._ne = (C.c_int64 * F)(*self.N)
+        self._bs = (C.c_int64 * F)(*self.block)
+        self._ow = (C.c_int32 * F)(*self.owner)
+        self._segoff_me = (C.c_int64 * F)(*self.seg_off[r])
+        self._tw_off = (C.c_int64 * W)(*self.A_off)
         # ---- step inputs / outputs
         self.cols = [torch.zeros(B, dtype=id_dtype, device=dev) for _ in range(F)]
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
         self.logits = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
-        self._ne = (C.c_int64 * F)(*self.N)
-        self._bs = (C.c_int64 * F)(*self.block)
-        self._ow = (C.c_int32 * F)(*self.owner)
         self.pool_graphs: list = []
+        self.small_graphs: list = []
+        self.cursor = None  # pipelined pool: index of the batch whose rows are staged in rows_in
+        torch.cuda.synchronize(dev)
 
     # ------------------------------------------------------------------------------------------
+    def _layout(self) -> None:
+        W, F, D, P = self.W, self.F, self.D, self.towers.num_params
+        rup = lambda x, m: -(-x // m) * m  # noqa: E731
+        self.Ppad = rup(P, D)
+        self.S = [sum(self.cap[d]) for d in range(W)]
+        self.seg_off = []
+        for d in range(W):
+            o, offs = 0, []
+            for f in range(F):
+                offs.append(o)
+                o += self.cap[d][f]
+            self.seg_off.append(offs)
+        # destination block d: [tower Ppad | gradient rows S_d x D | counts F, keys S_d (int64) | pad]
+        self.Asz = [self.Ppad + self.S[d] * D + rup(2 * (F + self.S[d]), D) for d in range(W)]
+        self.A_off = [sum(self.Asz[:d]) for d in range(W)]
+        self.A_total = sum(self.Asz)
+        self.RB_off = [sum(self.S[:d]) for d in range(W)]
+        if W * max(self.S) >= (1 << 18) or self.A_total // D >= 2 ** 31:
+            raise _lib.TTError("sharded step: exchange too large for one step (lookups per owner < 2^18)")
+
     def layer_views(self):
         """[(W, b)] per tower (query, candidate) as views of the flat parameter buffer."""
         out, o, D = [], 0, self.D
@@ -308,41 +419,108 @@ class FusedShardedTwoTowerStep:
             out.append(layers)
         return out
 
+    def grad_rows(self, parity: int) -> torch.Tensor:
+        """[F * B, D] view of the gradient rows T1 wrote for the batch of this parity, in lookup
+        (feature, bag) order (-1 positions: zeros) — tests."""
+        pos = self.pos_out[parity].long()
+        rows = self.sendA.view(-1, self.D)
+        out = rows[pos.clamp(min=0)].clone()
+        out[pos < 0] = 0
+        return out
+
+    def tower_grad_sent(self) -> torch.Tensor:
+        """This rank's tower gradient x 1/W as sent in exchange A (tests)."""
+        return self.sendA[self.A_off[0]:self.A_off[0] + self.towers.num_params].clone()
+
+    def rows_for(self, parity: int) -> torch.Tensor:
+        """[F * B, D] bf16 rows T1 reads for the batch of this parity (tests)."""
+        pos = self.pos_in[parity].long()
+        out = self.rows_in[pos.clamp(min=0)].clone()
+        out[pos < 0] = 0
+        return out
+
     def load_batch(self, cols: Sequence[torch.Tensor], labels: torch.Tensor) -> None:
         for dst, src in zip(self.cols, cols):
             dst.copy_(src, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
 
-    def step(self) -> None:
+    # ---- the step's pieces ----------------------------------------------------------------------
+    def _route(self, cols: Sequence[torch.Tensor], parity: int) -> None:
         lib = _lib.load()
-        st = stream_handle(self.device)
-        F, B, W, C_ = self.F, self.B, self.W, self.C
-        ts, tw = self.tables, self.towers
-        # input_dist: route + ids all-to-all
-        check(lib.tt_shard_route_cols(F, B, ptr_array(list(self.cols)), id_dtype_code(self.cols[0].dtype), self._ne,
-                                      self._bs, self._ow, W, C_, ptr(self.send), ptr(self.pos), ptr(self.flags),
-                                      ptr(self.route_ws), self.route_ws.numel(), st),
-              "shard_route_cols")
-        self.comm.all_to_all(self.recv, self.send)
-        # owner lookup (+ dedup insert), rows back
-        check(lib.tt_shard_gather_rows_bf16(ptr(ts.weights), ts._tm, ts.T, F, W, C_, ptr(self.recv),
-                                            ptr(self.rows_out), ptr(self.flags[1:]), ptr(ts._dd_ws), ts._dd_ws.numel(),
-                                            ts._dd_cap, st),
-              "shard_gather_rows")
-        self.comm.all_to_all(self.rows_in, self.rows_out)
-        # towers (dX straight into the gradient rows the owners receive)
-        tw.fwd_bwd_indexed([self.pos[:B], self.pos[B:]], [self.rows_in, self.rows_in],
-                           [self.grad_out, self.grad_out], self.params, self.labels, self.logits)
-        # gradient rows to the owners (with overlap_comm: beside the towers' weight gradients (T2)
-        # and their reduction, and the towers' all-reduce beside the owner's row-wise Adagrad)
-        h_rows = self.comm.all_to_all(self.grad_in, self.grad_out, async_op=self.overlap_comm)
+        check(lib.tt_shard_route_segs(self.F, self.B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ne,
+                                      self._bs, self._ow, self.W, ptr(self.segs), ptr(self.sendA),
+                                      ptr(self.pos_in[parity]), ptr(self.pos_out[parity]), ptr(self.flags),
+                                      ptr(self.route_ws), self.route_ws.numel(), stream_handle(self.device)),
+              "shard_route_segs")
+
+    def _exchange_a(self) -> None:
+        r = self.rank
+        self.comm.all_to_all(self.recvA, self.sendA, out_splits=[self.Asz[r]] * self.W, in_splits=list(self.Asz))
+
+    def _gather(self, parity: int) -> None:
+        r, ts = self.rank, self.tables
+        ws = self.dd_ws[parity]
+        check(_lib.load().tt_shard_gather_segs_bf16(
+            ptr(ts.weights), ts._tm, ts.T, self.F, self.W, ptr(self.recvA), self.Asz[r] // 2,
+            (self.Ppad + self.S[r] * self.D) // 2, self._segoff_me, self.S[r], ptr(self.rows_out), ptr(self.flags[1:]),
+            ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device)), "shard_gather_segs")
+
+    def _exchange_b(self) -> None:
+        r, D = self.rank, self.D
+        self.comm.all_to_all(self.rows_in[:sum(self.S)], self.rows_out[:self.W * self.S[r]],
+                             out_splits=list(self.S), in_splits=[self.S[r]] * self.W)
+
+    def _towers(self, parity: int, labels: torch.Tensor) -> None:
+        lib, tw, B = _lib.load(), self.towers, self.B
+        pin, pout = self.pos_in[parity], self.pos_out[parity]
+        check(lib.tt_tower_fwd_bwd_indexed2_bf16(
+            C.byref(tw.shape), B, ptr_array([pin[:B], pin[B:]]), ptr_array([pout[:B], pout[B:]]),
+            ptr_array([self.rows_in, self.rows_in]), ptr_array([self.sendA, self.sendA]), ptr(self.params),
+            ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
+            "tower_fwd_bwd_indexed2")
         tw.wgrad(self.loss)
-        tw.update(self.params, do_adam=False, grads_out=self.grads)
-        h_dense = self.comm.all_reduce_mean(self.grads, async_op=self.overlap_comm)
-        h_rows.wait()
-        ts.dedup_rowwise_adagrad(self.grad_in, self.nslots, self.lr_emb, self.eps, flat=True)
-        h_dense.wait()
-        tw.adam_grads(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense)
+        check(lib.tt_tower_grads_replicated(C.byref(tw.shape), B, ptr(self.params), ptr(self.sendA), self.W,
+                                            self._tw_off, 1.0 / self.W, ptr(tw.ws), tw.nbytes,
+                                            stream_handle(self.device)), "tower_grads_replicated")
+
+    def _owner_update(self, parity: int) -> None:
+        lib, ts, r, tw = _lib.load(), self.tables, self.rank, self.towers
+        ws = self.dd_ws[parity]
+        check(lib.tt_dedup_rowwise_adagrad(ts._tm, ts.T, self._fm_src, self.W, self.S[r], ptr(self.recvA), self.D,
+                                           ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws), ws.numel(),
+                                           self.max_lookups, stream_handle(self.device)), "dedup_rowwise_adagrad")
+        check(lib.tt_tower_adam_grads_sum(C.byref(tw.shape), self.B, ptr(self.params), ptr(self.recvA), self.W,
+                                          self.Asz[r], ptr(self.exp_avg), ptr(self.exp_avg_sq), self.lr_dense, 0.9,
+                                          0.999, 1e-8, 0.0, ptr(self.adam_state), ptr(tw.ws), tw.nbytes,
+                                          stream_handle(self.device)), "tower_adam_grads_sum")
+
+    # ---- public steps ---------------------------------------------------------------------------
+    def step(self) -> None:
+        """One synchronous step on the batch in ``cols`` / ``labels`` (no next batch known: the
+        rows are fetched first, at the price of one more exchange)."""
+        self._route(self.cols, 0)
+        self._exchange_a()
+        self._gather(0)
+        self._exchange_b()
+        self._towers(0, self.labels)
+        self._exchange_a()
+        self._owner_update(0)
+
+    def prime(self, cols: Sequence[torch.Tensor], parity: int) -> None:
+        """Stage the rows of a batch (the pipelined loop's first step)."""
+        self._route(cols, parity)
+        self._exchange_a()
+        self._gather(parity)
+        self._exchange_b()
+
+    def step_pipelined(self, labels: torch.Tensor, parity: int, next_cols: Sequence[torch.Tensor]) -> None:
+        """Step on the staged batch (rows in place, parity ``parity``), staging ``next_cols``."""
+        self._towers(parity, labels)
+        self._route(next_cols, parity ^ 1)
+        self._exchange_a()
+        self._owner_update(parity)
+        self._gather(parity ^ 1)
+        self._exchange_b()
 
     # ---- checkpoint (03_model_training.py:474-502 / :1015-1054 format) -------------------------
     def spans(self, f: int) -> List[Tuple[int, int]]:
@@ -358,9 +536,11 @@ class FusedShardedTwoTowerStep:
         return out
 
     def gathered_state_dict(self, feature_names: Sequence[str] = ("user_id", "product_id"),
-                            prefix: str = "two_tower.") -> Dict[str, torch.Tensor]:
+                            prefix: str = "two_tower.", optimizer: bool = False) -> Dict[str, torch.Tensor]:
         """Collective: rank 0 returns the full state dict the reference's gather_and_get_state_dict
-        writes (full tables + towers), other ranks {}."""
+        writes (full tables + towers), other ranks {}. ``optimizer``: also the row-wise Adagrad state
+        of every table (gathered like the tables) and the towers' Adam moments and step under
+        ``optim.*`` keys (the reference saves no optimizer state; this makes resume exact)."""
         from .lifecycle import _dense_items, _tower_views
 
         sd = {}
@@ -368,14 +548,23 @@ class FusedShardedTwoTowerStep:
             full = self.comm.gather_rows(self.tables.table_view(f), self.spans(f), self.N[f])
             if self.rank == 0:
                 sd[f"{prefix}ebc.embedding_bags.t_{name}.weight"] = full
+            if optimizer:
+                st = self.comm.gather_rows(self.tables.state_view(f).unsqueeze(1), self.spans(f), self.N[f])
+                if self.rank == 0:
+                    sd[f"optim.ebc.t_{name}.rowwise_adagrad_state"] = st[:, 0].clone()
         if self.rank == 0:
             towers = _tower_views(self.params, [self.D, self.D], self.layer_sizes)
             sd.update({k: v.clone() for k, v in _dense_items(towers, prefix).items()})
+            if optimizer:
+                sd["optim.towers.exp_avg"] = self.exp_avg.clone()
+                sd["optim.towers.exp_avg_sq"] = self.exp_avg_sq.clone()
+                sd["optim.towers.step"] = self.adam_state[:1].clone()
         return sd
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], feature_names: Sequence[str] = ("user_id", "product_id"),
                         prefix: str = "two_tower.") -> None:
-        """Every rank takes its blocks of the full tables and the towers from a gathered dict."""
+        """Every rank takes its blocks of the full tables and the towers from a gathered dict (and
+        the optimizer state when the dict holds ``optim.*`` keys; otherwise it is reset)."""
         from .lifecycle import _dense_items, _tower_views
 
         with torch.no_grad():
@@ -383,25 +572,45 @@ class FusedShardedTwoTowerStep:
                 lo, n = self.spans(f)[self.rank]
                 if n:
                     self.tables.table_view(f)[:n].copy_(sd[f"{prefix}ebc.embedding_bags.t_{name}.weight"][lo:lo + n])
+                    key = f"optim.ebc.t_{name}.rowwise_adagrad_state"
+                    if key in sd:
+                        self.tables.state_view(f)[:n].copy_(sd[key][lo:lo + n])
+                    else:
+                        self.tables.state_view(f).zero_()
             towers = _tower_views(self.params, [self.D, self.D], self.layer_sizes)
             for k, v in _dense_items(towers, prefix).items():
                 v.copy_(sd[k])
+            if "optim.towers.exp_avg" in sd:
+                self.exp_avg.copy_(sd["optim.towers.exp_avg"])
+                self.exp_avg_sq.copy_(sd["optim.towers.exp_avg_sq"])
+                self.adam_state.zero_()
+                self.adam_state[:1].copy_(sd["optim.towers.step"])
+            else:
+                self.exp_avg.zero_()
+                self.exp_avg_sq.zero_()
+                self.adam_state.zero_()
         self.towers.update(self.params, do_adam=False)
 
-    def check(self) -> None:
-        """Raise if any step so far overflowed a segment or received a key outside its shard."""
-        f = self.flags.cpu().tolist()
+    def check(self, collective: bool = True) -> None:
+        """Raise if any step so far overflowed a segment or received a key outside its shard. With
+        ``collective`` (default) the flags are first max-reduced over the ranks, so every rank
+        raises together (call it on every rank, outside any graph capture)."""
+        f = self.flags.clone()
+        if collective:
+            self.comm.all_reduce_max_(f)
+        f = f.cpu().tolist()
         if f[0]:
-            raise _lib.TTError(f"sharded step: a segment exceeded its capacity C={self.C} (skewed ids): "
+            raise _lib.TTError(f"sharded step: a segment exceeded its capacity {self.caps_f} (skewed ids): "
                                "results are invalid; raise `capacity`")
         if f[1]:
             raise _lib.TTError("sharded step: an owner received a key outside its shard")
 
     def release_graphs(self) -> None:
-        """Drop the captured graphs (call before tearing down the process group: a live graph
-        holds references to the RCCL communicator's work)."""
+        """Drop the captured graphs (before tearing down the process group: a live graph holds
+        references to the RCCL communicator's work)."""
         torch.cuda.synchronize(self.device)
         self.pool_graphs = []
+        self.small_graphs = []
         self._pool_inputs = []
         import gc
 
@@ -409,30 +618,77 @@ class FusedShardedTwoTowerStep:
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------------------------------
+    def _staged(self, batches: Sequence) -> list:
+        staged = []
+        for cols, labels in batches:
+            cols = list(cols)
+            if len(cols) != self.F:
+                raise _lib.TTError("capture_pool: one id column per feature expected")
+            for c in cols:
+                if c.dtype != self.id_dtype or not c.is_contiguous() or c.numel() != self.B or c.device != self.device:
+                    raise _lib.TTError("capture_pool: batch columns must be contiguous [B] device tensors of the "
+                                       "step's id dtype")
+            lab = labels.to(torch.int32).contiguous()
+            if lab.numel() != self.B:
+                raise _lib.TTError("capture_pool: labels must be [B]")
+            staged.append((cols, lab))
+        return staged
+
     def capture_pool(self, batches: Sequence, steps_per_graph: int = 1) -> None:
-        """HIP graphs over resident (cols, labels) batches, k steps per graph (RCCL collectives
-        inside; needs a capturable comm)."""
+        """Pipelined HIP graphs over a cyclic pool of resident (cols, labels) batches (len even, a
+        multiple of k = ``steps_per_graph``): graph j runs the steps of batches j*k .. j*k+k-1, each
+        staging the next batch of the pool; ``small_graphs[i]`` runs batch i alone. Replay them in
+        pool order with ``run(n)`` (the step keeps the cursor). Needs a capturable comm."""
         if not self.comm.capturable:
             raise _lib.TTError("capture_pool: the comm is not graph-capturable")
         k = int(steps_per_graph)
-        if k < 1 or len(batches) % k:
-            raise _lib.TTError("capture_pool: the batch count must be a multiple of steps_per_graph")
-        staged = [(list(c), l.to(torch.int32).contiguous()) for c, l in batches]
-        self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]
-        keep = self.cols, self.labels
-        self.pool_graphs = []
-        torch.cuda.synchronize(self.device)
-        for j in range(0, len(staged), k):
+        n = len(batches)
+        if k < 1 or n % k or n % 2:
+            raise _lib.TTError("capture_pool: the batch count must be even and a multiple of steps_per_graph")
+        staged = self._staged(batches)
+        self._pool_inputs = [staged]
+        self.pool_k = k
+        # stage batch 0 eagerly, then retire every eager collective before capturing
+        self.prime(staged[0][0], 0)
+        self.cursor = 0
+        self.comm.retire()
+
+        def cap(idx):
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                    for cols, labels in staged[j:j + k]:
-                        self.cols, self.labels = cols, labels
-                        self.step()
+                    for i in idx:
+                        self.step_pipelined(staged[i][1], i % 2, staged[(i + 1) % n][0])
             torch.cuda.current_stream(self.device).wait_stream(s)
-            self.pool_graphs.append(g)
-        self.cols, self.labels = keep
+            return g
+
         torch.cuda.synchronize(self.device)
-        self.steps_per_graph = k
+        self.pool_graphs = [cap(range(j, j + k)) for j in range(0, n, k)]
+        self.small_graphs = [cap([i]) for i in range(n)] if k > 1 else list(self.pool_graphs)
+        torch.cuda.synchronize(self.device)
+
+    def run(self, n: int) -> None:
+        """Replay n pipelined steps from the pool, continuing at the cursor."""
+        i, nb, k = self.cursor, len(self.small_graphs), self.pool_k
+        while n > 0:
+            if i % k == 0 and n >= k:
+                self.pool_graphs[i // k].replay()
+                i, n = i + k, n - k
+            else:
+                self.small_graphs[i].replay()
+                i, n = i + 1, n - 1
+            i %= nb
+        self.cursor = i
+
+    def run_eager(self, batches: Sequence, n: int) -> None:
+        """n pipelined steps over a cyclic pool without graphs (continuing at the cursor)."""
+        nb = len(batches)
+        if self.cursor is None:
+            self.prime(list(batches[0][0]), 0)
+            self.cursor = 0
+        for _ in range(n):
+            i = self.cursor
+            self.step_pipelined(batches[i][1].to(torch.int32), i % 2, list(batches[(i + 1) % nb][0]))
+            self.cursor = (i + 1) % nb
