@@ -458,6 +458,34 @@ int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* par
                             float eps, float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes,
                             void* stream);
 
+/* T2 (tt_tower_wgrad) with the NEXT batch's route count pass (tt_shard_route_segs' first half: its
+ * arguments, route_ws its workspace) as extra workgroups of the same launch. */
+int tt_tower_wgrad_route_count(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                               int F, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
+                               const int64_t* block_sizes, const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                               int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                               size_t route_ws_bytes, void* stream);
+/* tt_tower_grads_replicated with the route's place pass (after tt_tower_wgrad_route_count on the same
+ * arguments) as extra workgroups: together the two launches do what tt_shard_route_segs does. */
+int tt_tower_grads_replicated_route_place(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
+                                          int copies, const int64_t* offsets, float scale, void* workspace,
+                                          size_t ws_bytes, int F, const void* const* cols, int id_dtype,
+                                          const int64_t* num_embeddings, const int64_t* block_sizes,
+                                          const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                          int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                          size_t route_ws_bytes, void* stream);
+/* The owner's whole update of the pipelined sharded step in ONE launch: tt_tower_adam_grads_sum
+ * (towers) and tt_dedup_rowwise_adagrad (emb_* arguments: the received gradient rows) share one
+ * round of resident waves. */
+int tt_tower_adam_grads_sum_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
+                                            int nsrc, int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr,
+                                            float beta1, float beta2, float eps, float weight_decay,
+                                            int64_t* step_state, void* workspace, size_t ws_bytes,
+                                            const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                                            int F, int64_t emb_B, const float* emb_grad, int64_t ldg, float* weights,
+                                            float* state, float emb_lr, float emb_eps, void* dedup_ws,
+                                            size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
+
 /* T3 with the gradient taken from `grads` (data-parallel towers: the all-reduced gradient) instead
  * of T2's partials: Adam + the bf16 weight copies. */
 int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,

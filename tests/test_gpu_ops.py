@@ -299,6 +299,47 @@ def test_dot_bce(ops, device, B, dim, ldt):
     np.testing.assert_allclose(dc.cpu().numpy(), cc.grad.numpy(), rtol=1e-4, atol=1e-8)
 
 
+def test_dot_bce_batch_of_one(ops, device):
+    """B = 1: the op (like torch's BCEWithLogits on [1] logits) is defined; the reference's task
+    squeezes the logits to 0-d (03_model_training.py:452) and BCEWithLogitsLoss then raises — the
+    oracle restatement and the drop-in TwoTowerTrainTask raise the same ValueError."""
+    g = torch.Generator().manual_seed(1)
+    q, c = torch.rand(1, 8, generator=g), torch.rand(1, 8, generator=g)
+    y = torch.ones(1, dtype=torch.int64)
+    qq, cc = q.clone().requires_grad_(True), c.clone().requires_grad_(True)
+    logits = (qq * cc).sum(1)  # not squeezed
+    loss = torch.nn.BCEWithLogitsLoss()(logits, y.float())
+    loss.backward()
+    k = ops.DotBCE(device, 1)
+    dq, dc = torch.empty(1, 8, device=device), torch.empty(1, 8, device=device)
+    lg, ls = k(q.to(device), c.to(device), y.to(device), dq=dq, dc=dc)
+    np.testing.assert_allclose(lg.cpu().numpy(), logits.detach().numpy(), rtol=1e-5)
+    np.testing.assert_allclose(float(ls), float(loss), rtol=1e-5)
+    np.testing.assert_allclose(dq.cpu().numpy(), qq.grad.numpy(), rtol=1e-4, atol=1e-8)
+    with pytest.raises(ValueError, match="must be the same as input size"):
+        ref.dot_bce(q, c, y)
+
+    import two_tower_recommender_model_amd as tt
+
+    tt.install_torchrec_alias()
+    from torchrec.datasets.utils import Batch
+    from torchrec.modules.embedding_configs import EmbeddingBagConfig
+    from torchrec.modules.embedding_modules import EmbeddingBagCollection
+    from torchrec.sparse.jagged_tensor import KeyedJaggedTensor
+
+    from two_tower_recommender_model_amd.task import TwoTower, TwoTowerTrainTask
+
+    ebc = EmbeddingBagCollection(tables=[EmbeddingBagConfig(name=f"t_{f}", embedding_dim=32, num_embeddings=10,
+                                                            feature_names=[f]) for f in ("user_id", "product_id")],
+                                 device=device)
+    task = TwoTowerTrainTask(TwoTower(ebc, [32, 32], device=device))
+    kjt = KeyedJaggedTensor.from_lengths_sync(["user_id", "product_id"], torch.tensor([3, 4], device=device),
+                                              torch.ones(2, dtype=torch.int32, device=device))
+    with pytest.raises(ValueError, match="must be the same as input size"):
+        task(Batch(dense_features=torch.zeros(1), sparse_features=kjt,
+                   labels=torch.ones(1, dtype=torch.int32, device=device)))
+
+
 def test_adam(ops, device):
     g = torch.Generator().manual_seed(0)
     p = torch.randn(49536, generator=g)

@@ -103,3 +103,15 @@ def test_block_bucketize_reassembles():
                 loc = int(loc)
                 got.append(p * bs[f] + loc if loc < bs[f] else loc * W + p)
         assert sorted(got) == sorted(values[offs[i]:offs[i + 1]].tolist())
+
+
+def test_batch_of_one_raises_like_the_reference():
+    """03_model_training.py:452 squeezes the logits of a batch of one to 0-d; BCEWithLogitsLoss then
+    rejects the [1] labels. The oracle keeps that behaviour (the drop-in task raises the same)."""
+    import pytest
+    import torch
+
+    from oracle import ref
+
+    with pytest.raises(ValueError, match="must be the same as input size"):
+        ref.dot_bce(torch.rand(1, 4), torch.rand(1, 4), torch.ones(1))

@@ -188,6 +188,21 @@ SIGNATURES = {
         [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
     ),
     "tt_tower_grads_replicated": (_int, [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _vp]),
+    "tt_tower_adam_grads_sum_rowwise_adagrad": (
+        _int,
+        [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm,
+         _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
+    ),
+    "tt_tower_wgrad_route_count": (
+        _int,
+        [_psh, _i64, _vp, _vp, _sz, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
+         _vp],
+    ),
+    "tt_tower_grads_replicated_route_place": (
+        _int,
+        [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp,
+         _vp, _vp, _vp, _vp, _sz, _vp],
+    ),
     "tt_tower_adam_grads_sum": (
         _int,
         [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp],
@@ -237,6 +252,9 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_indexed2_bf16",
     "tt_tower_grads_replicated",
     "tt_tower_adam_grads_sum",
+    "tt_tower_adam_grads_sum_rowwise_adagrad",
+    "tt_tower_wgrad_route_count",
+    "tt_tower_grads_replicated_route_place",
 ]
 
 _lib = None

@@ -26,7 +26,7 @@ ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["api.cpp", "kjt.hip", "embedding.hip", "gemm.hip", "loss_adam.hip", "tower.hip", "dedup.hip", "shard.hip"]
-HEADERS = [CSRC / "tt_common.h", CSRC / "dedup.h", INCLUDE / "tt_mi355x.h"]
+HEADERS = [CSRC / "tt_common.h", CSRC / "dedup.h", CSRC / "shard.h", INCLUDE / "tt_mi355x.h"]
 
 CFLAGS = [
     "-O3",

@@ -50,7 +50,8 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_fwd_bwd_indexed, tt_tower_wgrad_rowwise_adagrad, tt_shard_route_cols, tt_shard_gather_rows,
 // tt_tower_adam_grads, tt_tower_update_pre
 // tt_shard_route_segs, tt_shard_gather_segs_bf16, tt_tower_fwd_bwd_indexed2_bf16, tt_tower_grads_replicated,
-// tt_tower_adam_grads_sum
-int tt_num_entry_points(void) { return 42; }
+// tt_tower_adam_grads_sum, tt_tower_adam_grads_sum_rowwise_adagrad, tt_tower_wgrad_route_count,
+// tt_tower_grads_replicated_route_place
+int tt_num_entry_points(void) { return 45; }
 
 }  // extern "C"

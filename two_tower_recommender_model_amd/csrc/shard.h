@@ -1,0 +1,134 @@
+// Device code of the sharded route (requester side of input_dist), shared by csrc/shard.hip (its
+// own launches) and csrc/tower.hip (the route of the next batch as extra workgroups of the towers'
+// T2 / T3 launches in the pipelined sharded step). See shard.hip for the exchange's layout.
+#pragma once
+
+#include "dedup.h"
+
+namespace tt {
+
+constexpr int RT_BLOCK = 256;  // bags per workgroup of the two route kernels
+constexpr int RT_MAXW = 16;
+
+struct RouteArgs {
+  const void* col[TT_MAX_FEATURES];
+  int64_t num_emb[TT_MAX_FEATURES];  // id mod N divisor
+  int64_t block[TT_MAX_FEATURES];    // row-wise block size (> 0), or 0: table-wise
+  int32_t owner[TT_MAX_FEATURES];    // table-wise owner rank
+  int id_dtype;
+  int F;
+  int W;
+  int64_t B;
+  int64_t C;
+  int nblk;           // workgroups per feature = ceil(B / RT_BLOCK)
+  int64_t* send;      // [W][F + F * C]
+  int32_t* pos;       // [F][B]
+  int32_t* overflow;  // sticky flag
+  int64_t* dl;        // [F][B] workspace: owner << 48 | local row, -1 = dropped
+  int32_t* cnt;       // [F][nblk][RT_MAXW] workspace: lookups per (block, owner)
+  // segment-table form (tt_shard_route_segs): per (owner d, feature f) capacity and addresses in
+  // the packed send buffer; pos_out (nullable) = the lookup's gradient row in that buffer
+  const tt_shard_seg_t* segs;
+  int32_t* pos_out;
+};
+
+// route pass 1 (thread per bag, coalesced): owner + local row of every lookup, and per-workgroup
+// per-owner counts (wave ballots, summed in wave order)
+// one 256-thread workgroup (bags blk * 256 .. of feature f); wc: RT_BLOCK / 64 x RT_MAXW ints of LDS
+__device__ __forceinline__ void route_count_block(const RouteArgs& a, int blk, int f, int (*wc)[RT_MAXW]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blk * RT_BLOCK + threadIdx.x;
+  int d = -1;
+  int64_t lr = 0;
+  if (b < a.B) {
+    const int64_t id = load_id(a.col[f], a.id_dtype, b);
+    if (id != 0) {
+      const int64_t row = py_mod64(id, a.num_emb[f]);
+      if (a.block[f] > 0) {
+        d = (int)udiv64(row, a.block[f]);
+        lr = row - (int64_t)d * a.block[f];
+      } else {
+        d = a.owner[f];
+        lr = row;
+      }
+    }
+    a.dl[(int64_t)f * a.B + b] = d >= 0 ? (int64_t)(((uint64_t)d << 48) | (uint64_t)lr) : -1;
+  }
+  for (int w = 0; w < a.W; ++w) {
+    const uint64_t m = __ballot(d == w);
+    if (lane == 0) wc[wid][w] = __popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < a.W) {
+    int t = 0;
+    for (int v = 0; v < RT_BLOCK / 64; ++v) t += wc[v][threadIdx.x];
+    a.cnt[((int64_t)f * a.nblk + blk) * RT_MAXW + threadIdx.x] = t;
+  }
+}
+
+// route pass 2: slot k = (lookups of the same owner in earlier workgroups) + (earlier waves) +
+// (earlier lanes): ascending bag order inside each (owner, feature) segment. SEGS: per-(owner,
+// feature) capacities and addresses from the segment table (tt_shard_route_segs), else the
+// uniform layout of tt_shard_route_cols.
+template <bool SEGS>
+__device__ __forceinline__ void route_place_block(const RouteArgs& a, int blk, int f, int* base, int (*wc)[RT_MAXW]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t seg_stride = (int64_t)a.F + (int64_t)a.F * a.C;
+  const int32_t* cf = a.cnt + (int64_t)f * a.nblk * RT_MAXW;
+  if (threadIdx.x < a.W) {
+    int t = 0, all = 0;
+    for (int q = 0; q < a.nblk; ++q) {
+      const int c = cf[q * RT_MAXW + threadIdx.x];
+      if (q < blk) t += c;
+      all += c;
+    }
+    base[threadIdx.x] = t;
+    if (blk == 0) {  // the segment header: lookups kept for this (owner, feature)
+      if (SEGS) {
+        const tt_shard_seg_t sg = a.segs[(int64_t)threadIdx.x * a.F + f];
+        if (all > sg.cap) atomicOr(a.overflow, 1);
+        a.send[sg.cnt_index] = all < sg.cap ? all : sg.cap;
+      } else {
+        if (all > a.C) atomicOr(a.overflow, 1);
+        a.send[(int64_t)threadIdx.x * seg_stride + f] = all < a.C ? all : a.C;
+      }
+    }
+  }
+  const int64_t b = (int64_t)blk * RT_BLOCK + threadIdx.x;
+  int64_t v = -1;
+  if (b < a.B) v = a.dl[(int64_t)f * a.B + b];
+  const int d = v >= 0 ? (int)(v >> 48) : -1;
+  int rank = 0;
+  for (int w = 0; w < a.W; ++w) {
+    const uint64_t m = __ballot(d == w);
+    if (d == w) rank = __popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wc[wid][w] = __popcll(m);
+  }
+  __syncthreads();
+  if (b >= a.B) return;
+  int32_t p = -1, po = -1;
+  if (d >= 0) {
+    int k = base[d] + rank;
+    for (int v2 = 0; v2 < wid; ++v2) k += wc[v2][d];
+    const int64_t key = (int64_t)(((uint64_t)f << DD_TABLE_SHIFT) | ((uint64_t)v & ((1ull << 48) - 1)));
+    if (SEGS) {
+      const tt_shard_seg_t sg = a.segs[(int64_t)d * a.F + f];
+      if (k < sg.cap) {
+        a.send[sg.key_index + k] = key;
+        p = sg.pos_in + k;
+        po = sg.pos_out + k;
+      } else {
+        atomicOr(a.overflow, 1);
+      }
+    } else if (k < a.C) {
+      a.send[(int64_t)d * seg_stride + a.F + (int64_t)f * a.C + k] = key;
+      p = (int32_t)(((int64_t)d * a.F + f) * a.C + k);
+    } else {
+      atomicOr(a.overflow, 1);
+    }
+  }
+  a.pos[(int64_t)f * a.B + b] = p;
+  if (SEGS) a.pos_out[(int64_t)f * a.B + b] = po;
+}
+
+}  // namespace tt

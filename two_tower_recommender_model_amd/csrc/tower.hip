@@ -23,6 +23,7 @@
 
 #include "tt_common.h"
 #include "dedup.h"
+#include "shard.h"
 
 namespace tt {
 
@@ -490,14 +491,14 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   // ---- 0. everything this wave will read from global: X rows first (the chain waits on them),
   // then every weight fragment of the step in order of use, then the biases
   f32x4 xv[4];
+  bf16x4 xb[4];  // R16: the bf16 rows as loaded (T1 stores bf16 to LDS anyway: no widening)
   const int nxv = in / 32;  // f32x4 loads per thread: TR rows x in/4 vectors over 256 threads
   const bool gather = a.gcol[t] != nullptr;
   const bool indexed = a.gpos[t] != nullptr;
   const int incol = a.s.in_col[t];  // read once, before any store (no vmcnt waits mid-chain)
-  int32_t rpos[4];                   // indexed: the source/destination row of each xv
-  int32_t opos[4];                   // indexed: the dX row of each xv (gpos_out, else rpos)
+  int32_t rpos[4];                   // indexed: the dX row of each xv (gpos_out, else its input row)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) rpos[i] = opos[i] = -1;
+  for (int i = 0; i < 4; ++i) rpos[i] = -1;
   if (gather || indexed) {
     // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros.
     // Indexed rows may be bf16 (tt_tower_fwd_bwd_indexed_bf16): byte offsets with the element size
@@ -513,10 +514,10 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         const int64_t gm = m0 + row;
         if (gm < B) {
           if (indexed) {
-            rpos[i] = a.gpos[t][gm];
-            opos[i] = a.gpos_out[t] ? a.gpos_out[t][gm] : rpos[i];
-            if (rpos[i] >= 0)
-              src[i] = reinterpret_cast<const char*>(a.gsrc[t]) + ((int64_t)rpos[i] * in + c4) * (r16 ? 2 : 4);
+            const int32_t pin = a.gpos[t][gm];
+            rpos[i] = pin >= 0 && a.gpos_out[t] ? a.gpos_out[t][gm] : pin;
+            if (pin >= 0)
+              src[i] = reinterpret_cast<const char*>(a.gsrc[t]) + ((int64_t)pin * in + c4) * (r16 ? 2 : 4);
           } else {
             const int64_t id = (a.dbg & 32) ? 1 : load_id(a.gcol[t], a.gid_dtype, gm);
             if (id != 0)
@@ -527,13 +528,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     }
     if (r16) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        xv[i] = (f32x4)(0.f);
-        if (src[i]) {
-          const bf16x4 v = *reinterpret_cast<const bf16x4*>(src[i]);
-          xv[i] = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
-        }
-      }
+      for (int i = 0; i < 4; ++i) xb[i] = src[i] ? *reinterpret_cast<const bf16x4*>(src[i]) : (bf16x4)(__bf16)0.f;
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) xv[i] = src[i] ? *reinterpret_cast<const f32x4*>(src[i]) : (f32x4)(0.f);
@@ -576,10 +571,14 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       const int e = tt + 256 * i;
       const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
       bf16x4 bv;
-      bv[0] = (__bf16)xv[i][0]; bv[1] = (__bf16)xv[i][1]; bv[2] = (__bf16)xv[i][2]; bv[3] = (__bf16)xv[i][3];
+      if (R16) {
+        bv = xb[i];
+      } else {
+        bv[0] = (__bf16)xv[i][0]; bv[1] = (__bf16)xv[i][1]; bv[2] = (__bf16)xv[i][2]; bv[3] = (__bf16)xv[i][3];
+      }
       *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
       const int64_t gm = m0 + row;
-      if (a.pooled_out && gm < B)
+      if (!R16 && a.pooled_out && gm < B)
         *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + incol + c4) = xv[i];
     }
   }
@@ -745,7 +744,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       float* dst = nullptr;
       if (gm < B) {
         if (indexed)
-          dst = opos[i] >= 0 ? a.gdst[t] + (int64_t)opos[i] * in + c4 : nullptr;
+          dst = rpos[i] >= 0 ? a.gdst[t] + (int64_t)rpos[i] * in + c4 : nullptr;
         else
           dst = a.gpooled + gm * a.ldp + incol + c4;
       }
@@ -1090,6 +1089,20 @@ __global__ void __launch_bounds__(256) tower_wgrad_dedup_kernel(WgradArgs a, con
     dd_update_block(d, (int)blockIdx.x - n_t2, smem);
 }
 
+// Pipelined sharded step: the NEXT batch's route rides in the towers' launches as extra
+// workgroups (it depends only on that batch's ids): its count pass beside T2's tiles, its place
+// pass beside T3's parameter workgroups (tower_update_route_kernel below) — two launches fewer.
+__global__ void __launch_bounds__(256) tower_wgrad_route_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
+                                                                RouteArgs r, int n_t2) {
+  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
+  if ((int)blockIdx.x < n_t2) {
+    wgrad_block(a, tiles, (int)blockIdx.x, smem);
+  } else {
+    const int j = (int)blockIdx.x - n_t2;
+    route_count_block(r, j % r.nblk, j / r.nblk, reinterpret_cast<int (*)[RT_MAXW]>(smem));
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // T3: reduce + Adam + bf16 weight copies
 
@@ -1203,6 +1216,17 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
 }
 
 __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) { update_block(a, (int)blockIdx.x, (int)gridDim.x); }
+
+__global__ void __launch_bounds__(256) tower_update_route_kernel(UpdateArgs a, RouteArgs r, int n_upd) {
+  __shared__ int base[RT_MAXW];
+  __shared__ int wc[RT_BLOCK / 64][RT_MAXW];
+  if ((int)blockIdx.x < n_upd) {
+    update_block(a, (int)blockIdx.x, n_upd);
+  } else {
+    const int j = (int)blockIdx.x - n_upd;
+    route_place_block<true>(r, j % r.nblk, j / r.nblk, base, wc);
+  }
+}
 
 // T3 + the embedding path's fused row-wise Adagrad (dedup.h) in ONE launch: workgroups [0, n_dd)
 // run dd_update_block (its slot workgroups fit one round of resident waves), the rest T3 (Adam with
@@ -1623,20 +1647,21 @@ int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, flo
   return check_launch("tower_wgrad_rowwise_adagrad");
 }
 
-static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
-                     float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
-                     int do_adam, float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes,
-                     void* stream, const float* adam_pre = nullptr, const DdUpdateArgs* dd = nullptr,
-                     int64_t dd_grid = 0, int out_copies = 1, const int64_t* out_off = nullptr,
-                     float out_scale = 1.f, int in_srcs = 1, int64_t in_stride = 0) {
+// T3 arguments (shared by every T3 launch form)
+static int t3_args(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                   float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state, int do_adam,
+                   float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes, const float* adam_pre,
+                   int out_copies, const int64_t* out_off, float out_scale, int in_srcs, int64_t in_stride,
+                   UpdateArgs& a, int64_t* grid) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
   if (!params || (do_adam && (!exp_avg || !exp_avg_sq || (!step_state && !adam_pre))))
     return fail(TT_EINVAL, "tower: null pointer");
+  if (out_copies > 16) return fail(TT_EINVAL, "tower: at most 16 gradient copies");
   char* ws = reinterpret_cast<char*>(workspace);
-  UpdateArgs a{};
+  a = UpdateArgs{};
   a.params = params;
   a.exp_avg = exp_avg;
   a.exp_avg_sq = exp_avg_sq;
@@ -1672,12 +1697,26 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
   a.grads_in = grads_in;
   a.adam_pre = adam_pre;
   a.out_copies = out_copies;
-  if (out_copies > 16) return fail(TT_EINVAL, "tower: at most 16 gradient copies");
   for (int q = 0; q < out_copies && out_off; ++q) a.out_off[q] = out_off[q];
   a.out_scale = out_scale;
   a.in_srcs = in_srcs;
   a.in_stride = in_stride;
-  const int64_t g3 = ceil_div(L.P, 256);
+  *grid = ceil_div(L.P, 256);
+  return TT_OK;
+}
+
+static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                     float lr, float beta1, float beta2, float eps, float weight_decay, int64_t* step_state,
+                     int do_adam, float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes,
+                     void* stream, const float* adam_pre = nullptr, const DdUpdateArgs* dd = nullptr,
+                     int64_t dd_grid = 0, int out_copies = 1, const int64_t* out_off = nullptr,
+                     float out_scale = 1.f, int in_srcs = 1, int64_t in_stride = 0) {
+  UpdateArgs a;
+  int64_t g3 = 0;
+  int rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, do_adam,
+                   grads_out, grads_in, workspace, ws_bytes, adam_pre, out_copies, out_off, out_scale, in_srcs,
+                   in_stride, a, &g3);
+  if (rc) return rc;
   if (dd) {
     if (dd_grid + g3 > INT32_MAX) return fail(TT_EINVAL, "tower_update_rowwise_adagrad: grid too large");
     tower_update_dedup_kernel<<<dim3((unsigned)(dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(a, *dd, (int)dd_grid);
@@ -1761,6 +1800,119 @@ int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* par
   if (!grads || nsrc < 1 || (nsrc > 1 && src_stride < L.P)) return fail(TT_EINVAL, "tower_adam_grads_sum: bad gradient");
   return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, 1,
                    nullptr, grads, workspace, ws_bytes, stream, nullptr, nullptr, 0, 1, 0, 1.f, nsrc, src_stride);
+}
+
+int tt_tower_adam_grads_sum_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
+                                            int nsrc, int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr,
+                                            float beta1, float beta2, float eps, float weight_decay,
+                                            int64_t* step_state, void* workspace, size_t ws_bytes,
+                                            const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                                            int F, int64_t emb_B, const float* emb_grad, int64_t ldg, float* weights,
+                                            float* state, float emb_lr, float emb_eps, void* dedup_ws,
+                                            size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!grads || !step_state || nsrc < 1 || (nsrc > 1 && src_stride < L.P))
+    return fail(TT_EINVAL, "tower_adam_grads_sum_rowwise_adagrad: bad gradient");
+  DdUpdateArgs d{};
+  int64_t dd_grid = 0;
+  rc = dedup_update_args(tables, T, features, F, emb_B, emb_grad, ldg, weights, state, emb_lr, emb_eps, dedup_ws,
+                         dedup_ws_bytes, dedup_max_lookups, d, &dd_grid);
+  if (rc) return rc;
+  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, 1, nullptr,
+                   grads, workspace, ws_bytes, stream, nullptr, &d, dd_grid, 1, nullptr, 1.f, nsrc, src_stride);
+}
+
+}  // extern "C"
+
+namespace tt {
+// shared by the two fused entry points: the next batch's route arguments (as tt_shard_route_segs)
+static int route_segs_args(int F, int64_t B, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
+                           const int64_t* block_sizes, const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                           int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                           size_t route_ws_bytes, RouteArgs& a) {
+  if (F < 1 || F > TT_MAX_FEATURES || W < 1 || W > RT_MAXW || B < 1) return fail(TT_EINVAL, "route: bad sizes");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "route: ids must be int32/int64");
+  if (!cols || !num_embeddings || !block_sizes || !owners || !segs || !send || !pos_in || !pos_out || !overflow)
+    return fail(TT_EINVAL, "route: null pointer");
+  if (!route_ws || route_ws_bytes < tt_shard_route_workspace_bytes(F, B))
+    return fail(TT_ECAPACITY, "route: workspace too small");
+  for (int f = 0; f < F; ++f) {
+    if (!cols[f] || num_embeddings[f] < 1) return fail(TT_EINVAL, "route: bad column");
+    if (block_sizes[f] < 0 || (block_sizes[f] == 0 && (owners[f] < 0 || owners[f] >= W)))
+      return fail(TT_EINVAL, "route: bad sharding of a feature");
+    if (block_sizes[f] > 0 && (num_embeddings[f] + block_sizes[f] - 1) / block_sizes[f] > W)
+      return fail(TT_EINVAL, "route: row blocks exceed the rank count");
+    if ((block_sizes[f] > 0 ? block_sizes[f] : num_embeddings[f]) >= (1ll << DD_TABLE_SHIFT))
+      return fail(TT_EINVAL, "route: local rows >= 2^40");
+    a.col[f] = cols[f];
+    a.num_emb[f] = num_embeddings[f];
+    a.block[f] = block_sizes[f];
+    a.owner[f] = owners[f];
+  }
+  a.id_dtype = id_dtype;
+  a.F = F;
+  a.W = W;
+  a.B = B;
+  a.C = 1;
+  a.nblk = (int)ceil_div(B, RT_BLOCK);
+  a.send = send;
+  a.pos = pos_in;
+  a.pos_out = pos_out;
+  a.segs = segs;
+  a.overflow = overflow;
+  char* ws = reinterpret_cast<char*>(route_ws);
+  a.dl = reinterpret_cast<int64_t*>(ws);
+  a.cnt = reinterpret_cast<int32_t*>(ws + align_up(sizeof(int64_t) * (size_t)F * (size_t)B, 256));
+  return TT_OK;
+}
+}  // namespace tt
+
+extern "C" {
+
+int tt_tower_wgrad_route_count(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                               int F, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
+                               const int64_t* block_sizes, const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                               int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                               size_t route_ws_bytes, void* stream) {
+  WgradArgs a{};
+  int64_t wgs = 0;
+  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
+  if (rc) return rc;
+  RouteArgs r{};
+  rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
+                       overflow, route_ws, route_ws_bytes, r);
+  if (rc) return rc;
+  tower_wgrad_route_kernel<<<dim3((unsigned)(wgs + (int64_t)r.nblk * F)), dim3(256), 0, as_stream(stream)>>>(
+      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), r, (int)wgs);
+  return check_launch("tower_wgrad_route_count");
+}
+
+int tt_tower_grads_replicated_route_place(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
+                                          int copies, const int64_t* offsets, float scale, void* workspace,
+                                          size_t ws_bytes, int F, const void* const* cols, int id_dtype,
+                                          const int64_t* num_embeddings, const int64_t* block_sizes,
+                                          const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                          int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                          size_t route_ws_bytes, void* stream) {
+  if (!params || !base || !offsets || copies < 1 || copies > 16) return fail(TT_EINVAL, "tower_grads_replicated: bad output");
+  RouteArgs r{};
+  int rc;
+  rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
+                       overflow, route_ws, route_ws_bytes, r);
+  if (rc) return rc;
+  int64_t off[16];
+  for (int q = 0; q < copies; ++q) off[q] = offsets[q];
+  if (copies == 1) off[1] = off[0];  // one copy takes the multi-copy path too (scale applied)
+  UpdateArgs a;
+  int64_t g3 = 0;
+  rc = t3_args(shape, B, params, nullptr, nullptr, 0.f, 0.9f, 0.999f, 1e-8f, 0.f, nullptr, 0, base, nullptr, workspace,
+               ws_bytes, nullptr, copies == 1 ? 2 : copies, off, scale, 1, 0, a, &g3);
+  if (rc) return rc;
+  tower_update_route_kernel<<<dim3((unsigned)(g3 + (int64_t)r.nblk * F)), dim3(256), 0, as_stream(stream)>>>(
+      a, r, (int)g3);
+  return check_launch("tower_grads_replicated_route_place");
 }
 
 int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,

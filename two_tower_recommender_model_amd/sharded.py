@@ -484,15 +484,16 @@ class FusedShardedTwoTowerStep:
                                             stream_handle(self.device)), "tower_grads_replicated")
 
     def _owner_update(self, parity: int) -> None:
+        """Adagrad over the received gradient rows + Adam on the fixed-order sum of the received
+        tower gradients, one launch."""
         lib, ts, r, tw = _lib.load(), self.tables, self.rank, self.towers
         ws = self.dd_ws[parity]
-        check(lib.tt_dedup_rowwise_adagrad(ts._tm, ts.T, self._fm_src, self.W, self.S[r], ptr(self.recvA), self.D,
-                                           ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws), ws.numel(),
-                                           self.max_lookups, stream_handle(self.device)), "dedup_rowwise_adagrad")
-        check(lib.tt_tower_adam_grads_sum(C.byref(tw.shape), self.B, ptr(self.params), ptr(self.recvA), self.W,
-                                          self.Asz[r], ptr(self.exp_avg), ptr(self.exp_avg_sq), self.lr_dense, 0.9,
-                                          0.999, 1e-8, 0.0, ptr(self.adam_state), ptr(tw.ws), tw.nbytes,
-                                          stream_handle(self.device)), "tower_adam_grads_sum")
+        check(lib.tt_tower_adam_grads_sum_rowwise_adagrad(
+            C.byref(tw.shape), self.B, ptr(self.params), ptr(self.recvA), self.W, self.Asz[r], ptr(self.exp_avg),
+            ptr(self.exp_avg_sq), self.lr_dense, 0.9, 0.999, 1e-8, 0.0, ptr(self.adam_state), ptr(tw.ws), tw.nbytes,
+            ts._tm, ts.T, self._fm_src, self.W, self.S[r], ptr(self.recvA), self.D, ptr(ts.weights), ptr(ts.state),
+            self.lr_emb, self.eps, ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device)),
+            "tower_adam_grads_sum_rowwise_adagrad")
 
     # ---- public steps ---------------------------------------------------------------------------
     def step(self) -> None:
@@ -514,9 +515,23 @@ class FusedShardedTwoTowerStep:
         self._exchange_b()
 
     def step_pipelined(self, labels: torch.Tensor, parity: int, next_cols: Sequence[torch.Tensor]) -> None:
-        """Step on the staged batch (rows in place, parity ``parity``), staging ``next_cols``."""
-        self._towers(parity, labels)
-        self._route(next_cols, parity ^ 1)
+        """Step on the staged batch (rows in place, parity ``parity``), staging ``next_cols``. The
+        next batch's route rides in the T2 and T3 launches (count / place workgroups)."""
+        lib, tw, B, dev = _lib.load(), self.towers, self.B, self.device
+        pin, pout = self.pos_in[parity], self.pos_out[parity]
+        check(lib.tt_tower_fwd_bwd_indexed2_bf16(
+            C.byref(tw.shape), B, ptr_array([pin[:B], pin[B:]]), ptr_array([pout[:B], pout[B:]]),
+            ptr_array([self.rows_in, self.rows_in]), ptr_array([self.sendA, self.sendA]), ptr(self.params),
+            ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), ptr(tw.ws), tw.nbytes, stream_handle(dev)),
+            "tower_fwd_bwd_indexed2")
+        route = (self.F, ptr_array(list(next_cols)), id_dtype_code(next_cols[0].dtype), self._ne, self._bs, self._ow,
+                 self.W, ptr(self.segs), ptr(self.sendA), ptr(self.pos_in[parity ^ 1]), ptr(self.pos_out[parity ^ 1]),
+                 ptr(self.flags), ptr(self.route_ws), self.route_ws.numel(), stream_handle(dev))
+        check(lib.tt_tower_wgrad_route_count(C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, *route),
+              "tower_wgrad_route_count")
+        check(lib.tt_tower_grads_replicated_route_place(C.byref(tw.shape), B, ptr(self.params), ptr(self.sendA), self.W,
+                                                        self._tw_off, 1.0 / self.W, ptr(tw.ws), tw.nbytes, *route),
+              "tower_grads_replicated_route_place")
         self._exchange_a()
         self._owner_update(parity)
         self._gather(parity ^ 1)

@@ -86,6 +86,10 @@ class TwoTowerTrainTask(nn.Module):
 
     def forward(self, batch: Batch):
         q, c = self.two_tower(batch.sparse_features)
+        if q.shape[0] == 1:
+            # the reference squeezes the [1] logits to 0-d (03_model_training.py:452) and
+            # BCEWithLogitsLoss then rejects the [1] labels: a batch of one cannot train there
+            raise ValueError(f"Target size ({batch.labels.shape}) must be the same as input size (torch.Size([]))")
         if self._k is None or self._k.device != q.device or self._k.max_batch < q.shape[0]:
             self._k = ops.DotBCE(q.device, max(self._max_batch, q.shape[0]))
         loss, logits = _DotBCE.apply(q, c, batch.labels, self._k)
