@@ -72,8 +72,8 @@ def _all_gather_rows(out: torch.Tensor, inp: torch.Tensor, pg) -> None:
 
 class _ShardedLookup(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, values, lengths, B, *params):
-        kt_values, saved = mod._forward_impl(values, lengths, B)
+    def forward(ctx, mod, dist_ctx, *params):
+        kt_values, saved = mod._lookup_output_dist(dist_ctx)
         ctx.mod = mod
         ctx.saved = saved
         return kt_values
@@ -81,7 +81,7 @@ class _ShardedLookup(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         ctx.mod._backward_impl(grad, ctx.saved)
-        return (None, None, None, None) + (None,) * len(ctx.mod._local_params())
+        return (None, None) + (None,) * len(ctx.mod._local_params())
 
 
 def _sharded_state_dict_hook(module, state_dict, prefix, local_metadata):
@@ -206,6 +206,7 @@ class ShardedEmbeddingBagCollection(nn.Module):
         self._f_table = f_table
         self._ts_cache: Dict[Tuple[str, int], object] = {}
         self._grad_anchor = nn.Parameter(torch.zeros(0, device=self._device))
+        self._prefetched: Dict[int, dict] = {}
         self._shard_of = {t: (lo, n) for (t, lo, n) in local_tables}
         self._register_state_dict_hook(_sharded_state_dict_hook)
         self._register_load_state_dict_pre_hook(_sharded_load_pre_hook, with_module=True)
@@ -244,6 +245,31 @@ class ShardedEmbeddingBagCollection(nn.Module):
 
     # -- forward
     def forward(self, features: KeyedJaggedTensor) -> KeyedTensor:
+        d = self._prefetched.pop(id(features), None)
+        if d is None:
+            d = self.input_dist(features)
+        elif d["stream"] is not None:  # staged by TrainPipelineSparseDist on its data-dist stream
+            cur = torch.cuda.current_stream(self._device)
+            cur.wait_event(d["event"])
+            for t in d["tensors"]:
+                t.record_stream(cur)
+        vals = _ShardedLookup.apply(self, d, self._grad_anchor)
+        return KeyedTensor(self._feature_names, self._dims, vals)
+
+    def prefetch(self, features: KeyedJaggedTensor) -> None:
+        """input_dist of a batch ahead of its forward (TrainPipelineSparseDist's second stage), on the
+        current stream; ``forward(features)`` of the same KJT object then consumes it."""
+        d = self.input_dist(features)
+        if torch.cuda.is_available() and self._device.type == "cuda":
+            s = torch.cuda.current_stream(self._device)
+            d["stream"] = s
+            d["event"] = torch.cuda.Event()
+            d["event"].record(s)
+        self._prefetched[id(features)] = d
+
+    def input_dist(self, features: KeyedJaggedTensor) -> dict:
+        """torchrec input_dist: KJT permute to the EBC's feature order, TW keys grouped by owner, RW
+        ids block-bucketized, then the counts / lengths / ids all-to-alls; returns the local KJTs."""
         if list(features.keys()) != self._feature_names:
             idx = [list(features.keys()).index(f) for f in self._feature_names]
             features = features.permute(idx)
@@ -252,10 +278,9 @@ class ShardedEmbeddingBagCollection(nn.Module):
         if values.dtype not in (torch.int32, torch.int64):
             values = values.to(torch.int64)
         lengths = features.lengths().to(torch.int32)
-        vals = _ShardedLookup.apply(self, values, lengths, B, self._grad_anchor)
-        return KeyedTensor(self._feature_names, self._dims, vals)
+        return self._input_dist_impl(values, lengths, B)
 
-    def _forward_impl(self, values: torch.Tensor, lengths: torch.Tensor, B: int):
+    def _input_dist_impl(self, values: torch.Tensor, lengths: torch.Tensor, B: int) -> dict:
         be, W, pg, dev = self._be, self._W, self._pg, self._device
         F = len(self._feature_names)
         offsets = be.complete_cumsum(lengths)
@@ -332,6 +357,16 @@ class ShardedEmbeddingBagCollection(nn.Module):
             vo += recv[s][1]
             rw_vals.append(v_recv[vo:vo + recv[s][2]])
             vo += recv[s][2]
+        tensors = [l_recv, v_recv] + tw_lens + rw_lens + tw_vals + rw_vals
+        return {"B": B, "Bm": Bm, "Bs": Bs, "tw_lens": tw_lens, "rw_lens": rw_lens, "tw_vals": tw_vals,
+                "rw_vals": rw_vals, "tensors": tensors, "stream": None}
+
+    def _lookup_output_dist(self, d: dict):
+        """Local lookups on the shards, then output_dist (TW all-to-all, RW reduce-scatter)."""
+        be, W, pg, dev = self._be, self._W, self._pg, self._device
+        B, Bm, Bs = d["B"], d["Bm"], d["Bs"]
+        tw_lens, rw_lens, tw_vals, rw_vals = d["tw_lens"], d["rw_lens"], d["tw_vals"], d["rw_vals"]
+        ntw, nrw, nme = len(self._tw_order), len(self._rw_feats), len(self._tw_me)
         saved = {"B": B, "Bm": Bm, "Bs": Bs}
         out = torch.empty(B, self._out_dim, dtype=torch.float32, device=dev)
         # ---- TW lookup + output all-to-all

@@ -2,10 +2,11 @@
 
 ``DistributedModelParallel(module=train_task, device=device)`` (03_model_training.py:812-815):
 one process per GPU. The module's EmbeddingBagCollections are placed by the sharding plan (the
-reference builds no plan argument, so the default planner runs, 03:809-815): at world size 1 they
-are materialised on the device (meta tables get torchrec's default init); at W > 1 each is replaced
-by a ShardedEmbeddingBagCollection (table-wise / row-wise shards, RCCL all-to-all and
-reduce-scatter over xGMI). Dense modules are replicated: parameters broadcast from rank 0 and
+reference builds no plan argument, so the default planner runs, 03:809-815): with a process group
+(the reference always initialises one, 03:751) each is replaced by a ShardedEmbeddingBagCollection
+(table-wise / row-wise shards, RCCL all-to-all and reduce-scatter over xGMI) — at world size 1 too,
+as torchrec does; without one (single-process use) the tables are materialised on the device (meta
+tables get torchrec's default init). Dense modules are replicated: parameters broadcast from rank 0 and
 gradients all-reduced (averaged) by torch DDP with the table parameters excluded, as torchrec does.
 """
 from __future__ import annotations
@@ -54,7 +55,7 @@ class DistributedModelParallel(nn.Module):
         self._sharded_paths: List[str] = []
         for path, ebc in [(n, m) for n, m in module.named_modules() if isinstance(m, EmbeddingBagCollection)]:
             mplan = plan.get_plan_for_module(path) or {}
-            if self._world_size == 1:
+            if self._pg is None:
                 ebc._materialize(self.device)
             else:
                 sharded = ShardedEmbeddingBagCollection(ebc, mplan, self._pg, self.device)

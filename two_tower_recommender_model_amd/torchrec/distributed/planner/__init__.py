@@ -5,7 +5,7 @@ The plan is explicit and deterministic (the cost-model search of torchrec's plan
 scope): a table larger than half of one rank's fair share of all table bytes is sharded ROW_WISE
 over every rank (contiguous row blocks of ceil(N / W)); the others are placed TABLE_WISE greedily
 on the rank with the least bytes. ``ParameterConstraints(sharding_types=[...])`` per table name
-overrides the choice. World size 1 places everything table-wise on rank 0.
+overrides the choice. World size 1 places everything table-wise on rank 0 unless a constraint says otherwise.
 """
 from __future__ import annotations
 
@@ -83,7 +83,7 @@ class EmbeddingShardingPlanner:
                 st = None
                 if forced is not None and forced.sharding_types:
                     st = forced.sharding_types[0]
-                if W == 1:
+                if st is None and W == 1:
                     st = ShardingType.TABLE_WISE.value
                 elif st is None:
                     st = ShardingType.ROW_WISE.value if size[c.name] > fair_half else ShardingType.TABLE_WISE.value

@@ -3,15 +3,32 @@
 ``TrainPipelineSparseDist(model, optimizer, device)`` and ``progress(iterator)`` as driven by the
 reference's train/evaluate loops (03_model_training.py:545, :618, :648): each call trains (or, in
 ``eval()`` mode, only runs forward on) one batch and returns the model output's second element
-``(loss, logits, labels)``; it raises StopIteration once the iterator is drained. The next batch's
-host->device copy is issued on a separate copy stream while the current batch computes (the
-H2D stage of torchrec's 3-stage pipeline; input_dist runs inside the sharded module's forward).
+``(loss, logits, labels)``; it raises StopIteration once the iterator is drained.
+
+Three stages over three streams, as torchrec's pipeline:
+  memcpy stream     host -> device copy of batch i+2
+  data-dist stream  input_dist of batch i+1 in every ShardedEmbeddingBagCollection of the model
+                    (KJT permute / bucketize + the counts, lengths and ids all-to-alls)
+  current stream    forward / backward / optimizer.step of batch i (its lookups consume the staged
+                    input_dist: ``ShardedEmbeddingBagCollection.prefetch``)
+Batch i's kernels are queued before batch i+1's input_dist starts, so the host-side waits of that
+input_dist (its split sizes) overlap batch i's device work. input_dist reads only ids, so running it
+before batch i's table update is exact. Without sharded modules the pipeline has two stages.
 """
 from __future__ import annotations
 
-from typing import Any, Iterator, Optional
+from typing import Any, Iterator, List, Optional
 
 import torch
+
+
+class _Staged:
+    __slots__ = ("batch", "h2d", "dist")
+
+    def __init__(self, batch, h2d):
+        self.batch = batch
+        self.h2d = h2d
+        self.dist = False
 
 
 class TrainPipelineBase:
@@ -19,51 +36,60 @@ class TrainPipelineBase:
         self._model = model
         self._optimizer = optimizer
         self._device = torch.device(device)
-        self._cur: Optional[Any] = None
-        self._next: Optional[Any] = None
-        self._next_event = None
+        self._cuda = self._device.type == "cuda"
+        self._memcpy_stream = torch.cuda.Stream(device=self._device) if self._cuda else None
+        self._cur: Optional[_Staged] = None    # batch i (input_dist staged)
+        self._next: Optional[_Staged] = None   # batch i+1 (copy issued)
         self._connected = False
-        self._memcpy_stream = torch.cuda.Stream(device=self._device) if self._device.type == "cuda" else None
 
-    def _to_device(self, batch):
-        if self._memcpy_stream is None:
-            return batch.to(self._device, non_blocking=True), None
+    def _sharded(self) -> List[Any]:
+        return []
+
+    def _fetch(self, it: Iterator) -> Optional[_Staged]:
+        try:
+            batch = next(it)
+        except StopIteration:
+            return None
+        if not self._cuda:
+            return _Staged(batch.to(self._device, non_blocking=True), None)
         with torch.cuda.stream(self._memcpy_stream):
             b = batch.to(self._device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._memcpy_stream)
-        return b, ev
+        return _Staged(b, ev)
 
-    def _fetch(self, it: Iterator):
-        batch = next(it)  # StopIteration propagates
-        return self._to_device(batch)
+    def _start_sparse_data_dist(self, st: Optional[_Staged]) -> None:
+        pass
+
+    def _wait(self, st: _Staged) -> None:
+        if st.h2d is not None:
+            cur = torch.cuda.current_stream(self._device)
+            cur.wait_event(st.h2d)
+            if hasattr(st.batch, "record_stream"):
+                st.batch.record_stream(cur)
 
     def progress(self, dataloader_iter: Iterator) -> Any:
         if self._cur is None:
-            if self._next is not None:
-                self._cur, ev = self._next, self._next_event
-                self._next = self._next_event = None
-            else:
-                self._cur, ev = self._fetch(dataloader_iter)
-            if ev is not None:
-                torch.cuda.current_stream(self._device).wait_event(ev)
-                if hasattr(self._cur, "record_stream"):
-                    self._cur.record_stream(torch.cuda.current_stream(self._device))
-        batch = self._cur
-        # stage the next batch's copy while this one computes
-        if self._next is None:
-            try:
-                self._next, self._next_event = self._fetch(dataloader_iter)
-            except StopIteration:
-                self._next = self._next_event = None
+            # (re)fill: batch i copied and its input_dist staged, batch i+1's copy issued
+            self._cur = self._fetch(dataloader_iter)
+            if self._cur is None:
+                raise StopIteration
+            self._start_sparse_data_dist(self._cur)
+            self._next = self._fetch(dataloader_iter)
+        st = self._cur
+        self._wait(st)
         training = self._model.training
         if training:
             self._optimizer.zero_grad(set_to_none=True)
-        losses, output = self._model(batch)
+        losses, output = self._model(st.batch)
         if training:
             torch.sum(losses, dim=0).backward()
             self._optimizer.step()
-        self._cur = None
+        # stages 2 and 1 for the following batches, behind batch i's queued kernels
+        self._cur, self._next = self._next, None
+        if self._cur is not None:
+            self._start_sparse_data_dist(self._cur)
+            self._next = self._fetch(dataloader_iter)
         return output
 
 
@@ -71,3 +97,27 @@ class TrainPipelineSparseDist(TrainPipelineBase):
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer, device: torch.device,
                  execute_all_batches: bool = True, apply_jit: bool = False):
         super().__init__(model, optimizer, device)
+        self._data_dist_stream = torch.cuda.Stream(device=self._device) if self._cuda else None
+
+    def _sharded(self) -> List[Any]:
+        from .embeddingbag import ShardedEmbeddingBagCollection
+
+        return [m for m in self._model.modules() if isinstance(m, ShardedEmbeddingBagCollection)]
+
+    def _start_sparse_data_dist(self, st: Optional[_Staged]) -> None:
+        mods = self._sharded()
+        if st is None or st.dist or not mods:
+            return
+        kjt = getattr(st.batch, "sparse_features", None)
+        if kjt is None:
+            return
+        if self._data_dist_stream is None:
+            for m in mods:
+                m.prefetch(kjt)
+        else:
+            with torch.cuda.stream(self._data_dist_stream):
+                if st.h2d is not None:
+                    self._data_dist_stream.wait_event(st.h2d)
+                for m in mods:
+                    m.prefetch(kjt)
+        st.dist = True
