@@ -61,6 +61,9 @@ def parse():
                          "= 537 MB touched: past the 256 MiB Infinity Cache)")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--steps-per-graph", type=int, default=8, choices=[1, 2, 4, 8])
+    ap.add_argument("--host-fed", action="store_true",
+                    help="feed host batches through the 3-stage host pipeline (pinned staging, async H2D on a "
+                         "copy stream, graph replay): the PCIe-inclusive rate, reported beside the resident one")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
     return ap.parse_args()
@@ -555,6 +558,32 @@ def run_single(args):
     return value, ms, loss, roofline, cpu, steps_run
 
 
+def run_host_fed(args):
+    """The fused step fed from HOST batches (host_pipeline.HostFedPipeline): numpy columns as the
+    reference's loader yields them -> pinned staging -> async H2D on a copy stream -> k-step graph
+    replays; the host copies overlap the device. pairs/s over K steps (PCIe-inclusive)."""
+    import itertools
+
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+    from two_tower_recommender_model_amd.host_pipeline import HostFedPipeline, synthetic_host_batches
+
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
+                             lr_dense=0.01, id_dtype=torch.int64, seed=0)
+    host = synthetic_host_batches([num_users, num_items], B, args.batches, seed=1)
+    pipe = HostFedPipeline(step, group=args.steps_per_graph, depth=3)
+    src = itertools.cycle(host)
+    pipe.run(src, max_steps=args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = pipe.run(src, max_steps=args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return n * B / dt, dt / n * 1e3, float(step.loss), n
+
+
 def run_multi(args, world, rank, local_rank):
     """N >= 1 ranks, one per GPU: the pipelined sharded single-hot step (row-wise shards of both
     tables; per step one all-to-all of [gradient rows | tower gradient | next batch's ids] and one of
@@ -642,6 +671,11 @@ def main():
             raise SystemExit(f"{args.workload}: the multi-hot workload runs at N = 1 (unsharded tables)")
         value, ms, loss, roofline, cpu, steps_run = run_multihot(args)
         config["parallelism"] = "single-gpu hipgraph, KJT input"
+    elif world == 1 and args.host_fed:
+        value, ms, loss, steps_run = run_host_fed(args)
+        roofline, cpu = None, None
+        config["parallelism"] = "single-gpu, host-fed: pinned staging + async H2D (copy stream) + hipgraph replay"
+        config["note"] = "PCIe-inclusive rate (inputs handed over in host memory); the resident-input line is the metric"
     elif world == 1 and not args.sharded:
         value, ms, loss, roofline, cpu, steps_run = run_single(args)
     else:

@@ -1,0 +1,151 @@
+"""Host-fed pipeline for the fused single-GPU step: TrainPipelineSparseDist's three stages
+(03_model_training.py:618, :648) around ``FusedTwoTowerStep`` graphs.
+
+The reference's loader yields host columns ``{user_id, product_id, label}`` (03:386-393) that
+``transform_to_torchrec_batch`` turns into a KJT on the host, one element at a time (03:353-380).
+Here the host only copies the raw columns; the transform (id 0 dropped, id % N) runs inside the
+step's kernels. Per group of ``group`` batches (one HIP graph of ``group`` steps per device slot):
+
+  stage 1  host     columns of group g+2 -> a pinned staging slot (CPU memcpy)
+           copy     pinned slot -> device slot of group g+2 (async H2D on the copy stream), after
+                    the graph that last read that device slot has finished (event)
+  stage 2  copy     the device slot of group g+1 is complete (its H2D event) — the single-hot
+                    step has no separate input_dist: the KJT build is fused into T1
+  stage 3  compute  graph replay of group g on the step's stream, after its H2D event
+
+``depth`` device / pinned slots rotate (3: one computing, one landing, one being filled), so the
+host's memcpy and the PCIe copy of later groups overlap the graph of the current one.
+"""
+from __future__ import annotations
+
+from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+class HostFedPipeline:
+    def __init__(self, step, group: int = 8, depth: int = 3):
+        """step: a FusedTwoTowerStep (single-hot columns). group: batches per graph replay."""
+        if getattr(step, "kjt_input", False):
+            raise _lib.TTError("HostFedPipeline: single-hot column input only")
+        self.step = step
+        self.group = int(group)
+        self.depth = int(depth)
+        if self.group < 1 or self.depth < 2:
+            raise _lib.TTError("HostFedPipeline: group >= 1, depth >= 2")
+        dev, B, F = step.device, step.B, step.F
+        self.device = dev
+        idt = step.id_dtype
+        # device slots: per slot, `group` batches of F id columns + labels (read in place by graphs)
+        self.dev_ids = [torch.zeros(self.group, F, B, dtype=idt, device=dev) for _ in range(self.depth)]
+        self.dev_lab = [torch.zeros(self.group, B, dtype=torch.int32, device=dev) for _ in range(self.depth)]
+        self.pin_ids = [torch.zeros(self.group, F, B, dtype=idt).pin_memory() for _ in range(self.depth)]
+        self.pin_lab = [torch.zeros(self.group, B, dtype=torch.int32).pin_memory() for _ in range(self.depth)]
+        # numpy views of the pinned slots: the host copy is a plain memcpy per column
+        self.pin_ids_np = [t.numpy() for t in self.pin_ids]
+        self.pin_lab_np = [t.numpy() for t in self.pin_lab]
+        self.copy_stream = torch.cuda.Stream(device=dev)
+        self.h2d_done: List[Optional[torch.cuda.Event]] = [None] * self.depth   # slot landed
+        self.slot_free: List[Optional[torch.cuda.Event]] = [None] * self.depth  # graph that read it ended
+        self.filled: List[int] = [0] * self.depth                               # batches in the slot
+        # one graph per slot (group steps, or fewer for a final partial group: eager steps)
+        batches = []
+        for s in range(self.depth):
+            for j in range(self.group):
+                batches.append(([self.dev_ids[s][j, f] for f in range(F)], self.dev_lab[s][j]))
+        step.capture_pool(batches, steps_per_graph=self.group)
+        self.graphs = list(step.pool_graphs)
+
+    # -- stage 1
+    def _fill(self, slot: int, it: Iterator) -> int:
+        """Host columns of up to `group` batches -> pinned slot -> async H2D. Returns the count."""
+        if self.h2d_done[slot] is not None:
+            self.h2d_done[slot].synchronize()  # the pinned buffer's previous copy has left
+        n = 0
+        for j in range(self.group):
+            try:
+                cols, labels = next(it)
+            except StopIteration:
+                break
+            for f, c in enumerate(cols):
+                self.pin_ids_np[slot][j, f] = np.asarray(c)
+            self.pin_lab_np[slot][j] = np.asarray(labels)
+            n += 1
+        self.filled[slot] = n
+        if n == 0:
+            return 0
+        with torch.cuda.stream(self.copy_stream):
+            if self.slot_free[slot] is not None:
+                self.copy_stream.wait_event(self.slot_free[slot])
+            self.dev_ids[slot][:n].copy_(self.pin_ids[slot][:n], non_blocking=True)
+            self.dev_lab[slot][:n].copy_(self.pin_lab[slot][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        self.h2d_done[slot] = ev
+        return n
+
+    # -- stage 3
+    def _compute(self, slot: int) -> None:
+        main = torch.cuda.current_stream(self.device)
+        main.wait_event(self.h2d_done[slot])
+        n = self.filled[slot]
+        if n == self.group:
+            self.graphs[slot].replay()
+        else:  # a final partial group: the same kernels, eagerly
+            st = self.step
+            keep = st.cols, st.labels
+            try:
+                for j in range(n):
+                    st.cols = [self.dev_ids[slot][j, f] for f in range(st.F)]
+                    st.labels = self.dev_lab[slot][j]
+                    st.step()
+            finally:
+                st.cols, st.labels = keep
+        ev = torch.cuda.Event()
+        ev.record(main)
+        self.slot_free[slot] = ev
+
+    def run(self, host_batches: Iterable[Tuple[Sequence, object]], max_steps: Optional[int] = None) -> int:
+        """Train on host batches ((id columns, labels) per batch: numpy arrays or CPU tensors of the
+        step's id dtype / int) until the iterable (or max_steps) is exhausted; returns the steps
+        run. Asynchronous: synchronize the device before reading results."""
+        it = iter(host_batches)
+        if max_steps is not None:
+            import itertools
+
+            it = itertools.islice(it, max_steps)
+        D = self.depth
+        steps = 0
+        # prologue: groups 0 .. depth-2 in flight
+        for g in range(D - 1):
+            self._fill(g % D, it)
+        g = 0
+        while True:
+            slot = g % D
+            if self.filled[slot] == 0:
+                break
+            self._compute(slot)
+            steps += self.filled[slot]
+            nxt = (g + D - 1) % D
+            self._fill(nxt, it)
+            g += 1
+        return steps
+
+
+def synthetic_host_batches(num_embeddings: Sequence[int], B: int, n: int, seed: int = 0, zero_frac: float = 0.0):
+    """n host batches of single-hot id columns (int64, uniform over [0, N)) and Bernoulli labels —
+    what the reference's dataloader yields per batch (03:386-393), as numpy arrays."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        cols = []
+        for N in num_embeddings:
+            c = rng.integers(0, N, B, dtype=np.int64)
+            if zero_frac:
+                c[rng.random(B) < zero_frac] = 0
+            cols.append(c)
+        out.append((cols, rng.integers(0, 2, B, dtype=np.int32)))
+    return out
