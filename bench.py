@@ -210,27 +210,31 @@ def cpu_model() -> str:
 
 
 def lookup_stats(step, batches):
-    """Kept lookups and unique (table, row) pairs per step, averaged over the resident batches."""
-    nnz = uniq = 0
+    """Kept lookups, unique (table, row) pairs and rows looked up exactly once per step, averaged
+    over the resident batches."""
+    nnz = uniq = once = 0
     for cols, _ in batches:
         keys = torch.cat([(c % n) + (t << 40) for t, (c, n) in enumerate(zip(cols, step.num_embeddings))])
         nz = torch.cat([c != 0 for c in cols])
         nnz += int(nz.sum())
-        uniq += int(torch.unique(keys[nz]).numel())
-    return nnz // len(batches), uniq // len(batches)
+        u, cnt = torch.unique(keys[nz], return_counts=True)
+        uniq += int(u.numel())
+        once += int((cnt == 1).sum())
+    n = len(batches)
+    return nnz // n, uniq // n, once // n
 
 
-def launch_bytes(step, nnz: int, uniq: int):
-    """Per launch of the one-stream step: ``alg`` = the launch's share of the
-    SURVEY.md 8(d) algorithmic bytes (the FBGEMM convention: every lookup's id + row in the forward,
-    4 B length + 4D pooled write + 4D gradient read per bag, unique rows' weight + state read and
-    write in the backward); ``design`` = what the launch moves by design (incl. the T1 -> T2 bf16
-    operand strips, the split-K slabs and the dedup slots); ``flop`` = tower MFMA flops.
-      t1 = gather + towers fwd/bwd + dedup insert: 8(d) ids fwd + rows + lengths + pooled (the
-           pooled rows stay on chip; T1 writes the pooled gradient dX instead, same bytes);
-      t2 = tower weight gradients (+ Adam scalars): no 8(d) bytes;
-      k3 = T3 (slab reduction + Adam + bf16 copies) + the fused row-wise Adagrad: 8(d) ids bwd +
-           gradient rows + unique rows' weight and state read-modify-write."""
+def launch_bytes(step, nnz: int, uniq: int, once: int):
+    """Per launch of the production ring step: ``alg`` = the launch's share of
+    the SURVEY.md 8(d) algorithmic bytes (the FBGEMM convention: every lookup's id + row in the
+    forward, 4 B length + 4D pooled write + 4D gradient read per bag, unique rows' weight + state
+    read and write in the backward); ``design`` = what the launch moves by design (incl. the T1 -> T2
+    bf16 operand strips, the split-K slabs and the dedup slots); ``flop`` = tower MFMA flops.
+      t1 = gather + towers fwd/bwd + the in-place update of the `once` rows looked up once: 8(d) ids
+           fwd + rows + lengths + pooled (kept on chip) and, for those rows, ids bwd + gradient
+           (on chip) + weight and state read-modify-write;
+      t2 = tower weight gradients + Adam scalars + the next batch's dedup insert: no 8(d) bytes;
+      k3 = resolver + update of the rows looked up more than once + T3: the rest of 8(d)."""
     D, B, F = step.dims[0], step.B, step.F
     L = step.layer_sizes
     idb = 8 if step.id_dtype == torch.int64 else 4
@@ -240,18 +244,20 @@ def launch_bytes(step, nnz: int, uniq: int):
     cdiv = lambda a, b: -(-a // b)  # noqa: E731
     S = min(64, cdiv(B, 256))  # staged T2 slices of whole 256-row passes (tower.hip tower_layout)
     S = cdiv(B, cdiv(cdiv(B, S), 256) * 256)
-    t1_design = (F * B * idb + B * 4 + nnz * 4 * D + B * 4 + F * B * 4 * D + opnd + nnz * 20)
-    emb_upd = uniq * (64 + 8 * D + 8) + nnz * 4 * D
-    t2_design = opnd + S * P * 4
-    k3_design = emb_upd + S * P * 4 + 6 * P * 4 + 4 * P
-    t1_alg = nnz * (8 + 4 * D) + F * B * (4 + 4 * D)
-    k3_alg = nnz * 8 + F * B * 4 * D + uniq * (8 * D + 8)
+    multi = nnz - once  # lookups of rows looked up more than once
+    t1_design = (F * B * idb + B * 4 + nnz * 4 * D + F * B * 12 + once * (8 * D + 8) + multi * 4 * D + opnd)
+    t2_design = opnd + S * P * 4 + F * B * (idb + 20)
+    k3_design = (F * B * (4 + 64) + (uniq - once) * (8 * D + 8) + multi * 4 * D + S * P * 4 + 6 * P * 4 + 4 * P)
+    t1_alg = nnz * (8 + 4 * D) + F * B * (4 + 4 * D) + once * (8 + 4 * D + 8 * D + 8)
+    k3_alg = multi * 8 + (F * B - once) * 4 * D + (uniq - once) * (8 * D + 8)
     return {"t1": {"alg_bytes": t1_alg, "design_bytes": t1_design, "flop": 8 * B * macs,
-                   "what": "tower_l2_kernel: EBC gather + both towers fwd/bwd + dedup insert"},
+                   "what": "tower_l2_kernel<UPD>: EBC gather + both towers fwd/bwd + row-wise Adagrad of the rows "
+                           "looked up once"},
             "t2": {"alg_bytes": 0, "design_bytes": t2_design, "flop": 4 * B * macs,
-                   "what": "tower_wgrad_kernel: tower weight gradients (staged operand strips) + Adam step scalars"},
+                   "what": "tower_wgrad_insert_kernel: tower weight gradients + Adam scalars + next batch's dedup insert"},
             "k3": {"alg_bytes": k3_alg, "design_bytes": k3_design, "flop": 0,
-                   "what": "tower_update_dedup_kernel: fused row-wise Adagrad + slab reduction + Adam + bf16 copies"},
+                   "what": "tower_update_dedup_resolve_kernel: next batch's deferred inserts + row-wise Adagrad of the "
+                           "rows looked up more than once + slab reduction + Adam + bf16 copies"},
             "_emb_path_bytes": t1_alg + k3_alg}
 
 
@@ -277,7 +283,7 @@ def pmc_traffic(kernel_name: str, workload: str = "northstar"):
     return None, None
 
 
-KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_kernel", "k3": "tower_update_dedup_kernel"}
+KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_insert_kernel", "k3": "tower_update_dedup_resolve_kernel"}
 
 
 def synth_kjt_batches(num_users, num_items, B, maxlen, n, device, ids, seed):
@@ -428,7 +434,7 @@ def cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen):
                       f"host CPU {cpu_model()}"}
 
 
-def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northstar"):
+def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northstar", once=None):
     """``roofline`` of the dominant launch (T1): achieved = its SURVEY 8(d) bytes / its average
     device time; ``traffic`` = its HBM bytes per launch from the committed PMC summary; per-launch
     design bytes, flops and MFMA fractions beside it; the whole embedding path (8(d) bytes per step)
@@ -454,7 +460,7 @@ def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northsta
             "frac_over_step": round(emb_path_bytes / ms_step / 1e6 / HBM_PEAK_GBS, 4)}
     if not timed:
         return {"bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq, "embedding_path": path}
+                "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq, "rows_looked_up_once": once, "embedding_path": path}
     dom = "t1"  # the longest launch, and the one that carries the forward's row reads
     emb_ms = timed.get("t1", 0.0) + timed.get("k3", 0.0)
     ach = out[dom]["alg_GB/s"]
@@ -465,10 +471,11 @@ def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northsta
     return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": out[dom]["pmc_hbm_bytes"],
             "traffic_source": out[dom]["pmc_source"], "alg_bytes_per_launch": out[dom]["alg_bytes"],
-            "alg_bytes_rule": "SURVEY 8(d) share of T1 per kept lookup: 8 B id + 4D row; per bag: 4 B length + "
-                              "4D pooled row (T1 keeps the pooled rows on chip and writes dX, the same bytes)",
+            "alg_bytes_rule": "SURVEY 8(d) share of T1: per kept lookup 8 B id + 4D row; per bag 4 B length + 4D "
+                              "pooled row (kept on chip); per row looked up once 8 B id + 4D gradient (on chip) + "
+                              "8D weight read/write + 8 B state read/write",
             "design_bytes_per_launch": out[dom]["design_bytes"], "ms_per_launch": out[dom]["ms"],
-            "kernels": out, "lookups": nnz, "unique_rows": uniq, "embedding_path": path}
+            "kernels": out, "lookups": nnz, "unique_rows": uniq, "rows_looked_up_once": once, "embedding_path": path}
 
 
 def run_single(args):
@@ -481,22 +488,14 @@ def run_single(args):
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
     nb = max(args.steps_per_graph, args.batches // args.steps_per_graph * args.steps_per_graph)
     batches = synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1)
-    # HIP graphs over the resident batches, k full steps per graph (no input copies): a graph
-    # launch costs the host ~35-55 us, more than a step's GPU time, so k > 1 keeps the GPU fed
-    # (graphs of k steps, plus single-step graphs for a remainder, so exactly K steps are timed)
+    # the production ring: HIP graphs of k full steps over the resident batches (no input copies;
+    # each step files the next batch's dedup table): a graph launch costs the host ~35-55 us, more
+    # than a step's GPU time, so k > 1 keeps the GPU fed (single-step graphs for a remainder)
     k = args.steps_per_graph
-    step.capture_pool(batches, steps_per_graph=k)
-    big = step.pool_graphs
-    step.capture_pool(batches, steps_per_graph=1)
-    small = step.pool_graphs
+    step.capture_ring(batches, steps_per_graph=k)
 
-    def run(n, i=0):
-        while n >= k:
-            big[(i // k) % len(big)].replay()
-            i, n = i + k, n - k
-        while n > 0:
-            small[i % len(small)].replay()
-            i, n = i + 1, n - 1
+    def run(n):
+        step.run(n)
 
     run(args.warmup)
     torch.cuda.synchronize()
@@ -511,20 +510,20 @@ def run_single(args):
     # ---- per-launch device time inside the replayed graphs: the same graphs re-captured with
     # event-record nodes around every kernel node (graph_timing.py), replayed for K steps;
     # eager steps with HIP events around each launch if the graph cannot be instrumented
-    nnz, uniq = lookup_stats(step, batches)
-    kern = launch_bytes(step, nnz, uniq)
+    nnz, uniq, once = lookup_stats(step, batches)
+    kern = launch_bytes(step, nnz, uniq, once)
     timed, timing_how = None, None
-    if step.gather and step.dedup_single and step.combined_bwd:
+    if step.ring_supported():
         try:
             from two_tower_recommender_model_amd.graph_timing import GraphLaunchTimer
 
-            step.capture_pool(batches, steps_per_graph=k, keep_graph=True)
+            step.capture_ring(batches, steps_per_graph=k, keep_graph=True)
             names = ["t1", "t2", "k3"]
-            timers = [GraphLaunchTimer(g, list(range(3 * k))) for g in step.pool_graphs]
+            timers = [GraphLaunchTimer(g, list(range(3 * k))) for g in step.ring_graphs]
             acc = {n: [] for n in names}
             n_done, j = 0, 0
             while n_done < args.steps:
-                step.pool_graphs[j % len(step.pool_graphs)].replay()
+                step.ring_graphs[j % len(step.ring_graphs)].replay()
                 torch.cuda.synchronize()
                 for i, t_ms in enumerate(timers[j % len(timers)].elapsed()):
                     acc[names[i % 3]].append(t_ms)
@@ -536,7 +535,7 @@ def run_single(args):
         except Exception as e:  # noqa: BLE001
             print(f"graph instrumentation unavailable ({e}); eager per-launch events", file=sys.stderr)
     if timed is None:
-        timed = step.timed_steps(batches, args.steps)
+        timed = step.timed_ring(args.steps) if step.ring_supported() else step.timed_steps(batches, args.steps)
         timing_how = "HIP events around each launch on its stream over K eager steps of the same sequence"
     # an event-record node in front of a kernel node adds its own dispatch latency to the measured
     # span (about 2 us a launch on this stack); the spans are scaled so that they sum to the step
@@ -549,7 +548,7 @@ def run_single(args):
         timing_how += ("; each span scaled by (step time without event nodes) / (sum of the spans) = "
                        f"{ms / tot:.3f}")
     roofline = roofline_report(kern, timed, nnz, uniq, step, B, ms,
-                               args.workload if args.ids == "uniform" else f"{args.workload}_{args.ids}")
+                               args.workload if args.ids == "uniform" else f"{args.workload}_{args.ids}", once)
     roofline["timing"] = timing_how
     roofline["event_span_ms"] = {n: round(v, 5) for n, v in raw.items()}
     cpu = None

@@ -285,6 +285,40 @@ int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void
                             const void* labels, int label_dtype, float grad_scale, float* logits,
                             const int32_t* dedup_tables, void* dedup_ws, size_t dedup_ws_bytes,
                             int64_t dedup_max_lookups, void* workspace, size_t ws_bytes, void* stream);
+/* ---- the pipelined fused step: dedup one step ahead, single-lookup rows updated inside T1 ----------
+ * Step i: T1 (gather + towers + in-place row-wise Adagrad of batch i's rows looked up ONCE, from
+ * batch i's dedup table completed by step i-1) -> T2 (weight gradients + the insert of batch i+1
+ * into the other table) -> K3 (deferred inserts of batch i+1 resolved, batch i's rows looked up more
+ * than once updated from dX, T3). The first batch's table is built by tt_dedup_insert_cols. */
+/* T1 as tt_tower_fwd_bwd_gather, plus: a kept lookup (t, m) whose slot in dedup_ws (its claim, count
+ * 1) says its row is looked up once in the step updates table_rows[t] / table_state[t] in place
+ * (lr, eps: torchrec RowWiseAdagrad, 03_model_training.py:791-795); dX goes to gpooled for the
+ * others (for every lookup with pooled_out). Shapes: in_dim in {64, 128}, widths [128, 64]. */
+int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
+                                   const int64_t* num_embeddings, float* const* table_rows, float* const* table_state,
+                                   float* pooled_out, int64_t ldp, float* gpooled, const float* params,
+                                   const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
+                                   float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
+                                   void* workspace, size_t ws_bytes, void* stream);
+/* tt_tower_wgrad_pre + the insert of the NEXT batch's lookups (i = t * B + m, key dedup_tables[t]
+ * << 40 | id mod N) into next_dedup_ws (first CAS here, the rest deferred to the resolver of the
+ * following tt_tower_update_pre_rowwise_adagrad_resolve). */
+int tt_tower_wgrad_pre_insert(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                              int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2,
+                              const void* const* next_cols, int id_dtype, const int64_t* num_embeddings,
+                              const int32_t* dedup_tables, void* next_dedup_ws, size_t dedup_ws_bytes,
+                              int64_t dedup_max_lookups, void* stream);
+/* tt_tower_update_pre_rowwise_adagrad over dedup_ws updating only the rows looked up MORE than once
+ * (the others were updated by T1; their slots are freed), plus the resolver of next_dedup_ws's
+ * deferred inserts (both workspaces: dedup_ws_bytes / dedup_max_lookups). */
+int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, int64_t B, float* params,
+                                                float* exp_avg, float* exp_avg_sq, float eps, float beta1,
+                                                float beta2, float weight_decay, float* grads_out, void* workspace,
+                                                size_t ws_bytes, const tt_table_meta_t* tables, int T,
+                                                const tt_feature_meta_t* features, int F, int64_t emb_B,
+                                                const float* grad, int64_t ldg, float* weights, float* state,
+                                                float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
+                                                size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 /* T1 for the sharded step (row-wise / table-wise shards, single-hot): tower t's input row m is row
  * pos[t][m] of rows_in[t] ([*][in_dim[t]] fp32: the rows returned by the owners' all-to-all; -1
  * -> zeros, a dropped id), and its gradient row dX is written to row pos[t][m] of grad_rows_out[t]

@@ -1,0 +1,48 @@
+"""The production ring of the fused step (dedup one step ahead; rows looked up once updated in place
+inside T1, the others by K3 from dX): bit for bit the classic step (insert in T1, every row updated
+by K3), over resident batches with dropped ids, ids past N, repeated rows (2..30 lookups) and hot
+rows (> 30), through HIP graphs of several steps and eagerly."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _batches(N, B, n, seed, device):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for s in range(n):
+        cols = [torch.randint(0, 2 * x, (B,), generator=g) for x in N]
+        cols[0][torch.rand(B, generator=g) < 0.03] = 0
+        cols[1][:5] = 17 + s % 2         # a row repeated 5 times (K3's narrow path)
+        cols[1][100:160] = 12_345        # a hot row (60 lookups: K3's hot role)
+        cols[0][200:203] = cols[0][300]  # a repeated user row
+        out.append(([c.to(device) for c in cols], torch.randint(0, 2, (B,), generator=g).to(torch.int32).to(device)))
+    return out
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("mode", ["graph", "eager"])
+def test_ring_equals_classic_step(device, D, mode):
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N, B = [30_000, 50_000], 2048
+    batches = _batches(N, B, 6, seed=D, device=device)
+    a = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=2)
+    b = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=2)
+    assert a.ring_supported()
+    a.capture_ring(batches, steps_per_graph=2)
+    if mode == "graph":
+        a.run(3)
+        a.run(3)  # continues at the cursor (mixed big / small graphs)
+    else:
+        a.run_eager(6)
+    for cols, lab in batches:
+        b.load_batch(cols, lab)
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.tables.weights, b.tables.weights)
+    assert torch.equal(a.tables.state, b.tables.state)
+    assert torch.equal(a.params, b.params) and torch.equal(a.exp_avg, b.exp_avg)
+    assert float(a.loss) == float(b.loss)
+    assert torch.equal(a.logits, b.logits)

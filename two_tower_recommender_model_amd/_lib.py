@@ -203,6 +203,20 @@ SIGNATURES = {
         [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp,
          _vp, _vp, _vp, _vp, _sz, _vp],
     ),
+    "tt_tower_fwd_bwd_gather_update": (
+        _int,
+        [_psh, _i64, _pvp, _int, _pi64, _pvp, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _f32, _f32, _vp, _sz,
+         _i64, _vp, _sz, _vp],
+    ),
+    "tt_tower_wgrad_pre_insert": (
+        _int,
+        [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _pvp, _int, _pi64, _pi32, _vp, _sz, _i64, _vp],
+    ),
+    "tt_tower_update_pre_rowwise_adagrad_resolve": (
+        _int,
+        [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64,
+         _vp, _vp, _f32, _f32, _vp, _vp, _sz, _i64, _vp],
+    ),
     "tt_tower_adam_grads_sum": (
         _int,
         [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp],
@@ -255,6 +269,9 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_adam_grads_sum_rowwise_adagrad",
     "tt_tower_wgrad_route_count",
     "tt_tower_grads_replicated_route_place",
+    "tt_tower_fwd_bwd_gather_update",
+    "tt_tower_wgrad_pre_insert",
+    "tt_tower_update_pre_rowwise_adagrad_resolve",
 ]
 
 _lib = None

@@ -51,7 +51,8 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_adam_grads, tt_tower_update_pre
 // tt_shard_route_segs, tt_shard_gather_segs_bf16, tt_tower_fwd_bwd_indexed2_bf16, tt_tower_grads_replicated,
 // tt_tower_adam_grads_sum, tt_tower_adam_grads_sum_rowwise_adagrad, tt_tower_wgrad_route_count,
-// tt_tower_grads_replicated_route_place
-int tt_num_entry_points(void) { return 45; }
+// tt_tower_grads_replicated_route_place, tt_tower_fwd_bwd_gather_update, tt_tower_wgrad_pre_insert,
+// tt_tower_update_pre_rowwise_adagrad_resolve
+int tt_num_entry_points(void) { return 48; }
 
 }  // extern "C"

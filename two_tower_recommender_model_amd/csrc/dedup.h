@@ -169,6 +169,7 @@ struct DdUpdateArgs {
   DedupWs ws;
   int hot_wgs;         // workgroups of the hot role; the slot role has slot_hw / 8 more
   int64_t slot_hw;     // half-waves of the slot role: ceil(L / DD_SPH), a multiple of 8
+  int skip_single;     // rows looked up once were updated by T1 (dd_mode 2): only free their slots
 };
 
 // Per-lane table / feature meta from LDS: indexing the kernel-argument arrays by a per-lane value
@@ -297,20 +298,17 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
       f32x4v g = part[0][hl];
 #pragma unroll
       for (int q = 1; q < 8; ++q) g += part[q][hl];
-      float sq = col_ok ? g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3] : 0.f;
+      float sq = col_ok ? rw_sq4(g) : 0.f;
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
       if (lane < 32) {
         float* wrow = weights + gm.lm->woff[t] + r * D;
         float* srow = state + gm.lm->soff[t] + r;
-        const float snew = *srow + sq / (float)D;
-        const float stdv = sqrtf(snew) + eps;
-        if (col_ok) {
-          f32x4v wv = *reinterpret_cast<const f32x4v*>(wrow + hl * 4);
-#pragma unroll
-          for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
-          *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
-        }
+        const float snew = rw_state(*srow, sq, D);
+        const float stdv = rw_stdv(snew, eps);
+        if (col_ok)
+          *reinterpret_cast<f32x4v*>(wrow + hl * 4) =
+              rw_apply(*reinterpret_cast<const f32x4v*>(wrow + hl * 4), g, lr, stdv);
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
           *srow = snew;
@@ -389,15 +387,17 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     const int item = __shfl(dw[q], hb + 2 + (hl < DD_INL ? hl : 0), 64);
     // hot slots (reset by the hot role, one 8-B store) are never taken here
     active[q] = word != DD_EMPTY && cnt <= DD_INL;
-    const int t = active[q] ? (int)(key >> DD_TABLE_SHIFT) : 0;
-    const int64_t r = active[q] ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
+    // skip_single: a row looked up once was updated in place by T1; its slot is only freed here
+    const bool upd = active[q] && !(a.skip_single && cnt == 1);
+    const int t = upd ? (int)(key >> DD_TABLE_SHIFT) : 0;
+    const int64_t r = upd ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
     D[q] = lm->dim[t];
-    col_ok[q] = active[q] && hl * 4 < D[q];
+    col_ok[q] = upd && hl * 4 < D[q];
     wrow[q] = weights + lm->woff[t] + r * D[q];
     srow[q] = state + lm->soff[t] + r;
     wv[q] = col_ok[q] ? *reinterpret_cast<const f32x4v*>(wrow[q] + hl * 4) : (f32x4v)(0.f);
-    s_old[q] = active[q] ? *srow[q] : 0.f;
-    c[q] = active[q] ? cnt : 0;
+    s_old[q] = upd ? *srow[q] : 0.f;
+    c[q] = upd ? cnt : 0;
     cmax[q] = max(c[q], __shfl_xor(c[q], 32, 64));
     mine[q] = hl < c[q] ? item : 0x7fffffff;
     g[q] = (f32x4v)(0.f);
@@ -430,23 +430,16 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   DD_STAMP(2);
 #pragma unroll
   for (int q = 0; q < DD_SPH; ++q) {
-    float sq = g[q][0] * g[q][0] + g[q][1] * g[q][1] + g[q][2] * g[q][2] + g[q][3] * g[q][3];
+    float sq = rw_sq4(g[q]);
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
-    if (active[q]) {
-      const float snew = s_old[q] + sq / (float)D[q];
-      const float stdv = sqrtf(snew) + eps;
-      if (col_ok[q]) {
-        f32x4v w = wv[q];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[q][v]) / stdv;
-        *reinterpret_cast<f32x4v*>(wrow[q] + hl * 4) = w;
-      }
-      if (hl == 0) {
-        *srow[q] = snew;
-        sp[q]->word = DD_EMPTY;
-      }
+    if (c[q] > 0) {
+      const float snew = rw_state(s_old[q], sq, D[q]);
+      const float stdv = rw_stdv(snew, eps);
+      if (col_ok[q]) *reinterpret_cast<f32x4v*>(wrow[q] + hl * 4) = rw_apply(wv[q], g[q], lr, stdv);
+      if (hl == 0) *srow[q] = snew;
     }
+    if (active[q] && hl == 0) sp[q]->word = DD_EMPTY;
   }
   DD_STAMP(3);
 }

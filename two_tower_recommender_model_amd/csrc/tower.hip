@@ -84,6 +84,13 @@ struct TowerArgs {
   const int32_t* gpos_out[2];  // nullable: dX row index in gdst (units of in_dim floats) when it differs
                                // from the input row (the pipelined sharded step's packed send buffer)
   int gsrc_bf16;
+  // in-place row-wise Adagrad of the rows looked up ONCE in the step (the pipelined fused step,
+  // tower_l2_kernel<..., UPD = true>): `dd` is this batch's dedup table, completed before T1 (by the
+  // previous step's T2 / K3); a kept lookup whose slot count is 1 updates its row and state here from
+  // its dX (the same arithmetic as the K3 update: rw_* helpers); the others leave dX for K3
+  float* uw[2];  // tower t's table rows (writable; == gtab[t])
+  float* us[2];  // tower t's table row-wise state
+  float ulr, ueps;
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
 };
@@ -435,8 +442,9 @@ constexpr int T1_THREADS = 576;
 constexpr int T1_BARRIERS = 7;
 
 // R16: indexed rows arrive as bf16 (sharded step, tt_tower_fwd_bwd_indexed_bf16); its own
-// instantiation, so the other modes' code and registers are untouched
-template <int IN_, int W0_, int W1_, bool R16 = false>
+// instantiation, so the other modes' code and registers are untouched. UPD: the in-place update of
+// single-lookup rows (TowerArgs::uw); gather mode only.
+template <int IN_, int W0_, int W1_, bool R16 = false, bool UPD = false>
 __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][TR * LSTR];   // X, later dZ0
   __shared__ __attribute__((aligned(16))) __bf16 hs[2][TR * LSTR];   // hidden activation (bf16)
@@ -444,11 +452,41 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) float outf[2][TR * FSTR];  // tower outputs, later dX (fp32)
   __shared__ float dlog[TR];
   __shared__ float lpart[TR];
+  // UPD: the fp32 rows as gathered, and per (tower, row) the lookup's table row (-1: not updated
+  // here) and its row-wise state, filed by the dedup wave
+  __shared__ __attribute__((aligned(16))) float xf[UPD ? 2 : 1][UPD ? TR * FSTR : 4];
+  __shared__ int64_t urow[2][TR];
+  __shared__ float ustate[2][TR];
 
   // wid via readfirstlane: the compiler then knows t (below) is wave-uniform and reads a.gcol[t],
   // a.gtab[t], ... with scalar loads (a per-lane index into the kernarg arrays is a vector load from
   // the kernarg segment: one more dependent memory hop in front of the row gather)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (UPD && wid == 8) {
+    // ---- the dedup wave (UPD): for each of the 2 x TR lookups, is its row looked up once in this
+    // step? (claim >= 0 and slot count 1 in the batch's completed table) -> row and state to LDS
+    const int tq = lane / TR, row = lane % TR;
+    const int64_t gm = (int64_t)blockIdx.x * TR + row;
+    int64_t r = -1;
+    int32_t cl = -1;
+    float st = 0.f;
+    if (gm < a.B) {
+      const int64_t id = load_id(tq ? a.gcol[1] : a.gcol[0], a.gid_dtype, gm);
+      if (id != 0) {
+        r = py_mod64(id, tq ? a.gmod[1] : a.gmod[0]);
+        cl = a.dd.claim[tq * a.B + gm];
+        st = (tq ? a.us[1] : a.us[0])[r];  // speculative: used only for a single-lookup row
+      }
+    }
+    __syncthreads();
+    const uint64_t word = cl >= 0 ? a.dd.slots[cl].word : DD_EMPTY;
+    const bool single = cl >= 0 && (word & DD_CNT_MASK) == 1;
+    urow[tq][row] = single ? r : -1;
+    ustate[tq][row] = st;
+#pragma unroll 1
+    for (int k = 1; k < T1_BARRIERS; ++k) __syncthreads();
+    return;
+  }
   if (wid == 8) {
     // ---- the dedup wave: files this workgroup's 2 x TR lookups (gather + dedup) into the hash
     // table; its CAS round trips count only in ITS vmcnt, so the 8 compute waves never wait on
@@ -577,6 +615,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         bv[0] = (__bf16)xv[i][0]; bv[1] = (__bf16)xv[i][1]; bv[2] = (__bf16)xv[i][2]; bv[3] = (__bf16)xv[i][3];
       }
       *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
+      if (UPD) *reinterpret_cast<f32x4*>(&xf[t][row * FSTR + c4]) = xv[i];
       const int64_t gm = m0 + row;
       if (!R16 && a.pooled_out && gm < B)
         *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + incol + c4) = xv[i];
@@ -748,7 +787,26 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         else
           dst = a.gpooled + gm * a.ldp + incol + c4;
       }
-      if (dst && !(a.dbg & 2)) *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
+      const f32x4 g = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
+      if (UPD) {
+        // the lanes of one row are consecutive (in / 4 of them, a power of two <= 32): reduce
+        // sum(G^2) over them in the K3 update's order, then update the row in place
+        const int64_t ur = urow[t][row];
+        const int lpr = in / 4;
+        float sq = rw_sq4(g);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1)
+          if (o < lpr) sq += __shfl_xor(sq, o, 64);
+        if (ur >= 0) {
+          const float snew = rw_state(ustate[t][row], sq, in);
+          const float stdv = rw_stdv(snew, a.ueps);
+          const f32x4 x = *reinterpret_cast<const f32x4*>(&xf[t][row * FSTR + c4]);
+          *reinterpret_cast<f32x4*>(a.uw[t] + ur * in + c4) = rw_apply(x, g, a.ulr, stdv);
+          if (c4 == 0) a.us[t][ur] = snew;
+          if (!a.pooled_out) dst = nullptr;  // dX is needed only for inspection (pooled_out mode)
+        }
+      }
+      if (dst && !(a.dbg & 2)) *reinterpret_cast<f32x4*>(dst) = g;
     }
   }
   T1_STAMP(15);
@@ -1089,6 +1147,46 @@ __global__ void __launch_bounds__(256) tower_wgrad_dedup_kernel(WgradArgs a, con
     dd_update_block(d, (int)blockIdx.x - n_t2, smem);
 }
 
+// Pipelined fused step: T2 with the NEXT batch's dedup insert as extra workgroups (one wave per
+// 64 lookups i = t * B + m: one returning CAS each, lookups that lost it deferred to the next
+// launch's resolver), so T1 of the next step finds a complete table and updates the rows looked up
+// once in place (tower_l2_kernel<..., UPD>).
+struct InsertArgs {
+  const void* col[2];
+  int64_t mod[2];
+  int32_t tab[2];
+  int id_dtype;
+  int64_t B;
+  DedupWs dd;
+};
+
+__device__ __forceinline__ void insert_next_block(const InsertArgs& ins, int blk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t grp = (int64_t)blk * 4 + (threadIdx.x >> 6);
+  const int64_t i = grp * 64 + lane;
+  DdPend p;
+  p.key = DD_EMPTY;
+  if (i < 2 * ins.B) {
+    const int t = i >= ins.B;
+    const int64_t m = i - (t ? ins.B : 0);
+    const int64_t id = load_id(t ? ins.col[1] : ins.col[0], ins.id_dtype, m);
+    const uint64_t key = id != 0 ? (((uint64_t)(t ? ins.tab[1] : ins.tab[0]) << DD_TABLE_SHIFT) |
+                                    (uint64_t)py_mod64(id, t ? ins.mod[1] : ins.mod[0]))
+                                 : DD_EMPTY;
+    dd_insert_begin(ins.dd, key, (int32_t)i, p);
+  }
+  if (grp < ins.dd.ovf_groups) dd_insert_defer_finish(ins.dd, p, (int32_t)(i < 2 * ins.B ? i : 0), (int)grp);
+}
+
+__global__ void __launch_bounds__(256) tower_wgrad_insert_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
+                                                                 InsertArgs ins, int n_t2) {
+  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
+  if ((int)blockIdx.x < n_t2)
+    wgrad_block(a, tiles, (int)blockIdx.x, smem);
+  else
+    insert_next_block(ins, (int)blockIdx.x - n_t2);
+}
+
 // Pipelined sharded step: the NEXT batch's route rides in the towers' launches as extra
 // workgroups (it depends only on that batch's ids): its count pass beside T2's tiles, its place
 // pass beside T3's parameter workgroups (tower_update_route_kernel below) — two launches fewer.
@@ -1226,6 +1324,21 @@ __global__ void __launch_bounds__(256) tower_update_route_kernel(UpdateArgs a, R
     const int j = (int)blockIdx.x - n_upd;
     route_place_block<true>(r, j % r.nblk, j / r.nblk, base, wc);
   }
+}
+
+// K3 of the pipelined fused step: resolver workgroups for the NEXT batch's deferred inserts, then
+// the update of this batch's rows looked up more than once (skip_single), then T3
+constexpr int K3_RES_WGS = 32;
+__global__ void __launch_bounds__(256) tower_update_dedup_resolve_kernel(UpdateArgs a, DdUpdateArgs d, DedupWs next,
+                                                                         int n_dd) {
+  __shared__ __attribute__((aligned(16))) char smem[DD_SMEM];
+  const int bid = (int)blockIdx.x;
+  if (bid < K3_RES_WGS)
+    dd_resolve_block(next, bid, K3_RES_WGS);
+  else if (bid < K3_RES_WGS + n_dd)
+    dd_update_block(d, bid - K3_RES_WGS, smem);
+  else
+    update_block(a, bid - K3_RES_WGS - n_dd, (int)gridDim.x - K3_RES_WGS - n_dd);
 }
 
 // T3 + the embedding path's fused row-wise Adagrad (dedup.h) in ONE launch: workgroups [0, n_dd)
@@ -1434,6 +1547,15 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
   if ((a.gcol[0] || a.gpos[0]) && !two)
     return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
+  if (a.uw[0]) {  // in-place update of single-lookup rows: compile-time shapes only
+    if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
+      tower_l2_kernel<128, 128, 64, false, true><<<g, b512, 0, as_stream(stream)>>>(a);
+    else if (two && i0 == 64 && i1 == 64 && w0 == 128 && w1 == 64)
+      tower_l2_kernel<64, 128, 64, false, true><<<g, b512, 0, as_stream(stream)>>>(a);
+    else
+      return fail(TT_EINVAL, "tower_gather_update: shapes in {64, 128} x [128, 64] only");
+    return check_launch("tower_fwd_bwd_gather_update");
+  }
   if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64 && a.gsrc_bf16)
     tower_l2_kernel<128, 128, 64, true><<<g, b512, 0, as_stream(stream)>>>(a);
   else if (two && a.gsrc_bf16)
@@ -1913,6 +2035,111 @@ int tt_tower_grads_replicated_route_place(const tt_tower_shape_t* shape, int64_t
   tower_update_route_kernel<<<dim3((unsigned)(g3 + (int64_t)r.nblk * F)), dim3(256), 0, as_stream(stream)>>>(
       a, r, (int)g3);
   return check_launch("tower_grads_replicated_route_place");
+}
+
+int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
+                                   const int64_t* num_embeddings, float* const* table_rows, float* const* table_state,
+                                   float* pooled_out, int64_t ldp, float* gpooled, const float* params,
+                                   const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
+                                   float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
+                                   void* workspace, size_t ws_bytes, void* stream) {
+  if (!cols || !num_embeddings || !table_rows || !table_state || !dedup_ws)
+    return fail(TT_EINVAL, "tower_gather_update: null pointer");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_gather_update: ids must be int32/int64");
+  if (dedup_max_lookups < 2 * B || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+      dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) || (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
+    return fail(TT_ECAPACITY, "tower_gather_update: dedup workspace too small / misaligned");
+  TowerArgs a{};
+  for (int t = 0; t < 2; ++t) {
+    if (!cols[t] || !table_rows[t] || !table_state[t] || num_embeddings[t] < 1)
+      return fail(TT_EINVAL, "tower_gather_update: bad column");
+    if (reinterpret_cast<uintptr_t>(table_rows[t]) & 15) return fail(TT_EINVAL, "tower_gather_update: rows not 16-B aligned");
+    a.gcol[t] = cols[t];
+    a.gtab[t] = table_rows[t];
+    a.gmod[t] = num_embeddings[t];
+    a.uw[t] = table_rows[t];
+    a.us[t] = table_state[t];
+  }
+  a.gid_dtype = id_dtype;
+  a.pooled_out = pooled_out;
+  a.ulr = lr;
+  a.ueps = eps;
+  dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
+  return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
+                   ws_bytes, stream);
+}
+
+int tt_tower_wgrad_pre_insert(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+                              int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2,
+                              const void* const* next_cols, int id_dtype, const int64_t* num_embeddings,
+                              const int32_t* dedup_tables, void* next_dedup_ws, size_t dedup_ws_bytes,
+                              int64_t dedup_max_lookups, void* stream) {
+  if (!adam_step_state || !next_cols || !num_embeddings || !dedup_tables || !next_dedup_ws)
+    return fail(TT_EINVAL, "tower_wgrad_pre_insert: null pointer");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_wgrad_pre_insert: ids must be int32/int64");
+  if (dedup_max_lookups < 2 * B || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+      dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
+      (reinterpret_cast<uintptr_t>(next_dedup_ws) & 63))
+    return fail(TT_ECAPACITY, "tower_wgrad_pre_insert: dedup workspace too small / misaligned");
+  WgradArgs a{};
+  int64_t wgs = 0;
+  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
+  if (rc) return rc;
+  TowerLayout L;
+  tower_layout(shape, B, &L);
+  a.step_state = adam_step_state;
+  a.adam_pre = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + L.o_counter);
+  a.lr = adam_lr;
+  a.beta1 = adam_beta1;
+  a.beta2 = adam_beta2;
+  InsertArgs ins{};
+  for (int t = 0; t < 2; ++t) {
+    if (!next_cols[t] || num_embeddings[t] < 1 || num_embeddings[t] >= (1ll << DD_TABLE_SHIFT) ||
+        dedup_tables[t] < 0 || dedup_tables[t] >= TT_MAX_TABLES)
+      return fail(TT_EINVAL, "tower_wgrad_pre_insert: bad column / table");
+    ins.col[t] = next_cols[t];
+    ins.mod[t] = num_embeddings[t];
+    ins.tab[t] = dedup_tables[t];
+  }
+  ins.id_dtype = id_dtype;
+  ins.B = B;
+  dedup_layout(next_dedup_ws, dedup_max_lookups, &ins.dd);
+  const int64_t n_ins = ceil_div(ceil_div(2 * B, 64), 4);  // 4 waves of 64 lookups per workgroup
+  tower_wgrad_insert_kernel<<<dim3((unsigned)(wgs + n_ins)), dim3(256), 0, as_stream(stream)>>>(
+      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), ins, (int)wgs);
+  return check_launch("tower_wgrad_pre_insert");
+}
+
+int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, int64_t B, float* params,
+                                                float* exp_avg, float* exp_avg_sq, float eps, float beta1,
+                                                float beta2, float weight_decay, float* grads_out, void* workspace,
+                                                size_t ws_bytes, const tt_table_meta_t* tables, int T,
+                                                const tt_feature_meta_t* features, int F, int64_t emb_B,
+                                                const float* grad, int64_t ldg, float* weights, float* state,
+                                                float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
+                                                size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+  if (!next_dedup_ws || (reinterpret_cast<uintptr_t>(next_dedup_ws) & 63))
+    return fail(TT_EINVAL, "tower_update_resolve: next dedup workspace null / misaligned");
+  DdUpdateArgs d{};
+  int64_t dd_grid = 0;
+  int rc = dedup_update_args(tables, T, features, F, emb_B, grad, ldg, weights, state, lr, emb_eps, dedup_ws,
+                             dedup_ws_bytes, dedup_max_lookups, d, &dd_grid);
+  if (rc) return rc;
+  d.skip_single = 1;
+  DedupWs next;
+  dedup_layout(next_dedup_ws, dedup_max_lookups, &next);
+  TowerLayout L;
+  rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
+  UpdateArgs a;
+  int64_t g3 = 0;
+  rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
+               nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0, a, &g3);
+  if (rc) return rc;
+  tower_update_dedup_resolve_kernel<<<dim3((unsigned)(K3_RES_WGS + dd_grid + g3)), dim3(256), 0,
+                                      as_stream(stream)>>>(a, d, next, (int)dd_grid);
+  return check_launch("tower_update_pre_rowwise_adagrad_resolve");
 }
 
 int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,

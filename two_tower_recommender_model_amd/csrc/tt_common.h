@@ -72,6 +72,18 @@ __device__ __forceinline__ int64_t udiv64(int64_t a, int64_t b) {
   return a / b;
 }
 
+// Row-wise Adagrad arithmetic (torchrec RowWiseAdagrad, 03_model_training.py:791-795) of one
+// 4-wide chunk of a row, shared by the update paths so that each computes bitwise-identical
+// results for the same gradient row: s += mean_d(G^2); w -= lr * G / (sqrt(s) + eps)
+__device__ __forceinline__ float rw_sq4(const f32x4v& g) { return g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3]; }
+__device__ __forceinline__ float rw_state(float s_old, float sq, int D) { return s_old + sq / (float)D; }
+__device__ __forceinline__ float rw_stdv(float snew, float eps) { return sqrtf(snew) + eps; }
+__device__ __forceinline__ f32x4v rw_apply(f32x4v w, const f32x4v& g, float lr, float stdv) {
+#pragma unroll
+  for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[v]) / stdv;
+  return w;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -19,9 +19,12 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence
 
+import ctypes as C
+
 import torch
 
 from . import _lib, ops
+from ._lib import FeatureMeta, check, id_dtype_code, ptr, ptr_array, stream_handle
 
 
 class FusedTwoTowerStep:
@@ -381,6 +384,154 @@ class FusedTwoTowerStep:
         outside step() (initialisation, loading a checkpoint)."""
         if self.towers is not None:
             self.towers.update(self.params, do_adam=False)
+
+    # ---- the pipelined ring (production): dedup one step ahead, single-lookup rows in T1 ---------
+    def ring_supported(self) -> bool:
+        return (self.gather and self.dedup_single and self.combined_bwd and self.layer_sizes == [128, 64]
+                and self.in_q == self.in_c and self.in_q in (64, 128) and self.F == 2)
+
+    def _ring_ws(self):
+        if getattr(self, "_ring", None) is None:
+            if not self.ring_supported():
+                raise _lib.TTError("ring: needs the fused gather + single-hot dedup path, towers [128, 64], "
+                                   "inputs of 64 or 128")
+            ts = self.tables
+            ts.ensure_dedup_workspace(self.F * self.B)
+            lib = _lib.load()
+            ws1 = torch.empty_like(ts._dd_ws)
+            check(lib.tt_dedup_workspace_init(ptr(ws1), ws1.numel(), ts._dd_cap, stream_handle(self.device)),
+                  "dedup_workspace_init")
+            self._ring = [ts._dd_ws, ws1]
+            self._ring_tab = (C.c_int32 * 2)(0, 1)
+            self._ring_ne = (C.c_int64 * 2)(*self.num_embeddings)
+        return self._ring
+
+    def ring_reset(self) -> None:
+        """Empty both dedup tables of the ring (a staged batch's table is otherwise left filled)."""
+        lib = _lib.load()
+        for ws in self._ring_ws():
+            check(lib.tt_dedup_workspace_init(ptr(ws), ws.numel(), self.tables._dd_cap, stream_handle(self.device)),
+                  "dedup_workspace_init")
+
+    def ring_prime(self, cols: Sequence[torch.Tensor], parity: int) -> None:
+        """Build the dedup table of the first batch of a ring (every later table is built by the
+        step before its batch)."""
+        ws = self._ring_ws()[parity]
+        ts = self.tables
+        check(_lib.load().tt_dedup_insert_cols(ts._tm, ts.T, ts._fm, ts.F, self.B, ptr_array(list(cols)),
+                                               id_dtype_code(cols[0].dtype), self._ring_ne, ptr(ws), ws.numel(),
+                                               ts._dd_cap, stream_handle(self.device)), "dedup_insert_cols")
+
+    def ring_step(self, cols: Sequence[torch.Tensor], labels: torch.Tensor, parity: int,
+                  next_cols: Sequence[torch.Tensor]) -> None:
+        """One production step on (cols, labels), whose dedup table (parity) is complete; files
+        next_cols into the other table. Three launches:
+          T1  gather + towers fwd/bwd + in-place row-wise Adagrad of the rows looked up once
+          T2  tower weight gradients + Adam scalars + insert of the next batch
+          K3  resolver of the next batch's deferred inserts + update of the rows looked up more
+              than once (from T1's dX) + T3 (slab reduction, Adam, bf16 weight copies)"""
+        lib, tw, ts, B, dev = _lib.load(), self.towers, self.tables, self.B, self.device
+        ring = self._ring_ws()
+        ws, wsn = ring[parity], ring[parity ^ 1]
+        st = stream_handle(dev)
+        self._mark("t1", 0)
+        check(lib.tt_tower_fwd_bwd_gather_update(
+            C.byref(tw.shape), B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ring_ne,
+            ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
+            ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
+            ptr(self.params), ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws),
+            ws.numel(), ts._dd_cap, ptr(tw.ws), tw.nbytes, st), "tower_fwd_bwd_gather_update")
+        self._mark("t1", 1)
+        self._mark("t2", 0)
+        check(lib.tt_tower_wgrad_pre_insert(
+            C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
+            0.999, ptr_array(list(next_cols)), id_dtype_code(next_cols[0].dtype), self._ring_ne, self._ring_tab,
+            ptr(wsn), wsn.numel(), ts._dd_cap, st), "tower_wgrad_pre_insert")
+        self._mark("t2", 1)
+        self._mark("k3", 0)
+        check(lib.tt_tower_update_pre_rowwise_adagrad_resolve(
+            C.byref(tw.shape), B, ptr(self.params), ptr(self.exp_avg), ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0,
+            ptr(self.grads), ptr(tw.ws), tw.nbytes, ts._tm, ts.T, ts._fm, ts.F, B, ptr(self.gpooled),
+            self.gpooled.stride(0), ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws), ptr(wsn),
+            ws.numel(), ts._dd_cap, st), "tower_update_pre_rowwise_adagrad_resolve")
+        self._mark("k3", 1)
+
+    def capture_ring(self, batches: Sequence, steps_per_graph: int = 1, keep_graph: bool = False) -> None:
+        """Production HIP graphs over a cyclic pool of resident (cols, labels) batches (len even, a
+        multiple of k): ring graph j runs the steps of batches j*k .. j*k+k-1, each filing the next
+        batch of the pool; ``ring_small[i]`` runs batch i alone. Replay with ``run(n)`` (the step
+        keeps the cursor: the batch whose dedup table is complete)."""
+        k = int(steps_per_graph)
+        n = len(batches)
+        if k < 1 or n % k or n % 2:
+            raise _lib.TTError("capture_ring: the batch count must be even and a multiple of steps_per_graph")
+        staged = []
+        for cols, labels in batches:
+            for c in cols:
+                if c.dtype != self.id_dtype or not c.is_contiguous() or c.numel() != self.B:
+                    raise _lib.TTError("capture_ring: batch columns must match the step's id dtype and batch")
+            staged.append((list(cols), labels.to(torch.int32).contiguous()))
+        self._ring_inputs = staged
+        self.ring_reset()
+        self.sync_weights()
+        self.ring_prime(staged[0][0], 0)
+        torch.cuda.synchronize(self.device)
+        self.ring_cursor = 0
+        self.ring_k = k
+
+        def cap(idx):
+            g = torch.cuda.CUDAGraph(keep_graph=keep_graph)
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    for i in idx:
+                        self.ring_step(staged[i][0], staged[i][1], i % 2, staged[(i + 1) % n][0])
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            return g
+
+        self.ring_graphs = [cap(range(j, j + k)) for j in range(0, n, k)]
+        self.ring_small = [cap([i]) for i in range(n)] if k > 1 else list(self.ring_graphs)
+        torch.cuda.synchronize(self.device)
+
+    def run(self, n: int) -> None:
+        """Replay n production steps from the ring, continuing at the cursor."""
+        i, nb, k = self.ring_cursor, len(self.ring_small), self.ring_k
+        while n > 0:
+            if i % k == 0 and n >= k:
+                self.ring_graphs[i // k].replay()
+                i, n = i + k, n - k
+            else:
+                self.ring_small[i].replay()
+                i, n = i + 1, n - 1
+            i %= nb
+        self.ring_cursor = i
+
+    def timed_ring(self, n: int) -> dict:
+        """n eager production steps (from the cursor) with a HIP event pair around every launch;
+        mean device time (ms) per launch name."""
+        self._timing = []
+        try:
+            for _ in range(n):
+                self._timing.append({})
+                self.run_eager(1)
+            torch.cuda.synchronize(self.device)
+            acc = {}
+            for m in self._timing:
+                for name, (a, b) in m.items():
+                    acc.setdefault(name, []).append(a.elapsed_time(b))
+        finally:
+            self._timing = None
+        return {k: sum(v) / len(v) for k, v in acc.items()}
+
+    def run_eager(self, n: int) -> None:
+        """n production steps over the captured ring's batches without graphs (timing / tests)."""
+        staged = self._ring_inputs
+        nb = len(staged)
+        for _ in range(n):
+            i = self.ring_cursor
+            self.ring_step(staged[i][0], staged[i][1], i % 2, staged[(i + 1) % nb][0])
+            self.ring_cursor = (i + 1) % nb
 
     # ------------------------------------------------------------------------------------------
     def capture(self, batches: Optional[Sequence] = None, keep_graph: bool = False) -> None:
