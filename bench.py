@@ -250,7 +250,7 @@ def launch_bytes(step, nnz: int, uniq: int, once: int):
     k3_design = (F * B * (4 + 64) + (uniq - once) * (8 * D + 8) + multi * 4 * D + S * P * 4 + 6 * P * 4 + 4 * P)
     t1_alg = nnz * (8 + 4 * D) + F * B * (4 + 4 * D) + once * (8 + 4 * D + 8 * D + 8)
     k3_alg = multi * 8 + (F * B - once) * 4 * D + (uniq - once) * (8 * D + 8)
-    return {"t1": {"alg_bytes": t1_alg, "design_bytes": t1_design, "flop": 8 * B * macs,
+    out = {"t1": {"alg_bytes": t1_alg, "design_bytes": t1_design, "flop": 8 * B * macs,
                    "what": "tower_l2_kernel<UPD>: EBC gather + both towers fwd/bwd + row-wise Adagrad of the rows "
                            "looked up once"},
             "t2": {"alg_bytes": 0, "design_bytes": t2_design, "flop": 4 * B * macs,
@@ -259,6 +259,15 @@ def launch_bytes(step, nnz: int, uniq: int, once: int):
                    "what": "tower_update_dedup_resolve_kernel: next batch's deferred inserts + row-wise Adagrad of the "
                            "rows looked up more than once + slab reduction + Adam + bf16 copies"},
             "_emb_path_bytes": t1_alg + k3_alg}
+    if getattr(step, "ring_tail", False):  # T2 + insert + row update, then T3
+        t3_design = S * P * 4 + 6 * P * 4 + 4 * P
+        out["tail"] = {"alg_bytes": k3_alg, "design_bytes": t2_design + k3_design - t3_design, "flop": 4 * B * macs,
+                       "what": "tower_tail_kernel: tower weight gradients + next batch's complete dedup insert + "
+                               "row-wise Adagrad of the rows looked up more than once"}
+        out["t3"] = {"alg_bytes": 0, "design_bytes": t3_design, "flop": 0,
+                     "what": "tower_update_kernel: slab reduction + Adam + bf16 weight copies"}
+        del out["t2"], out["k3"]
+    return out
 
 
 def pmc_traffic(kernel_name: str, workload: str = "northstar"):
@@ -283,7 +292,8 @@ def pmc_traffic(kernel_name: str, workload: str = "northstar"):
     return None, None
 
 
-KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_insert_kernel", "k3": "tower_update_dedup_resolve_kernel"}
+KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_insert_kernel", "k3": "tower_update_dedup_resolve_kernel",
+                "tail": "tower_tail_kernel", "t3": "tower_update_kernel"}
 
 
 def synth_kjt_batches(num_users, num_items, B, maxlen, n, device, ids, seed):
@@ -462,11 +472,11 @@ def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northsta
         return {"bound": "hbm", "kernel": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernels": out, "lookups": nnz, "unique_rows": uniq, "rows_looked_up_once": once, "embedding_path": path}
     dom = "t1"  # the longest launch, and the one that carries the forward's row reads
-    emb_ms = timed.get("t1", 0.0) + timed.get("k3", 0.0)
+    emb_ms = timed.get("t1", 0.0) + timed.get("k3", timed.get("tail", 0.0))
     ach = out[dom]["alg_GB/s"]
     path.update({"ms_t1_k3": round(emb_ms, 5), "GB/s_over_t1_k3": round(emb_path_bytes / emb_ms / 1e6, 1),
                  "frac_over_t1_k3": round(emb_path_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4),
-                 "note": "SURVEY 8(d) bytes per step: over the whole step, and over T1 + K3 (the launches that "
+                 "note": "SURVEY 8(d) bytes per step: over the whole step, and over T1 + K3 or the tail launch (the launches that "
                          "carry the embedding work; both also run tower work)"})
     return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": out[dom]["pmc_hbm_bytes"],
@@ -518,15 +528,16 @@ def run_single(args):
             from two_tower_recommender_model_amd.graph_timing import GraphLaunchTimer
 
             step.capture_ring(batches, steps_per_graph=k, keep_graph=True)
-            names = ["t1", "t2", "k3"]
-            timers = [GraphLaunchTimer(g, list(range(3 * k))) for g in step.ring_graphs]
+            names = ["t1", "tail", "t3"] if step.ring_tail else ["t1", "t2", "k3"]
+            nl = len(names)
+            timers = [GraphLaunchTimer(g, list(range(nl * k))) for g in step.ring_graphs]
             acc = {n: [] for n in names}
             n_done, j = 0, 0
             while n_done < args.steps:
                 step.ring_graphs[j % len(step.ring_graphs)].replay()
                 torch.cuda.synchronize()
                 for i, t_ms in enumerate(timers[j % len(timers)].elapsed()):
-                    acc[names[i % 3]].append(t_ms)
+                    acc[names[i % nl]].append(t_ms)
                 n_done, j = n_done + k, j + 1
             timed = {n: sum(v) / len(v) for n, v in acc.items()}
             timing_how = "HIP event-record nodes around each kernel node of the replayed step graphs (K steps)"

@@ -299,7 +299,7 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
                                    float* pooled_out, int64_t ldp, float* gpooled, const float* params,
                                    const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
                                    float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
-                                   void* workspace, size_t ws_bytes, void* stream);
+                                   const void* const* next_cols, void* workspace, size_t ws_bytes, void* stream);
 /* tt_tower_wgrad_pre + the insert of the NEXT batch's lookups (i = t * B + m, key dedup_tables[t]
  * << 40 | id mod N) into next_dedup_ws (first CAS here, the rest deferred to the resolver of the
  * following tt_tower_update_pre_rowwise_adagrad_resolve). */
@@ -319,6 +319,19 @@ int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, i
                                                 const float* grad, int64_t ldg, float* weights, float* state,
                                                 float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
                                                 size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
+/* The step's backward tail in one launch (the production ring; the two launches above are its
+ * A/B variant): T2 (tt_tower_wgrad_pre: weight gradients, bias sums, loss, Adam scalars) + the
+ * COMPLETE insert of next_cols into next_dedup_ws (no deferred entries, no resolver) + the
+ * row-wise Adagrad of dedup_ws's rows looked up more than once, from grad (lr, emb_eps:
+ * 03_model_training.py:791-795); T3 follows as tt_tower_update_pre. */
+int tt_tower_wgrad_pre_insert_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                              size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
+                                              float adam_beta1, float adam_beta2, const void* const* next_cols,
+                                              int id_dtype, const int64_t* num_embeddings, const int32_t* dedup_tables,
+                                              const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                                              int F, const float* grad, int64_t ldg, float* weights, float* state,
+                                              float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
+                                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 /* T1 for the sharded step (row-wise / table-wise shards, single-hot): tower t's input row m is row
  * pos[t][m] of rows_in[t] ([*][in_dim[t]] fp32: the rows returned by the owners' all-to-all; -1
  * -> zeros, a dropped id), and its gradient row dX is written to row pos[t][m] of grad_rows_out[t]

@@ -1,5 +1,5 @@
 """EXPERIMENT: per-phase wall time of T1 from s_memrealtime stamps (100 MHz) of every workgroup,
-inside the full single-GPU step (dedup insert on). Stamps: 0 start, 1 X + weights in LDS/regs,
+inside the production ring step (in-place update of single-lookup rows). Stamps: 0 start, 1 X + weights in LDS/regs,
 2 layer 0, 3 layer 1, 4 logits, 5 dZ1, 6 dZ0, 7 dX in LDS, 15 dX stored; dedup wave: 9 passed the
 barriers, 8 inserts finished."""
 import os, sys
@@ -11,11 +11,14 @@ dev = torch.device("cuda:0")
 N = [50_000_000, 100_000_000]; B = 8192
 st = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, dev)
 g = torch.Generator(device=dev).manual_seed(1)
-st.load_batch([torch.randint(0, n, (B,), generator=g, device=dev) for n in N], torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32))
+# the production ring over 64 resident batches (eager launches)
+batches = [([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
+            torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32)) for _ in range(64)]
+st.capture_ring(batches, steps_per_graph=8)
 nwg = B // 32
 off = st.towers.nbytes - ((max(2 * nwg, 1024) * 64 + 255) // 256 * 256)
 for it in range(6):
-    st.step()
+    st.run_eager(1)
     torch.cuda.synchronize()
     stm = st.towers.ws[off:off + nwg * 128].view(torch.int64).view(nwg, 16).cpu().double()
     if it < 2:

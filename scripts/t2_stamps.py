@@ -11,15 +11,17 @@ dev = torch.device("cuda:0")
 N = [50_000_000, 100_000_000]; B = 8192
 st = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, dev)
 g = torch.Generator(device=dev).manual_seed(1)
-st.load_batch([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
-              torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32))
-nres = 64  # resolver workgroups first (they do not stamp)
+# the production ring (T2 = tower_wgrad_insert_kernel: tiles first, then bias, then inserts)
+batches = [([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
+            torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32)) for _ in range(64)]
+st.capture_ring(batches, steps_per_graph=8)
+nres = 0
 ntile = 6 * 32
 nbias = (2 * (128 + 64) + 1 + 3) // 4
 nwg = nres + ntile + nbias
 off = st.towers.nbytes - ((max(2 * (B // 32), 1024) * 64 + 255) // 256 * 256)
 for it in range(6):
-    st.step()
+    st.run_eager(1)
     torch.cuda.synchronize()
     stm = st.towers.ws[off:off + nwg * 64].view(torch.int64).view(nwg, 8).cpu().double()
     if it < 2:

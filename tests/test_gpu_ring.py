@@ -1,5 +1,6 @@
 """The production ring of the fused step (dedup one step ahead; rows looked up once updated in place
-inside T1, the others by K3 from dX): bit for bit the classic step (insert in T1, every row updated
+inside T1, the others by the tail launch from dX, then T3; or T2 + deferred insert, then resolver +
+update + T3): bit for bit the classic step (insert in T1, every row updated
 by K3), over resident batches with dropped ids, ids past N, repeated rows (2..30 lookups) and hot
 rows (> 30), through HIP graphs of several steps and eagerly."""
 import pytest
@@ -22,7 +23,7 @@ def _batches(N, B, n, seed, device):
 
 
 @pytest.mark.parametrize("D", [64, 128])
-@pytest.mark.parametrize("mode", ["graph", "eager"])
+@pytest.mark.parametrize("mode", ["graph", "eager", "graph_two_launch_tail"])
 def test_ring_equals_classic_step(device, D, mode):
     from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
 
@@ -31,8 +32,9 @@ def test_ring_equals_classic_step(device, D, mode):
     a = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=2)
     b = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=2)
     assert a.ring_supported()
+    a.ring_tail = mode != "graph_two_launch_tail"
     a.capture_ring(batches, steps_per_graph=2)
-    if mode == "graph":
+    if mode != "eager":
         a.run(3)
         a.run(3)  # continues at the cursor (mixed big / small graphs)
     else:

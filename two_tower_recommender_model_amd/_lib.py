@@ -206,7 +206,7 @@ SIGNATURES = {
     "tt_tower_fwd_bwd_gather_update": (
         _int,
         [_psh, _i64, _pvp, _int, _pi64, _pvp, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _f32, _f32, _vp, _sz,
-         _i64, _vp, _sz, _vp],
+         _i64, _pvp, _vp, _sz, _vp],
     ),
     "tt_tower_wgrad_pre_insert": (
         _int,
@@ -215,6 +215,11 @@ SIGNATURES = {
     "tt_tower_update_pre_rowwise_adagrad_resolve": (
         _int,
         [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64,
+         _vp, _vp, _f32, _f32, _vp, _vp, _sz, _i64, _vp],
+    ),
+    "tt_tower_wgrad_pre_insert_rowwise_adagrad": (
+        _int,
+        [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _pvp, _int, _pi64, _pi32, _ptm, _int, _pfm, _int, _vp, _i64,
          _vp, _vp, _f32, _f32, _vp, _vp, _sz, _i64, _vp],
     ),
     "tt_tower_adam_grads_sum": (
@@ -272,6 +277,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_gather_update",
     "tt_tower_wgrad_pre_insert",
     "tt_tower_update_pre_rowwise_adagrad_resolve",
+    "tt_tower_wgrad_pre_insert_rowwise_adagrad",
 ]
 
 _lib = None

@@ -53,6 +53,7 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_adam_grads_sum, tt_tower_adam_grads_sum_rowwise_adagrad, tt_tower_wgrad_route_count,
 // tt_tower_grads_replicated_route_place, tt_tower_fwd_bwd_gather_update, tt_tower_wgrad_pre_insert,
 // tt_tower_update_pre_rowwise_adagrad_resolve
-int tt_num_entry_points(void) { return 48; }
+// tt_tower_wgrad_pre_insert_rowwise_adagrad
+int tt_num_entry_points(void) { return 49; }
 
 }  // extern "C"

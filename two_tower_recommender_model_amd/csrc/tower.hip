@@ -91,6 +91,10 @@ struct TowerArgs {
   float* uw[2];  // tower t's table rows (writable; == gtab[t])
   float* us[2];  // tower t's table row-wise state
   float ulr, ueps;
+  // UPD, nullable: the NEXT batch's id columns; the dedup wave touches every 64-B segment of this
+  // tile's next rows and their state (a prefetch into the memory-side cache and this XCD's TLB;
+  // the values are discarded)
+  const void* pcol[2];
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
 };
@@ -483,8 +487,39 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     const bool single = cl >= 0 && (word & DD_CNT_MASK) == 1;
     urow[tq][row] = single ? r : -1;
     ustate[tq][row] = st;
+    // the next batch's rows of this tile, after the compute waves' gather has landed (barrier 1):
+    // 64-B segment k = j * 64 + lane of row k / SEG, all loads in flight across the remaining
+    // barriers (a barrier waits only on LDS counters), consumed once after the last one
+    constexpr int SEG = (IN_ ? IN_ : 128) * 4 / 64;  // 64-B segments per row (UPD: IN_ is 64 or 128)
+    constexpr int NPF = 2 * TR * SEG / 64;
+    uint32_t pv[NPF];
+    uint32_t pf = 0;
+    const bool pref = a.pcol[0] != nullptr;
+    if (pref) {
+      const float* base = nullptr;
+      if (gm < a.B) {
+        const int64_t idn = load_id(tq ? a.pcol[1] : a.pcol[0], a.gid_dtype, gm);
+        if (idn != 0) {
+          const int64_t rn = py_mod64(idn, tq ? a.gmod[1] : a.gmod[0]);
+          base = (tq ? a.gtab[1] : a.gtab[0]) + rn * IN_;
+          pf = __float_as_uint((tq ? a.us[1] : a.us[0])[rn]);
+        }
+      }
+      const uint64_t b64 = reinterpret_cast<uint64_t>(base);
+#pragma unroll
+      for (int j = 0; j < NPF; ++j) {
+        const int k = j * 64 + lane, lk = k / SEG;  // lookup lk = tq * TR + row of the wave's lane order
+        const uint64_t p = (uint64_t)__shfl((long long)b64, lk, 64);
+        pv[j] = p ? *reinterpret_cast<const uint32_t*>(p + (k % SEG) * 64) : 0u;
+      }
+    }
 #pragma unroll 1
     for (int k = 1; k < T1_BARRIERS; ++k) __syncthreads();
+    if (pref) {
+#pragma unroll
+      for (int j = 0; j < NPF; ++j) pf ^= pv[j];
+      if (pf == 0x7fc00123u && a.B < 0) a.logits[0] = 0.f;  // never taken: keeps the loads
+    }
     return;
   }
   if (wid == 8) {
@@ -1178,13 +1213,19 @@ __device__ __forceinline__ void insert_next_block(const InsertArgs& ins, int blk
   if (grp < ins.dd.ovf_groups) dd_insert_defer_finish(ins.dd, p, (int32_t)(i < 2 * ins.B ? i : 0), (int)grp);
 }
 
+// EXPERIMENT (TT_RING_STAMPS): s_memrealtime of wave 0 at the start / end of each workgroup's role
+#define RING_STAMP(p, k) \
+  do { if ((p) && threadIdx.x == 0 && blockIdx.x < 1024) (p)[(int64_t)blockIdx.x * 2 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+
 __global__ void __launch_bounds__(256) tower_wgrad_insert_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
-                                                                 InsertArgs ins, int n_t2) {
+                                                                 InsertArgs ins, int n_t2, int64_t* stamps) {
   __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
+  RING_STAMP(stamps, 0);
   if ((int)blockIdx.x < n_t2)
     wgrad_block(a, tiles, (int)blockIdx.x, smem);
   else
     insert_next_block(ins, (int)blockIdx.x - n_t2);
+  RING_STAMP(stamps, 1);
 }
 
 // Pipelined sharded step: the NEXT batch's route rides in the towers' launches as extra
@@ -1238,9 +1279,13 @@ struct UpdateArgs {
   float out_scale;
   int in_srcs;
   int64_t in_stride;
+  int64_t* stamps;  // EXPERIMENT (TT_RING_STAMPS): [workgroups][4] s_memrealtime per phase
 };
+#define T3_STAMP(k) \
+  do { if (a.stamps && threadIdx.x == 0 && bid < 512) a.stamps[(int64_t)bid * 4 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
+  T3_STAMP(0);
   const int64_t i = (int64_t)bid * 256 + threadIdx.x;
   int64_t t_step = 0;
   float step_size = 0.f, bc2_sqrt = 1.f;
@@ -1255,18 +1300,39 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
     bc2_sqrt = (float)sqrt(bc2);
   }
   if (i < a.P) {
-    int sg = 0;
-    while (sg + 1 < a.nseg && i >= a.seg_off[sg + 1]) ++sg;
-    const int64_t e = i - a.seg_off[sg];
+    // this element's segment: a loop over the (wave-uniform) segment list with scalar kernarg
+    // loads and per-lane selects — a per-lane index into the kernarg arrays would be a chain of
+    // dependent vector loads from the kernarg segment (several us per launch)
+    int64_t soff = 0, swc = 0;
+    int sisw = 0, sk = 1, sn = 1;
+#pragma unroll
+    for (int q = 0; q < 2 * 2 * MAXL; ++q) {
+      if (q < a.nseg && i >= a.seg_off[q]) {
+        soff = a.seg_off[q];
+        sisw = a.seg_isw[q];
+        sk = a.seg_k[q];
+        sn = a.seg_n[q];
+        swc = a.seg_wc[q];
+      }
+    }
+    const int64_t e = i - soff;
     float p = a.params[i];
     float g = 0.f;
     if (a.grads_in) {
       g = a.grads_in[i];
       for (int q = 1; q < a.in_srcs; ++q) g += a.grads_in[(int64_t)q * a.in_stride + i];
     } else if (a.do_adam || a.grads_out) {
-      if (a.seg_isw[sg]) {
-#pragma unroll 8
-        for (int s = 0; s < a.S; ++s) g += a.slab[(int64_t)s * a.P + i];
+      if (sisw) {
+        // a round's 32 slab loads all in flight (one memory latency per 32 slabs, not per load);
+        // the sum keeps the sequential order s = 0, 1, ...
+        for (int s0 = 0; s0 < a.S; s0 += 32) {
+          float v[32];
+#pragma unroll
+          for (int u = 0; u < 32; ++u) v[u] = s0 + u < a.S ? a.slab[(int64_t)(s0 + u) * a.P + i] : 0.f;
+#pragma unroll
+          for (int u = 0; u < 32; ++u)
+            if (s0 + u < a.S) g += v[u];
+        }
       } else {
         g = a.slab[i];  // bias gradient, reduced over the T1 workgroups by T2's bias waves
       }
@@ -1279,6 +1345,7 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
         }
       }
     }
+    T3_STAMP(1);
     if (a.do_adam) {
       if (a.wd != 0.f) g = g + a.wd * p;
       float m = a.exp_avg[i];
@@ -1290,14 +1357,15 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
       a.exp_avg_sq[i] = v;
       a.params[i] = p;
     }
-    if (a.seg_isw[sg]) {
-      const int K = a.seg_k[sg], N = a.seg_n[sg];
+    if (sisw) {
+      const int K = sk, N = sn;
       const int64_t n = e / K, k = e - n * K;
-      a.wb[a.seg_wc[sg] + e] = (__bf16)p;
-      a.wtb[a.seg_wc[sg] + k * N + n] = (__bf16)p;
-      a.wbf[a.seg_wc[sg] + frag_off((int)n, (int)k, K)] = (__bf16)p;   // W as [N][K]
-      a.wtbf[a.seg_wc[sg] + frag_off((int)k, (int)n, N)] = (__bf16)p;  // W^T as [K][N]
+      a.wb[swc + e] = (__bf16)p;
+      a.wtb[swc + k * N + n] = (__bf16)p;
+      a.wbf[swc + frag_off((int)n, (int)k, K)] = (__bf16)p;   // W as [N][K]
+      a.wtbf[swc + frag_off((int)k, (int)n, N)] = (__bf16)p;  // W^T as [K][N]
     }
+    T3_STAMP(2);
   }
   if (a.do_adam && !a.adam_pre) {
     __syncthreads();
@@ -1330,15 +1398,51 @@ __global__ void __launch_bounds__(256) tower_update_route_kernel(UpdateArgs a, R
 // the update of this batch's rows looked up more than once (skip_single), then T3
 constexpr int K3_RES_WGS = 32;
 __global__ void __launch_bounds__(256) tower_update_dedup_resolve_kernel(UpdateArgs a, DdUpdateArgs d, DedupWs next,
-                                                                         int n_dd) {
+                                                                         int n_dd, int64_t* stamps) {
   __shared__ __attribute__((aligned(16))) char smem[DD_SMEM];
   const int bid = (int)blockIdx.x;
+  RING_STAMP(stamps, 0);
   if (bid < K3_RES_WGS)
     dd_resolve_block(next, bid, K3_RES_WGS);
   else if (bid < K3_RES_WGS + n_dd)
     dd_update_block(d, bid - K3_RES_WGS, smem);
   else
     update_block(a, bid - K3_RES_WGS - n_dd, (int)gridDim.x - K3_RES_WGS - n_dd);
+  RING_STAMP(stamps, 1);
+}
+
+// The pipelined fused step's backward tail, one launch: T2 (weight gradients, bias sums, loss,
+// Adam scalars) + the NEXT batch's complete insert (probing in place: its latency hides behind the
+// tiles, so no deferral and no resolver launch) + the update of this batch's rows looked up more
+// than once. The three roles read only what T1 (or the previous step) wrote; T3 follows as its own
+// launch (it needs every T2 slab: in-launch, that hand-off across the 8 XCDs' L2s cost more than
+// the launch boundary it saves — DESIGN.md section 5).
+// the NEXT batch's lookups, one per thread, inserted completely (probing in place)
+__device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, int blk) {
+  const int64_t i = (int64_t)blk * 256 + threadIdx.x;
+  if (i >= 2 * ins.B) return;
+  const int t = i >= ins.B;
+  const int64_t m = i - (t ? ins.B : 0);
+  const int64_t id = load_id(t ? ins.col[1] : ins.col[0], ins.id_dtype, m);
+  const uint64_t key = id != 0 ? (((uint64_t)(t ? ins.tab[1] : ins.tab[0]) << DD_TABLE_SHIFT) |
+                                  (uint64_t)py_mod64(id, t ? ins.mod[1] : ins.mod[0]))
+                               : DD_EMPTY;
+  dd_insert(ins.dd, key, (int32_t)i);
+}
+
+__global__ void __launch_bounds__(256) tower_tail_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
+                                                         InsertArgs ins, DdUpdateArgs d, int n_ins, int n_t2,
+                                                         int64_t* stamps) {
+  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
+  int b = (int)blockIdx.x;
+  RING_STAMP(stamps, 0);
+  if (b < n_ins)
+    insert_next_full_block(ins, b);
+  else if ((b -= n_ins) < n_t2)
+    wgrad_block(a2, tiles, b, smem);  // n_ins % 8 == 0: b keeps the XCD placement of wgrad_block
+  else
+    dd_update_block(d, b - n_t2, smem);
+  RING_STAMP(stamps, 1);
 }
 
 // T3 + the embedding path's fused row-wise Adagrad (dedup.h) in ONE launch: workgroups [0, n_dd)
@@ -1493,6 +1597,26 @@ int tt_tower_workspace_init(const tt_tower_shape_t* shape, int64_t B, void* work
 }
 
 }  // extern "C"
+
+namespace tt {
+// the NEXT batch's insert role (tt_tower_wgrad_pre_insert, tt_tower_tail_rowwise_adagrad_insert)
+static int insert_args(int64_t B, const void* const* next_cols, int id_dtype, const int64_t* num_embeddings,
+                       const int32_t* dedup_tables, void* next_dedup_ws, int64_t dedup_max_lookups, InsertArgs& ins) {
+  for (int t = 0; t < 2; ++t) {
+    if (!next_cols[t] || num_embeddings[t] < 1 || num_embeddings[t] >= (1ll << DD_TABLE_SHIFT) ||
+        dedup_tables[t] < 0 || dedup_tables[t] >= TT_MAX_TABLES)
+      return fail(TT_EINVAL, "tower insert: bad column / table");
+    ins.col[t] = next_cols[t];
+    ins.mod[t] = num_embeddings[t];
+    ins.tab[t] = dedup_tables[t];
+  }
+  ins.id_dtype = id_dtype;
+  ins.B = B;
+  dedup_layout(next_dedup_ws, dedup_max_lookups, &ins.dd);
+  return TT_OK;
+}
+
+}  // namespace tt
 
 namespace tt {
 // shared by tt_tower_fwd_bwd / tt_tower_fwd_bwd_gather: checks, T1 arguments, launch
@@ -1844,6 +1968,11 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
     tower_update_dedup_kernel<<<dim3((unsigned)(dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(a, *dd, (int)dd_grid);
     return check_launch("tower_update_rowwise_adagrad");
   }
+  if (getenv("TT_RING_STAMPS") && g3 <= 512) {
+    TowerLayout L;
+    tower_layout(shape, B, &L);
+    a.stamps = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 6144;
+  }
   tower_update_kernel<<<dim3((unsigned)g3), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_update");
 }
@@ -2042,7 +2171,7 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
                                    float* pooled_out, int64_t ldp, float* gpooled, const float* params,
                                    const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
                                    float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
-                                   void* workspace, size_t ws_bytes, void* stream) {
+                                   const void* const* next_cols, void* workspace, size_t ws_bytes, void* stream) {
   if (!cols || !num_embeddings || !table_rows || !table_state || !dedup_ws)
     return fail(TT_EINVAL, "tower_gather_update: null pointer");
   if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_gather_update: ids must be int32/int64");
@@ -2059,6 +2188,10 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
     a.gmod[t] = num_embeddings[t];
     a.uw[t] = table_rows[t];
     a.us[t] = table_state[t];
+    if (next_cols) {
+      if (!next_cols[t]) return fail(TT_EINVAL, "tower_gather_update: null next column");
+      a.pcol[t] = next_cols[t];
+    }
   }
   a.gid_dtype = id_dtype;
   a.pooled_out = pooled_out;
@@ -2093,20 +2226,12 @@ int tt_tower_wgrad_pre_insert(const tt_tower_shape_t* shape, int64_t B, float* l
   a.beta1 = adam_beta1;
   a.beta2 = adam_beta2;
   InsertArgs ins{};
-  for (int t = 0; t < 2; ++t) {
-    if (!next_cols[t] || num_embeddings[t] < 1 || num_embeddings[t] >= (1ll << DD_TABLE_SHIFT) ||
-        dedup_tables[t] < 0 || dedup_tables[t] >= TT_MAX_TABLES)
-      return fail(TT_EINVAL, "tower_wgrad_pre_insert: bad column / table");
-    ins.col[t] = next_cols[t];
-    ins.mod[t] = num_embeddings[t];
-    ins.tab[t] = dedup_tables[t];
-  }
-  ins.id_dtype = id_dtype;
-  ins.B = B;
-  dedup_layout(next_dedup_ws, dedup_max_lookups, &ins.dd);
+  rc = insert_args(B, next_cols, id_dtype, num_embeddings, dedup_tables, next_dedup_ws, dedup_max_lookups, ins);
+  if (rc) return rc;
   const int64_t n_ins = ceil_div(ceil_div(2 * B, 64), 4);  // 4 waves of 64 lookups per workgroup
+  int64_t* stamps = getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 4096 : nullptr;
   tower_wgrad_insert_kernel<<<dim3((unsigned)(wgs + n_ins)), dim3(256), 0, as_stream(stream)>>>(
-      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), ins, (int)wgs);
+      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), ins, (int)wgs, stamps);
   return check_launch("tower_wgrad_pre_insert");
 }
 
@@ -2137,9 +2262,55 @@ int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, i
   rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
                nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0, a, &g3);
   if (rc) return rc;
+  int64_t* stamps = getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 6144 : nullptr;
+  if (stamps && (K3_RES_WGS + dd_grid + g3 > 1024 || L.nwg > 256)) stamps = nullptr;
   tower_update_dedup_resolve_kernel<<<dim3((unsigned)(K3_RES_WGS + dd_grid + g3)), dim3(256), 0,
-                                      as_stream(stream)>>>(a, d, next, (int)dd_grid);
+                                      as_stream(stream)>>>(a, d, next, (int)dd_grid, stamps);
   return check_launch("tower_update_pre_rowwise_adagrad_resolve");
+}
+
+int tt_tower_wgrad_pre_insert_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                              size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
+                                              float adam_beta1, float adam_beta2, const void* const* next_cols,
+                                              int id_dtype, const int64_t* num_embeddings, const int32_t* dedup_tables,
+                                              const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                                              int F, const float* grad, int64_t ldg, float* weights, float* state,
+                                              float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
+                                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+  if (!adam_step_state || !next_cols || !num_embeddings || !dedup_tables || !next_dedup_ws)
+    return fail(TT_EINVAL, "tower_tail: null pointer");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_tail: ids must be int32/int64");
+  if (dedup_max_lookups < 2 * B || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+      dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
+      (reinterpret_cast<uintptr_t>(next_dedup_ws) & 63))
+    return fail(TT_ECAPACITY, "tower_tail: dedup workspace too small / misaligned");
+  WgradArgs a2{};
+  int64_t wgs = 0;
+  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a2, &wgs);
+  if (rc) return rc;
+  TowerLayout L;
+  tower_layout(shape, B, &L);
+  char* ws = reinterpret_cast<char*>(workspace);
+  a2.step_state = adam_step_state;
+  a2.adam_pre = reinterpret_cast<float*>(ws + L.o_counter);
+  a2.lr = adam_lr;
+  a2.beta1 = adam_beta1;
+  a2.beta2 = adam_beta2;
+  InsertArgs ins{};
+  rc = insert_args(B, next_cols, id_dtype, num_embeddings, dedup_tables, next_dedup_ws, dedup_max_lookups, ins);
+  if (rc) return rc;
+  DdUpdateArgs d{};
+  int64_t dd_grid = 0;
+  rc = dedup_update_args(tables, T, features, F, B, grad, ldg, weights, state, lr, emb_eps, dedup_ws, dedup_ws_bytes,
+                         dedup_max_lookups, d, &dd_grid);
+  if (rc) return rc;
+  d.skip_single = 1;
+  const int64_t n_ins = ceil_div(ceil_div(2 * B, 256), 8) * 8;  // one lookup per thread; % 8 == 0
+  int64_t* stamps = getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
+  if (stamps && L.nwg > 256) stamps = nullptr;
+  tower_tail_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
+      a2, reinterpret_cast<const WgradTile*>(ws + a2.tiles_off), ins, d, (int)n_ins, (int)wgs, stamps);
+  return check_launch("tower_wgrad_pre_insert_rowwise_adagrad");
 }
 
 int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,

@@ -17,6 +17,8 @@ No host synchronisation inside ``step()``: buffers are sized for the worst case 
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Sequence
 
 import ctypes as C
@@ -161,6 +163,13 @@ class FusedTwoTowerStep:
         if self.dedup_single:
             self.tables.ensure_dedup_workspace(F * B)
         self.materialize_pooled = bool(materialize_pooled)
+        # ring: T1 touches the next batch's rows after its own gather (cache / TLB prefetch);
+        # TT_PREFETCH_NEXT=0 turns it off (A/B measurement)
+        self.prefetch_next = os.environ.get("TT_PREFETCH_NEXT", "1") != "0"
+        # ring: T2 + complete next-batch insert + update of the rows looked up more than once in one
+        # launch, then T3 alone; TT_RING_TAIL=0: T2 + deferred insert, then resolver + update + T3
+        # (A/B measurement)
+        self.ring_tail = os.environ.get("TT_RING_TAIL", "1") != "0"
         self.combined_bwd = bool(combined_bwd)
         # in-graph kernel timing (bench): while a list, step() records an event pair per launch
         self._timing: Optional[list] = None
@@ -426,10 +435,11 @@ class FusedTwoTowerStep:
                   next_cols: Sequence[torch.Tensor]) -> None:
         """One production step on (cols, labels), whose dedup table (parity) is complete; files
         next_cols into the other table. Three launches:
-          T1  gather + towers fwd/bwd + in-place row-wise Adagrad of the rows looked up once
-          T2  tower weight gradients + Adam scalars + insert of the next batch
-          K3  resolver of the next batch's deferred inserts + update of the rows looked up more
-              than once (from T1's dX) + T3 (slab reduction, Adam, bf16 weight copies)"""
+          T1    gather + towers fwd/bwd + in-place row-wise Adagrad of the rows looked up once
+          tail  T2 (tower weight gradients, Adam scalars) + complete insert of the next batch +
+                update of the rows looked up more than once (from T1's dX)
+          T3    slab reduction, Adam, bf16 weight copies
+        (ring_tail False: T2 + deferred insert of the next batch, then resolver + row update + T3)."""
         lib, tw, ts, B, dev = _lib.load(), self.towers, self.tables, self.B, self.device
         ring = self._ring_ws()
         ws, wsn = ring[parity], ring[parity ^ 1]
@@ -440,8 +450,24 @@ class FusedTwoTowerStep:
             ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
             ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
             ptr(self.params), ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws),
-            ws.numel(), ts._dd_cap, ptr(tw.ws), tw.nbytes, st), "tower_fwd_bwd_gather_update")
+            ws.numel(), ts._dd_cap, ptr_array(list(next_cols)) if self.prefetch_next else None, ptr(tw.ws), tw.nbytes,
+            st), "tower_fwd_bwd_gather_update")
         self._mark("t1", 1)
+        if self.ring_tail:
+            self._mark("tail", 0)
+            check(lib.tt_tower_wgrad_pre_insert_rowwise_adagrad(
+                C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
+                0.999, ptr_array(list(next_cols)), id_dtype_code(next_cols[0].dtype), self._ring_ne, self._ring_tab,
+                ts._tm, ts.T, ts._fm, ts.F, ptr(self.gpooled), self.gpooled.stride(0), ptr(ts.weights), ptr(ts.state),
+                self.lr_emb, self.eps, ptr(ws), ptr(wsn), ws.numel(), ts._dd_cap, st),
+                "tower_wgrad_pre_insert_rowwise_adagrad")
+            self._mark("tail", 1)
+            self._mark("t3", 0)
+            check(lib.tt_tower_update_pre(C.byref(tw.shape), B, ptr(self.params), ptr(self.exp_avg),
+                                          ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads), ptr(tw.ws),
+                                          tw.nbytes, st), "tower_update_pre")
+            self._mark("t3", 1)
+            return
         self._mark("t2", 0)
         check(lib.tt_tower_wgrad_pre_insert(
             C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
