@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -q -m gpu ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
 echo "pytest exit=$rc" >> gpurun_out/gpu_tests.log
 tail -25 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi  # a failing test may be a GPU fault: run nothing more

@@ -1,9 +1,11 @@
 """Parity of the PRODUCTION step at the BASELINE.json sizes.
 
-The step under test is exactly what bench.py times: ``FusedTwoTowerStep`` with its defaults (T1 =
-EBC gather + bf16-MFMA towers fwd/bwd-data + dot/BCE + dedup insert, T2 = weight gradients +
-deferred inserts, K3 = fused row-wise Adagrad + slab reduction + Adam) replayed from HIP graphs over
-resident batches; for config 5 the multi-hot KJT path (tt_pooled_fwd -> towers -> tiled
+The step under test is what bench.py times: the production ring of ``FusedTwoTowerStep`` (T1 = EBC
+gather + bf16-MFMA towers fwd/bwd-data + dot/BCE + in-place row-wise Adagrad of the rows looked up
+once, from the dedup table the previous step built; tail = weight gradients + the next batch's
+insert + row-wise Adagrad of the other rows; T3 = slab reduction + Adam) replayed from HIP graphs
+over resident batches, with ``materialize_pooled`` so that T1 also writes the gathered rows and
+every dX row for the checks; for config 5 the multi-hot KJT path (tt_pooled_fwd -> towers -> tiled
 tt_bwd_prepare -> tt_bwd_rowwise_adagrad). Shapes:
 
   north star  100M items x 50M users, D 128, B 8192 (tables of 1.28e10 / 6.4e9 fp32 elements: far
@@ -20,8 +22,8 @@ otherwise be a bf16-tower comparison (the gradient rows dX that T1 writes):
   ``F.embedding_bag`` sum over the same rows, rtol 1e-6;
 * towers: logits, dX and the tower gradients against the fp64 emulation of the kernels' rounding
   points (tests/tower_emul.py), relative Frobenius error < 2e-3; loss rtol 1e-4;
-* K3 (tables + row-wise state of every touched row): ``oracle.rowwise_adagrad_from_lookups`` fed
-  T1's dX, rtol 1e-5 (weights atol 1e-5 x lr, state atol 1e-12) — eps 1e-10, lr 0.01 (03:791-795);
+* the embedding update (T1's in-place rows + the tail's; tables + row-wise state of every touched
+  row): ``oracle.rowwise_adagrad_from_lookups`` fed T1's dX, rtol 1e-5 (weights atol 1e-5 x lr, state atol 1e-12) — eps 1e-10, lr 0.01 (03:791-795);
 * Adam: the oracle's torch.optim.Adam restatement fed the kernels' own tower gradient, rtol 1e-5
   (absolute floors: 1e-6 x max|g| on the moments, 1e-5 x lr on the parameters, where m = 0.9 m0 +
   0.1 g cancels).
@@ -130,13 +132,13 @@ def test_production_step_at_baseline_size(device, case, ids):
     N, D, B = CASES[case]["N"], CASES[case]["D"], CASES[case]["B"]
     st = FusedTwoTowerStep(N, [D, D], [0], [1], LAYERS, B, device, lr_emb=LR, lr_dense=LR, id_dtype=torch.int64,
                            seed=0, materialize_pooled=True)
-    # the production configuration bench.py times: fused gather + single-hot dedup + 3 launches
-    assert st.towers is not None and st.gather and st.dedup_single and st.combined_bwd
+    # the production configuration bench.py times: the ring (fused gather + single-hot dedup)
+    assert st.towers is not None and st.ring_supported()
     if case == "northstar":
         assert st.tables.rows[1] * D > 2 ** 31 and st.tables.weight_offsets[1] > 2 ** 31
     batches = _single_hot_batches(N, B, ids, device, seed=11 if ids == "uniform" else 12)
-    st.capture_pool(batches, steps_per_graph=1)
-    st.pool_graphs[0].replay()
+    st.capture_ring(batches, steps_per_graph=1)
+    st.run(1)
     torch.cuda.synchronize()
     cols, lab = batches[1]
     # state before step 2 (touched rows only; the tables themselves stay on the GPU)
@@ -147,7 +149,7 @@ def test_production_step_at_baseline_size(device, case, ids):
     params0, m0, v0 = st.params.cpu().clone(), st.exp_avg.cpu().clone(), st.exp_avg_sq.cpu().clone()
     step0 = int(st.adam_state[0])
     assert step0 == 1
-    st.pool_graphs[1].replay()
+    st.run(1)
     torch.cuda.synchronize()
     # (1) gathered rows: bit-exact (id 0 -> zeros)
     pooled = st.pooled.cpu()
@@ -160,7 +162,7 @@ def test_production_step_at_baseline_size(device, case, ids):
     grads = st.grads.cpu()
     prm = _check_towers(pooled[:, :D], pooled[:, D:], params0, st, lab, st.logits.cpu(), gp[:, :D], gp[:, D:],
                         grads, B)
-    # (3) K3: fused row-wise Adagrad fed T1's own dX rows (lookup i = (feature, bag), kept lookups only)
+    # (3) row-wise Adagrad (T1 in place + tail) fed T1's own dX rows (lookup i = (feature, bag), kept lookups)
     for t in range(2):
         k = keep[t].cpu()
         _check_rowwise_adagrad(st.tables.table_view(t), st.tables.state_view(t), uniq[t], before[t][0], before[t][1],
