@@ -585,10 +585,14 @@ def run_host_fed(args):
     host = synthetic_host_batches([num_users, num_items], B, args.batches, seed=1)
     pipe = HostFedPipeline(step, group=args.steps_per_graph, depth=3)
     src = itertools.cycle(host)
-    pipe.run(src, max_steps=args.warmup)
+    # whole groups, and enough of them that the pipeline's fill (two groups copied before the first
+    # replay) and drain do not dominate: at least 64 groups timed
+    g = args.steps_per_graph
+    steps = max(64 * g, -(-args.steps // g) * g)
+    pipe.run(src, max_steps=max(args.warmup, 4 * g))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n = pipe.run(src, max_steps=args.steps)
+    n = pipe.run(src, max_steps=steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return n * B / dt, dt / n * 1e3, float(step.loss), n
