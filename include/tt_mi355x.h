@@ -477,14 +477,15 @@ int tt_shard_route_segs(int F, int64_t B, const void* const* cols, int id_dtype,
                         size_t ws_bytes, void* stream);
 /* owner: source s's block of the received buffer starts at recv + s * block_i64 (int64 units), its
  * counts at + counts_i64, feature f's keys at + counts_i64 + F + seg_off[f] (seg_off: host [F],
- * ascending, slots = S). Slot j of source s: rows_out[s * S + j] = the local row (bf16, round to
- * nearest even) and, with dedup_ws, lookup s * S + j inserted for tt_dedup_rowwise_adagrad (one
- * pseudo-feature per source: B = S, out_row = the row of source s's gradient block). Tables: one
- * per feature (table f = feature f), one dim. A key outside the shard sets *bad (sticky). */
+ * ascending, slots = S). Slot j of source s: rows_out[s * out_stride + j] (out_stride >= S rows) =
+ * the local row (bf16, round to nearest even) and, with dedup_ws, lookup s * S + j inserted for
+ * tt_dedup_rowwise_adagrad (one pseudo-feature per source: B = S, out_row = the row of source s's
+ * gradient block). Tables: one per feature (table f = feature f), one dim. A key outside the shard
+ * sets *bad (sticky). */
 int tt_shard_gather_segs_bf16(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
                               const int64_t* recv, int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
-                              int64_t slots, void* rows_out, int32_t* bad, void* dedup_ws, size_t dedup_ws_bytes,
-                              int64_t dedup_max_lookups, void* stream);
+                              int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad, void* dedup_ws,
+                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 /* T1 of the pipelined sharded step: tt_tower_fwd_bwd_indexed_bf16 with the dX row of (tower t,
  * bag m) written at row pos_out[t][m] (units of in_dim floats) of grad_rows_out[t] — the gradient
  * region of exchange A's send buffer — instead of at its input row. */
@@ -498,6 +499,11 @@ int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, con
  * exchange A: DDP's mean all-reduce becomes a fixed-order sum on the receivers. */
 int tt_tower_grads_replicated(const tt_tower_shape_t* shape, int64_t B, float* params, float* base, int copies,
                               const int64_t* offsets, float scale, void* workspace, size_t ws_bytes, void* stream);
+/* tt_tower_adam_grads_sum with the step scalars a preceding tt_tower_wgrad_pre (or launch U of
+ * the pipelined sharded step) wrote into the workspace: no pow() per thread, no arrival ticket. */
+int tt_tower_adam_pre_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
+                                int64_t src_stride, float* exp_avg, float* exp_avg_sq, float eps, float beta1,
+                                float beta2, float weight_decay, void* workspace, size_t ws_bytes, void* stream);
 /* T3 with Adam on the gradient sum_{s < nsrc} grads[s * src_stride + i] (ascending s: identical on
  * every rank) + the bf16 weight copies. */
 int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
@@ -505,6 +511,39 @@ int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* par
                             float eps, float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes,
                             void* stream);
 
+/* The pipelined sharded step's launch U (after exchange A): T2 with Adam's step scalars
+ * (tt_tower_wgrad_pre; adam_step_state advanced) + the count pass
+ * of a later batch's route (arguments as tt_shard_route_segs) + the owner's row-wise Adagrad over
+ * the received gradient rows (arguments as tt_dedup_rowwise_adagrad: Fsrc pseudo-features, B =
+ * emb_B) — one launch, the tower weight gradients beside the embedding update (input_dist /
+ * EBC backward + FBGEMM rowwise Adagrad and the dense backward of 03_model_training.py:417-455). */
+int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                               size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
+                                               float adam_beta1, float adam_beta2, int F, const void* const* cols,
+                                               int id_dtype,
+                                               const int64_t* num_embeddings, const int64_t* block_sizes,
+                                               const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                               int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                               size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
+                                               const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
+                                               const float* emb_grad, int64_t ldg, float* weights, float* state,
+                                               float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                               int64_t dedup_max_lookups, void* stream);
+/* Launch G: the tower gradient x scale into `copies` destinations (as tt_tower_grads_replicated) +
+ * the place pass of the route counted by launch U + the owner's gather of the next batch's rows
+ * (arguments as tt_shard_gather_segs_bf16). */
+int tt_tower_grads_replicated_route_place_gather(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
+                                                 int copies, const int64_t* offsets, float scale, void* workspace,
+                                                 size_t ws_bytes, int F, const void* const* cols, int id_dtype,
+                                                 const int64_t* num_embeddings, const int64_t* block_sizes,
+                                                 const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                                                 int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow,
+                                                 void* route_ws, size_t route_ws_bytes, const float* weights,
+                                                 const tt_table_meta_t* tables, int T, const int64_t* recv,
+                                                 int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
+                                                 int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad,
+                                                 void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
+                                                 void* stream);
 /* T2 (tt_tower_wgrad) with the NEXT batch's route count pass (tt_shard_route_segs' first half: its
  * arguments, route_ws its workspace) as extra workgroups of the same launch. */
 int tt_tower_wgrad_route_count(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,

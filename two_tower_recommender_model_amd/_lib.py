@@ -181,7 +181,7 @@ SIGNATURES = {
     ),
     "tt_shard_gather_segs_bf16": (
         _int,
-        [_vp, _ptm, _int, _int, _int, _vp, _i64, _i64, _pi64, _i64, _vp, _vp, _vp, _sz, _i64, _vp],
+        [_vp, _ptm, _int, _int, _int, _vp, _i64, _i64, _pi64, _i64, _vp, _i64, _vp, _vp, _sz, _i64, _vp],
     ),
     "tt_tower_fwd_bwd_indexed2_bf16": (
         _int,
@@ -221,6 +221,19 @@ SIGNATURES = {
         _int,
         [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _pvp, _int, _pi64, _pi32, _ptm, _int, _pfm, _int, _vp, _i64,
          _vp, _vp, _f32, _f32, _vp, _vp, _sz, _i64, _vp],
+    ),
+    "tt_tower_adam_pre_grads_sum": (
+        _int, [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _sz, _vp],
+    ),
+    "tt_tower_wgrad_route_count_rowwise_adagrad": (
+        _int,
+        [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp,
+         _vp, _f32, _f32, _vp, _sz, _i64, _vp],
+    ),
+    "tt_tower_grads_replicated_route_place_gather": (
+        _int,
+        [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _ptm, _int, _vp, _i64,
+         _i64, _pi64, _i64, _vp, _i64, _vp, _vp, _sz, _i64, _vp],
     ),
     "tt_tower_adam_grads_sum": (
         _int,
@@ -278,6 +291,9 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_wgrad_pre_insert",
     "tt_tower_update_pre_rowwise_adagrad_resolve",
     "tt_tower_wgrad_pre_insert_rowwise_adagrad",
+    "tt_tower_wgrad_route_count_rowwise_adagrad",
+    "tt_tower_grads_replicated_route_place_gather",
+    "tt_tower_adam_pre_grads_sum",
 ]
 
 _lib = None

@@ -131,4 +131,90 @@ __device__ __forceinline__ void route_place_block(const RouteArgs& a, int blk, i
   if (SEGS) a.pos_out[(int64_t)f * a.B + b] = po;
 }
 
+// Owner side of the pipelined exchange (tt_shard_gather_segs_bf16, and the pipelined step's
+// combined launch in csrc/tower.hip): the keys of source s sit in source block s of the received
+// buffer (int64 view: block s at s * blk64, counts at + cnt64, the slots of feature f at + cnt64 + F
+// + seg_off[f]); slot j of source s (j < S) -> rows_out[s * out_stride + j] (bf16) and, with the
+// dedup on, lookup s * S + j. A half-wave per slot.
+struct GatherSegArgs {
+  const float* weights;
+  tt_table_meta_t tables[TT_MAX_TABLES];
+  int T;
+  int F;
+  int W;
+  int D;
+  int64_t S;
+  int64_t out_stride;  // rows between source blocks of rows_out (>= S)
+  int64_t blk64, cnt64;
+  int64_t seg_off[TT_MAX_FEATURES + 1];
+  const int64_t* recv;
+  __bf16* rows_out;
+  DedupWs dd;
+  int dd_on;
+  int32_t* bad;
+};
+
+__device__ __forceinline__ void shard_gather_block(const GatherSegArgs& a, int blk) {
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t n = (int64_t)a.W * a.S;
+  const int64_t i = ((int64_t)blk * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (i >= n) return;
+  const int64_t s = i / a.S, j = i - s * a.S;
+  // feature of slot j and its segment start: a loop over the (uniform) feature list with scalar
+  // kernarg loads (a per-lane index into the kernarg arrays is a dependent vector load)
+  int f = 0;
+  int64_t so = a.seg_off[0];
+  for (int q = 1; q < a.F; ++q)
+    if (j >= a.seg_off[q]) {
+      f = q;
+      so = a.seg_off[q];
+    }
+  const int64_t k = j - so;
+  const int64_t* blkp = a.recv + s * a.blk64 + a.cnt64;
+  const int64_t cnt = blkp[f];
+  uint64_t key = DD_EMPTY;
+  const float* src = nullptr;
+  if (k < cnt) {
+    key = (uint64_t)blkp[a.F + j];
+    const int t = (int)(key >> DD_TABLE_SHIFT);
+    const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
+    int64_t woff = 0, nrows = 0;
+    int dim = 0;
+    for (int u = 0; u < a.T; ++u)
+      if (u == t) {
+        woff = a.tables[u].weight_offset;
+        nrows = a.tables[u].num_rows;
+        dim = a.tables[u].dim;
+      }
+    if (t == f && t < a.T && r < nrows && dim == a.D) {
+      src = a.weights + woff + r * a.D;
+    } else {
+      key = DD_EMPTY;
+      if (hl == 0) atomicOr(a.bad, 1);
+    }
+  }
+  DdPend pend;
+  if (a.dd_on && hl == 0) dd_insert_begin(a.dd, key, (int32_t)i, pend);
+  if (src) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
+    typedef __attribute__((ext_vector_type(4))) float f32x4g;
+    __bf16* dst = a.rows_out + (s * a.out_stride + j) * a.D;
+    for (int c = hl * 4; c < a.D; c += 128) {
+      const f32x4g v = *reinterpret_cast<const f32x4g*>(src + c);
+      bf16x4v o;
+      o[0] = (__bf16)v[0];
+      o[1] = (__bf16)v[1];
+      o[2] = (__bf16)v[2];
+      o[3] = (__bf16)v[3];
+      *reinterpret_cast<bf16x4v*>(dst + c) = o;
+    }
+  }
+  if (a.dd_on && hl == 0) dd_insert_finish(a.dd, pend, (int32_t)i);
+}
+
+int gather_segs_args(const float* weights, const tt_table_meta_t* tables, int T, int F, int W, const int64_t* recv,
+                     int64_t block_i64, int64_t counts_i64, const int64_t* seg_off, int64_t slots, void* rows_out,
+                     int64_t out_stride, int32_t* bad, void* dedup_ws, size_t dedup_ws_bytes,
+                     int64_t dedup_max_lookups, GatherSegArgs& a);
+
 }  // namespace tt

@@ -103,67 +103,56 @@ __global__ void __launch_bounds__(256) shard_gather_rows_kernel(GatherArgs a) {
 }
 
 
-// owner side of the pipelined exchange (tt_shard_gather_segs_bf16): the keys of source s sit in
-// source block s of the received buffer (int64 view: block s at s * blk64, counts at + cnt64, the
-// slots of feature f at + cnt64 + F + seg_off[f]); slot j of source s (j < S) -> rows_out[s * S + j]
-// (bf16) and, with the dedup on, lookup s * S + j
-struct GatherSegArgs {
-  const float* weights;
-  tt_table_meta_t tables[TT_MAX_TABLES];
-  int T;
-  int F;
-  int W;
-  int D;
-  int64_t S;
-  int64_t blk64, cnt64;
-  int64_t seg_off[TT_MAX_FEATURES + 1];
-  const int64_t* recv;
-  __bf16* rows_out;
-  DedupWs dd;
-  int dd_on;
-  int32_t* bad;
-};
+__global__ void __launch_bounds__(256) shard_gather_segs_kernel(GatherSegArgs a) { shard_gather_block(a, (int)blockIdx.x); }
 
-__global__ void __launch_bounds__(256) shard_gather_segs_kernel(GatherSegArgs a) {
-  const int lane = threadIdx.x & 63, hl = lane & 31;
-  const int64_t n = (int64_t)a.W * a.S;
-  const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
-  if (i >= n) return;
-  const int64_t s = i / a.S, j = i - s * a.S;
-  int f = 0;
-  while (f + 1 < a.F && j >= a.seg_off[f + 1]) ++f;
-  const int64_t k = j - a.seg_off[f];
-  const int64_t* blk = a.recv + s * a.blk64 + a.cnt64;
-  const int64_t cnt = blk[f];
-  uint64_t key = DD_EMPTY;
-  const float* src = nullptr;
-  if (k < cnt) {
-    key = (uint64_t)blk[a.F + j];
-    const int t = (int)(key >> DD_TABLE_SHIFT);
-    const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
-    if (t == f && t < a.T && r < a.tables[t].num_rows && a.tables[t].dim == a.D) {
-      src = a.weights + a.tables[t].weight_offset + r * a.D;
-    } else {
-      key = DD_EMPTY;
-      if (hl == 0) atomicOr(a.bad, 1);
-    }
+// host: the owner-side gather's arguments (tt_shard_gather_segs_bf16 and the pipelined step's
+// combined launch in csrc/tower.hip)
+int gather_segs_args(const float* weights, const tt_table_meta_t* tables, int T, int F, int W, const int64_t* recv,
+                     int64_t block_i64, int64_t counts_i64, const int64_t* seg_off, int64_t slots, void* rows_out,
+                     int64_t out_stride, int32_t* bad, void* dedup_ws, size_t dedup_ws_bytes,
+                     int64_t dedup_max_lookups, GatherSegArgs& a) {
+  if (T < 1 || T > TT_MAX_TABLES || F < 1 || F > TT_MAX_FEATURES || F > T || W < 1 || slots < 0)
+    return fail(TT_EINVAL, "shard_gather_segs: bad sizes");
+  if (!weights || !tables || !recv || !rows_out || !bad || !seg_off)
+    return fail(TT_EINVAL, "shard_gather_segs: null pointer");
+  a = GatherSegArgs{};
+  a.D = tables[0].dim;
+  for (int t = 0; t < T; ++t) {
+    if (tables[t].dim != a.D) return fail(TT_EINVAL, "shard_gather_segs: tables must share one dim");
+    if (tables[t].weight_offset % 4) return fail(TT_EINVAL, "shard_gather_segs: rows must be 16-B aligned");
+    a.tables[t] = tables[t];
   }
-  DdPend pend;
-  if (a.dd_on && hl == 0) dd_insert_begin(a.dd, key, (int32_t)i, pend);
-  if (src) {
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
-    __bf16* dst = a.rows_out + i * a.D;
-    for (int c = hl * 4; c < a.D; c += 128) {
-      const f32x4v v = *reinterpret_cast<const f32x4v*>(src + c);
-      bf16x4v o;
-      o[0] = (__bf16)v[0];
-      o[1] = (__bf16)v[1];
-      o[2] = (__bf16)v[2];
-      o[3] = (__bf16)v[3];
-      *reinterpret_cast<bf16x4v*>(dst + c) = o;
-    }
+  if (a.D % 4 || (reinterpret_cast<uintptr_t>(weights) & 15) || (reinterpret_cast<uintptr_t>(rows_out) & 7))
+    return fail(TT_EINVAL, "shard_gather_segs: D % 4 == 0 and aligned buffers required");
+  for (int f = 0; f <= F; ++f) {
+    a.seg_off[f] = f < F ? seg_off[f] : slots;
+    if (a.seg_off[f] < 0 || a.seg_off[f] > slots || (f && a.seg_off[f] < a.seg_off[f - 1]))
+      return fail(TT_EINVAL, "shard_gather_segs: segment offsets must ascend within [0, slots]");
   }
-  if (a.dd_on && hl == 0) dd_insert_finish(a.dd, pend, (int32_t)i);
+  if (block_i64 < counts_i64 + F + slots || counts_i64 < 0) return fail(TT_EINVAL, "shard_gather_segs: bad block layout");
+  const int64_t n = (int64_t)W * slots;
+  if (n > INT32_MAX) return fail(TT_EINVAL, "shard_gather_segs: too many slots");
+  a.weights = weights;
+  a.T = T;
+  a.F = F;
+  a.W = W;
+  a.S = slots;
+  if (out_stride < slots) return fail(TT_EINVAL, "shard_gather_segs: out_stride < slots");
+  a.out_stride = out_stride;
+  a.blk64 = block_i64;
+  a.cnt64 = counts_i64;
+  a.recv = recv;
+  a.rows_out = reinterpret_cast<__bf16*>(rows_out);
+  a.bad = bad;
+  if (dedup_ws) {
+    if (dedup_max_lookups < n || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+        dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
+        (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
+      return fail(TT_ECAPACITY, "shard_gather_segs: dedup workspace too small / misaligned");
+    dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
+    a.dd_on = 1;
+  }
+  return TT_OK;
 }
 
 }  // namespace tt
@@ -326,47 +315,13 @@ int tt_shard_route_segs(int F, int64_t B, const void* const* cols, int id_dtype,
 
 int tt_shard_gather_segs_bf16(const float* weights, const tt_table_meta_t* tables, int T, int F, int W,
                               const int64_t* recv, int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
-                              int64_t slots, void* rows_out, int32_t* bad, void* dedup_ws, size_t dedup_ws_bytes,
-                              int64_t dedup_max_lookups, void* stream) {
-  if (T < 1 || T > TT_MAX_TABLES || F < 1 || F > TT_MAX_FEATURES || F > T || W < 1 || slots < 0)
-    return fail(TT_EINVAL, "shard_gather_segs: bad sizes");
-  if (!weights || !tables || !recv || !rows_out || !bad || !seg_off)
-    return fail(TT_EINVAL, "shard_gather_segs: null pointer");
+                              int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad, void* dedup_ws,
+                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
   GatherSegArgs a{};
-  a.D = tables[0].dim;
-  for (int t = 0; t < T; ++t) {
-    if (tables[t].dim != a.D) return fail(TT_EINVAL, "shard_gather_segs: tables must share one dim");
-    if (tables[t].weight_offset % 4) return fail(TT_EINVAL, "shard_gather_segs: rows must be 16-B aligned");
-    a.tables[t] = tables[t];
-  }
-  if (a.D % 4 || (reinterpret_cast<uintptr_t>(weights) & 15) || (reinterpret_cast<uintptr_t>(rows_out) & 7))
-    return fail(TT_EINVAL, "shard_gather_segs: D % 4 == 0 and aligned buffers required");
-  for (int f = 0; f <= F; ++f) {
-    a.seg_off[f] = f < F ? seg_off[f] : slots;
-    if (a.seg_off[f] < 0 || a.seg_off[f] > slots || (f && a.seg_off[f] < a.seg_off[f - 1]))
-      return fail(TT_EINVAL, "shard_gather_segs: segment offsets must ascend within [0, slots]");
-  }
-  if (block_i64 < counts_i64 + F + slots || counts_i64 < 0) return fail(TT_EINVAL, "shard_gather_segs: bad block layout");
+  int rc = gather_segs_args(weights, tables, T, F, W, recv, block_i64, counts_i64, seg_off, slots, rows_out, out_stride,
+                            bad, dedup_ws, dedup_ws_bytes, dedup_max_lookups, a);
+  if (rc) return rc;
   const int64_t n = (int64_t)W * slots;
-  if (n > INT32_MAX) return fail(TT_EINVAL, "shard_gather_segs: too many slots");
-  a.weights = weights;
-  a.T = T;
-  a.F = F;
-  a.W = W;
-  a.S = slots;
-  a.blk64 = block_i64;
-  a.cnt64 = counts_i64;
-  a.recv = recv;
-  a.rows_out = reinterpret_cast<__bf16*>(rows_out);
-  a.bad = bad;
-  if (dedup_ws) {
-    if (dedup_max_lookups < n || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
-        dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) ||
-        (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
-      return fail(TT_ECAPACITY, "shard_gather_segs: dedup workspace too small / misaligned");
-    dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
-    a.dd_on = 1;
-  }
   if (n == 0) return TT_OK;
   shard_gather_segs_kernel<<<dim3((unsigned)ceil_div(n, 8)), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("shard_gather_segs");

@@ -1242,6 +1242,25 @@ __global__ void __launch_bounds__(256) tower_wgrad_route_kernel(WgradArgs a, con
   }
 }
 
+// Pipelined sharded step, launch U (after exchange A brought the gradient rows of batch i and the
+// ids of batch i+1): T2 of batch i (weight-gradient tiles, bias sums, loss) beside the owner's
+// row-wise Adagrad of batch i's rows and the count pass of batch i+2's route — all three read only
+// what T1 and the exchange wrote, so the tower weight gradients overlap the embedding update.
+__global__ void __launch_bounds__(256) tower_wgrad_route_rowwise_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
+                                                                        RouteArgs r, DdUpdateArgs d, int n_t2,
+                                                                        int n_cnt) {
+  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
+  const int b = (int)blockIdx.x;
+  if (b < n_t2) {
+    wgrad_block(a, tiles, b, smem);
+  } else if (b < n_t2 + n_cnt) {
+    const int j = b - n_t2;
+    route_count_block(r, j % r.nblk, j / r.nblk, reinterpret_cast<int (*)[RT_MAXW]>(smem));
+  } else {
+    dd_update_block(d, b - n_t2 - n_cnt, smem);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // T3: reduce + Adam + bf16 weight copies
 
@@ -1391,6 +1410,25 @@ __global__ void __launch_bounds__(256) tower_update_route_kernel(UpdateArgs a, R
   } else {
     const int j = (int)blockIdx.x - n_upd;
     route_place_block<true>(r, j % r.nblk, j / r.nblk, base, wc);
+  }
+}
+
+// Pipelined sharded step, launch G (after launch U updated this rank's rows): the owner's gather of
+// batch i+1's rows (bf16, into exchange B's row blocks, filing batch i+1's dedup table), the tower
+// gradient of batch i x 1/W into exchange B's tower block of every destination (slab reduction, no
+// Adam), and the place pass of batch i+2's route.
+__global__ void __launch_bounds__(256) tower_grads_place_gather_kernel(UpdateArgs a, RouteArgs r, GatherSegArgs g,
+                                                                       int n_upd, int n_place) {
+  __shared__ int base[RT_MAXW];
+  __shared__ int wc[RT_BLOCK / 64][RT_MAXW];
+  const int b = (int)blockIdx.x;
+  if (b < n_upd) {
+    update_block(a, b, n_upd);
+  } else if (b < n_upd + n_place) {
+    const int j = b - n_upd;
+    route_place_block<true>(r, j % r.nblk, j / r.nblk, base, wc);
+  } else {
+    shard_gather_block(g, b - n_upd - n_place);
   }
 }
 
@@ -2053,6 +2091,19 @@ int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* par
                    nullptr, grads, workspace, ws_bytes, stream, nullptr, nullptr, 0, 1, 0, 1.f, nsrc, src_stride);
 }
 
+int tt_tower_adam_pre_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
+                                int64_t src_stride, float* exp_avg, float* exp_avg_sq, float eps, float beta1,
+                                float beta2, float weight_decay, void* workspace, size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  if (!grads || nsrc < 1 || (nsrc > 1 && src_stride < L.P)) return fail(TT_EINVAL, "tower_adam_pre_grads_sum: bad gradient");
+  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
+  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, nullptr,
+                   grads, workspace, ws_bytes, stream, pre, nullptr, 0, 1, nullptr, 1.f, nsrc, src_stride);
+}
+
 int tt_tower_adam_grads_sum_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
                                             int nsrc, int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr,
                                             float beta1, float beta2, float eps, float weight_decay,
@@ -2164,6 +2215,83 @@ int tt_tower_grads_replicated_route_place(const tt_tower_shape_t* shape, int64_t
   tower_update_route_kernel<<<dim3((unsigned)(g3 + (int64_t)r.nblk * F)), dim3(256), 0, as_stream(stream)>>>(
       a, r, (int)g3);
   return check_launch("tower_grads_replicated_route_place");
+}
+
+int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                               size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
+                                               float adam_beta1, float adam_beta2, int F, const void* const* cols,
+                                               int id_dtype,
+                                               const int64_t* num_embeddings, const int64_t* block_sizes,
+                                               const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                               int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                               size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
+                                               const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
+                                               const float* emb_grad, int64_t ldg, float* weights, float* state,
+                                               float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                               int64_t dedup_max_lookups, void* stream) {
+  if (!adam_step_state) return fail(TT_EINVAL, "tower_wgrad_route_rowwise: null Adam step state");
+  WgradArgs a{};
+  int64_t wgs = 0;
+  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
+  if (rc) return rc;
+  TowerLayout L;
+  tower_layout(shape, B, &L);
+  a.step_state = adam_step_state;  // the loss wave advances Adam's step and writes its scalars
+  a.adam_pre = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + L.o_counter);
+  a.lr = adam_lr;
+  a.beta1 = adam_beta1;
+  a.beta2 = adam_beta2;
+  RouteArgs r{};
+  rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
+                       overflow, route_ws, route_ws_bytes, r);
+  if (rc) return rc;
+  DdUpdateArgs d{};
+  int64_t dd_grid = 0;
+  rc = dedup_update_args(tables, T, features, Fsrc, emb_B, emb_grad, ldg, weights, state, emb_lr, emb_eps, dedup_ws,
+                         dedup_ws_bytes, dedup_max_lookups, d, &dd_grid);
+  if (rc) return rc;
+  const int64_t n_cnt = (int64_t)r.nblk * F;
+  if (wgs + n_cnt + dd_grid > INT32_MAX) return fail(TT_EINVAL, "tower_wgrad_route_rowwise: grid too large");
+  tower_wgrad_route_rowwise_kernel<<<dim3((unsigned)(wgs + n_cnt + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
+      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), r, d, (int)wgs,
+      (int)n_cnt);
+  return check_launch("tower_wgrad_route_count_rowwise_adagrad");
+}
+
+int tt_tower_grads_replicated_route_place_gather(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
+                                                 int copies, const int64_t* offsets, float scale, void* workspace,
+                                                 size_t ws_bytes, int F, const void* const* cols, int id_dtype,
+                                                 const int64_t* num_embeddings, const int64_t* block_sizes,
+                                                 const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                                                 int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow,
+                                                 void* route_ws, size_t route_ws_bytes, const float* weights,
+                                                 const tt_table_meta_t* tables, int T, const int64_t* recv,
+                                                 int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
+                                                 int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad,
+                                                 void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
+                                                 void* stream) {
+  if (!params || !base || !offsets || copies < 1 || copies > 16) return fail(TT_EINVAL, "tower_grads_replicated: bad output");
+  RouteArgs r{};
+  int rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
+                           overflow, route_ws, route_ws_bytes, r);
+  if (rc) return rc;
+  GatherSegArgs g{};
+  rc = gather_segs_args(weights, tables, T, F, W, recv, block_i64, counts_i64, seg_off, slots, rows_out, out_stride,
+                        bad, dedup_ws, dedup_ws_bytes, dedup_max_lookups, g);
+  if (rc) return rc;
+  int64_t off[16];
+  for (int q = 0; q < copies; ++q) off[q] = offsets[q];
+  if (copies == 1) off[1] = off[0];  // one copy takes the multi-copy path too (scale applied)
+  UpdateArgs a;
+  int64_t g3 = 0;
+  rc = t3_args(shape, B, params, nullptr, nullptr, 0.f, 0.9f, 0.999f, 1e-8f, 0.f, nullptr, 0, base, nullptr, workspace,
+               ws_bytes, nullptr, copies == 1 ? 2 : copies, off, scale, 1, 0, a, &g3);
+  if (rc) return rc;
+  const int64_t n_place = (int64_t)r.nblk * F, n_gather = ceil_div((int64_t)W * slots, 8);
+  if (g3 + n_place + n_gather > INT32_MAX) return fail(TT_EINVAL, "tower_grads_place_gather: grid too large");
+  tower_grads_place_gather_kernel<<<dim3((unsigned)(g3 + n_place + n_gather)), dim3(256), 0, as_stream(stream)>>>(
+      a, r, g, (int)g3, (int)n_place);
+  return check_launch("tower_grads_replicated_route_place_gather");
 }
 
 int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,

@@ -5,25 +5,29 @@ reference (03_model_training.py:798-829, :618): every table row-wise (block ceil
 table-wise sharded over the ranks, the towers data-parallel (DDP: gradients averaged over ranks),
 each rank training on its own local batch of B pairs.
 
-Pipelined schedule: TWO collectives per step. Per rank, step i (batch i's rows already returned):
+Pipelined schedule: TWO collectives per step, the route of every batch computed two steps ahead
+(it depends only on that batch's ids). Per rank, step i (batch i's rows already returned, batch
+i+1's keys already placed in exchange A's key region):
 
   T1 (indexed)    towers fwd/bwd reading rows_in[pos_in], dX -> exchange A's gradient region
-  T2, T3          towers' weight gradients, the reduced gradient x 1/W copied into the tower
-                  region of every destination block of exchange A
-  route(i+1)      next batch's ids -> owners (segment (d, f) of fixed capacity; transform_to_
-                  torchrec_batch's id % N and drop-0 inline) -> exchange A's key region
-  all-to-all A    [gradient rows(i) | tower gradient(i) | keys(i+1)]   requester -> owner
-  Adagrad(i)      owner's fused row-wise Adagrad over the received gradient rows
+  all-to-all A    [gradient rows(i) | keys(i+1)]                          requester -> owner
+  launch U        owner's fused row-wise Adagrad(i) over the received gradient rows  |  T2(i):
+                  the towers' weight gradients  |  count pass of route(i+2)
+  launch G        owner's gather(i+1): the rows the received keys name (bf16) into exchange B,
+                  filed for Adagrad(i+1)  |  the reduced tower gradient(i) x 1/W into the tower
+                  block of every destination of exchange B  |  place pass of route(i+2) (ids %
+                  N and drop-0 inline, segment (d, f) of fixed capacity) -> exchange A's key region
+  all-to-all B    [rows(i+1) | tower gradient(i)]                         owner -> requester
   Adam(i)         fixed-order sum of the W received tower gradients (= DDP's mean all-reduce)
-  gather(i+1)     owner copies the rows the received keys name (bf16), files them for Adagrad(i+1)
-  all-to-all B    rows(i+1)                                            owner -> requester
 
-Every exchange has a fixed size (per-destination capacities), so with RCCL (backend "nccl") the
-step is captured into HIP graphs like the single-GPU step. Batch i+1's rows are gathered after
-Adagrad(i) has updated the owner's shard, so results are those of the synchronous loop. The
+The tower weight gradients run beside the embedding update (launch U) and their reduction beside
+the gather (launch G): T1, the two exchanges, U, G and Adam are the step's critical path. Every
+exchange has a fixed size (per-destination capacities), so with RCCL (backend "nccl") the step is
+captured into HIP graphs like the single-GPU step. Batch i+1's rows are gathered after Adagrad(i)
+has updated the owner's shard, so results are those of the synchronous loop. The
 embedding gradient a row receives is the sum over ranks of the per-rank mean-loss gradients
 (TorchRec's sharded EBC semantics); lookups of a row are summed in ascending (source rank, slot)
-order. ``step()`` (no next batch known) runs the same kernels in order with one extra exchange.
+order. ``step()`` (no next batch known) runs the same kernels in order with four exchanges.
 A segment over capacity or a key outside a shard raises on ``check()`` (sticky device flags,
 all-reduced over the ranks).
 """
@@ -335,8 +339,8 @@ class FusedShardedTwoTowerStep:
         # ---- buffers
         self.sendA = torch.zeros(self.A_total, dtype=torch.float32, device=dev)
         self.recvA = torch.zeros(W * self.Asz[r], dtype=torch.float32, device=dev)
-        self.rows_out = torch.zeros(max(1, W * self.S[r]), D, dtype=torch.bfloat16, device=dev)
-        self.rows_in = torch.zeros(max(1, sum(self.S)), D, dtype=torch.bfloat16, device=dev)
+        self.rows_out = torch.zeros(W * self.RSTR, D, dtype=torch.bfloat16, device=dev)
+        self.rows_in = torch.zeros(W * self.RSTR, D, dtype=torch.bfloat16, device=dev)
         self.pos_in = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
         self.pos_out = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(2, dtype=torch.int32, device=dev)  # {overflow, bad key}
@@ -345,12 +349,12 @@ class FusedShardedTwoTowerStep:
         for d in range(W):
             for f in range(F):
                 e = segs[d * F + f]
-                ids64 = (self.A_off[d] + self.Ppad + self.S[d] * D) // 2
+                ids64 = (self.A_off[d] + self.S[d] * D) // 2
                 e.cap = self.cap[d][f]
                 e.key_index = ids64 + F + self.seg_off[d][f]
                 e.cnt_index = ids64 + f
                 e.pos_in = self.RB_off[d] + self.seg_off[d][f]
-                e.pos_out = (self.A_off[d] + self.Ppad) // D + self.seg_off[d][f]
+                e.pos_out = self.A_off[d] // D + self.seg_off[d][f]
         raw = torch.frombuffer(bytearray(bytes(segs)), dtype=torch.uint8)
         self.segs = raw.to(dev)
         # dedup workspaces: batch i inserts at gather(i), Adagrad(i) consumes: two in flight
@@ -367,12 +371,16 @@ class FusedShardedTwoTowerStep:
         for s in range(W):
             self._fm_src[s].table = 0
             self._fm_src[s].out_offset = 0
-            self._fm_src[s].out_row = (s * self.Asz[r] + self.Ppad) // D
+            self._fm_src[s].out_row = s * self.Asz[r] // D
         self._ne = (C.c_int64 * F)(*self.N)
         self._bs = (C.c_int64 * F)(*self.block)
         self._ow = (C.c_int32 * F)(*self.owner)
         self._segoff_me = (C.c_int64 * F)(*self.seg_off[r])
-        self._tw_off = (C.c_int64 * W)(*self.A_off)
+        # this rank's tower gradient x 1/W into exchange B's tower block of every destination (float
+        # offsets into rows_out), and where Adam finds the W received ones in rows_in
+        self._tw_off = (C.c_int64 * W)(*[(d * self.RSTR + self.Smax) * D // 2 for d in range(W)])
+        self._tw_in = self.Smax * D // 2
+        self._tw_stride = self.RSTR * D // 2
         # ---- step inputs / outputs
         self.cols = [torch.zeros(B, dtype=id_dtype, device=dev) for _ in range(F)]
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -396,11 +404,15 @@ class FusedShardedTwoTowerStep:
                 offs.append(o)
                 o += self.cap[d][f]
             self.seg_off.append(offs)
-        # destination block d: [tower Ppad | gradient rows S_d x D | counts F, keys S_d (int64) | pad]
-        self.Asz = [self.Ppad + self.S[d] * D + rup(2 * (F + self.S[d]), D) for d in range(W)]
+        # exchange A (fp32), destination block d: [gradient rows S_d x D | counts F, keys S_d (int64) | pad]
+        self.Asz = [self.S[d] * D + rup(2 * (F + self.S[d]), D) for d in range(W)]
         self.A_off = [sum(self.Asz[:d]) for d in range(W)]
         self.A_total = sum(self.Asz)
-        self.RB_off = [sum(self.S[:d]) for d in range(W)]
+        # exchange B (bf16 rows), one stride RSTR per block: [rows S | pad to Smax | tower gradient as
+        # fp32 bits (2 Ppad bf16 slots)] — equal splits, and the W tower gradients at a fixed stride
+        self.Smax = max(self.S)
+        self.RSTR = self.Smax + 2 * self.Ppad // D
+        self.RB_off = [d * self.RSTR for d in range(W)]
         if W * max(self.S) >= (1 << 18) or self.A_total // D >= 2 ** 31:
             raise _lib.TTError("sharded step: exchange too large for one step (lookups per owner < 2^18)")
 
@@ -429,8 +441,9 @@ class FusedShardedTwoTowerStep:
         return out
 
     def tower_grad_sent(self) -> torch.Tensor:
-        """This rank's tower gradient x 1/W as sent in exchange A (tests)."""
-        return self.sendA[self.A_off[0]:self.A_off[0] + self.towers.num_params].clone()
+        """This rank's tower gradient x 1/W as sent in exchange B (tests)."""
+        f = self.rows_out.view(-1).view(torch.float32)
+        return f[self._tw_off[0]:self._tw_off[0] + self.towers.num_params].clone()
 
     def rows_for(self, parity: int) -> torch.Tensor:
         """[F * B, D] bf16 rows T1 reads for the batch of this parity (tests)."""
@@ -458,19 +471,20 @@ class FusedShardedTwoTowerStep:
         self.comm.all_to_all(self.recvA, self.sendA, out_splits=[self.Asz[r]] * self.W, in_splits=list(self.Asz))
 
     def _gather(self, parity: int) -> None:
+        check(_lib.load().tt_shard_gather_segs_bf16(*self._gather_args(parity)), "shard_gather_segs")
+
+    def _gather_args(self, parity: int):
         r, ts = self.rank, self.tables
         ws = self.dd_ws[parity]
-        check(_lib.load().tt_shard_gather_segs_bf16(
-            ptr(ts.weights), ts._tm, ts.T, self.F, self.W, ptr(self.recvA), self.Asz[r] // 2,
-            (self.Ppad + self.S[r] * self.D) // 2, self._segoff_me, self.S[r], ptr(self.rows_out), ptr(self.flags[1:]),
-            ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device)), "shard_gather_segs")
+        return (ptr(ts.weights), ts._tm, ts.T, self.F, self.W, ptr(self.recvA), self.Asz[r] // 2,
+                self.S[r] * self.D // 2, self._segoff_me, self.S[r], ptr(self.rows_out), self.RSTR,
+                ptr(self.flags[1:]), ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device))
 
     def _exchange_b(self) -> None:
-        r, D = self.rank, self.D
-        self.comm.all_to_all(self.rows_in[:sum(self.S)], self.rows_out[:self.W * self.S[r]],
-                             out_splits=list(self.S), in_splits=[self.S[r]] * self.W)
+        self.comm.all_to_all(self.rows_in, self.rows_out, out_splits=[self.RSTR] * self.W,
+                             in_splits=[self.RSTR] * self.W)
 
-    def _towers(self, parity: int, labels: torch.Tensor) -> None:
+    def _t1(self, parity: int, labels: torch.Tensor) -> None:
         lib, tw, B = _lib.load(), self.towers, self.B
         pin, pout = self.pos_in[parity], self.pos_out[parity]
         check(lib.tt_tower_fwd_bwd_indexed2_bf16(
@@ -478,64 +492,83 @@ class FusedShardedTwoTowerStep:
             ptr_array([self.rows_in, self.rows_in]), ptr_array([self.sendA, self.sendA]), ptr(self.params),
             ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
             "tower_fwd_bwd_indexed2")
-        tw.wgrad(self.loss)
-        check(lib.tt_tower_grads_replicated(C.byref(tw.shape), B, ptr(self.params), ptr(self.sendA), self.W,
-                                            self._tw_off, 1.0 / self.W, ptr(tw.ws), tw.nbytes,
-                                            stream_handle(self.device)), "tower_grads_replicated")
 
-    def _owner_update(self, parity: int) -> None:
-        """Adagrad over the received gradient rows + Adam on the fixed-order sum of the received
-        tower gradients, one launch."""
-        lib, ts, r, tw = _lib.load(), self.tables, self.rank, self.towers
+    def _rows_update(self, parity: int) -> None:
+        """The owner's fused row-wise Adagrad over the received gradient rows (one pseudo-feature
+        per source rank, lookups summed in ascending (source, slot) order)."""
+        ts, r = self.tables, self.rank
         ws = self.dd_ws[parity]
-        check(lib.tt_tower_adam_grads_sum_rowwise_adagrad(
-            C.byref(tw.shape), self.B, ptr(self.params), ptr(self.recvA), self.W, self.Asz[r], ptr(self.exp_avg),
-            ptr(self.exp_avg_sq), self.lr_dense, 0.9, 0.999, 1e-8, 0.0, ptr(self.adam_state), ptr(tw.ws), tw.nbytes,
-            ts._tm, ts.T, self._fm_src, self.W, self.S[r], ptr(self.recvA), self.D, ptr(ts.weights), ptr(ts.state),
-            self.lr_emb, self.eps, ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device)),
-            "tower_adam_grads_sum_rowwise_adagrad")
+        check(_lib.load().tt_dedup_rowwise_adagrad(ts._tm, ts.T, self._fm_src, self.W, self.S[r], ptr(self.recvA),
+                                                  self.D, ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps,
+                                                  ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device)),
+              "dedup_rowwise_adagrad")
+
+    def _adam(self) -> None:
+        """Adam on the fixed-order sum of the W tower gradients received in exchange B, with the
+        step scalars T2 wrote (launch U / tt_tower_wgrad_pre advanced the step)."""
+        tw = self.towers
+        grads = self.rows_in.data_ptr() + 4 * self._tw_in
+        check(_lib.load().tt_tower_adam_pre_grads_sum(
+            C.byref(tw.shape), self.B, ptr(self.params), grads, self.W, self._tw_stride, ptr(self.exp_avg),
+            ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
+            "tower_adam_pre_grads_sum")
+
+    def _route_args(self, cols: Sequence[torch.Tensor], parity: int):
+        return (self.F, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ne, self._bs, self._ow, self.W,
+                ptr(self.segs), ptr(self.sendA), ptr(self.pos_in[parity]), ptr(self.pos_out[parity]),
+                ptr(self.flags), ptr(self.route_ws), self.route_ws.numel())
 
     # ---- public steps ---------------------------------------------------------------------------
     def step(self) -> None:
-        """One synchronous step on the batch in ``cols`` / ``labels`` (no next batch known: the
-        rows are fetched first, at the price of one more exchange)."""
+        """One synchronous step on the batch in ``cols`` / ``labels`` (no later batch known: ids,
+        rows, gradient rows and tower gradients each take an exchange)."""
+        lib, tw = _lib.load(), self.towers
         self._route(self.cols, 0)
         self._exchange_a()
         self._gather(0)
         self._exchange_b()
-        self._towers(0, self.labels)
+        self._t1(0, self.labels)
+        check(lib.tt_tower_wgrad_pre(C.byref(tw.shape), self.B, ptr(self.loss), ptr(tw.ws), tw.nbytes,
+                                     ptr(self.adam_state), self.lr_dense, 0.9, 0.999, None, 0, 0,
+                                     stream_handle(self.device)), "tower_wgrad_pre")
+        check(lib.tt_tower_grads_replicated(C.byref(tw.shape), self.B, ptr(self.params),
+                                            self.rows_out.data_ptr(), self.W, self._tw_off, 1.0 / self.W, ptr(tw.ws),
+                                            tw.nbytes, stream_handle(self.device)), "tower_grads_replicated")
         self._exchange_a()
-        self._owner_update(0)
+        self._rows_update(0)
+        self._exchange_b()
+        self._adam()
 
-    def prime(self, cols: Sequence[torch.Tensor], parity: int) -> None:
-        """Stage the rows of a batch (the pipelined loop's first step)."""
+    def prime(self, cols: Sequence[torch.Tensor], parity: int, next_cols: Optional[Sequence[torch.Tensor]] = None) -> None:
+        """Stage the rows of a batch (the pipelined loop's first step) and, with ``next_cols``, place
+        the following batch's keys (its route, parity ^ 1)."""
         self._route(cols, parity)
         self._exchange_a()
         self._gather(parity)
         self._exchange_b()
+        if next_cols is not None:
+            self._route(next_cols, parity ^ 1)
 
-    def step_pipelined(self, labels: torch.Tensor, parity: int, next_cols: Sequence[torch.Tensor]) -> None:
-        """Step on the staged batch (rows in place, parity ``parity``), staging ``next_cols``. The
-        next batch's route rides in the T2 and T3 launches (count / place workgroups)."""
-        lib, tw, B, dev = _lib.load(), self.towers, self.B, self.device
-        pin, pout = self.pos_in[parity], self.pos_out[parity]
-        check(lib.tt_tower_fwd_bwd_indexed2_bf16(
-            C.byref(tw.shape), B, ptr_array([pin[:B], pin[B:]]), ptr_array([pout[:B], pout[B:]]),
-            ptr_array([self.rows_in, self.rows_in]), ptr_array([self.sendA, self.sendA]), ptr(self.params),
-            ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), ptr(tw.ws), tw.nbytes, stream_handle(dev)),
-            "tower_fwd_bwd_indexed2")
-        route = (self.F, ptr_array(list(next_cols)), id_dtype_code(next_cols[0].dtype), self._ne, self._bs, self._ow,
-                 self.W, ptr(self.segs), ptr(self.sendA), ptr(self.pos_in[parity ^ 1]), ptr(self.pos_out[parity ^ 1]),
-                 ptr(self.flags), ptr(self.route_ws), self.route_ws.numel(), stream_handle(dev))
-        check(lib.tt_tower_wgrad_route_count(C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, *route),
-              "tower_wgrad_route_count")
-        check(lib.tt_tower_grads_replicated_route_place(C.byref(tw.shape), B, ptr(self.params), ptr(self.sendA), self.W,
-                                                        self._tw_off, 1.0 / self.W, ptr(tw.ws), tw.nbytes, *route),
-              "tower_grads_replicated_route_place")
+    def step_pipelined(self, labels: torch.Tensor, parity: int, next2_cols: Sequence[torch.Tensor]) -> None:
+        """Step on the staged batch i (rows in place, parity ``parity``; batch i+1's keys placed),
+        staging batch i+1's rows and routing ``next2_cols`` (batch i+2, same parity)."""
+        lib, tw, ts, r, B, dev = _lib.load(), self.towers, self.tables, self.rank, self.B, self.device
+        self._t1(parity, labels)
         self._exchange_a()
-        self._owner_update(parity)
-        self._gather(parity ^ 1)
+        route = self._route_args(next2_cols, parity)
+        ws = self.dd_ws[parity]
+        check(lib.tt_tower_wgrad_route_count_rowwise_adagrad(
+            C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
+            0.999, *route, ts._tm, ts.T, self._fm_src, self.W,
+            self.S[r], ptr(self.recvA), self.D, ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws),
+            ws.numel(), self.max_lookups, stream_handle(dev)), "tower_wgrad_route_count_rowwise_adagrad")
+        g = self._gather_args(parity ^ 1)
+        g = g[:3] + g[5:]  # the combined launch takes F and W from the route's arguments
+        check(lib.tt_tower_grads_replicated_route_place_gather(
+            C.byref(tw.shape), B, ptr(self.params), self.rows_out.data_ptr(), self.W, self._tw_off, 1.0 / self.W,
+            ptr(tw.ws), tw.nbytes, *route, *g), "tower_grads_replicated_route_place_gather")
         self._exchange_b()
+        self._adam()
 
     # ---- checkpoint (03_model_training.py:474-502 / :1015-1054 format) -------------------------
     def spans(self, f: int) -> List[Tuple[int, int]]:
@@ -663,8 +696,8 @@ class FusedShardedTwoTowerStep:
         staged = self._staged(batches)
         self._pool_inputs = [staged]
         self.pool_k = k
-        # stage batch 0 eagerly, then retire every eager collective before capturing
-        self.prime(staged[0][0], 0)
+        # stage batch 0 (and place batch 1's keys) eagerly, then retire every eager collective
+        self.prime(staged[0][0], 0, staged[1][0])
         self.cursor = 0
         self.comm.retire()
 
@@ -675,7 +708,7 @@ class FusedShardedTwoTowerStep:
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     for i in idx:
-                        self.step_pipelined(staged[i][1], i % 2, staged[(i + 1) % n][0])
+                        self.step_pipelined(staged[i][1], i % 2, staged[(i + 2) % n][0])
             torch.cuda.current_stream(self.device).wait_stream(s)
             return g
 
@@ -700,10 +733,12 @@ class FusedShardedTwoTowerStep:
     def run_eager(self, batches: Sequence, n: int) -> None:
         """n pipelined steps over a cyclic pool without graphs (continuing at the cursor)."""
         nb = len(batches)
+        if nb % 2:
+            raise _lib.TTError("run_eager: the pool needs an even number of batches")
         if self.cursor is None:
-            self.prime(list(batches[0][0]), 0)
+            self.prime(list(batches[0][0]), 0, list(batches[1][0]))
             self.cursor = 0
         for _ in range(n):
             i = self.cursor
-            self.step_pipelined(batches[i][1].to(torch.int32), i % 2, list(batches[(i + 1) % nb][0]))
+            self.step_pipelined(batches[i][1].to(torch.int32), i % 2, list(batches[(i + 2) % nb][0]))
             self.cursor = (i + 1) % nb
