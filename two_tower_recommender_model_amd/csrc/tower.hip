@@ -2006,7 +2006,7 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
     tower_update_dedup_kernel<<<dim3((unsigned)(dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(a, *dd, (int)dd_grid);
     return check_launch("tower_update_rowwise_adagrad");
   }
-  if (getenv("TT_RING_STAMPS") && g3 <= 512) {
+  if (getenv("TT_RING_STAMPS")) {  // workgroups [0, 512) stamp
     TowerLayout L;
     tower_layout(shape, B, &L);
     a.stamps = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 6144;
