@@ -38,6 +38,15 @@ constexpr int LSTR = MAXW + 8;        // bf16 LDS row stride (272 B: conflict-li
 constexpr int FSTR = MAXW + 4;        // fp32 LDS row stride
 constexpr int MAXL = 4;
 
+// T1 -> T2 operand strips (X^T, activations, dZ^T; bf16), tile-major: element (feature f, batch
+// row m) of a strip block with nf features sits at ((m / 32) * nf + f) * 32 + m % 32, blocks of
+// nf x Bp elements (Bp = B rounded up to 32). One T1 workgroup's 32-row tile of a block is one
+// contiguous run (whole cache lines written once), and a T2 chunk of 32 rows x 16 features is 1 KB
+// contiguous (a full-rate load per wave instruction) instead of 16 scattered 64-B pieces.
+__device__ __forceinline__ int64_t strip_at(int64_t f, int64_t m, int64_t nf) {
+  return (((m >> 5) * nf + f) << 5) + (m & 31);
+}
+
 struct TowerArgs {
   tt_tower_shape_t s;
   int64_t B;
@@ -57,12 +66,13 @@ struct TowerArgs {
   float grad_scale;
   float* logits;
   // T1 -> T2 buffers
-  __bf16* xt;           // [2][in_max][B]
+  __bf16* xt;           // [2] blocks of in_max x Bp (strip_at)
   __bf16* act;          // [2][MAXL][MAXW][B]  (layer-l OUTPUT, transposed; layers 0..L-2 used)
   __bf16* dzt;          // [2][MAXL][MAXW][B]
   float* dbpart;        // [2][MAXL][nwg][MAXW]
   float* loss_part;     // [nwg]
   int64_t in_max;
+  int64_t Bp;           // strip rows per block (B rounded up to 32)
   int nwg;
   // fused single-hot gather (tt_tower_fwd_bwd_gather): tower t's input row m is table row
   // (gcol[t][m] mod gmod[t]) of gtab[t] (zeros for id 0) instead of pooled row m
@@ -190,7 +200,7 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
             bf16x8 v;
             for (int j = 0; j < 8; ++j) v[j] = xs[(rb + j) * LSTR + k];
             const int64_t gm = m0 + rb;
-            __bf16* dst = a.xt + ((int64_t)t * a.in_max + k0 + k) * B + gm;
+            __bf16* dst = a.xt + (int64_t)t * a.in_max * a.Bp + strip_at(k0 + k, gm, a.in_max);
             if (gm + 8 <= B) {
               *reinterpret_cast<bf16x8*>(dst) = v;
             } else {
@@ -221,7 +231,7 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
           }
           if (l < L - 1) {
             const int64_t gm = m0 + i * 16 + q4 * 4;
-            __bf16* dst = a.act + (((int64_t)t * MAXL + l) * MAXW + col) * B + gm;
+            __bf16* dst = a.act + ((int64_t)t * MAXL + l) * MAXW * a.Bp + strip_at(col, gm, MAXW);
             if (gm + 4 <= B) {
               *reinterpret_cast<bf16x4*>(dst) = pk;
             } else {
@@ -285,7 +295,7 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
         s += __shfl_xor(s, 2, 64);
         if ((threadIdx.x & 3) == 0) dbp[c] = s;
         const int64_t gm = m0 + rb;
-        __bf16* dst = a.dzt + (((int64_t)t * MAXL + (L - 1)) * MAXW + c) * B + gm;
+        __bf16* dst = a.dzt + ((int64_t)t * MAXL + (L - 1)) * MAXW * a.Bp + strip_at(c, gm, MAXW);
         if (gm + 8 <= B) {
           *reinterpret_cast<bf16x8*>(dst) = v;
         } else {
@@ -323,7 +333,7 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
             dz[cur ^ 1][row * LSTR + col] = (__bf16)z;
           }
           const int64_t gm = m0 + i * 16 + q4 * 4;
-          __bf16* dst = a.dzt + (((int64_t)t * MAXL + (l - 1)) * MAXW + col) * B + gm;
+          __bf16* dst = a.dzt + ((int64_t)t * MAXL + (l - 1)) * MAXW * a.Bp + strip_at(col, gm, MAXW);
           if (gm + 4 <= B) {
             *reinterpret_cast<bf16x4*>(dst) = pk;
           } else {
@@ -664,7 +674,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     bf16x8 v;
     for (int j = 0; j < 8; ++j) v[j] = xs[t][(rb + j) * LSTR + k];
     const int64_t gm = m0 + rb;
-    __bf16* dst = a.xt + ((int64_t)t * a.in_max + k) * B + gm;
+    __bf16* dst = a.xt + (int64_t)t * a.in_max * a.Bp + strip_at(k, gm, a.in_max);
     if (gm + 8 <= B) {
       *reinterpret_cast<bf16x8*>(dst) = v;
     } else {
@@ -690,7 +700,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         hs[t][row * LSTR + col] = pk[rr];
       }
       const int64_t gm = m0 + i * 16 + q4 * 4;
-      if (!(a.dbg & 1)) store_t4(a.act + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
+      if (!(a.dbg & 1)) store_t4(a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + strip_at(col, gm, MAXW), pk, gm, B);
     }
   }
   __syncthreads();
@@ -751,7 +761,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     s += __shfl_xor(s, 2, 64);
     if ((tt & 3) == 0) a.dbpart[(((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW + c] = s;
     const int64_t gm = m0 + rb;
-    __bf16* dst = a.dzt + (((int64_t)t * MAXL + 1) * MAXW + c) * B + gm;
+    __bf16* dst = a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + strip_at(c, gm, MAXW);
     if (a.dbg & 1) {
     } else if (gm + 8 <= B) {
       *reinterpret_cast<bf16x8*>(dst) = v;
@@ -782,7 +792,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         xs[t][row * LSTR + col] = pk[rr];
       }
       const int64_t gm = m0 + i * 16 + q4 * 4;
-      if (!(a.dbg & 1)) store_t4(a.dzt + (((int64_t)t * MAXL + 0) * MAXW + col) * B + gm, pk, gm, B);
+      if (!(a.dbg & 1)) store_t4(a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + strip_at(col, gm, MAXW), pk, gm, B);
     }
     s += __shfl_xor(s, 16, 64);
     s += __shfl_xor(s, 32, 64);
@@ -864,6 +874,7 @@ struct WgradArgs {
   int64_t P;
   int64_t B;
   int64_t in_max;
+  int64_t Bp;      // strip rows per block (strip_at)
   int S;
   int64_t mslice;  // rows per slice (multiple of 32)
   int ntiles;
@@ -929,17 +940,22 @@ __device__ __forceinline__ void wgrad_lds_block(const WgradArgs& a, int lb, char
   const int K = a.K[t][l];
   const int NT = min(T2_NT, a.width[l] - n0);  // 64, or 32 for the last tile of a width % 64 layer
   const int64_t B = a.B;
-  const __bf16* Z = a.dzt + (((int64_t)t * MAXL + l) * MAXW + n0) * B;
-  const __bf16* A = l == 0 ? a.xt + (int64_t)t * a.in_max * B : a.act + ((int64_t)t * MAXL + l - 1) * MAXW * B;
+  const __bf16* Z = a.dzt + ((int64_t)t * MAXL + l) * MAXW * a.Bp;  // strip blocks (strip_at)
+  const __bf16* A = l == 0 ? a.xt + (int64_t)t * a.in_max * a.Bp : a.act + ((int64_t)t * MAXL + l - 1) * MAXW * a.Bp;
+  const int64_t anf = l == 0 ? a.in_max : MAXW;
   const int64_t mb = (int64_t)s * a.mslice;
   const int64_t me = min(mb + a.mslice, B);
-  // loader: 4 threads per 64-B operand row segment (32 batch rows), 64 rows per pass
+  // loader: 4 threads per 64-B operand row segment (32 batch rows), 64 rows per pass; row i's
+  // chunk at batch row m (a multiple of 32) starts at src[i] + (m / 32) * tstr[i]
   const int seg = (tid & 3) * 8, frow = tid >> 2;
   const __bf16* src[3];
+  int64_t tstr[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int f = frow + 64 * i;
-    src[i] = f < T2_NT ? (f < NT ? Z + (int64_t)f * B : nullptr) : (f - T2_NT < K ? A + (int64_t)(f - T2_NT) * B : nullptr);
+    src[i] = f < T2_NT ? (f < NT ? Z + ((int64_t)(n0 + f) << 5) : nullptr)
+                       : (f - T2_NT < K ? A + ((int64_t)(f - T2_NT) << 5) : nullptr);
+    tstr[i] = (f < T2_NT ? (int64_t)MAXW : anf) << 5;
   }
   const int nh = wid >> 1, kh = wid & 1;  // wave: dW rows [32 nh, +32) x columns [64 kh, +64)
   f32x4 acc[2][4];
@@ -954,7 +970,8 @@ __device__ __forceinline__ void wgrad_lds_block(const WgradArgs& a, int lb, char
       const int64_t m = p0 + c * T2_MB + seg;  // B % 8 == 0: a segment is wholly in or out
 #pragma unroll
       for (int i = 0; i < 3; ++i)
-        ld[c][i] = (src[i] && m < me) ? *reinterpret_cast<const bf16x8*>(src[i] + m) : (bf16x8)(__bf16)0.f;
+        ld[c][i] = (src[i] && m < me) ? *reinterpret_cast<const bf16x8*>(src[i] + (m >> 5) * tstr[i] + seg)
+                                      : (bf16x8)(__bf16)0.f;
     }
 #pragma unroll
     for (int c = 0; c < T2_PF; ++c) {
@@ -1067,9 +1084,10 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
   const int s = (int)(lb / a.ntiles);
   const WgradTile tl = tiles[lb % a.ntiles];
   const int64_t B = a.B;
-  const __bf16* Z = a.dzt + ((int64_t)tl.t * MAXL + tl.l) * MAXW * B;  // [n][B]
-  const __bf16* A = tl.l == 0 ? a.xt + (int64_t)tl.t * a.in_max * B
-                              : a.act + ((int64_t)tl.t * MAXL + tl.l - 1) * MAXW * B;  // [k][B]
+  const __bf16* Z = a.dzt + ((int64_t)tl.t * MAXL + tl.l) * MAXW * a.Bp;  // strip blocks (strip_at)
+  const __bf16* A = tl.l == 0 ? a.xt + (int64_t)tl.t * a.in_max * a.Bp
+                              : a.act + ((int64_t)tl.t * MAXL + tl.l - 1) * MAXW * a.Bp;
+  const int64_t anf = tl.l == 0 ? a.in_max : MAXW;
   const int64_t mw = a.mslice / 4;
   int64_t mb = (int64_t)s * a.mslice + wid * mw;
   int64_t me = mb + mw;
@@ -1078,10 +1096,13 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
   f32x4 acc[2][2];
   for (int i = 0; i < 2; ++i)
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
-  const __bf16* z0 = Z + (int64_t)(tl.n0 + r) * B;
-  const __bf16* z1 = Z + (int64_t)(tl.n0 + 16 + r) * B;
-  const __bf16* a0 = A + (int64_t)(tl.k0 + r) * B;
-  const __bf16* a1 = A + (int64_t)(tl.k0 + 16 + r) * B;
+  // feature row bases in the tile-major strips; batch row o of a row: + (o / 32) * nf * 32 + o % 32
+  const __bf16* z0 = Z + ((int64_t)(tl.n0 + r) << 5);
+  const __bf16* z1 = Z + ((int64_t)(tl.n0 + 16 + r) << 5);
+  const __bf16* a0 = A + ((int64_t)(tl.k0 + r) << 5);
+  const __bf16* a1 = A + ((int64_t)(tl.k0 + 16 + r) << 5);
+  auto zo = [&](int64_t o) { return (((o >> 5) * MAXW) << 5) + (o & 31); };
+  auto ao = [&](int64_t o) { return (((o >> 5) * anf) << 5) + (o & 31); };
   int64_t m = mb;
   // 4 k-steps per iteration: their 16 fragment loads are issued before the first MFMA
   for (; m + 128 <= me; m += 128) {
@@ -1089,10 +1110,10 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t o = m + 32 * u + q * 8;
-      fa0[u] = *reinterpret_cast<const bf16x8*>(z0 + o);
-      fa1[u] = *reinterpret_cast<const bf16x8*>(z1 + o);
-      fb0[u] = *reinterpret_cast<const bf16x8*>(a0 + o);
-      fb1[u] = *reinterpret_cast<const bf16x8*>(a1 + o);
+      fa0[u] = *reinterpret_cast<const bf16x8*>(z0 + zo(o));
+      fa1[u] = *reinterpret_cast<const bf16x8*>(z1 + zo(o));
+      fb0[u] = *reinterpret_cast<const bf16x8*>(a0 + ao(o));
+      fb1[u] = *reinterpret_cast<const bf16x8*>(a1 + ao(o));
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1104,10 +1125,10 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
   }
   for (; m + 32 <= me; m += 32) {
     const int64_t o = m + q * 8;
-    const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(z0 + o);
-    const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(z1 + o);
-    const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(a0 + o);
-    const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(a1 + o);
+    const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(z0 + zo(o));
+    const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(z1 + zo(o));
+    const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(a0 + ao(o));
+    const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(a1 + ao(o));
     acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb0, acc[0][0], 0, 0, 0);
     acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb1, acc[0][1], 0, 0, 0);
     acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb0, acc[1][0], 0, 0, 0);
@@ -1118,10 +1139,10 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
     for (int j = 0; j < 8; ++j) {
       const int64_t mm = m + q * 8 + j;
       const bool ok = mm < me;
-      fa0[j] = ok ? z0[mm] : (__bf16)0.f;
-      fa1[j] = ok ? z1[mm] : (__bf16)0.f;
-      fb0[j] = ok ? a0[mm] : (__bf16)0.f;
-      fb1[j] = ok ? a1[mm] : (__bf16)0.f;
+      fa0[j] = ok ? z0[zo(mm)] : (__bf16)0.f;
+      fa1[j] = ok ? z1[zo(mm)] : (__bf16)0.f;
+      fb0[j] = ok ? a0[ao(mm)] : (__bf16)0.f;
+      fb1[j] = ok ? a1[ao(mm)] : (__bf16)0.f;
     }
     acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb0, acc[0][0], 0, 0, 0);
     acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb1, acc[0][1], 0, 0, 0);
@@ -1502,6 +1523,7 @@ struct TowerLayout {
   int64_t woff[2][MAXL], boff[2][MAXL], wcoff[2][MAXL];
   int32_t K[2][MAXL];
   int64_t in_max;
+  int64_t Bp;        // strip rows per block (B rounded up to 32)
   int nwg;
   int S;
   int64_t mslice;
@@ -1576,9 +1598,10 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
     off += align_up(bytes, 256);
     return r;
   };
-  L.o_xt = take(2 * (size_t)L.in_max * B * 2);
-  L.o_act = take(2 * (size_t)MAXL * MAXW * B * 2);
-  L.o_dzt = take(2 * (size_t)MAXL * MAXW * B * 2);
+  L.Bp = ceil_div(B, 32) * 32;
+  L.o_xt = take(2 * (size_t)L.in_max * L.Bp * 2);
+  L.o_act = take(2 * (size_t)MAXL * MAXW * L.Bp * 2);
+  L.o_dzt = take(2 * (size_t)MAXL * MAXW * L.Bp * 2);
   L.o_dbpart = take(2 * (size_t)MAXL * L.nwg * MAXW * 4);
   L.o_slab = take((size_t)L.S * L.P * 4);
   L.o_losspart = take((size_t)L.nwg * 4);
@@ -1701,6 +1724,7 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   a.dbpart = reinterpret_cast<float*>(ws + L.o_dbpart);
   a.loss_part = reinterpret_cast<float*>(ws + L.o_losspart);
   a.in_max = L.in_max;
+  a.Bp = L.Bp;
   a.nwg = L.nwg;
   if (const char* e = getenv("TT_T1_DEBUG")) a.dbg = atoi(e);
   if (a.dbg & 8) a.stamps = reinterpret_cast<int64_t*>(ws + L.o_dbg);
@@ -1748,6 +1772,7 @@ static int wgrad_args(const tt_tower_shape_t* shape, int64_t B, float* loss, voi
   a.P = L.P;
   a.B = B;
   a.in_max = L.in_max;
+  a.Bp = L.Bp;
   a.S = L.S;
   a.mslice = L.mslice;
   a.ntiles = L.ntiles;
