@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--host-fed", action="store_true",
                     help="feed host batches through the 3-stage host pipeline (pinned staging, async H2D on a "
                          "copy stream, graph replay): the PCIe-inclusive rate, reported beside the resident one")
+    ap.add_argument("--no-kjt-ahead", action="store_true",
+                    help="multi-hot workloads: group each batch inside its own step instead of one step ahead")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
     return ap.parse_args()
@@ -332,11 +334,11 @@ def run_multihot(args):
     cap = max(v.numel() for v, _, _ in batches)
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01, lr_dense=0.01,
                              id_dtype=torch.int64, seed=0, max_lookups=cap)
-    step.capture_pool_kjt(batches)
+    # pipelined grouping: batch i+1's tt_bwd_prepare runs on the side stream during step i
+    step.capture_pool_kjt(batches, ahead=not args.no_kjt_ahead)
 
-    def run(n, i=0):
-        for j in range(n):
-            step.pool_graphs[(i + j) % len(step.pool_graphs)].replay()
+    def run(n):
+        step.replay_pool(n)
 
     run(args.warmup)
     torch.cuda.synchronize()
@@ -348,13 +350,11 @@ def run_multihot(args):
     value = args.steps * B / dt
     loss = float(step.loss)
     # per-launch device time: eager steps with HIP events around each launch on its stream
-    keep = step.values, step.offsets, step.labels
     step._timing = []
     try:
         for i in range(min(args.steps, 20)):
-            step.values, step.offsets, step.labels = batches[i % len(batches)]
             step._timing.append({})
-            step.step()
+            step.pool_step_eager()
         torch.cuda.synchronize()
         acc = {}
         for mk in step._timing:
@@ -362,7 +362,6 @@ def run_multihot(args):
                 acc.setdefault(name, []).append(a.elapsed_time(b))
     finally:
         step._timing = None
-        step.values, step.offsets, step.labels = keep
     timed = {k: sum(v) / len(v) for k, v in acc.items()}
     nnz = sum(v.numel() for v, _, _ in batches) // len(batches)
     uniq = 0

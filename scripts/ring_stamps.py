@@ -21,7 +21,7 @@ batches = [([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
             torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32)) for _ in range(64)]
 st.capture_ring(batches, steps_per_graph=8)
 nwg = B // 32
-off = st.towers.nbytes - ((max(2 * nwg, 1024) * 64 + 255) // 256 * 256)
+off = st.towers.nbytes - (((max(2 * nwg, 1024) * 8 + nwg * 16 * 9) * 8 + 255) // 256 * 256)
 base = st.towers.ws[off:off + 8192 * 8].view(torch.int64)
 ntile, nbias = 6 * 32, (2 * (128 + 64) + 1 + 3) // 4
 roles_t2 = [("tiles", 0, ntile), ("bias", ntile, ntile + nbias), ("insert", ntile + nbias, 1024)]

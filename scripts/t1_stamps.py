@@ -16,7 +16,7 @@ batches = [([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
             torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32)) for _ in range(64)]
 st.capture_ring(batches, steps_per_graph=8)
 nwg = B // 32
-off = st.towers.nbytes - ((max(2 * nwg, 1024) * 64 + 255) // 256 * 256)
+off = st.towers.nbytes - (((max(2 * nwg, 1024) * 8 + nwg * 16 * 9) * 8 + 255) // 256 * 256)
 for it in range(6):
     st.run_eager(1)
     torch.cuda.synchronize()

@@ -19,7 +19,7 @@ nres = 0
 ntile = 6 * 32
 nbias = (2 * (128 + 64) + 1 + 3) // 4
 nwg = nres + ntile + nbias
-off = st.towers.nbytes - ((max(2 * (B // 32), 1024) * 64 + 255) // 256 * 256)
+off = st.towers.nbytes - (((max(2 * (B // 32), 1024) * 8 + (B // 32) * 16 * 9) * 8 + 255) // 256 * 256)
 for it in range(6):
     st.run_eager(1)
     torch.cuda.synchronize()

@@ -135,3 +135,42 @@ def test_config3_shape_step_vs_oracle(device, precision):
     if precision == "fp32":
         for f in range(F):
             np.testing.assert_allclose(st.tables.table_view(f).cpu().numpy(), s0.tables[f].numpy(), rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("hot", [False, True], ids=["uniform", "zipf"])
+def test_multihot_pipelined_grouping_bitwise(device, hot):
+    """The pipelined pool (capture_pool_kjt(ahead=True): batch i+1's backward grouping built on the
+    side stream during step i, two alternating workspaces) trains exactly like the unpipelined
+    pool: 4 batches x 2 cycles of graph replays, tables / row-wise state / tower parameters / loss
+    bitwise equal; then 3 eager pipelined steps (pool_step_eager) continue bitwise like 3 more
+    unpipelined graph replays. Zipf ids exercise the hot-row kernels."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    rng = np.random.default_rng(23 if hot else 24)
+    B, D, layers, N = 256, 128, [128, 64], [2000, 3000]
+    host = [_kjt(rng, B, N, 9, hot) for _ in range(4)]
+    g = torch.Generator().manual_seed(5)
+    batches = [(torch.from_numpy(v).to(device), torch.from_numpy(o).to(device),
+                torch.randint(0, 2, (B,), generator=g).to(torch.int32).to(device)) for v, o in host]
+    cap = max(v.size for v, _ in host)
+
+    def make():
+        return FusedTwoTowerStep(N, [D, D], [0], [1], layers, B, device, lr_emb=0.02, lr_dense=0.01, seed=6,
+                                 max_lookups=cap)
+
+    ref_st, pipe = make(), make()
+    ref_st.capture_pool_kjt(batches)
+    pipe.capture_pool_kjt(batches, ahead=True)
+    for i in range(8):
+        ref_st.pool_graphs[i % 4].replay()
+    pipe.replay_pool(8)
+    torch.cuda.synchronize()
+    for a, b in ((ref_st.tables.weights, pipe.tables.weights), (ref_st.tables.state, pipe.tables.state),
+                 (ref_st.params, pipe.params), (ref_st.loss, pipe.loss)):
+        assert torch.equal(a, b)
+    for i in range(3):
+        ref_st.pool_graphs[i].replay()
+        pipe.pool_step_eager()
+    torch.cuda.synchronize()
+    assert torch.equal(ref_st.tables.weights, pipe.tables.weights) and torch.equal(ref_st.params, pipe.params)
+    assert torch.equal(ref_st.tables.state, pipe.tables.state)

@@ -108,6 +108,10 @@ struct TowerArgs {
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
 };
+// EXPERIMENT (TT_T1_DEBUG bit 64 with 8): lane 0 of every wave at its arrival at barrier k (1..7),
+// at its start (0) and its end (8): [nwg][16][9] after the 8192 stamps of the other launches
+#define T1_WSTAMP(k) \
+  do { if (a.stamps && (a.dbg & 64) && lane == 0) a.stamps[8192 + ((int64_t)blockIdx.x * 16 + (k)) * 9 + wid] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 #define T1_STAMP(k) \
   do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 
@@ -477,6 +481,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   // the kernarg segment: one more dependent memory hop in front of the row gather)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (UPD && wid == 8) {
+    T1_WSTAMP(0);
     // ---- the dedup wave (UPD): for each of the 2 x TR lookups, is its row looked up once in this
     // step? (claim >= 0 and slot count 1 in the batch's completed table) -> row and state to LDS
     const int tq = lane / TR, row = lane % TR;
@@ -492,6 +497,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         st = (tq ? a.us[1] : a.us[0])[r];  // speculative: used only for a single-lookup row
       }
     }
+    T1_WSTAMP(1);
     __syncthreads();
     const uint64_t word = cl >= 0 ? a.dd.slots[cl].word : DD_EMPTY;
     const bool single = cl >= 0 && (word & DD_CNT_MASK) == 1;
@@ -524,12 +530,16 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       }
     }
 #pragma unroll 1
-    for (int k = 1; k < T1_BARRIERS; ++k) __syncthreads();
+    for (int k = 1; k < T1_BARRIERS; ++k) {
+      T1_WSTAMP(k + 1);
+      __syncthreads();
+    }
     if (pref) {
 #pragma unroll
       for (int j = 0; j < NPF; ++j) pf ^= pv[j];
       if (pf == 0x7fc00123u && a.B < 0) a.logits[0] = 0.f;  // never taken: keeps the loads
     }
+    T1_WSTAMP(8);
     return;
   }
   if (wid == 8) {
@@ -563,6 +573,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   }
   const int t = wid >> 2, w4 = wid & 3;
   T1_STAMP(0);
+  T1_WSTAMP(0);
   const int tt = threadIdx.x & 255;  // thread index inside the tower group
   const int r16 = lane & 15, q4 = lane >> 4;
   const int64_t B = a.B;
@@ -666,6 +677,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + incol + c4) = xv[i];
     }
   }
+  T1_WSTAMP(1);
   __syncthreads();
   T1_STAMP(1);
   // X^T for T2's dW0 (fire-and-forget stores)
@@ -703,6 +715,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       if (!(a.dbg & 1)) store_t4(a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + strip_at(col, gm, MAXW), pk, gm, B);
     }
   }
+  T1_WSTAMP(2);
   __syncthreads();
   T1_STAMP(2);
   // ---- 2. layer 1: out = relu(h W1^T + b1) (fp32)
@@ -719,6 +732,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         outf[t][row * FSTR + col] = fmaxf(acc[i][j][rr] + bias1[j], 0.f);
       }
   }
+  T1_WSTAMP(3);
   __syncthreads();
   T1_STAMP(3);
   // ---- 3. logits, BCE, dlogit: 16 threads per row
@@ -742,6 +756,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       lpart[row] = lo;
     }
   }
+  T1_WSTAMP(4);
   __syncthreads();
   T1_STAMP(4);
   // ---- 4. dZ1 = dlogit * other * (self > 0): thread -> (column, 8 consecutive rows)
@@ -770,6 +785,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         if (gm + j < B) dst[j] = v[j];
     }
   }
+  T1_WSTAMP(5);
   __syncthreads();
   T1_STAMP(5);
   // ---- 5. dZ0 = (dZ1 W1) * (h > 0)  -> xs (X is no longer needed)
@@ -798,6 +814,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     s += __shfl_xor(s, 32, 64);
     if (q4 == 0) a.dbpart[(((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW + col] = s;
   }
+  T1_WSTAMP(6);
   __syncthreads();
   T1_STAMP(6);
   // ---- 6. dX = dZ0 W0 -> LDS (outf is free since phase 4) -> pooled gradient, whole rows
@@ -817,6 +834,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     for (int i = 0; i < TR; ++i) p += lpart[i];
     a.loss_part[blockIdx.x] = p;
   }
+  T1_WSTAMP(7);
   __syncthreads();
   T1_STAMP(7);
 #pragma unroll
@@ -854,6 +872,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       if (dst && !(a.dbg & 2)) *reinterpret_cast<f32x4*>(dst) = g;
     }
   }
+  T1_WSTAMP(8);
   T1_STAMP(15);
 }
 
@@ -1611,7 +1630,7 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.o_wbf = take((size_t)L.PW * 2);
   L.o_wtbf = take((size_t)L.PW * 2);
   L.o_tiles = take((size_t)nt * sizeof(WgradTile));
-  L.o_dbg = take((size_t)std::max<int64_t>(L.nwg * 2, 1024) * 8 * sizeof(int64_t));
+  L.o_dbg = take((size_t)(std::max<int64_t>(L.nwg * 2, 1024) * 8 + L.nwg * 16 * 9) * sizeof(int64_t));
   L.total = off;
   *lay = L;
   return TT_OK;

@@ -211,25 +211,69 @@ class FusedTwoTowerStep:
         self.offsets.copy_(offsets.to(torch.int32), non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
 
-    def capture_pool_kjt(self, batches: Sequence, keep_graph: bool = False) -> None:
-        """One graph per resident multi-hot batch (values, offsets int32, labels), read in place."""
+    def capture_pool_kjt(self, batches: Sequence, keep_graph: bool = False, ahead: bool = False) -> None:
+        """One graph per resident multi-hot batch (values, offsets int32, labels), read in place.
+        ahead: the pipelined form (``step(next_kjt=...)``): graph i groups batch i+1 of the pool
+        while it trains on batch i, so the graphs must be replayed in pool order from the cursor
+        (``replay_pool``); the pool length must be even (the two grouping workspaces alternate)."""
         staged = []
         for values, offsets, labels in batches:
             if values.dtype != self.id_dtype or offsets.dtype != torch.int32 or values.numel() > self.max_lookups \
                     or offsets.numel() != self.F * self.B + 1:
                 raise _lib.TTError("capture_pool_kjt: batch does not match the step's dtype / capacity")
             staged.append((values.contiguous(), offsets.contiguous(), labels.to(torch.int32).contiguous()))
+        n = len(staged)
+        if ahead and n % 2:
+            raise _lib.TTError("capture_pool_kjt(ahead=True): the batch count must be even")
         self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]
         keep = self.values, self.offsets, self.labels
         self.pool_graphs = []
+        self.pool_ahead = bool(ahead)
+        self._kjt_pool = staged
+        if ahead:
+            self.kjt_ring_prime(staged[0][0], staged[0][1], 0)
         try:
-            for v, o, lab in staged:
+            for i, (v, o, lab) in enumerate(staged):
                 self.values, self.offsets, self.labels = v, o, lab
-                self.capture(None, keep_graph=keep_graph)
+                nxt = (staged[(i + 1) % n][0], staged[(i + 1) % n][1]) if ahead else None
+                self.capture(None, keep_graph=keep_graph, next_kjt=nxt, parity=i % 2)
                 self.pool_graphs.append(self.graph)
         finally:
             self.values, self.offsets, self.labels = keep
         self.steps_per_graph = 1
+        self.pool_cursor = 0
+
+    def kjt_ring_prime(self, values: torch.Tensor, offsets: torch.Tensor, parity: int) -> None:
+        """Group the first batch of a pipelined multi-hot sequence into workspace ``parity`` (every
+        later batch is grouped by the step before it)."""
+        ts = self.tables
+        ts.use_bwd_workspace(1 - parity)  # both workspaces exist before any graph capture
+        ts.use_bwd_workspace(parity)
+        ts.bwd_prepare(values, offsets, self.B, max_lookups=self.max_lookups)
+
+    def replay_pool(self, n: int) -> None:
+        """Replay n pool graphs in pool order, continuing at the cursor (the pipelined pool needs
+        the order: graph i expects batch i's grouping from graph i-1)."""
+        i, nb = self.pool_cursor, len(self.pool_graphs)
+        for _ in range(n):
+            self.pool_graphs[i].replay()
+            i = (i + 1) % nb
+        self.pool_cursor = i
+
+    def pool_step_eager(self) -> None:
+        """One step of the captured multi-hot pool at the cursor without graphs (timing / tests)."""
+        staged, i = self._kjt_pool, self.pool_cursor
+        n = len(staged)
+        keep = self.values, self.offsets, self.labels
+        self.values, self.offsets, self.labels = staged[i]
+        try:
+            if self.pool_ahead:
+                self.step(next_kjt=(staged[(i + 1) % n][0], staged[(i + 1) % n][1]), parity=i % 2)
+            else:
+                self.step()
+        finally:
+            self.values, self.offsets, self.labels = keep
+        self.pool_cursor = (i + 1) % n
 
     def _towers_fwd(self):
         L = len(self.layer_sizes)
@@ -264,18 +308,34 @@ class FusedTwoTowerStep:
                     ops.linear_bwd_data([dy], [y], [W_], relu=True, outs=[dx], precision=pr)
                     ops.linear_bwd_weight([dy], [y], [x], relu=True, dws=[gW], dbs=[gb], precision=pr)
 
-    def step(self) -> None:
-        """One training step on the batch currently in ``cols`` / ``labels``."""
+    def step(self, next_kjt: Optional[Sequence[torch.Tensor]] = None, parity: int = 0) -> None:
+        """One training step on the batch currently in ``cols`` / ``labels`` (multi-hot: ``values`` /
+        ``offsets`` / ``labels``).
+        next_kjt (multi-hot input only): the pipelined form. This batch's backward grouping is
+        already complete in grouping workspace ``parity`` (built by the previous step, or by
+        ``kjt_ring_prime``); the grouping of next_kjt = (values, offsets) is built into workspace
+        1 - parity on the side stream, beside this step's forward, towers and update."""
         B, F = self.B, self.F
         main = torch.cuda.current_stream(self.device)
+        ahead = next_kjt is not None
+        if ahead and not (self.kjt_input and self.side is not None):
+            raise _lib.TTError("step(next_kjt): needs multi-hot input (max_lookups) and overlap_prepare")
         if self.kjt_mode == "kjt":
             # materialise the KJT (values / lengths / offsets) from the single-hot columns, or take
             # the multi-hot KJT as loaded; then the KJT-form kernels
             if not self.kjt_input:
                 ops.kjt_build_mod_dropzero(self.cols, self.num_embeddings, self.values, self.lengths, self.offsets,
                                            self.lpk)
-            prepare = lambda: self.tables.bwd_prepare(self.values, self.offsets, B,  # noqa: E731
-                                                      max_lookups=self.max_lookups)
+            if ahead:
+                ts = self.tables
+
+                def prepare():
+                    ts.use_bwd_workspace(1 - parity)
+                    ts.bwd_prepare(next_kjt[0], next_kjt[1], B, max_lookups=self.max_lookups)
+                    ts.use_bwd_workspace(parity)
+            else:
+                prepare = lambda: self.tables.bwd_prepare(self.values, self.offsets, B,  # noqa: E731
+                                                          max_lookups=self.max_lookups)
             self.offsets_used = self.offsets
         elif self.dedup_single:
             # single-hot columns, two-launch dedup: the insert runs inside T1 (gather) or here
@@ -336,11 +396,13 @@ class FusedTwoTowerStep:
                 self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
                                    grads_out=self.grads)
                 self._mark("t2t3", 1)
-            if self.side is not None and prepare is not None:
+            if self.side is not None and prepare is not None and not ahead:
                 main.wait_stream(self.side)
             self._mark("upd", 0)
             self._emb_update()
             self._mark("upd", 1)
+            if ahead:
+                main.wait_stream(self.side)
             if self.side2 is not None:
                 main.wait_stream(self.side2)
             return
@@ -349,9 +411,11 @@ class FusedTwoTowerStep:
         self.dot_bce(self.qy[L - 1], self.cy[L - 1], self.labels, logits=self.logits, loss=self.loss,
                      dq=self.qdy[L - 1], dc=self.cdy[L - 1])
         self._towers_bwd()
-        if self.side is not None and prepare is not None:
+        if self.side is not None and prepare is not None and not ahead:
             main.wait_stream(self.side)
         self._emb_update()
+        if ahead:
+            main.wait_stream(self.side)
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, self.lr_dense)
 
     def _mark(self, name: str, end: int) -> None:
@@ -560,7 +624,8 @@ class FusedTwoTowerStep:
             self.ring_cursor = (i + 1) % nb
 
     # ------------------------------------------------------------------------------------------
-    def capture(self, batches: Optional[Sequence] = None, keep_graph: bool = False) -> None:
+    def capture(self, batches: Optional[Sequence] = None, keep_graph: bool = False,
+                next_kjt: Optional[Sequence[torch.Tensor]] = None, parity: int = 0) -> None:
         """Record ``step()`` into a HIP graph (replayed by ``replay()``). With ``batches`` (a list of
         resident (cols, labels) device batches) the graph holds one full step per batch, in order."""
         self.sync_weights()
@@ -572,7 +637,7 @@ class FusedTwoTowerStep:
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 if batches is None:
-                    self.step()
+                    self.step(next_kjt=next_kjt, parity=parity)
                 else:
                     for cols, labels in batches:
                         self.cols, self.labels = list(cols), labels

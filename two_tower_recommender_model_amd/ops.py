@@ -244,6 +244,23 @@ class TableSet:
         self._bwd_cap = cap
         check(lib.tt_bwd_workspace_init(ptr(self._bwd_ws), nbytes, cap, stream_handle(self.device)), "bwd_ws_init")
 
+    def use_bwd_workspace(self, k: int) -> None:
+        """Select grouping workspace k (0 or 1) for the following tt_bwd_prepare /
+        tt_bwd_rowwise_adagrad calls: a pipelined caller groups batch i+1 into one workspace while
+        batch i's update reads the other. Workspace 1 is allocated (same capacity) on first use."""
+        if self._bwd_ws is None:
+            raise _lib.TTError("use_bwd_workspace: call ensure_bwd_workspace first")
+        if not hasattr(self, "_bwd_wss"):
+            self._bwd_wss = [self._bwd_ws, None]
+        if self._bwd_wss[0] is not self._bwd_ws and self._bwd_wss[1] is not self._bwd_ws:
+            self._bwd_wss = [self._bwd_ws, None]  # the workspace was re-sized
+        if self._bwd_wss[k] is None:
+            ws = torch.empty_like(self._bwd_wss[0])
+            check(_lib_().tt_bwd_workspace_init(ptr(ws), ws.numel(), self._bwd_cap, stream_handle(self.device)),
+                  "bwd_ws_init")
+            self._bwd_wss[k] = ws
+        self._bwd_ws = self._bwd_wss[k]
+
     def bwd_prepare(self, values: torch.Tensor, offsets: torch.Tensor, B: int, max_lookups: int,
                     bounds_check: bool = False) -> None:
         self.ensure_bwd_workspace(max_lookups)
