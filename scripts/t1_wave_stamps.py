@@ -6,7 +6,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-# extra TT_T1_DEBUG bits from argv[1]: 4 = every lookup reads row 0, 32 = no id load (id 1)
+# extra TT_T1_DEBUG bits from argv[1]: 4 = every lookup reads row 0, 32 = no id load (id 1),
+# 2 = no dX store, 128 = no in-place row / state store
 os.environ["TT_T1_DEBUG"] = str(72 | (int(sys.argv[1]) if len(sys.argv) > 1 else 0))
 import torch  # noqa: E402
 
@@ -28,13 +29,13 @@ for it in range(4):
     if it < 3:
         continue
     w = st.towers.ws[off:off + dbg_bytes].view(torch.int64)[8192:8192 + nwg * 16 * 9].view(nwg, 16, 9).cpu().double()
-    w = w[:, :9, :]  # points 0..8
+    w = w[:, :11, :]  # points 0..8, then 9 = past barrier 7, 10 = first dX / row store issued
     t0 = w[:, 0, :].min(dim=1, keepdim=True).values  # workgroup start
     rel = (w - t0.unsqueeze(1)) / 100.0  # us, [wg, point, wave]
     print(f"it{it}: arrival (us from the workgroup's first wave start), median over workgroups")
     print("  point  " + " ".join(f"  w{j}" for j in range(9)) + "   last  phase")
     prev = torch.zeros(nwg, dtype=torch.float64)
-    for k in range(9):
+    for k in list(range(8)) + [9, 10, 8]:
         med = rel[:, k, :].median(dim=0).values
         last = rel[:, k, :].max(dim=1).values
         ph = float((last - prev).median())

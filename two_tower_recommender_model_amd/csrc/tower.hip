@@ -443,6 +443,66 @@ __device__ __forceinline__ void mma_frags(f32x4 (&acc)[2][2], const __bf16* As, 
   }
 }
 
+// T1's W0 image in LDS: [hidden unit][input column] bf16 in 256-B rows whose 16-B chunks are
+// XOR-swizzled by row (CDNA4 guide T10, layout (b)). Layer 0 takes its W0 fragments from global
+// memory and files them here; the dX product reads the SAME image transposed
+// (ds_read_b64_tr_b16) instead of loading a second, transposed copy of W0 from global memory.
+__device__ __forceinline__ int w0_off(int row, int ch) {  // byte offset of 16-B chunk ch of row
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// f0 (B fragments of W0 as layer 0 reads it: lane r + 16 q of fragment (k-step s, tile j) holds
+// W0[tile * 16 + r][s * 32 + 8 q .. + 7], one 16-B chunk) -> the image
+__device__ __forceinline__ void w0_image_store(char* img, const Frags& f0, int K, int N, int w4) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int nk = K >> 5, nt = N >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (w4 + 4 * j < nt && s < nk)
+        *reinterpret_cast<bf16x8*>(img + w0_off((w4 + 4 * j) * 16 + r, 4 * s + q)) = f0.f[s][j];
+}
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// acc = A (LDS rows, K = W0 columns) x W0 (the image, [K = hidden][N = input]): the B fragment of
+// (k-step s, n-tile nt) is B[s * 32 + 8 q + e][nt * 16 + r] = image[row s * 32 + 8 q + e][col nt * 16 + r],
+// two transposed reads of 4 image rows x 16 columns each (lane 4 q' + p of a 16-lane group
+// addresses row q', columns 4 p .. 4 p + 3; lane i receives column i). Every lane of the wave
+// executes the reads (wave-uniform conditions only: the read needs a full EXEC mask).
+__device__ __forceinline__ void mma_w0_tr(f32x4 (&acc)[2][2], const __bf16* As, const char* img, int K, int N,
+                                          int w4) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int qq = (lane & 15) >> 2, p = lane & 3;
+  const int nk = K >> 5, nt = N >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4)(0.f);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s < nk) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(As + r * LSTR + s * 32 + q * 8);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(As + (16 + r) * LSTR + s * 32 + q * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (w4 + 4 * j < nt) {
+          const int row = s * 32 + 8 * q + qq, ch = 2 * (w4 + 4 * j) + (p >> 1);
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(img + w0_off(row, ch) + 8 * (p & 1)));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(img + w0_off(row + 4, ch) + 8 * (p & 1)));
+          const bf16x8 b = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b, acc[0][j], 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b, acc[1][j], 0, 0, 0);
+        }
+    }
+  }
+}
+
 __device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int64_t gm, int64_t B) {
   if (gm + 4 <= B) {
     *reinterpret_cast<bf16x4*>(dst) = pk;
@@ -470,9 +530,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) float outf[2][TR * FSTR];  // tower outputs, later dX (fp32)
   __shared__ float dlog[TR];
   __shared__ float lpart[TR];
-  // UPD: the fp32 rows as gathered, and per (tower, row) the lookup's table row (-1: not updated
-  // here) and its row-wise state, filed by the dedup wave
-  __shared__ __attribute__((aligned(16))) float xf[UPD ? 2 : 1][UPD ? TR * FSTR : 4];
+  __shared__ __attribute__((aligned(16))) char w0img[2][128 * 256];  // W0 image (w0_off), per tower
+  // UPD: per (tower, row) the lookup's table row (-1: not updated here) and its row-wise state,
+  // filed by the dedup wave (the fp32 rows as gathered stay in the compute waves' registers)
   __shared__ int64_t urow[2][TR];
   __shared__ float ustate[2][TR];
 
@@ -511,7 +571,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     uint32_t pv[NPF];
     uint32_t pf = 0;
     const bool pref = a.pcol[0] != nullptr;
-    if (pref) {
+    auto issue_prefetch = [&]() {
       const float* base = nullptr;
       if (gm < a.B) {
         const int64_t idn = load_id(tq ? a.pcol[1] : a.pcol[0], a.gid_dtype, gm);
@@ -528,15 +588,25 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         const uint64_t p = (uint64_t)__shfl((long long)b64, lk, 64);
         pv[j] = p ? *reinterpret_cast<const uint32_t*>(p + (k % SEG) * 64) : 0u;
       }
-    }
+    };
+    const bool late = (a.dbg & 256) != 0;  // experiment: prefetch after the last barrier
+    if (pref && !late) issue_prefetch();
+    uint32_t touch = 0;
 #pragma unroll 1
     for (int k = 1; k < T1_BARRIERS; ++k) {
+      if (k == 5 && (a.dbg & 512) && r >= 0) {
+        // experiment: re-touch this lookup's row and state (translation) ahead of the in-place update
+        touch = *reinterpret_cast<const uint32_t*>((tq ? a.gtab[1] : a.gtab[0]) + r * IN_) ^
+                __float_as_uint((tq ? a.us[1] : a.us[0])[r]);
+      }
       T1_WSTAMP(k + 1);
       __syncthreads();
     }
-    if (pref) {
+    if (pref && late) issue_prefetch();
+    if (pref || touch) {
+      pf ^= touch;
 #pragma unroll
-      for (int j = 0; j < NPF; ++j) pf ^= pv[j];
+      for (int j = 0; j < NPF; ++j) pf ^= pref ? pv[j] : 0u;
       if (pf == 0x7fc00123u && a.B < 0) a.logits[0] = 0.f;  // never taken: keeps the loads
     }
     T1_WSTAMP(8);
@@ -639,14 +709,13 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       }
     }
   }
-  Frags f0, f1, g1, g0;
+  Frags f0, f1, g1;
   if (a.dbg & 16) {
-    for (int s_ = 0; s_ < 4; ++s_) for (int j_ = 0; j_ < 2; ++j_) { f0.f[s_][j_] = (bf16x8)(__bf16)0.f; f1.f[s_][j_] = f0.f[s_][j_]; g1.f[s_][j_] = f0.f[s_][j_]; g0.f[s_][j_] = f0.f[s_][j_]; }
+    for (int s_ = 0; s_ < 4; ++s_) for (int j_ = 0; j_ < 2; ++j_) { f0.f[s_][j_] = (bf16x8)(__bf16)0.f; f1.f[s_][j_] = f0.f[s_][j_]; g1.f[s_][j_] = f0.f[s_][j_]; }
   } else {
   load_frags(f0, a.wbf + a.wcoff[t][0], in, in, W0, w4);      // W0 [W0][in]
   load_frags(f1, a.wbf + a.wcoff[t][1], W0, W0, W1, w4);      // W1 [W1][W0]
   load_frags(g1, a.wtbf + a.wcoff[t][1], W1, W1, W0, w4);     // W1^T [W0][W1]
-  load_frags(g0, a.wtbf + a.wcoff[t][0], W0, W0, in, w4);     // W0^T [in][W0]
   }
   float bias0[2], bias1[2];
 #pragma unroll
@@ -671,7 +740,6 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         bv[0] = (__bf16)xv[i][0]; bv[1] = (__bf16)xv[i][1]; bv[2] = (__bf16)xv[i][2]; bv[3] = (__bf16)xv[i][3];
       }
       *reinterpret_cast<bf16x4*>(xs[t] + row * LSTR + c4) = bv;
-      if (UPD) *reinterpret_cast<f32x4*>(&xf[t][row * FSTR + c4]) = xv[i];
       const int64_t gm = m0 + row;
       if (!R16 && a.pooled_out && gm < B)
         *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + incol + c4) = xv[i];
@@ -697,6 +765,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   f32x4 acc[2][2];
   // ---- 1. layer 0: h = relu(X W0^T + b0)
   mma_frags(acc, xs[t], f0, in, W0, w4);
+  w0_image_store(w0img[t], f0, in, W0, w4);  // read back transposed by the dX product (phase 6)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     if (w4 + 4 * j >= W0 / 16) continue;
@@ -818,7 +887,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __syncthreads();
   T1_STAMP(6);
   // ---- 6. dX = dZ0 W0 -> LDS (outf is free since phase 4) -> pooled gradient, whole rows
-  mma_frags(acc, xs[t], g0, W0, in, w4);
+  mma_w0_tr(acc, xs[t], w0img[t], W0, in, w4);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     if (w4 + 4 * j >= in / 16) continue;
@@ -837,8 +906,10 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   T1_WSTAMP(7);
   __syncthreads();
   T1_STAMP(7);
+  T1_WSTAMP(9);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    if (i == 1) T1_WSTAMP(10);
     if (i < nxv) {
       const int e = tt + 256 * i;
       const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
@@ -863,9 +934,11 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         if (ur >= 0) {
           const float snew = rw_state(ustate[t][row], sq, in);
           const float stdv = rw_stdv(snew, a.ueps);
-          const f32x4 x = *reinterpret_cast<const f32x4*>(&xf[t][row * FSTR + c4]);
-          *reinterpret_cast<f32x4*>(a.uw[t] + ur * in + c4) = rw_apply(x, g, a.ulr, stdv);
-          if (c4 == 0) a.us[t][ur] = snew;
+          const f32x4 x = xv[i];
+          if (!(a.dbg & 128)) {
+            *reinterpret_cast<f32x4*>(a.uw[t] + ur * in + c4) = rw_apply(x, g, a.ulr, stdv);
+            if (c4 == 0) a.us[t][ur] = snew;
+          }
           if (!a.pooled_out) dst = nullptr;  // dX is needed only for inspection (pooled_out mode)
         }
       }
