@@ -305,10 +305,10 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
         float* wrow = weights + gm.lm->woff[t] + r * D;
         float* srow = state + gm.lm->soff[t] + r;
         const float snew = rw_state(*srow, sq, D);
-        const float stdv = rw_stdv(snew, eps);
+        const float step = rw_step(snew, lr, eps);
         if (col_ok)
           *reinterpret_cast<f32x4v*>(wrow + hl * 4) =
-              rw_apply(*reinterpret_cast<const f32x4v*>(wrow + hl * 4), g, lr, stdv);
+              rw_apply(*reinterpret_cast<const f32x4v*>(wrow + hl * 4), g, step);
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
           *srow = snew;
@@ -435,8 +435,8 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
     if (c[q] > 0) {
       const float snew = rw_state(s_old[q], sq, D[q]);
-      const float stdv = rw_stdv(snew, eps);
-      if (col_ok[q]) *reinterpret_cast<f32x4v*>(wrow[q] + hl * 4) = rw_apply(wv[q], g[q], lr, stdv);
+      const float step = rw_step(snew, lr, eps);
+      if (col_ok[q]) *reinterpret_cast<f32x4v*>(wrow[q] + hl * 4) = rw_apply(wv[q], g[q], step);
       if (hl == 0) *srow[q] = snew;
     }
     if (active[q] && hl == 0) sp[q]->word = DD_EMPTY;

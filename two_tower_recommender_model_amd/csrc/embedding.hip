@@ -843,16 +843,16 @@ __global__ void __launch_bounds__(256) bwd_adagrad_narrow_kernel(EmbMeta m, cons
         if (v1) g += x1;
       }
     }
-    // row-wise Adagrad: s += mean(G^2); w += (-lr * G) / (sqrt(s) + eps)
+    // row-wise Adagrad: s += mean(G^2); w += G * (-lr / (sqrt(s) + eps)) (rw_step, tt_common.h)
     float sq = g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
     if (active) {
       const float snew = s_old + sq / (float)D;
-      const float stdv = sqrtf(snew) + eps;
+      const float step = rw_step(snew, lr, eps);
       if (col_ok) {
 #pragma unroll
-        for (int v = 0; v < 4; ++v) wv[v] = wv[v] + (-lr * g[v]) / stdv;
+        for (int v = 0; v < 4; ++v) wv[v] = fmaf(g[v], step, wv[v]);
         *reinterpret_cast<f32x4v*>(wrow + hl * 4) = wv;
       }
       if (hl == 0) *srow = snew;
@@ -924,11 +924,11 @@ __global__ void __launch_bounds__(256) bwd_adagrad_direct_kernel(EmbMeta m, cons
       for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
       if (on[k]) {
         const float snew = s_old[k] + sq / (float)D[k];
-        const float stdv = sqrtf(snew) + eps;
+        const float step = rw_step(snew, lr, eps);
         if (hl * 4 < D[k]) {
           f32x4v w = wv[k];
 #pragma unroll
-          for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[k][v]) / stdv;
+          for (int v = 0; v < 4; ++v) w[v] = fmaf(g[k][v], step, w[v]);
           *reinterpret_cast<f32x4v*>(wrow[k] + hl * 4) = w;
         }
         if (hl == 0) *srow[k] = snew;
@@ -998,14 +998,14 @@ __device__ __forceinline__ void adagrad_row(const EmbMeta& m, const BagRow& br, 
   }
   sq = wave_sum(sq);
   const float snew = *srow + sq / (float)D;
-  const float stdv = sqrtf(snew) + eps;
+  const float step = rw_step(snew, lr, eps);
 #pragma unroll
   for (int k = 0; k < ADA_KMAX; ++k) {
     const int c = lane + k * 64;
     if (c < ncol) {
       vf x = *reinterpret_cast<vf*>(w + c * VEC);
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) x[v] = x[v] + (-lr * gsave[k][v]) / stdv;
+      for (int v = 0; v < VEC; ++v) x[v] = fmaf(gsave[k][v], step, x[v]);
       *reinterpret_cast<vf*>(w + c * VEC) = x;
     }
   }
@@ -1183,12 +1183,12 @@ __device__ __forceinline__ void hot_item(const EmbMeta& m, const BagRow& br, con
     sq = (redf[0] + redf[1]) + (redf[2] + redf[3]);
     float* srow = state + tm.state_offset + row;
     const float snew = *srow + sq / (float)D;
-    const float stdv = sqrtf(snew) + eps;
+    const float step = rw_step(snew, lr, eps);
     float* wrow = weights + tm.weight_offset + row * D;
 #pragma unroll
     for (int k = 0; k < HOT_DMAX / 256; ++k) {
       const int c = tid + 256 * k;
-      if (c < D) wrow[c] = wrow[c] + (-lr * tot[k]) / stdv;
+      if (c < D) wrow[c] = fmaf(tot[k], step, wrow[c]);
     }
     __syncthreads();
     if (tid == 0) *srow = snew;
@@ -1262,12 +1262,12 @@ __global__ void __launch_bounds__(256) bwd_hot_final_kernel(EmbMeta m, float* __
     sq = wave_sum(sq);
     float* srow = state + tm.state_offset + row;
     const float snew = *srow + sq / (float)D;
-    const float stdv = sqrtf(snew) + eps;
+    const float step = rw_step(snew, lr, eps);
     float* wrow = weights + tm.weight_offset + row * D;
 #pragma unroll
     for (int k = 0; k < HOT_DMAX / 64; ++k) {
       const int c = lane + 64 * k;
-      if (c < D) wrow[c] = wrow[c] + (-lr * tot[k]) / stdv;
+      if (c < D) wrow[c] = fmaf(tot[k], step, wrow[c]);
     }
     if (lane == 0) *srow = snew;
   }

@@ -503,12 +503,30 @@ __device__ __forceinline__ void mma_w0_tr(f32x4 (&acc)[2][2], const __bf16* As, 
   }
 }
 
-__device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int64_t gm, int64_t B) {
-  if (gm + 4 <= B) {
+// lane value from another lane of its 16-lane row by DPP (no LDS round trip: ds_bpermute is one)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// sum over each 16-lane row, every lane of the row receives it: quad_perm [1,0,3,2], quad_perm
+// [2,3,0,1], row_half_mirror, row_mirror (each step adds the mirrored partner's partial sum, so
+// partners compute identical values)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;
+}
+
+// 4 consecutive rows r0.. of one strip feature (tile-local row r0, nval valid rows in the tile)
+__device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int r0, int nval) {
+  if (r0 + 4 <= nval) {
     *reinterpret_cast<bf16x4*>(dst) = pk;
   } else {
     for (int rr = 0; rr < 4; ++rr)
-      if (gm + rr < B) dst[rr] = pk[rr];
+      if (r0 + rr < nval) dst[rr] = pk[rr];
   }
 }
 
@@ -544,25 +562,31 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     T1_WSTAMP(0);
     // ---- the dedup wave (UPD): for each of the 2 x TR lookups, is its row looked up once in this
     // step? (claim >= 0 and slot count 1 in the batch's completed table) -> row and state to LDS
+    // All of this wave's dependent global round trips (id -> claim / state -> slot word; the next
+    // batch's id) finish before barrier 1: the compute waves spend ~5 us gathering there, while a
+    // round trip after barrier 1 made this wave the last arrival at barrier 2 (by 0.8-1.2 us).
     const int tq = lane / TR, row = lane % TR;
     const int64_t gm = (int64_t)blockIdx.x * TR + row;
+    const bool pref = a.pcol[0] != nullptr;
     int64_t r = -1;
     int32_t cl = -1;
     float st = 0.f;
+    int64_t idn = 0;
     if (gm < a.B) {
       const int64_t id = load_id(tq ? a.gcol[1] : a.gcol[0], a.gid_dtype, gm);
+      if (pref) idn = load_id(tq ? a.pcol[1] : a.pcol[0], a.gid_dtype, gm);
       if (id != 0) {
         r = py_mod64(id, tq ? a.gmod[1] : a.gmod[0]);
         cl = a.dd.claim[tq * a.B + gm];
         st = (tq ? a.us[1] : a.us[0])[r];  // speculative: used only for a single-lookup row
       }
     }
-    T1_WSTAMP(1);
-    __syncthreads();
     const uint64_t word = cl >= 0 ? a.dd.slots[cl].word : DD_EMPTY;
     const bool single = cl >= 0 && (word & DD_CNT_MASK) == 1;
     urow[tq][row] = single ? r : -1;
     ustate[tq][row] = st;
+    T1_WSTAMP(1);
+    __syncthreads();
     // the next batch's rows of this tile, after the compute waves' gather has landed (barrier 1):
     // 64-B segment k = j * 64 + lane of row k / SEG, all loads in flight across the remaining
     // barriers (a barrier waits only on LDS counters), consumed once after the last one
@@ -570,11 +594,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     constexpr int NPF = 2 * TR * SEG / 64;
     uint32_t pv[NPF];
     uint32_t pf = 0;
-    const bool pref = a.pcol[0] != nullptr;
     auto issue_prefetch = [&]() {
       const float* base = nullptr;
       if (gm < a.B) {
-        const int64_t idn = load_id(tq ? a.pcol[1] : a.pcol[0], a.gid_dtype, gm);
         if (idn != 0) {
           const int64_t rn = py_mod64(idn, tq ? a.gmod[1] : a.gmod[0]);
           base = (tq ? a.gtab[1] : a.gtab[0]) + rn * IN_;
@@ -648,6 +670,16 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   const int r16 = lane & 15, q4 = lane >> 4;
   const int64_t B = a.B;
   const int64_t m0 = (int64_t)blockIdx.x * TR;
+  const int nval = (int)min((int64_t)TR, B - m0);  // valid rows of this tile (32-bit row tests)
+  // this tile's run of each T1 -> T2 strip (tile-major, strip_at): wave-uniform bases, so a
+  // store's address is base + (feature * TR + row) in 32 bits
+  const int64_t tile_el = (int64_t)blockIdx.x * TR;
+  __bf16* const xt_tile = a.xt + (int64_t)t * a.in_max * a.Bp + tile_el * a.in_max;
+  __bf16* const act_tile = a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + tile_el * MAXW;
+  __bf16* const dz0_tile = a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + tile_el * MAXW;
+  __bf16* const dz1_tile = a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + tile_el * MAXW;
+  float* const db0 = a.dbpart + (((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW;
+  float* const db1 = a.dbpart + (((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW;
   const int in = IN_ ? IN_ : a.s.in_dim[t];
   const int W0 = W0_ ? W0_ : a.s.width[0];
   const int W1 = W1_ ? W1_ : a.s.width[1];
@@ -727,6 +759,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   // the label of the row this thread scores in phase 3 (loaded now: no global load after the CAS)
   const int64_t lrow = m0 + (threadIdx.x >> 4);
   const float ylab = lrow < B ? lbl(a.labels, a.label_dtype, lrow) : 0.f;
+  const float gscale = a.grad_scale / (float)B;
 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -745,6 +778,11 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         *reinterpret_cast<f32x4*>(a.pooled_out + gm * a.ldp + incol + c4) = xv[i];
     }
   }
+  // vmcnt(0) while only this wave's loads are outstanding (X, weight fragments, biases, label; the
+  // fragments and biases come from L2 right behind X). Without it the compiler's merge of the
+  // label-dtype branches leaves the biases "pending", and their first use in phase 1 becomes a
+  // vmcnt(0) issued AFTER phase 1's strip stores: a wait for HBM store acknowledgements mid-chain.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   T1_WSTAMP(1);
   __syncthreads();
   T1_STAMP(1);
@@ -753,13 +791,12 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     const int k = e / (TR / 8), rb = (e % (TR / 8)) * 8;
     bf16x8 v;
     for (int j = 0; j < 8; ++j) v[j] = xs[t][(rb + j) * LSTR + k];
-    const int64_t gm = m0 + rb;
-    __bf16* dst = a.xt + (int64_t)t * a.in_max * a.Bp + strip_at(k, gm, a.in_max);
-    if (gm + 8 <= B) {
+    __bf16* dst = xt_tile + k * TR + rb;
+    if (rb + 8 <= nval) {
       *reinterpret_cast<bf16x8*>(dst) = v;
     } else {
       for (int j = 0; j < 8; ++j)
-        if (gm + j < B) dst[j] = v[j];
+        if (rb + j < nval) dst[j] = v[j];
     }
   }
   f32x4 acc[2][2];
@@ -780,8 +817,8 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         pk[rr] = (__bf16)v;
         hs[t][row * LSTR + col] = pk[rr];
       }
-      const int64_t gm = m0 + i * 16 + q4 * 4;
-      if (!(a.dbg & 1)) store_t4(a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + strip_at(col, gm, MAXW), pk, gm, B);
+      const int r0 = i * 16 + q4 * 4;
+      if (!(a.dbg & 1)) store_t4(act_tile + col * TR + r0, pk, r0, nval);
     }
   }
   T1_WSTAMP(2);
@@ -806,18 +843,31 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   T1_STAMP(3);
   // ---- 3. logits, BCE, dlogit: 16 threads per row
   {
+    // 16 lanes per row, 4 consecutive columns per lane (one 16-B LDS read per tower), DPP sum
+    // over the row's lanes; BCE from one exp, one log and one reciprocal (hardware
+    // transcendentals, ~1 ulp) — the phase is one dependent chain per wave, so its length is its
+    // instruction count
     const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
     float d = 0.f;
-    for (int c = sub; c < W1; c += 16) d += outf[0][row * FSTR + c] * outf[1][row * FSTR + c];
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) d += __shfl_xor(d, o, 64);
+    for (int c = sub * 4; c < W1; c += 64) {
+      const f32x4 u = *reinterpret_cast<const f32x4*>(&outf[0][row * FSTR + c]);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(&outf[1][row * FSTR + c]);
+      d = fmaf(u[0], v[0], d);
+      d = fmaf(u[1], v[1], d);
+      d = fmaf(u[2], v[2], d);
+      d = fmaf(u[3], v[3], d);
+    }
+    d = row16_sum(d);
     const int64_t gm = m0 + row;
     float lo = 0.f, dl = 0.f;
     if (gm < B) {
       const float x = d, y = ylab;
-      const float lsig = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+      const float e = __expf(-fabsf(x));  // exp(-|x|) in (0, 1]
+      const float l1p = e < 1e-4f ? e * (1.f - 0.5f * e) : __logf(1.f + e);
+      const float lsig = fminf(x, 0.f) - l1p;  // log(sigmoid(x))
       lo = (1.f - y) * x - lsig;
-      dl = (1.f / (1.f + expf(-x)) - y) / (float)B * a.grad_scale;
+      const float rc = __builtin_amdgcn_rcpf(1.f + e);
+      dl = ((x >= 0.f ? rc : e * rc) - y) * gscale;  // (sigmoid(x) - y) * grad_scale / B
       if (sub == 0) a.logits[gm] = x;
     }
     if (sub == 0) {
@@ -836,22 +886,21 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     for (int j = 0; j < 8; ++j) {
       const int row = rb + j;
       float z = outf[t][row * FSTR + c] > 0.f ? dlog[row] * outf[1 - t][row * FSTR + c] : 0.f;
-      if (m0 + row >= B) z = 0.f;
+      if (row >= nval) z = 0.f;
       s += z;
       v[j] = (__bf16)z;
       dzs[t][row * LSTR + c] = v[j];
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    if ((tt & 3) == 0) a.dbpart[(((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW + c] = s;
-    const int64_t gm = m0 + rb;
-    __bf16* dst = a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + strip_at(c, gm, MAXW);
+    s += dpp_f<0xB1>(s);  // the 4 lanes of a column are one quad: xor 1, then xor 2
+    s += dpp_f<0x4E>(s);
+    if ((tt & 3) == 0) db1[c] = s;
+    __bf16* dst = dz1_tile + c * TR + rb;
     if (a.dbg & 1) {
-    } else if (gm + 8 <= B) {
+    } else if (rb + 8 <= nval) {
       *reinterpret_cast<bf16x8*>(dst) = v;
     } else {
       for (int j = 0; j < 8; ++j)
-        if (gm + j < B) dst[j] = v[j];
+        if (rb + j < nval) dst[j] = v[j];
     }
   }
   T1_WSTAMP(5);
@@ -871,17 +920,17 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       for (int rr = 0; rr < 4; ++rr) {
         const int row = i * 16 + q4 * 4 + rr;
         float z = (float)hs[t][row * LSTR + col] > 0.f ? acc[i][j][rr] : 0.f;
-        if (m0 + row >= B) z = 0.f;
+        if (row >= nval) z = 0.f;
         s += z;
         pk[rr] = (__bf16)z;
         xs[t][row * LSTR + col] = pk[rr];
       }
-      const int64_t gm = m0 + i * 16 + q4 * 4;
-      if (!(a.dbg & 1)) store_t4(a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + strip_at(col, gm, MAXW), pk, gm, B);
+      const int r0 = i * 16 + q4 * 4;
+      if (!(a.dbg & 1)) store_t4(dz0_tile + col * TR + r0, pk, r0, nval);
     }
     s += __shfl_xor(s, 16, 64);
     s += __shfl_xor(s, 32, 64);
-    if (q4 == 0) a.dbpart[(((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW + col] = s;
+    if (q4 == 0) db0[col] = s;
   }
   T1_WSTAMP(6);
   __syncthreads();
@@ -933,10 +982,10 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
           if (o < lpr) sq += __shfl_xor(sq, o, 64);
         if (ur >= 0) {
           const float snew = rw_state(ustate[t][row], sq, in);
-          const float stdv = rw_stdv(snew, a.ueps);
+          const float step = rw_step(snew, a.ulr, a.ueps);
           const f32x4 x = xv[i];
           if (!(a.dbg & 128)) {
-            *reinterpret_cast<f32x4*>(a.uw[t] + ur * in + c4) = rw_apply(x, g, a.ulr, stdv);
+            *reinterpret_cast<f32x4*>(a.uw[t] + ur * in + c4) = rw_apply(x, g, step);
             if (c4 == 0) a.us[t][ur] = snew;
           }
           if (!a.pooled_out) dst = nullptr;  // dX is needed only for inspection (pooled_out mode)

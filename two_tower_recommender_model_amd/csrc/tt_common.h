@@ -59,6 +59,8 @@ __device__ __forceinline__ int64_t load_id(const void* values, int id_dtype, int
 // Python's a % n (result takes the divisor's sign): transform_to_torchrec_batch's `id % N`,
 // 03_model_training.py:361, on tensors of either sign
 __device__ __forceinline__ int64_t py_mod64(int64_t a, int64_t n) {
+  // ids already in [0, n) (what a well-formed dataset holds): no division at all
+  if ((uint64_t)a < (uint64_t)n) return a;
   // 32-bit fast path (ids and table sizes below 2^32: the usual case): a 64-bit remainder is a
   // long emulated sequence on CDNA, a 32-bit one a short float-reciprocal sequence
   if ((uint64_t)a <= 0xffffffffull && (uint64_t)n <= 0xffffffffull && n > 0) return (int64_t)((uint32_t)a % (uint32_t)n);
@@ -74,13 +76,15 @@ __device__ __forceinline__ int64_t udiv64(int64_t a, int64_t b) {
 
 // Row-wise Adagrad arithmetic (torchrec RowWiseAdagrad, 03_model_training.py:791-795) of one
 // 4-wide chunk of a row, shared by the update paths so that each computes bitwise-identical
-// results for the same gradient row: s += mean_d(G^2); w -= lr * G / (sqrt(s) + eps)
+// results for the same gradient row: s += mean_d(G^2); w -= lr * G / (sqrt(s) + eps).
+// rw_step is the row's factor -lr / (sqrt(s) + eps), divided once per row; rw_apply is one fma
+// per element (a precise division per element was ~10 VALU instructions each)
 __device__ __forceinline__ float rw_sq4(const f32x4v& g) { return g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3]; }
 __device__ __forceinline__ float rw_state(float s_old, float sq, int D) { return s_old + sq / (float)D; }
-__device__ __forceinline__ float rw_stdv(float snew, float eps) { return sqrtf(snew) + eps; }
-__device__ __forceinline__ f32x4v rw_apply(f32x4v w, const f32x4v& g, float lr, float stdv) {
+__device__ __forceinline__ float rw_step(float snew, float lr, float eps) { return -lr / (sqrtf(snew) + eps); }
+__device__ __forceinline__ f32x4v rw_apply(f32x4v w, const f32x4v& g, float step) {
 #pragma unroll
-  for (int v = 0; v < 4; ++v) w[v] = w[v] + (-lr * g[v]) / stdv;
+  for (int v = 0; v < 4; ++v) w[v] = fmaf(g[v], step, w[v]);
   return w;
 }
 
