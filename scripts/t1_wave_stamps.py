@@ -29,13 +29,14 @@ for it in range(4):
     if it < 3:
         continue
     w = st.towers.ws[off:off + dbg_bytes].view(torch.int64)[8192:8192 + nwg * 16 * 9].view(nwg, 16, 9).cpu().double()
-    w = w[:, :11, :]  # points 0..8, then 9 = past barrier 7, 10 = first dX / row store issued
+    w = w[:, :15, :]  # points 0..8, 9 = past barrier 7, 10 = first dX / row store issued,
+    # 11 = phase 1 after the X^T strip, 12 = after layer 0's MFMA, 13 = after the W0 image, 14 = phase 5 after its MFMA
     t0 = w[:, 0, :].min(dim=1, keepdim=True).values  # workgroup start
     rel = (w - t0.unsqueeze(1)) / 100.0  # us, [wg, point, wave]
     print(f"it{it}: arrival (us from the workgroup's first wave start), median over workgroups")
     print("  point  " + " ".join(f"  w{j}" for j in range(9)) + "   last  phase")
     prev = torch.zeros(nwg, dtype=torch.float64)
-    for k in list(range(8)) + [9, 10, 8]:
+    for k in [0, 1, 11, 12, 13, 2, 3, 4, 5, 14, 6, 7, 9, 10, 8]:
         med = rel[:, k, :].median(dim=0).values
         last = rel[:, k, :].max(dim=1).values
         ph = float((last - prev).median())

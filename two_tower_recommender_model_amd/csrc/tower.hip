@@ -799,10 +799,13 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         if (rb + j < nval) dst[j] = v[j];
     }
   }
+  T1_WSTAMP(11);
   f32x4 acc[2][2];
   // ---- 1. layer 0: h = relu(X W0^T + b0)
   mma_frags(acc, xs[t], f0, in, W0, w4);
+  T1_WSTAMP(12);
   w0_image_store(w0img[t], f0, in, W0, w4);  // read back transposed by the dX product (phase 6)
+  T1_WSTAMP(13);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     if (w4 + 4 * j >= W0 / 16) continue;
@@ -908,6 +911,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   T1_STAMP(5);
   // ---- 5. dZ0 = (dZ1 W1) * (h > 0)  -> xs (X is no longer needed)
   mma_frags(acc, dzs[t], g1, W1, W0, w4);
+  T1_WSTAMP(14);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     if (w4 + 4 * j >= W0 / 16) continue;
