@@ -357,10 +357,16 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   const int64_t hw = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
   const int64_t nhw = a.slot_hw;
   int hq[DD_SPH];
+  uint64_t lk[DD_SPH];
+  // spec (every mode but skip_single): the claiming lookup's own key is its slot's key, so its row,
+  // row state and own gradient row are loaded beside the slot (from lkey[i]) instead of after it —
+  // the update of a row looked up once (the common case) waits two dependent round trips, not three
+  const bool spec = !a.skip_single;
 #pragma unroll
   for (int q = 0; q < DD_SPH; ++q) {
     const int64_t i = hw + q * nhw;
     hq[q] = i < a.n ? ws.claim[i] : -1;
+    lk[q] = spec && i < a.n ? ws.lkey[i] : DD_EMPTY;
   }
   DSlot* sp[DD_SPH];
   int dw[DD_SPH];
@@ -377,8 +383,24 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   int c[DD_SPH], cmax[DD_SPH], mine[DD_SPH], D[DD_SPH];
   float* wrow[DD_SPH];
   float* srow[DD_SPH];
-  f32x4v wv[DD_SPH], g[DD_SPH];
+  f32x4v wv[DD_SPH], g[DD_SPH], gown[DD_SPH];
   float s_old[DD_SPH];
+  if (spec) {
+#pragma unroll
+    for (int q = 0; q < DD_SPH; ++q) {
+      const bool cl = hq[q] >= 0;
+      const int t = cl ? (int)(lk[q] >> DD_TABLE_SHIFT) : 0;
+      const int64_t r = cl ? (int64_t)(lk[q] & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
+      D[q] = lm->dim[t];
+      col_ok[q] = cl && hl * 4 < D[q];
+      wrow[q] = weights + lm->woff[t] + r * D[q];
+      srow[q] = state + lm->soff[t] + r;
+      wv[q] = col_ok[q] ? *reinterpret_cast<const f32x4v*>(wrow[q] + hl * 4) : (f32x4v)(0.f);
+      s_old[q] = cl ? *srow[q] : 0.f;
+      const int64_t i = hw + q * nhw;
+      gown[q] = col_ok[q] ? *reinterpret_cast<const f32x4v*>(gm.row((int)i) + hl * 4) : (f32x4v)(0.f);
+    }
+  }
 #pragma unroll
   for (int q = 0; q < DD_SPH; ++q) {
     const uint64_t word = ((uint64_t)(uint32_t)__shfl(dw[q], hb + 1, 64) << 32) | (uint32_t)__shfl(dw[q], hb, 64);
@@ -389,14 +411,18 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     active[q] = word != DD_EMPTY && cnt <= DD_INL;
     // skip_single: a row looked up once was updated in place by T1; its slot is only freed here
     const bool upd = active[q] && !(a.skip_single && cnt == 1);
-    const int t = upd ? (int)(key >> DD_TABLE_SHIFT) : 0;
-    const int64_t r = upd ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
-    D[q] = lm->dim[t];
-    col_ok[q] = upd && hl * 4 < D[q];
-    wrow[q] = weights + lm->woff[t] + r * D[q];
-    srow[q] = state + lm->soff[t] + r;
-    wv[q] = col_ok[q] ? *reinterpret_cast<const f32x4v*>(wrow[q] + hl * 4) : (f32x4v)(0.f);
-    s_old[q] = upd ? *srow[q] : 0.f;
+    if (!spec) {
+      const int t = upd ? (int)(key >> DD_TABLE_SHIFT) : 0;
+      const int64_t r = upd ? (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1)) : 0;
+      D[q] = lm->dim[t];
+      col_ok[q] = upd && hl * 4 < D[q];
+      wrow[q] = weights + lm->woff[t] + r * D[q];
+      srow[q] = state + lm->soff[t] + r;
+      wv[q] = col_ok[q] ? *reinterpret_cast<const f32x4v*>(wrow[q] + hl * 4) : (f32x4v)(0.f);
+      s_old[q] = upd ? *srow[q] : 0.f;
+    } else {
+      col_ok[q] = col_ok[q] && upd;  // the claimer's key is the slot's: the loads above are its row's
+    }
     c[q] = upd ? cnt : 0;
     cmax[q] = max(c[q], __shfl_xor(c[q], 32, 64));
     mine[q] = hl < c[q] ? item : 0x7fffffff;
@@ -406,11 +432,12 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
 #pragma unroll
   for (int q = 0; q < DD_SPH; ++q) single = single && cmax[q] <= 1;
   if (single) {
-    // the common case (uniform ids): one gradient row per slot, all loads in flight together
+    // the common case (uniform ids): one gradient row per slot, all loads in flight together (spec:
+    // the claimer's own row, already loaded — the slot's one lookup IS the claimer)
 #pragma unroll
     for (int q = 0; q < DD_SPH; ++q) {
       const int b0 = __shfl(mine[q], hb, 64);  // the slot's one lookup, held by lane 0 of the half
-      if (col_ok[q] && c[q] == 1) g[q] += *reinterpret_cast<const f32x4v*>(gm.row(b0) + hl * 4);
+      if (col_ok[q] && c[q] == 1) g[q] += spec ? gown[q] : *reinterpret_cast<const f32x4v*>(gm.row(b0) + hl * 4);
     }
   } else {
 #pragma unroll

@@ -159,7 +159,7 @@ __device__ __forceinline__ void shard_gather_block(const GatherSegArgs& a, int b
   const int64_t n = (int64_t)a.W * a.S;
   const int64_t i = ((int64_t)blk * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   if (i >= n) return;
-  const int64_t s = i / a.S, j = i - s * a.S;
+  const int64_t s = (int64_t)((uint32_t)i / (uint32_t)a.S), j = i - s * a.S;  // W * S < 2^31 (host-checked)
   // feature of slot j and its segment start: a loop over the (uniform) feature list with scalar
   // kernarg loads (a per-lane index into the kernarg arrays is a dependent vector load)
   int f = 0;
@@ -172,10 +172,13 @@ __device__ __forceinline__ void shard_gather_block(const GatherSegArgs& a, int b
   const int64_t k = j - so;
   const int64_t* blkp = a.recv + s * a.blk64 + a.cnt64;
   const int64_t cnt = blkp[f];
+  // the slot's key is loaded beside its segment's count (slot j lies inside the block: a stale
+  // value past the count is never used), not after it: one dependent round trip fewer
+  const uint64_t kraw = (uint64_t)blkp[a.F + j];
   uint64_t key = DD_EMPTY;
   const float* src = nullptr;
   if (k < cnt) {
-    key = (uint64_t)blkp[a.F + j];
+    key = kraw;
     const int t = (int)(key >> DD_TABLE_SHIFT);
     const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
     int64_t woff = 0, nrows = 0;

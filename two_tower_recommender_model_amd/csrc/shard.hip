@@ -111,7 +111,8 @@ int gather_segs_args(const float* weights, const tt_table_meta_t* tables, int T,
                      int64_t block_i64, int64_t counts_i64, const int64_t* seg_off, int64_t slots, void* rows_out,
                      int64_t out_stride, int32_t* bad, void* dedup_ws, size_t dedup_ws_bytes,
                      int64_t dedup_max_lookups, GatherSegArgs& a) {
-  if (T < 1 || T > TT_MAX_TABLES || F < 1 || F > TT_MAX_FEATURES || F > T || W < 1 || slots < 0)
+  if (T < 1 || T > TT_MAX_TABLES || F < 1 || F > TT_MAX_FEATURES || F > T || W < 1 || slots < 0 ||
+      (int64_t)W * slots >= (1ll << 31))
     return fail(TT_EINVAL, "shard_gather_segs: bad sizes");
   if (!weights || !tables || !recv || !rows_out || !bad || !seg_off)
     return fail(TT_EINVAL, "shard_gather_segs: null pointer");
