@@ -37,3 +37,51 @@ def test_auroc_accumulates_batches_and_alias():
 
     assert hasattr(torchmetrics, "AUROC")
     assert torch.isnan(binary_auroc(torch.rand(4), torch.ones(4)))
+
+
+def _auroc_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    try:
+        m = AUROC(task="binary").to("cpu")
+        rng = np.random.default_rng(rank)
+        for n in ([300, 41] if rank == 1 else ([517] if rank == 0 else [])):  # uneven; rank 2 holds nothing
+            y = rng.integers(0, 2, n)
+            s = np.round(rng.random(n), 2).astype(np.float32)  # ties, within and across ranks
+            m(torch.from_numpy(s), torch.from_numpy(y))
+        q.put((rank, float(m.compute())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_auroc_compute_syncs_all_ranks(world):
+    """compute() in a process group: the AUROC of every rank's predictions (torchmetrics'
+    sync_on_compute), the same value on every rank — the reference's evaluate() at W = 8."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_auroc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ys, ss = [], []
+    for rank in range(world):
+        rng = np.random.default_rng(rank)
+        for n in ([300, 41] if rank == 1 else ([517] if rank == 0 else [])):
+            ys.append(rng.integers(0, 2, n))
+            ss.append(np.round(rng.random(n), 2).astype(np.float32))
+    want = roc_auc_score(np.concatenate(ys), np.concatenate(ss))
+    for rank in range(world):
+        assert got[rank] == pytest.approx(want, abs=1e-6)

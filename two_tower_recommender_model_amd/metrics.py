@@ -6,6 +6,11 @@ reference's evaluate() runs unchanged.
 AUROC = P(score+ > score-) + 0.5 P(score+ == score-): the trapezoidal area under the ROC curve
 whose thresholds are the distinct scores (torchmetrics' exact binary AUROC, no binning). Computed
 from one sort: the Mann-Whitney U statistic with tied scores given their average rank.
+
+In a process group of more than one rank, compute() is over the predictions of EVERY rank (as
+torchmetrics' Metric.compute, sync_on_compute=True by default, gathers the metric states of all
+processes): the reference's evaluate() at W = 8 prints the AUROC of the whole evaluation set, while
+its average loss stays per-rank (03_model_training.py:549-559).
 """
 from __future__ import annotations
 
@@ -14,6 +19,23 @@ import types
 from typing import List, Optional
 
 import torch
+import torch.distributed as dist
+
+
+def _gather_cat(x: torch.Tensor) -> torch.Tensor:
+    """Concatenation (rank order) of every rank's 1-D ``x`` of any length (torchmetrics'
+    gather_all_tensors for uneven sizes: lengths first, then padded tensors)."""
+    world = dist.get_world_size()
+    n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    sizes = [int(v) for v in ns]
+    m = max(sizes)
+    pad = torch.zeros(m, dtype=x.dtype, device=x.device)
+    pad[:x.numel()] = x
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    return torch.cat([o[:k] for o, k in zip(outs, sizes)])
 
 
 def binary_auroc(preds: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
@@ -65,9 +87,15 @@ class AUROC:
         return binary_auroc(preds, target)
 
     def compute(self) -> torch.Tensor:
-        if not self._preds:
+        dev = self.device
+        preds = torch.cat(self._preds) if self._preds else torch.zeros(0, dtype=torch.float32, device=dev)
+        target = torch.cat(self._target) if self._target else torch.zeros(0, dtype=torch.float32, device=dev)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            preds = _gather_cat(preds.to(torch.float64))
+            target = _gather_cat(target.to(torch.float64))
+        if preds.numel() == 0:
             return torch.tensor(float("nan"), dtype=torch.float64)
-        return binary_auroc(torch.cat(self._preds), torch.cat(self._target)).to(torch.float32)
+        return binary_auroc(preds, target).to(torch.float32)
 
     def reset(self) -> None:
         self._preds.clear()
