@@ -38,8 +38,11 @@ from .types import ParameterSharding, ShardingType
 class EmbeddingBagCollectionSharder:
     """torchrec.distributed.embeddingbag.EmbeddingBagCollectionSharder (get_default_sharders())."""
 
-    def __init__(self, fused_params: Optional[dict] = None, qcomm_codecs_registry=None):
+    def __init__(self, fused_params: Optional[dict] = None, qcomm_codecs_registry=None, lookup_backend=None):
+        """lookup_backend: the local lookup of the sharded modules this sharder builds (None = the
+        HIP kernels, ops.HIP_BACKEND; the multi-process CPU tests pass their oracle-backed one)."""
         self.fused_params = fused_params or {}
+        self.lookup_backend = lookup_backend
 
     def sharding_types(self, compute_device_type: str) -> List[str]:
         return [ShardingType.TABLE_WISE.value, ShardingType.ROW_WISE.value]

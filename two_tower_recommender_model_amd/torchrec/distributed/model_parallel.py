@@ -58,7 +58,9 @@ class DistributedModelParallel(nn.Module):
             if self._pg is None:
                 ebc._materialize(self.device)
             else:
-                sharded = ShardedEmbeddingBagCollection(ebc, mplan, self._pg, self.device)
+                backend = next((getattr(sh, "lookup_backend", None) for sh in self._sharders
+                                if getattr(sh, "lookup_backend", None) is not None), None)
+                sharded = ShardedEmbeddingBagCollection(ebc, mplan, self._pg, self.device, backend=backend)
                 if path == "":
                     module = sharded
                 else:
