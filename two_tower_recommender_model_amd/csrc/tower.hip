@@ -1412,11 +1412,22 @@ __global__ void __launch_bounds__(256) tower_wgrad_route_kernel(WgradArgs a, con
 // ids of batch i+1): T2 of batch i (weight-gradient tiles, bias sums, loss) beside the owner's
 // row-wise Adagrad of batch i's rows and the count pass of batch i+2's route — all three read only
 // what T1 and the exchange wrote, so the tower weight gradients overlap the embedding update.
+// n_dd > 0: the owner's update workgroups come FIRST in the grid (they carry the launch's longest
+// chain, claim -> slot -> rows -> stores; dispatched behind the T2 tiles, the last of them started
+// ~4.5 us late), then the T2 tiles, then the route count
 __global__ void __launch_bounds__(256) tower_wgrad_route_rowwise_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
                                                                         RouteArgs r, DdUpdateArgs d, int n_t2,
-                                                                        int n_cnt) {
+                                                                        int n_cnt, int n_dd) {
   __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
-  const int b = (int)blockIdx.x;
+  int b = (int)blockIdx.x;
+  if (n_dd > 0) {
+    if (b < n_dd) {
+      dd_update_block(d, b, smem);
+      return;
+    }
+    b -= n_dd;
+    if (b >= n_t2 + n_cnt) return;
+  }
   if (b < n_t2) {
     wgrad_block(a, tiles, b, smem);
   } else if (b < n_t2 + n_cnt) {
@@ -2422,9 +2433,10 @@ int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, in
   if (rc) return rc;
   const int64_t n_cnt = (int64_t)r.nblk * F;
   if (wgs + n_cnt + dd_grid > INT32_MAX) return fail(TT_EINVAL, "tower_wgrad_route_rowwise: grid too large");
+  static const bool dd_first = !getenv("TT_U_DD_FIRST") || atoi(getenv("TT_U_DD_FIRST")) != 0;  // A/B switch
   tower_wgrad_route_rowwise_kernel<<<dim3((unsigned)(wgs + n_cnt + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
       a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), r, d, (int)wgs,
-      (int)n_cnt);
+      (int)n_cnt, dd_first ? (int)dd_grid : 0);
   return check_launch("tower_wgrad_route_count_rowwise_adagrad");
 }
 
