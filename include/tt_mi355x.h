@@ -285,6 +285,19 @@ int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void
                             const void* labels, int label_dtype, float grad_scale, float* logits,
                             const int32_t* dedup_tables, void* dedup_ws, size_t dedup_ws_bytes,
                             int64_t dedup_max_lookups, void* workspace, size_t ws_bytes, void* stream);
+/* T1 with the multi-hot EBC forward fused in (KeyedJaggedTensor input, one key per tower, L = 2,
+ * towers [128, 64], inputs 64 or 128 wide): tower t's input row m is the SUM pool of bag (t, m),
+ * i.e. rows values[offsets[t*B + m] .. offsets[t*B + m + 1]) of table_rows[t] (num_rows[t] rows;
+ * ids are taken as the EBC takes them, an id >= num_rows[t] reads row 0) — bit-identical to
+ * tt_pooled_fwd (SUM) followed by tt_tower_fwd_bwd, without materialising the pooled rows unless
+ * pooled_out (nullable) is given. Replaces self.ebc(kjt) + the towers' forward/backward of
+ * 03_model_training.py:417-455 for the config-5 multi-hot shape. offsets: complete, key-major
+ * [2B + 1] int32. dX goes to gpooled's columns in_col[t] (ld = ldp) for tt_bwd_rowwise_adagrad. */
+int tt_tower_fwd_bwd_kjt(const tt_tower_shape_t* shape, int64_t B, const void* values, int id_dtype,
+                         const int32_t* offsets, const int64_t* num_rows, const float* const* table_rows,
+                         float* pooled_out, int64_t ldp, float* gpooled, const float* params,
+                         const void* labels, int label_dtype, float grad_scale, float* logits,
+                         void* workspace, size_t ws_bytes, void* stream);
 /* ---- the pipelined fused step: dedup one step ahead, single-lookup rows updated inside T1 ----------
  * Step i: T1 (gather + towers + in-place row-wise Adagrad of batch i's rows looked up ONCE, from
  * batch i's dedup table completed by step i-1) -> T2 (weight gradients + the insert of batch i+1

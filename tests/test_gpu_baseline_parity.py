@@ -195,8 +195,8 @@ def test_production_multihot_step_config5(device):
     batches = _kjt_batches(N, B, 39, device, seed=4)
     cap = max(v.numel() for v, _, _ in batches)
     st = FusedTwoTowerStep(N, [D, D], [0], [1], LAYERS, B, device, lr_emb=LR, lr_dense=LR, id_dtype=torch.int64,
-                           seed=0, max_lookups=cap)
-    assert st.towers is not None and st.kjt_input
+                           seed=0, max_lookups=cap, materialize_pooled=True)
+    assert st.towers is not None and st.kjt_input and st.gather_kjt  # sum pool inside T1
     st.capture_pool_kjt(batches)
     st.pool_graphs[0].replay()
     torch.cuda.synchronize()

@@ -75,8 +75,8 @@ def test_multihot_step_bf16_graph(device):
 
     def run():
         st = FusedTwoTowerStep(N, [D, D], [0], [1], layers, B, device, lr_emb=0.02, lr_dense=0.01, seed=5,
-                               max_lookups=cap)
-        assert st.towers is not None  # the fused bf16 tower kernels
+                               max_lookups=cap, materialize_pooled=True)
+        assert st.towers is not None and st.gather_kjt  # the fused bf16 tower kernels, sum pool inside T1
         s0 = _state(st, N, D)
         st.capture_pool_kjt(batches)
         st.pool_graphs[0].replay()
@@ -174,3 +174,37 @@ def test_multihot_pipelined_grouping_bitwise(device, hot):
     torch.cuda.synchronize()
     assert torch.equal(ref_st.tables.weights, pipe.tables.weights) and torch.equal(ref_st.params, pipe.params)
     assert torch.equal(ref_st.tables.state, pipe.tables.state)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_multihot_pool_inside_t1_bitwise(device, D):
+    """tt_tower_fwd_bwd_kjt (the sum pool of every bag inside T1) against tt_pooled_fwd followed by
+    the unfused T1 on the same KJT: pooled rows, logits, dX, loss, and after 3 eager steps the
+    tables, row-wise state and tower parameters, all bitwise (the rows are added in bag order from
+    zero in both). Bags of 0..40 ids (empty bags, bags longer than one 32-id chunk), B not a multiple
+    of the 32-row tile."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    rng = np.random.default_rng(31 + D)
+    B, N = 200, [3000, 5000]
+    batches = [_kjt(rng, B, N, 40) for _ in range(3)]
+    cap = max(v.size for v, _ in batches)
+    g = torch.Generator().manual_seed(4)
+    labels = [torch.randint(0, 2, (B,), generator=g).to(torch.int32).to(device) for _ in batches]
+    outs = []
+    for fuse in (False, True):
+        st = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, lr_emb=0.02, lr_dense=0.01, seed=6,
+                               max_lookups=cap, fuse_gather=fuse, materialize_pooled=True)
+        assert st.gather_kjt == fuse and st.towers is not None
+        per = []
+        for (v, o), lab in zip(batches, labels):
+            st.load_kjt(torch.from_numpy(v).to(device), torch.from_numpy(o).to(device), lab)
+            st.step()
+            torch.cuda.synchronize()
+            per.append([x.cpu().clone() for x in (st.pooled, st.logits, st.gpooled, st.loss)])
+        outs.append((per, st.tables.weights.cpu(), st.tables.state.cpu(), st.params.cpu()))
+    (p0, w0, s0, q0), (p1, w1, s1, q1) = outs
+    for a_, b_ in zip(p0, p1):
+        for x, y in zip(a_, b_):
+            assert torch.equal(x, y)
+    assert torch.equal(w0, w1) and torch.equal(s0, s1) and torch.equal(q0, q1)

@@ -139,6 +139,10 @@ SIGNATURES = {
         [_psh, _i64, _pvp, _int, _pi64, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _pi32, _vp, _sz, _i64,
          _vp, _sz, _vp],
     ),
+    "tt_tower_fwd_bwd_kjt": (
+        _int,
+        [_psh, _i64, _vp, _int, _vp, _pi64, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
+    ),
     "tt_tower_wgrad_rowwise_adagrad": (
         _int,
         [_psh, _i64, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64,
@@ -261,6 +265,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd",
     "tt_tower_wgrad",
     "tt_tower_fwd_bwd_gather",
+    "tt_tower_fwd_bwd_kjt",
     "tt_tower_update",
     "tt_pooled_fwd_cols",
     "tt_bwd_prepare_cols",

@@ -105,6 +105,11 @@ struct TowerArgs {
   // tile's next rows and their state (a prefetch into the memory-side cache and this XCD's TLB;
   // the values are discarded)
   const void* pcol[2];
+  // multi-hot EBC forward fused in (tt_tower_fwd_bwd_kjt, tower_l2_kernel<..., MH = true>): tower
+  // t's input row m is the SUM of rows values[moff[t][m] .. moff[t][m + 1]) of gtab[t] (gmod[t]
+  // rows: an id >= gmod[t] reads row 0, never out of bounds)
+  const void* mval;
+  const int32_t* moff[2];
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
 };
@@ -530,6 +535,77 @@ __device__ __forceinline__ void store_t4(__bf16* dst, const bf16x4& pk, int r0, 
   }
 }
 
+// Multi-hot EBC forward inside T1 (MH): thread tt of tower t's 256-thread group owns the float4
+// column c4 of rows (tt + 256 i) / LPR, i < NXV, as the single-hot gather does. The LPR lanes of a
+// row group walk the concatenation of their NXV bags (bag order kept inside each bag) in chunks of
+// LPR ids, one coalesced id read per chunk (the next chunk's ids in flight beside this chunk's
+// rows), ids broadcast by lane shuffles, R rows in flight per lane whatever the bag lengths. Each
+// bag's rows are added in bag order starting from zero: the fp32 sums are bit-identical to
+// tt_pooled_fwd (SUM) of the same bag.
+template <int IN_>
+__device__ __forceinline__ void mh_gather(const TowerArgs& a, int t, int tt, int64_t m0, int64_t B,
+                                          f32x4 (&xv)[4]) {
+  constexpr int LPR = IN_ / 4;   // lanes per row: 32 (D 128) or 16 (D 64)
+  constexpr int NXV = IN_ / 32;  // rows (bags) per thread: 4 or 2
+  constexpr int R = IN_ == 128 ? 16 : 8;  // rows in flight per lane (D 64: 8, no spills)
+  static_assert(LPR % R == 0, "a chunk is a whole number of rounds");
+  const int lane = threadIdx.x & 63;
+  const int lg = lane & (LPR - 1), gb = lane & ~(LPR - 1);
+  const float* tab = t ? a.gtab[1] : a.gtab[0];
+  const int32_t* off = t ? a.moff[1] : a.moff[0];
+  const uint64_t nrows = (uint64_t)(t ? a.gmod[1] : a.gmod[0]);
+  const float* colp = tab + lg * 4;
+  int s[NXV], p[NXV + 1];
+  p[0] = 0;
+#pragma unroll
+  for (int i = 0; i < NXV; ++i) {
+    const int64_t gm = m0 + (tt + 256 * i) / LPR;
+    s[i] = 0;
+    int n = 0;
+    if (gm < B) {
+      s[i] = off[gm];
+      n = off[gm + 1] - s[i];
+    }
+    p[i + 1] = p[i] + n;
+    xv[i] = (f32x4)(0.f);
+  }
+  const int total = p[NXV];
+  // combined position k (< total) -> element offset of its table row (an id >= rows reads row 0)
+  auto row_at = [&](int k) -> int64_t {
+    int si = s[0], pi = 0;
+#pragma unroll
+    for (int i = 1; i < NXV; ++i)
+      if (k >= p[i]) {
+        si = s[i];
+        pi = p[i];
+      }
+    const int64_t id = load_id(a.mval, a.gid_dtype, (int64_t)si + (k - pi));
+    return (uint64_t)id < nrows ? id * IN_ : 0;
+  };
+  int64_t nxt = lg < total ? row_at(lg) : 0;
+  for (int k0 = 0; __ballot(k0 < total) != 0; k0 += LPR) {
+    const int64_t cur = nxt;
+    if (k0 + LPR + lg < total) nxt = row_at(k0 + LPR + lg);
+#pragma unroll
+    for (int k = 0; k < LPR; k += R) {
+      if (__ballot(k0 + k < total) == 0) break;
+      f32x4 r[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int64_t o = __shfl((long long)cur, gb + k + u, 64);
+        r[u] = k0 + k + u < total ? *reinterpret_cast<const f32x4*>(colp + o) : (f32x4)(0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int kk = k0 + k + u;
+#pragma unroll
+        for (int i = 0; i < NXV; ++i)
+          if (kk >= p[i] && kk < p[i + 1]) xv[i] += r[u];
+      }
+    }
+  }
+}
+
 // IN_/W0_/W1_: compile-time tower input width and layer widths (0 = read from the shape at run
 // time). With them fixed every fragment load is unconditional, so the waitcnt that guards X (issued
 // first) does not also wait for the weight fragments issued behind it.
@@ -540,7 +616,7 @@ constexpr int T1_BARRIERS = 7;
 // R16: indexed rows arrive as bf16 (sharded step, tt_tower_fwd_bwd_indexed_bf16); its own
 // instantiation, so the other modes' code and registers are untouched. UPD: the in-place update of
 // single-lookup rows (TowerArgs::uw); gather mode only.
-template <int IN_, int W0_, int W1_, bool R16 = false, bool UPD = false>
+template <int IN_, int W0_, int W1_, bool R16 = false, bool UPD = false, bool MH = false>
 __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][TR * LSTR];   // X, later dZ0
   __shared__ __attribute__((aligned(16))) __bf16 hs[2][TR * LSTR];   // hidden activation (bf16)
@@ -695,7 +771,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   int32_t rpos[4];                   // indexed: the dX row of each xv (gpos_out, else its input row)
 #pragma unroll
   for (int i = 0; i < 4; ++i) rpos[i] = -1;
-  if (gather || indexed) {
+  if constexpr (MH) {
+    mh_gather<IN_>(a, t, tt, m0, B, xv);
+  } else if (gather || indexed) {
     // single-hot: the embedding row itself (EBC forward fused in); id 0 -> empty bag -> zeros.
     // Indexed rows may be bf16 (tt_tower_fwd_bwd_indexed_bf16): byte offsets with the element size
     const bool r16 = R16;
@@ -1844,7 +1922,7 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if ((!pooled && !a.gcol[0] && !a.gpos[0]) || (!gpooled && !a.gpos[0]) || !params || !labels || !logits)
+  if ((!pooled && !a.gcol[0] && !a.gpos[0] && !a.mval) || (!gpooled && !a.gpos[0]) || !params || !labels || !logits)
     return fail(TT_EINVAL, "tower: null pointer");
   if (label_dtype != TT_I32 && label_dtype != TT_I64 && label_dtype != TT_F32)
     return fail(TT_EINVAL, "tower: labels must be int32/int64/float32");
@@ -1889,6 +1967,15 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
   if ((a.gcol[0] || a.gpos[0]) && !two)
     return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
+  if (a.mval) {  // multi-hot EBC forward fused in: compile-time shapes only
+    if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
+      tower_l2_kernel<128, 128, 64, false, false, true><<<g, b512, 0, as_stream(stream)>>>(a);
+    else if (two && i0 == 64 && i1 == 64 && w0 == 128 && w1 == 64)
+      tower_l2_kernel<64, 128, 64, false, false, true><<<g, b512, 0, as_stream(stream)>>>(a);
+    else
+      return fail(TT_EINVAL, "tower_fwd_bwd_kjt: shapes in {64, 128} x [128, 64] only");
+    return check_launch("tower_fwd_bwd_kjt");
+  }
   if (a.uw[0]) {  // in-place update of single-lookup rows: compile-time shapes only
     if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
       tower_l2_kernel<128, 128, 64, false, true><<<g, b512, 0, as_stream(stream)>>>(a);
@@ -2002,6 +2089,29 @@ int tt_tower_fwd_bwd_gather(const tt_tower_shape_t* shape, int64_t B, const void
     dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
     a.dd_on = 1;
   }
+  return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
+                   ws_bytes, stream);
+}
+
+int tt_tower_fwd_bwd_kjt(const tt_tower_shape_t* shape, int64_t B, const void* values, int id_dtype,
+                         const int32_t* offsets, const int64_t* num_rows, const float* const* table_rows,
+                         float* pooled_out, int64_t ldp, float* gpooled, const float* params, const void* labels,
+                         int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
+                         void* stream) {
+  if (!values || !offsets || !num_rows || !table_rows) return fail(TT_EINVAL, "tower_fwd_bwd_kjt: null pointer");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_fwd_bwd_kjt: ids must be int32/int64");
+  TowerArgs a{};
+  for (int t = 0; t < 2; ++t) {
+    if (!table_rows[t] || num_rows[t] < 1) return fail(TT_EINVAL, "tower_fwd_bwd_kjt: bad table");
+    if (reinterpret_cast<uintptr_t>(table_rows[t]) & 15)
+      return fail(TT_EINVAL, "tower_fwd_bwd_kjt: rows not 16-B aligned");
+    a.gtab[t] = table_rows[t];
+    a.gmod[t] = num_rows[t];
+    a.moff[t] = offsets + (int64_t)t * B;  // key-major: tower t's bags follow the previous key's B
+  }
+  a.mval = values;
+  a.gid_dtype = id_dtype;
+  a.pooled_out = pooled_out;
   return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
                    ws_bytes, stream);
 }

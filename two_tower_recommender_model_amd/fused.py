@@ -176,6 +176,13 @@ class FusedTwoTowerStep:
         self.gather = (fuse_gather and self.towers is not None and kjt_mode == "cols" and self.F == 2
                        and self.qf == [0] and self.cf == [1] and len(self.layer_sizes) == 2
                        and max(self.dims) <= 128)
+        # multi-hot KJT input: the EBC forward (sum pool of every bag) runs inside T1
+        # (tt_tower_fwd_bwd_kjt) for one key per tower, towers [128, 64] over 64- or 128-wide rows
+        # (TT_KJT_POOL_IN_T1=0: tt_pooled_fwd + T1 instead, A/B measurement)
+        self.gather_kjt = (fuse_gather and os.environ.get("TT_KJT_POOL_IN_T1", "1") != "0"
+                           and self.towers is not None and self.kjt_input and self.F == 2
+                           and self.qf == [0] and self.cf == [1] and self.layer_sizes == [128, 64]
+                           and self.dims[0] == self.dims[1] and self.dims[0] in (64, 128))
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         # warm every scratch workspace so graph capture allocates nothing new (the all-zero batch
         # drops every id, so the tables are untouched; the towers' parameters are restored)
@@ -345,7 +352,7 @@ class FusedTwoTowerStep:
             # single-hot columns: the transform (drop id 0, id mod N) is applied inside the kernels
             prepare = lambda: self.tables.bwd_prepare_cols(self.cols, self.num_embeddings)  # noqa: E731
             self.offsets_used = None
-        if prepare is not None:
+        def launch_prepare():
             if self.side is not None:
                 self.side.wait_stream(main)
                 with torch.cuda.stream(self.side):
@@ -356,6 +363,13 @@ class FusedTwoTowerStep:
                 self._mark("prep", 0)
                 prepare()
                 self._mark("prep", 1)
+
+        # the next batch's grouping beside this step's embedding update rather than beside T1: T1's
+        # workgroups each take a whole CU's LDS, so the grouping kernels' workgroups would hold CUs
+        # T1 waits for
+        defer_prepare = ahead and self.gather_kjt
+        if prepare is not None and not defer_prepare:
+            launch_prepare()
         if self.gather:
             # EBC forward (and, with the single-hot dedup, its insert) fused into T1
             self._mark("t1", 0)
@@ -364,10 +378,12 @@ class FusedTwoTowerStep:
                                        self.params, self.labels, self.logits,
                                        pooled_out=self.pooled if self.materialize_pooled else None,
                                        dedup=self.tables if self.dedup_single else None, dedup_tables=(0, 1))
-        elif self.kjt_mode == "kjt":
+        elif self.kjt_mode == "kjt" and not self.gather_kjt:
             self._mark("fwd", 0)
             self.tables.pooled_fwd(self.values, self.offsets, B, out=self.pooled)
             self._mark("fwd", 1)
+        elif self.kjt_mode == "kjt":
+            pass  # the sum pool runs inside T1 (below)
         else:
             self.tables.pooled_fwd_cols(self.cols, self.num_embeddings, out=self.pooled)
         if self.towers is not None and self.gather and self.dedup_single and self.combined_bwd:
@@ -383,7 +399,16 @@ class FusedTwoTowerStep:
             return
         if self.towers is not None:
             # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update
-            if not self.gather:
+            if self.gather_kjt:
+                self._mark("t1", 0)
+                self.towers.fwd_bwd_kjt(self.values, self.offsets,
+                                        [self.tables.table_view(0), self.tables.table_view(1)], self.gpooled,
+                                        self.params, self.labels, self.logits,
+                                        pooled_out=self.pooled if self.materialize_pooled else None)
+                self._mark("t1", 1)
+                if defer_prepare:
+                    launch_prepare()
+            elif not self.gather:
                 self._mark("t1", 0)
                 self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
                 self._mark("t1", 1)

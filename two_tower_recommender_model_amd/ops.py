@@ -584,6 +584,27 @@ class FusedTowers:
                                               dd_bytes, dd_cap, ptr(self.ws), self.nbytes,
                                               stream_handle(self.device)), "tower_fwd_bwd_gather")
 
+    def fwd_bwd_kjt(self, values, offsets, table_rows, gpooled, params, labels, logits, pooled_out=None,
+                    grad_scale: float = 1.0) -> None:
+        """T1 with the multi-hot EBC forward fused in: tower t's input row m is the sum pool of bag
+        (t, m) of the key-major KJT (``values``, complete int32 ``offsets`` [2B + 1]) over the table
+        view ``table_rows[t]`` ([rows, in_dim[t]] fp32); bit-identical to ``pooled_fwd`` + ``fwd_bwd``.
+        ``pooled_out`` (optional) receives the pooled rows."""
+        ldt = {torch.int32: TT_I32, torch.int64: TT_I64, torch.float32: TT_F32}[labels.dtype]
+        if offsets.dtype != torch.int32 or offsets.numel() != 2 * self.B + 1:
+            raise _lib.TTError("fwd_bwd_kjt: offsets must be int32 [2B + 1]")
+        for t in range(2):
+            if table_rows[t].shape[1] != self.shape.in_dim[t] or not table_rows[t].is_contiguous():
+                raise _lib.TTError("fwd_bwd_kjt: table view does not match the tower input")
+        if pooled_out is not None and pooled_out.stride(0) != gpooled.stride(0):
+            raise ValueError("pooled_out and the gradient must share a row stride")
+        nr = (C.c_int64 * 2)(*[int(table_rows[t].shape[0]) for t in range(2)])
+        check(_lib_().tt_tower_fwd_bwd_kjt(C.byref(self.shape), self.B, ptr(values), id_dtype_code(values.dtype),
+                                           ptr(offsets), nr, ptr_array(list(table_rows)), ptr(pooled_out),
+                                           gpooled.stride(0), ptr(gpooled), ptr(params), ptr(labels), ldt,
+                                           float(grad_scale), ptr(logits), ptr(self.ws), self.nbytes,
+                                           stream_handle(self.device)), "tower_fwd_bwd_kjt")
+
     def fwd_bwd_indexed(self, pos, rows_in, grad_rows_out, params, labels, logits, grad_scale: float = 1.0) -> None:
         """T1 of the sharded step: tower t's input row m is ``rows_in[t][pos[t][m]]`` (-1: zeros) and
         its input gradient goes to ``grad_rows_out[t][pos[t][m]]``."""
