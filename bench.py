@@ -672,11 +672,23 @@ def run_multi(args, world, rank, local_rank):
     loss = float(step.loss)
     step.release_graphs()  # before the process group is destroyed
     r = step.rank
+    # SURVEY 8(d) embedding-path bytes per rank and step over the whole step's time (no per-launch
+    # timing in this mode): every rank routes B x F lookups and owns ~B x F of the W x B x F lookups
+    # for the update; U counted on this rank's resident batches (distinct (table, row) per batch)
+    FB = 2 * B
+    uniq = sum(int(torch.unique(torch.cat([c[0][c[0] != 0] % N[0], c[1][c[1] != 0] % N[1] + (1 << 40)])).numel())
+               for c, _ in batches) // len(batches)
+    emb_bytes = FB * (16 + 4 * D) + FB * (4 + 8 * D) + uniq * (8 * D + 8)
+    ach = emb_bytes / (dt / args.steps) / 1e9
+    roofline = {"bound": "hbm", "kernel": "whole sharded step (per rank)", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_step": emb_bytes, "unique_rows": uniq,
+                "timing": "SURVEY 8(d) bytes per rank over the max-over-ranks step time (collectives included)"}
     info = {"capacity": cap, "capacity_needed": int(need), "resident_batches": nb,
             "exchange_A_bytes_sent": 4 * step.A_total,
             "exchange_B_bytes_sent": 2 * D * world * step.S[r],
             "collectives_per_step": 2, "mode": mode}
-    return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info
+    return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
 
 
 def main():
@@ -713,8 +725,8 @@ def main():
         else:  # --sharded without a launcher (e.g. under rocprofv3): a one-rank group
             dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
                                     device_id=torch.device("cuda", local_rank))
-        value, ms, loss, sharded_info = run_multi(args, world, rank, local_rank)
-        roofline, cpu, steps_run = None, None, args.steps
+        value, ms, loss, sharded_info, roofline = run_multi(args, world, rank, local_rank)
+        cpu, steps_run = None, args.steps
         config["parallelism"] = (f"row-wise sharded tables + data-parallel towers x{world}: pipelined, 2 RCCL "
                                  f"all-to-alls per step ([grad rows | tower grad | next ids], next rows), "
                                  f"{sharded_info['mode']}")
