@@ -176,8 +176,10 @@ def test_multihot_pipelined_grouping_bitwise(device, hot):
     assert torch.equal(ref_st.tables.state, pipe.tables.state)
 
 
-@pytest.mark.parametrize("D", [64, 128])
-def test_multihot_pool_inside_t1_bitwise(device, D):
+@pytest.mark.parametrize("D,id_dtype,empty", [(64, torch.int64, False), (128, torch.int64, False),
+                                               (128, torch.int32, False), (128, torch.int64, True)],
+                         ids=["d64", "d128", "d128-int32", "d128-empty-batch"])
+def test_multihot_pool_inside_t1_bitwise(device, D, id_dtype, empty):
     """tt_tower_fwd_bwd_kjt (the sum pool of every bag inside T1) against tt_pooled_fwd followed by
     the unfused T1 on the same KJT: pooled rows, logits, dX, loss, and after 3 eager steps the
     tables, row-wise state and tower parameters, all bitwise (the rows are added in bag order from
@@ -188,17 +190,19 @@ def test_multihot_pool_inside_t1_bitwise(device, D):
     rng = np.random.default_rng(31 + D)
     B, N = 200, [3000, 5000]
     batches = [_kjt(rng, B, N, 40) for _ in range(3)]
-    cap = max(v.size for v, _ in batches)
+    if empty:  # a batch whose every bag is empty (all ids dropped upstream): zero rows, no lookups
+        batches[1] = (np.zeros(0, np.int64), np.zeros(2 * B + 1, np.int32))
+    cap = max(1, max(v.size for v, _ in batches))
     g = torch.Generator().manual_seed(4)
     labels = [torch.randint(0, 2, (B,), generator=g).to(torch.int32).to(device) for _ in batches]
     outs = []
     for fuse in (False, True):
         st = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, lr_emb=0.02, lr_dense=0.01, seed=6,
-                               max_lookups=cap, fuse_gather=fuse, materialize_pooled=True)
+                               max_lookups=cap, fuse_gather=fuse, materialize_pooled=True, id_dtype=id_dtype)
         assert st.gather_kjt == fuse and st.towers is not None
         per = []
         for (v, o), lab in zip(batches, labels):
-            st.load_kjt(torch.from_numpy(v).to(device), torch.from_numpy(o).to(device), lab)
+            st.load_kjt(torch.from_numpy(v).to(id_dtype).to(device), torch.from_numpy(o).to(device), lab)
             st.step()
             torch.cuda.synchronize()
             per.append([x.cpu().clone() for x in (st.pooled, st.logits, st.gpooled, st.loss)])
