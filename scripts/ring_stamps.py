@@ -17,8 +17,19 @@ N = [50_000_000, 100_000_000]
 B = 8192
 st = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, dev)
 g = torch.Generator(device=dev).manual_seed(1)
-batches = [([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
-            torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32)) for _ in range(64)]
+
+
+def ids(n):
+    if os.environ.get("IDS", "uniform") == "uniform":
+        return torch.randint(0, n, (B,), generator=g, device=dev)
+    # Zipf-like (s ~ 1.05) over permuted ranks, as bench.py --ids zipf
+    u01 = torch.rand(B, generator=g, device=dev, dtype=torch.float64)
+    r = torch.floor(torch.exp(u01 * torch.log(torch.tensor(float(n), device=dev, dtype=torch.float64))))
+    return (r.to(torch.int64) * 2654435761) % n
+
+
+batches = [([ids(n) for n in N], torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32))
+           for _ in range(64)]
 st.capture_ring(batches, steps_per_graph=8)
 nwg = B // 32
 off = st.towers.nbytes - (((max(2 * nwg, 1024) * 8 + nwg * 16 * 9) * 8 + 255) // 256 * 256)
@@ -53,7 +64,8 @@ for it in range(6):
         n_ins, dd = 64, int(os.environ.get("K3_DD", "576"))
         show("tail", base[4096:6144], [("insert", 0, n_ins), ("tiles", n_ins, n_ins + ntile),
                                        ("bias", n_ins + ntile, n_ins + ntile + nbias),
-                                       ("rows", n_ins + ntile + nbias, n_ins + ntile + nbias + dd)])
+                                       ("hot", n_ins + ntile + nbias, n_ins + ntile + nbias + 64),
+                                       ("slots", n_ins + ntile + nbias + 64, n_ins + ntile + nbias + dd)])
         continue
     show("T2", base[4096:6144], roles_t2)
     k3 = base[6144:8192]

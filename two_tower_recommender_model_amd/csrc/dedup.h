@@ -249,14 +249,32 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
     const int D = gm.lm->dim[t];
     const bool col_ok = hl * 4 < D;
     f32x4v acc = (f32x4v)(0.f);
-    int seen = 0;  // matches before this pass (global position of list[0])
-    for (int64_t c0 = 0; c0 < n; c0 += DD_HOT_CH) {
+    // the row's lookups: cnt of them (its slot word's count). Up to DD_HOT_CH they are listed in
+    // LDS by ONE scan over the step's keys (the next pass's keys in flight beside this pass's
+    // matching), then summed; longer lists are summed pass by pass. Either way group grp adds the
+    // matches at global positions == grp (mod 8) in ascending order (the same adds, bit for bit).
+    const int cnt = (int)(ws.slots[h].word & DD_CNT_MASK);
+    const bool one_list = cnt <= DD_HOT_CH;
+    int seen = 0;  // matches before this pass (global position of the pass's first match)
+    const int nn = (int)n;  // lookups < 2^18 (DD_CNT_BITS): 32-bit indices
+    uint64_t kc[DD_HOT_PT], kn[DD_HOT_PT];
+#pragma unroll
+    for (int q = 0; q < DD_HOT_PT; ++q) {
+      const int i = DD_HOT_PT * tid + q;
+      kc[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
+    }
+    for (int c0 = 0; c0 < nn; c0 += DD_HOT_CH) {
       // thread tid covers lookups [c0 + PT tid, c0 + PT tid + PT): PT-bit match mask
-      const int64_t i0 = c0 + DD_HOT_PT * tid;
+      const int i0 = c0 + DD_HOT_PT * tid;
+#pragma unroll
+      for (int q = 0; q < DD_HOT_PT; ++q) {
+        const int i = i0 + DD_HOT_CH + q;
+        kn[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
+      }
       uint32_t mask = 0;
 #pragma unroll
       for (int q = 0; q < DD_HOT_PT; ++q)
-        if (i0 + q < n && ws.lkey[i0 + q] == key) mask |= 1u << q;
+        if (kc[q] == key) mask |= 1u << q;
       const int mc = __popc(mask);
       int inc = mc;
 #pragma unroll
@@ -272,25 +290,44 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
         if (w < wid) base += wtot[w];
         total += wtot[w];
       }
-      int pos = base + inc - mc;
+      int pos = base + inc - mc + (one_list ? seen : 0);
       for (int q = 0; q < DD_HOT_PT; ++q)
-        if (mask & (1u << q)) list[pos++] = (int)(i0 + q);
+        if (mask & (1u << q)) {
+          if (pos < DD_HOT_CH) list[pos] = i0 + q;  // one list: at most cnt <= DD_HOT_CH matches
+          ++pos;
+        }
       __syncthreads();
-      // group grp takes global positions == grp (mod 8), ascending
-      // (4 rows in flight per group; added in ascending position order as before)
-      int p = (grp - (seen & 7) + 8) & 7;
-      for (; p + 24 < total; p += 32) {
-        f32x4v x[4];
+      if (!one_list) {
+        int p = (grp - (seen & 7) + 8) & 7;
+        for (; p + 24 < total; p += 32) {
+          f32x4v x[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+          for (int u = 0; u < 4; ++u)
+            x[u] = col_ok ? *reinterpret_cast<const f32x4v*>(gm.row(list[p + 8 * u]) + hl * 4) : (f32x4v)(0.f);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc += x[u];
+        }
+        for (; p < total; p += 8)
+          if (col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
+        __syncthreads();
+      }
+      seen += total;
+#pragma unroll
+      for (int q = 0; q < DD_HOT_PT; ++q) kc[q] = kn[q];
+    }
+    if (one_list) {  // 8 rows in flight per group
+      seen = min(seen, DD_HOT_CH);
+      int p = grp;
+      for (; p + 56 < seen; p += 64) {
+        f32x4v x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
           x[u] = col_ok ? *reinterpret_cast<const f32x4v*>(gm.row(list[p + 8 * u]) + hl * 4) : (f32x4v)(0.f);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc += x[u];
+        for (int u = 0; u < 8; ++u) acc += x[u];
       }
-      for (; p < total; p += 8)
+      for (; p < seen; p += 8)
         if (col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
-      seen += total;
-      __syncthreads();
     }
     part[grp][hl] = acc;
     __syncthreads();
@@ -443,14 +480,16 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
 #pragma unroll
     for (int q = 0; q < DD_SPH; ++q) {
       if (cmax[q] > 1) mine[q] = dd_bitonic<32>(mine[q]);
-      for (int i = 0; i < cmax[q]; i += 2) {
-        const int b0 = __shfl(mine[q], hb + i, 64);
-        const int b1 = __shfl(mine[q], hb + min(i + 1, 31), 64);
-        f32x4v x0 = (f32x4v)(0.f), x1 = (f32x4v)(0.f);
-        if (col_ok[q] && i < c[q]) x0 = *reinterpret_cast<const f32x4v*>(gm.row(b0) + hl * 4);
-        if (col_ok[q] && i + 1 < c[q]) x1 = *reinterpret_cast<const f32x4v*>(gm.row(b1) + hl * 4);
-        if (i < c[q]) g[q] += x0;
-        if (i + 1 < c[q]) g[q] += x1;
+      for (int i = 0; i < cmax[q]; i += 4) {  // 4 gradient rows in flight, added in ascending order
+        f32x4v x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int b = __shfl(mine[q], hb + min(i + u, 31), 64);
+          x[u] = col_ok[q] && i + u < c[q] ? *reinterpret_cast<const f32x4v*>(gm.row(b) + hl * 4) : (f32x4v)(0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (i + u < c[q]) g[q] += x[u];
       }
     }
   }
