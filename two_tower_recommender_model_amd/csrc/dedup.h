@@ -46,6 +46,10 @@ struct DedupWs {
   Ovf* ovf;          // [groups][64], key EMPTY between steps (the resolver clears what it filed)
   int32_t ovf_groups;
   int64_t* stamps;  // EXPERIMENT (TT_DD_STAMPS): [update workgroups][8] s_memrealtime per phase
+  // hot rows split over a team of workgroups (dd_hot_role): partial sums [hot_cap][DD_HOT_TEAM][128]
+  // and per hot row the team's arrival counter (zero between launches: reset by the last arriver)
+  float* hotp;
+  int32_t* hcnt;
 };
 #define DD_STAMP(k) \
   do { if (ws.stamps && threadIdx.x == 0) ws.stamps[(int64_t)bid * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
@@ -227,11 +231,39 @@ __device__ __forceinline__ int dd_bitonic(int v) {
 
 constexpr int DD_HOT_PT = 16;                // lookups per thread per scan pass (4096 a pass)
 constexpr int DD_HOT_CH = 256 * DD_HOT_PT;  // lookups scanned per pass of a hot workgroup (LDS list)
+constexpr int DD_HOT_TEAM = 8;              // at most this many workgroups share one hot row
 // LDS of the hot role (list + wave totals + group partials), provided by the launching kernel so a
 // combined launch can overlay it on its other roles' LDS
 constexpr int DD_SMEM_HOT = DD_HOT_CH * 4 + 16 + 8 * 32 * 16;
 constexpr int DD_SMEM = DD_SMEM_HOT + (int)sizeof(DdMeta);  // + the per-workgroup meta copy
 
+// members per hot row: as many as the hot workgroups allow in one round (at least 1), at most one
+// per scan pass and DD_HOT_TEAM (every workgroup computes it from the same nh)
+__device__ __forceinline__ int dd_hot_team(int nh, int64_t n, int hot_wgs) {
+  const int npass = (int)((n + DD_HOT_CH - 1) / DD_HOT_CH);
+  return max(1, min(min(DD_HOT_TEAM, npass), hot_wgs / max(1, nh)));
+}
+
+// every hot workgroup checks in once; the last one resets the hot-row count and the ticket
+__device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs) {
+  if (threadIdx.x == 0) {
+    const int tk = atomicAdd(&ws.ctr[1], 1);
+    if (tk == hot_wgs - 1) {
+      atomicExch(&ws.ctr[0], 0);
+      atomicExch(&ws.ctr[1], 0);
+    }
+  }
+}
+
+// Rows looked up more than DD_INL times in the step. A row is split over a team of K workgroups
+// (dd_hot_team): member k scans passes k, k + K, ... of the step's keys (4096
+// a pass, the next pass's keys in flight beside this pass's matching), its 8 groups add the pass's
+// matches at positions == group (mod 8) in ascending order (8 rows in flight), and the group sums
+// are added in group order: the member's partial. Members publish their partial write-through
+// (relaxed agent-scope stores: sc1) and add to the row's counter; the member whose add returns
+// K - 1 reads the K partials (sc1 loads, after its add returned) and adds them in member order —
+// the same sum whichever member arrives last — then applies the row-wise Adagrad step. No member
+// waits on another (cdna_hip_programming.md Guideline 16: counter form, the last arriver combines).
 __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
                                             float* __restrict__ weights, float* __restrict__ state, float lr,
                                             float eps, const DedupWs& ws, int hot_wgs, int bid, char* smem) {
@@ -241,7 +273,11 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = tid >> 5, hl = tid & 31;
   const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
-  for (int j = bid; j < nh; j += hot_wgs) {
+  const int nn = (int)n;  // lookups < 2^18 (DD_CNT_BITS): 32-bit indices
+  const int npass = (nn + DD_HOT_CH - 1) / DD_HOT_CH;
+  const int K = dd_hot_team(nh, n, hot_wgs);
+  for (int w = bid; w < nh * K; w += hot_wgs) {
+    const int j = w / K, k = w - j * K;
     const int32_t h = ws.hot[j];
     const uint64_t key = ws.slots[h].word >> DD_CNT_BITS;
     const int t = (int)(key >> DD_TABLE_SHIFT);
@@ -249,26 +285,18 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
     const int D = gm.lm->dim[t];
     const bool col_ok = hl * 4 < D;
     f32x4v acc = (f32x4v)(0.f);
-    // the row's lookups: cnt of them (its slot word's count). Up to DD_HOT_CH they are listed in
-    // LDS by ONE scan over the step's keys (the next pass's keys in flight beside this pass's
-    // matching), then summed; longer lists are summed pass by pass. Either way group grp adds the
-    // matches at global positions == grp (mod 8) in ascending order (the same adds, bit for bit).
-    const int cnt = (int)(ws.slots[h].word & DD_CNT_MASK);
-    const bool one_list = cnt <= DD_HOT_CH;
-    int seen = 0;  // matches before this pass (global position of the pass's first match)
-    const int nn = (int)n;  // lookups < 2^18 (DD_CNT_BITS): 32-bit indices
     uint64_t kc[DD_HOT_PT], kn[DD_HOT_PT];
 #pragma unroll
     for (int q = 0; q < DD_HOT_PT; ++q) {
-      const int i = DD_HOT_PT * tid + q;
+      const int i = k * DD_HOT_CH + DD_HOT_PT * tid + q;
       kc[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
     }
-    for (int c0 = 0; c0 < nn; c0 += DD_HOT_CH) {
-      // thread tid covers lookups [c0 + PT tid, c0 + PT tid + PT): PT-bit match mask
-      const int i0 = c0 + DD_HOT_PT * tid;
+    for (int p = k; p < npass; p += K) {
+      // thread tid covers lookups [i0, i0 + PT): PT-bit match mask
+      const int i0 = p * DD_HOT_CH + DD_HOT_PT * tid;
 #pragma unroll
       for (int q = 0; q < DD_HOT_PT; ++q) {
-        const int i = i0 + DD_HOT_CH + q;
+        const int i = i0 + K * DD_HOT_CH + q;
         kn[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
       }
       uint32_t mask = 0;
@@ -286,48 +314,28 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
       __syncthreads();
       int base = 0, total = 0;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        if (w < wid) base += wtot[w];
-        total += wtot[w];
+      for (int w4 = 0; w4 < 4; ++w4) {
+        if (w4 < wid) base += wtot[w4];
+        total += wtot[w4];
       }
-      int pos = base + inc - mc + (one_list ? seen : 0);
+      int pos = base + inc - mc;
       for (int q = 0; q < DD_HOT_PT; ++q)
-        if (mask & (1u << q)) {
-          if (pos < DD_HOT_CH) list[pos] = i0 + q;  // one list: at most cnt <= DD_HOT_CH matches
-          ++pos;
-        }
+        if (mask & (1u << q)) list[pos++] = i0 + q;
       __syncthreads();
-      if (!one_list) {
-        int p = (grp - (seen & 7) + 8) & 7;
-        for (; p + 24 < total; p += 32) {
-          f32x4v x[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            x[u] = col_ok ? *reinterpret_cast<const f32x4v*>(gm.row(list[p + 8 * u]) + hl * 4) : (f32x4v)(0.f);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) acc += x[u];
-        }
-        for (; p < total; p += 8)
-          if (col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
-        __syncthreads();
-      }
-      seen += total;
-#pragma unroll
-      for (int q = 0; q < DD_HOT_PT; ++q) kc[q] = kn[q];
-    }
-    if (one_list) {  // 8 rows in flight per group
-      seen = min(seen, DD_HOT_CH);
-      int p = grp;
-      for (; p + 56 < seen; p += 64) {
+      int pp = grp;
+      for (; pp + 56 < total; pp += 64) {
         f32x4v x[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-          x[u] = col_ok ? *reinterpret_cast<const f32x4v*>(gm.row(list[p + 8 * u]) + hl * 4) : (f32x4v)(0.f);
+          x[u] = col_ok ? *reinterpret_cast<const f32x4v*>(gm.row(list[pp + 8 * u]) + hl * 4) : (f32x4v)(0.f);
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += x[u];
       }
-      for (; p < seen; p += 8)
-        if (col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[p]) + hl * 4);
+      for (; pp < total; pp += 8)
+        if (col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[pp]) + hl * 4);
+      __syncthreads();  // the list and wtot are rewritten by the next pass
+#pragma unroll
+      for (int q = 0; q < DD_HOT_PT; ++q) kc[q] = kn[q];
     }
     part[grp][hl] = acc;
     __syncthreads();
@@ -335,33 +343,57 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
       f32x4v g = part[0][hl];
 #pragma unroll
       for (int q = 1; q < 8; ++q) g += part[q][hl];
-      float sq = col_ok ? rw_sq4(g) : 0.f;
+      bool last = true;
+      if (K > 1) {
+        float* mine = ws.hotp + ((int64_t)j * DD_HOT_TEAM + k) * 128 + hl * 4;
+        if (lane < 32) {
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
-      if (lane < 32) {
-        float* wrow = weights + gm.lm->woff[t] + r * D;
-        float* srow = state + gm.lm->soff[t] + r;
-        const float snew = rw_state(*srow, sq, D);
-        const float step = rw_step(snew, lr, eps);
-        if (col_ok)
-          *reinterpret_cast<f32x4v*>(wrow + hl * 4) =
-              rw_apply(*reinterpret_cast<const f32x4v*>(wrow + hl * 4), g, step);
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-          *srow = snew;
-          ws.slots[h].word = DD_EMPTY;
+          for (int v = 0; v < 4; ++v) __hip_atomic_store(mine + v, g[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial has left this CU
+        int prev = 0;
+        if (lane == 0) prev = __hip_atomic_fetch_add(&ws.hcnt[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev = __shfl(prev, 0, 64);
+        last = prev == K - 1;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+          const float* all = ws.hotp + (int64_t)j * DD_HOT_TEAM * 128 + hl * 4;
+          f32x4v pk[DD_HOT_TEAM];
+#pragma unroll
+          for (int q = 0; q < DD_HOT_TEAM; ++q)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              pk[q][v] = q < K ? __hip_atomic_load(all + q * 128 + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+          g = pk[0];
+#pragma unroll
+          for (int q = 1; q < DD_HOT_TEAM; ++q)
+            if (q < K) g += pk[q];
+          if (lane == 0) __hip_atomic_store(&ws.hcnt[j], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (last) {
+        float sq = col_ok ? rw_sq4(g) : 0.f;
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+        if (lane < 32) {
+          float* wrow = weights + gm.lm->woff[t] + r * D;
+          float* srow = state + gm.lm->soff[t] + r;
+          const float snew = rw_state(*srow, sq, D);
+          const float step = rw_step(snew, lr, eps);
+          if (col_ok)
+            *reinterpret_cast<f32x4v*>(wrow + hl * 4) =
+                rw_apply(*reinterpret_cast<const f32x4v*>(wrow + hl * 4), g, step);
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) {
+            *srow = snew;
+            ws.slots[h].word = DD_EMPTY;
+          }
         }
       }
     }
     __syncthreads();
   }
-  if (tid == 0) {
-    const int tk = atomicAdd(&ws.ctr[1], 1);
-    if (tk == hot_wgs - 1) {
-      atomicExch(&ws.ctr[0], 0);
-      atomicExch(&ws.ctr[1], 0);
-    }
-  }
+  dd_hot_ticket(ws, hot_wgs);
 }
 
 // host: validate + fill the update launch's arguments; *grid = its workgroup count
@@ -381,6 +413,13 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   DdMeta* lm = reinterpret_cast<DdMeta*>(smem + DD_SMEM_HOT);
   const GradMap gm{a.grad, a.ldg, (uint32_t)m.B, lm};
   if (bid < a.hot_wgs) {
+    // a workgroup with no hot work item (most of them at uniform ids) only checks in: the ticket
+    // that resets the hot-row count once every hot workgroup has read it
+    const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
+    if (bid >= nh * dd_hot_team(nh, a.n, a.hot_wgs)) {
+      dd_hot_ticket(ws, a.hot_wgs);
+      return;
+    }
     dd_meta_fill(m, lm);
     __syncthreads();
     dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem);

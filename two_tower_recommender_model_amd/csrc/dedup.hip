@@ -56,6 +56,9 @@ size_t dedup_layout(void* base, int64_t L, DedupWs* w) {
   t.ovf = reinterpret_cast<DedupWs::Ovf*>(take(sizeof(DedupWs::Ovf) * 64 * (size_t)t.ovf_groups));
   int64_t* dbg = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * 8 * (L / (8 * DD_SPH) + 64)));
   t.stamps = getenv("TT_DD_STAMPS") ? dbg : nullptr;
+  const int64_t hot_cap = L / (DD_INL + 1) + 1;
+  t.hotp = reinterpret_cast<float*>(take(sizeof(float) * 128 * DD_HOT_TEAM * hot_cap));
+  t.hcnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * hot_cap));
   t.cap = cap;
   t.L = L;
   t.hot_cap = (int32_t)(L / (DD_INL + 1) + 1);
@@ -135,7 +138,12 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
   a.state = state;
   a.lr = lr;
   a.eps = eps;
-  a.hot_wgs = (int)std::min<int64_t>(64, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
+  // a hot row takes a team of up to DD_HOT_TEAM workgroups (dd_hot_role, dd_hot_team)
+  // 64 hot workgroups: every one that finds no hot row still checks in, and at uniform ids (no hot
+  // rows) 128 cost the ring's tail launch ~0.3 us on MI355X while halving the Zipf tail's hot rows
+  int64_t hot_max = 64;
+  if (const char* e = getenv("TT_DD_HOT_WGS")) hot_max = std::max(8, atoi(e));  // EXPERIMENT (A/B)
+  a.hot_wgs = (int)std::min<int64_t>(hot_max, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
   a.slot_hw = ceil_div(ceil_div(max_lookups, DD_SPH), 8) * 8;
   *grid = a.hot_wgs + a.slot_hw / 8;
   return TT_OK;
@@ -160,6 +168,7 @@ int tt_dedup_workspace_init(void* workspace, size_t ws_bytes, int64_t max_lookup
   // every slot word EMPTY (all ones; items unused), counters 0
   if (hipMemsetAsync(w.slots, 0xff, sizeof(DSlot) * w.cap, st) != hipSuccess ||
       hipMemsetAsync(w.ctr, 0, sizeof(int32_t) * 4, st) != hipSuccess ||
+      hipMemsetAsync(w.hcnt, 0, sizeof(int32_t) * w.hot_cap, st) != hipSuccess ||
       hipMemsetAsync(w.ovf, 0xff, sizeof(DedupWs::Ovf) * 64 * w.ovf_groups, st) != hipSuccess)
     return fail(TT_EINVAL, "dedup_workspace_init: memset failed");
   if (hipStreamSynchronize(st) != hipSuccess) return fail(TT_EINVAL, "dedup_workspace_init: sync failed");
