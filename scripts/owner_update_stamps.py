@@ -30,7 +30,7 @@ pool = [([torch.randint(0, n, (B,), generator=g, device=dev) for n in N],
          torch.randint(0, 2, (B,), generator=g, device=dev, dtype=torch.int32)) for _ in range(8)]
 L = st.max_lookups
 off, cap = dbg_offset(L)
-hot_wgs = min(128, max(1, L // 31))
+hot_wgs = min(64, max(1, L // 31))
 for it in range(6):
     p = (st.cursor or 0) % 2 if st.cursor is not None else 0
     st.run_eager(pool, 1)
