@@ -1038,44 +1038,71 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   __syncthreads();
   T1_STAMP(7);
   T1_WSTAMP(9);
+  // ---- 8. dX from LDS; UPD: the in-place row-wise Adagrad of the rows looked up once. A thread's
+  // rows go through each step together — their shuffle reductions and sqrt / division chains
+  // interleave instead of running row after row; each row's arithmetic is the K3 update's (sum(G^2)
+  // over the row's lanes by xor 16, 8, 4, 2, 1, then rw_state / rw_step / rw_apply)
+  f32x4 gq[4];
+  float* dstq[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (i == 1) T1_WSTAMP(10);
+    dstq[i] = nullptr;
+    gq[i] = (f32x4)(0.f);
     if (i < nxv) {
       const int e = tt + 256 * i;
       const int row = e / (in / 4), c4 = (e % (in / 4)) * 4;
       const int64_t gm = m0 + row;
-      float* dst = nullptr;
       if (gm < B) {
         if (indexed)
-          dst = rpos[i] >= 0 ? a.gdst[t] + (int64_t)rpos[i] * in + c4 : nullptr;
+          dstq[i] = rpos[i] >= 0 ? a.gdst[t] + (int64_t)rpos[i] * in + c4 : nullptr;
         else
-          dst = a.gpooled + gm * a.ldp + incol + c4;
+          dstq[i] = a.gpooled + gm * a.ldp + incol + c4;
       }
-      const f32x4 g = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
-      if (UPD) {
-        // the lanes of one row are consecutive (in / 4 of them, a power of two <= 32): reduce
-        // sum(G^2) over them in the K3 update's order, then update the row in place
-        const int64_t ur = urow[t][row];
-        const int lpr = in / 4;
-        float sq = rw_sq4(g);
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1)
-          if (o < lpr) sq += __shfl_xor(sq, o, 64);
-        if (ur >= 0) {
-          const float snew = rw_state(ustate[t][row], sq, in);
-          const float step = rw_step(snew, a.ulr, a.ueps);
-          const f32x4 x = xv[i];
-          if (!(a.dbg & 128)) {
-            *reinterpret_cast<f32x4*>(a.uw[t] + ur * in + c4) = rw_apply(x, g, step);
-            if (c4 == 0) a.us[t][ur] = snew;
-          }
-          if (!a.pooled_out) dst = nullptr;  // dX is needed only for inspection (pooled_out mode)
-        }
-      }
-      if (dst && !(a.dbg & 2)) *reinterpret_cast<f32x4*>(dst) = g;
+      gq[i] = *reinterpret_cast<const f32x4*>(&outf[t][row * FSTR + c4]);
     }
   }
+  if (UPD) {
+    const int lpr = in / 4;  // the lanes of one row are consecutive (a power of two <= 32)
+    float sq[4], s_old[4], snew[4], step[4];
+    int64_t ur[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ur[i] = -1;
+      sq[i] = 0.f;
+      s_old[i] = 0.f;
+      if (i < nxv) {
+        const int row = (tt + 256 * i) / (in / 4);
+        ur[i] = urow[t][row];
+        s_old[i] = ustate[t][row];
+        sq[i] = rw_sq4(gq[i]);
+      }
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)
+      if (o < lpr)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < nxv) sq[i] += __shfl_xor(sq[i], o, 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      snew[i] = rw_state(s_old[i], sq[i], in);
+      step[i] = rw_step(snew[i], a.ulr, a.ueps);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < nxv && ur[i] >= 0) {
+        const int c4 = ((tt + 256 * i) % (in / 4)) * 4;
+        if (!(a.dbg & 128)) {
+          *reinterpret_cast<f32x4*>(a.uw[t] + ur[i] * in + c4) = rw_apply(xv[i], gq[i], step[i]);
+          if (c4 == 0) a.us[t][ur[i]] = snew[i];
+        }
+        if (!a.pooled_out) dstq[i] = nullptr;  // dX is needed only for inspection (pooled_out mode)
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < nxv && dstq[i] && !(a.dbg & 2)) *reinterpret_cast<f32x4*>(dstq[i]) = gq[i];
   T1_WSTAMP(8);
   T1_STAMP(15);
 }
