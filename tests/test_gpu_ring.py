@@ -48,3 +48,29 @@ def test_ring_equals_classic_step(device, D, mode):
     assert torch.equal(a.params, b.params) and torch.equal(a.exp_avg, b.exp_avg)
     assert float(a.loss) == float(b.loss)
     assert torch.equal(a.logits, b.logits)
+
+
+def test_ring_mixed_graph_sizes(device):
+    """capture_ring(k = 4) also captures aligned 2-step graphs; run(3) + run(2) replays a 2-step
+    graph, single steps and a 4-step one; align_ring() regroups the graphs from the cursor; the
+    8 steps train bit for bit like 8 classic steps."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N, B = [30_000, 50_000], 2048
+    batches = _batches(N, B, 8, seed=5, device=device)
+    a = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=2)
+    b = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=2)
+    a.capture_ring(batches, steps_per_graph=4)
+    assert sorted(a.ring_mid) == [2]
+    a.run(3)
+    a.run(2)
+    a.align_ring(3)  # grouping for 3 steps from the cursor (5) is the current one: 1 step, then 2
+    assert a.ring_offset == 0
+    a.run(3)
+    for cols, lab in batches:
+        b.load_batch(cols, lab)
+        b.step()
+    torch.cuda.synchronize()
+    assert a.ring_cursor == 0
+    assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
+    assert torch.equal(a.params, b.params) and float(a.loss) == float(b.loss)

@@ -593,33 +593,63 @@ class FusedTwoTowerStep:
         torch.cuda.synchronize(self.device)
         self.ring_cursor = 0
         self.ring_k = k
+        self._ring_keep = keep_graph
+        self.ring_small = [self._ring_graph([i]) for i in range(n)]
+        self._ring_groups(0)
 
-        def cap(idx):
-            g = torch.cuda.CUDAGraph(keep_graph=keep_graph)
-            s = torch.cuda.Stream(device=self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
-                    for i in idx:
-                        self.ring_step(staged[i][0], staged[i][1], i % 2, staged[(i + 1) % n][0])
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            return g
+    def _ring_graph(self, idx) -> torch.cuda.CUDAGraph:
+        """One HIP graph of the production steps of pool batches ``idx`` (in order)."""
+        staged, n = self._ring_inputs, len(self._ring_inputs)
+        g = torch.cuda.CUDAGraph(keep_graph=self._ring_keep)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for i in idx:
+                    self.ring_step(staged[i][0], staged[i][1], i % 2, staged[(i + 1) % n][0])
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        _lib.graph_upload(g, self.device)
+        return g
 
-        self.ring_graphs = [cap(range(j, j + k)) for j in range(0, n, k)]
-        self.ring_small = [cap([i]) for i in range(n)] if k > 1 else list(self.ring_graphs)
+    def _ring_groups(self, offset: int) -> None:
+        """The multi-step graphs, grouped from pool position ``offset``: k-step graphs, and (k a
+        power of two) k/2, k/4, ..., 2-step ones at the same alignment, so a run replays few graph
+        launches (one costs the host ~35-55 us, about one step of GPU time: single-step graphs leave
+        the GPU idle between them)."""
+        n, k = len(self._ring_inputs), self.ring_k
+        span = lambda j, sz: [(offset + j + t) % n for t in range(sz)]  # noqa: E731
+        self.ring_offset = offset % n
+        self.ring_graphs = [self._ring_graph(span(j, k)) for j in range(0, n, k)] if k > 1 else list(self.ring_small)
+        self.ring_mid = {}
+        sz = k // 2 if k & (k - 1) == 0 else 0
+        while sz >= 2:
+            self.ring_mid[sz] = [self._ring_graph(span(j, sz)) for j in range(0, n, sz)]
+            sz //= 2
         torch.cuda.synchronize(self.device)
+
+    def align_ring(self, n_next: int = 0) -> None:
+        """Regroup the multi-step graphs for a run of ``n_next`` steps from the cursor (the training
+        state is untouched: only how the steps are grouped into graph launches changes): the run
+        replays its n_next % k remainder first, in aligned smaller graphs (the first launch is the
+        cheapest: the GPU starts sooner), then n_next // k full graphs — no single-step graphs when
+        the remainder is a sum of the captured sizes."""
+        off = (self.ring_cursor + (n_next % self.ring_k)) % len(self.ring_small)
+        if self.ring_k > 1 and off != self.ring_offset:
+            self._ring_groups(off)
 
     def run(self, n: int) -> None:
         """Replay n production steps from the ring, continuing at the cursor."""
         i, nb, k = self.ring_cursor, len(self.ring_small), self.ring_k
+        mid = self.ring_mid
         while n > 0:
-            if i % k == 0 and n >= k:
-                self.ring_graphs[i // k].replay()
-                i, n = i + k, n - k
+            r = (i - self.ring_offset) % nb  # position relative to the graphs' grouping
+            if r % k == 0 and n >= k:
+                self.ring_graphs[r // k].replay()
+                sz = k
             else:
-                self.ring_small[i].replay()
-                i, n = i + 1, n - 1
-            i %= nb
+                sz = next((m for m in sorted(mid, reverse=True) if r % m == 0 and n >= m), 1)
+                (mid[sz][r // sz] if sz > 1 else self.ring_small[i]).replay()
+            i, n = (i + sz) % nb, n - sz
         self.ring_cursor = i
 
     def timed_ring(self, n: int) -> dict:
