@@ -608,7 +608,8 @@ class FusedTwoTowerStep:
                 for i in idx:
                     self.ring_step(staged[i][0], staged[i][1], i % 2, staged[(i + 1) % n][0])
         torch.cuda.current_stream(self.device).wait_stream(s)
-        _lib.graph_upload(g, self.device)
+        if not self._ring_keep:  # keep_graph: instantiated later, by its user
+            _lib.graph_upload(g, self.device)
         return g
 
     def _ring_groups(self, offset: int) -> None:
@@ -699,6 +700,8 @@ class FusedTwoTowerStep:
                         self.step()
         self.cols, self.labels = keep_cols, keep_labels
         torch.cuda.current_stream(self.device).wait_stream(s)
+        if not keep_graph:
+            _lib.graph_upload(g, self.device)
         torch.cuda.synchronize(self.device)
         self.graph = g
 
