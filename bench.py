@@ -518,12 +518,12 @@ def run_single(args):
     def run(n):
         step.run(n)
 
+    # group the timed steps into graph launches (the remainder in aligned smaller graphs first, then
+    # k-step graphs): a warmup or step count that is not a multiple of k would otherwise leave
+    # single-step graphs in the timed region. Regrouped BEFORE the warmup, so the warmup's steps
+    # run right up to the timed region (no capture pause between them)
+    step.align_ring(args.steps, after=args.warmup)
     run(args.warmup)
-    # group the timed steps into graph launches from the cursor (the remainder in aligned smaller
-    # graphs first, then k-step graphs): a warmup or step count that is not a multiple of k would
-    # otherwise leave single-step graphs in the timed region, each a host launch (~35-55 us) for
-    # ~40 us of GPU work
-    step.align_ring(args.steps)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)

@@ -628,13 +628,13 @@ class FusedTwoTowerStep:
             sz //= 2
         torch.cuda.synchronize(self.device)
 
-    def align_ring(self, n_next: int = 0) -> None:
-        """Regroup the multi-step graphs for a run of ``n_next`` steps from the cursor (the training
-        state is untouched: only how the steps are grouped into graph launches changes): the run
-        replays its n_next % k remainder first, in aligned smaller graphs (the first launch is the
-        cheapest: the GPU starts sooner), then n_next // k full graphs — no single-step graphs when
-        the remainder is a sum of the captured sizes."""
-        off = (self.ring_cursor + (n_next % self.ring_k)) % len(self.ring_small)
+    def align_ring(self, n_next: int = 0, after: int = 0) -> None:
+        """Regroup the multi-step graphs for a run of ``n_next`` steps that starts ``after`` steps
+        from the cursor (the training state is untouched: only how the steps are grouped into graph
+        launches changes): that run replays its n_next % k remainder first, in aligned smaller
+        graphs (the first launch is the cheapest: the GPU starts sooner), then n_next // k full
+        graphs — no single-step graphs when the remainder is a sum of the captured sizes."""
+        off = (self.ring_cursor + after + (n_next % self.ring_k)) % len(self.ring_small)
         if self.ring_k > 1 and off != self.ring_offset:
             self._ring_groups(off)
 
