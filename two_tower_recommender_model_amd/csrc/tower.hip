@@ -1564,6 +1564,7 @@ struct UpdateArgs {
   __bf16* wtb;
   __bf16* wbf;
   __bf16* wtbf;
+  int skip_plain;  // wb / wtb unused by this shape's T1 (tower_l2_kernel): not written
   float lr, beta1, beta2, eps, wd;
   int64_t* step_state;
   int do_adam;
@@ -1661,8 +1662,10 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
     if (sisw) {
       const int K = sk, N = sn;
       const int64_t n = e / K, k = e - n * K;
-      a.wb[swc + e] = (__bf16)p;
-      a.wtb[swc + k * N + n] = (__bf16)p;
+      if (!a.skip_plain) {
+        a.wb[swc + e] = (__bf16)p;
+        a.wtb[swc + k * N + n] = (__bf16)p;
+      }
       a.wbf[swc + frag_off((int)n, (int)k, K)] = (__bf16)p;   // W as [N][K]
       a.wtbf[swc + frag_off((int)k, (int)n, N)] = (__bf16)p;  // W^T as [K][N]
     }
@@ -2292,6 +2295,9 @@ static int t3_args(const tt_tower_shape_t* shape, int64_t B, float* params, floa
   a.wtb = reinterpret_cast<__bf16*>(ws + L.o_wtb);
   a.wbf = reinterpret_cast<__bf16*>(ws + L.o_wbf);
   a.wtbf = reinterpret_cast<__bf16*>(ws + L.o_wtbf);
+  // the plain [out][in] / [in][out] bf16 copies are read only by tower_fwd_bwd_kernel, which
+  // launch_t1 uses for shapes other than two layers over inputs <= 128 wide
+  a.skip_plain = shape->L == 2 && shape->in_dim[0] <= 128 && shape->in_dim[1] <= 128;
   a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.wd = weight_decay;
   a.step_state = step_state;
   a.do_adam = do_adam;
