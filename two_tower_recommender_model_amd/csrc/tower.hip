@@ -864,17 +864,31 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   T1_WSTAMP(1);
   __syncthreads();
   T1_STAMP(1);
-  // X^T for T2's dW0 (fire-and-forget stores)
-  for (int e = tt; e < ((a.dbg & 1) ? 0 : in * (TR / 8)); e += 256) {
-    const int k = e / (TR / 8), rb = (e % (TR / 8)) * 8;
-    bf16x8 v;
-    for (int j = 0; j < 8; ++j) v[j] = xs[t][(rb + j) * LSTR + k];
-    __bf16* dst = xt_tile + k * TR + rb;
-    if (rb + 8 <= nval) {
-      *reinterpret_cast<bf16x8*>(dst) = v;
-    } else {
-      for (int j = 0; j < 8; ++j)
-        if (rb + j < nval) dst[j] = v[j];
+  // X^T for T2's dW0 (fire-and-forget stores). A 16-lane group takes a block of 16 columns x 8
+  // rows of X with two transposed LDS reads (ds_read_b64_tr_b16: lane 4 q' + p addresses row q',
+  // columns 4 p .. 4 p + 3 of a 4-row block; lane i receives column i): lane i then holds rows
+  // r0 .. r0 + 7 of column c0 + i, one 16-B strip store. Every lane executes the reads (full EXEC):
+  // groups past the last block read block 0 and store nothing.
+  if (!(a.dbg & 1)) {
+    const int g16 = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int nblk = (in / 16) * (TR / 8);  // blocks of 16 columns x 8 rows
+    for (int b0 = w4 * 4; b0 < nblk; b0 += 16) {  // wave-uniform
+      const int b = b0 + g16;
+      const bool own = b < nblk;
+      const int cb = own ? b % (in / 16) : 0, r0 = own ? (b / (in / 16)) * 8 : 0;
+      const __bf16* src = xs[t] + (r0 + qq) * LSTR + cb * 16 + 4 * pp;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)src);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(src + 4 * LSTR));
+      const bf16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      if (own) {
+        __bf16* dst = xt_tile + (cb * 16 + i16) * TR + r0;
+        if (r0 + 8 <= nval) {
+          *reinterpret_cast<bf16x8*>(dst) = v;
+        } else {
+          for (int j = 0; j < 8; ++j)
+            if (r0 + j < nval) dst[j] = v[j];
+        }
+      }
     }
   }
   T1_WSTAMP(11);
