@@ -626,7 +626,7 @@ def run_multi(args, world, rank, local_rank):
 
     num_users, num_items, D, B, layers = WORKLOADS[args.workload]
     N = [num_users, num_items]
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", local_rank % torch.cuda.device_count())  # (rehearsal: ranks may share one GPU)
     comm = TorchComm(always_collective=True)
     k = args.steps_per_graph
     nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k
@@ -643,11 +643,14 @@ def run_multi(args, world, rank, local_rank):
     step.step()  # creates the RCCL communicators before any capture
     mode = "hipgraph"
     ok = torch.ones(1, device=dev)
-    try:
-        step.capture_pool(batches, steps_per_graph=k)
-    except Exception as e:  # noqa: BLE001 - fall back to eager launches, same work per step
-        print(f"rank {rank}: graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
-        ok.zero_()
+    if os.environ.get("TT_REHEARSE_GLOO") == "1":
+        ok.zero_()  # gloo collectives are not capturable: eager steps
+    else:
+        try:
+            step.capture_pool(batches, steps_per_graph=k)
+        except Exception as e:  # noqa: BLE001 - fall back to eager launches, same work per step
+            print(f"rank {rank}: graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
+            ok.zero_()
     torch.cuda.synchronize()
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
     if float(ok) < 1:
@@ -721,11 +724,19 @@ def main():
     elif world == 1 and not args.sharded:
         value, ms, loss, roofline, cpu, steps_run = run_single(args)
     else:
+        # TT_REHEARSE_GLOO=1 (testing only, never a bench line): gloo collectives and ranks sharing the
+        # visible GPUs, to run the N > 1 code path (routes, capacities, flags, eager collectives) on a
+        # one-GPU box; the production path is RCCL, one GPU per rank
+        rehearse = os.environ.get("TT_REHEARSE_GLOO") == "1"
+        if rehearse:
+            local_rank = local_rank % torch.cuda.device_count()
         torch.cuda.set_device(local_rank)
         from two_tower_recommender_model_amd.sharded import graph_safe_nccl_env
 
         graph_safe_nccl_env()  # RCCL collectives inside HIP graphs (before the process group exists)
-        if "RANK" in os.environ:
+        if rehearse:
+            dist.init_process_group("gloo")
+        elif "RANK" in os.environ:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:  # --sharded without a launcher (e.g. under rocprofv3): a one-rank group
             dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),

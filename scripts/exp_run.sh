@@ -1,5 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-bash scripts/gpu_round.sh || exit $?
-OUT=gpurun_out/pmc_ns bash scripts/pmc_traffic.sh > gpurun_out/pmc_ns.log 2>&1 || exit $?
+timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_multiproc_rehearsal.py > gpurun_out/t_reh.log 2>&1 || exit $?
