@@ -15,16 +15,17 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_two_processes_gloo_rehearsal():
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_multiprocess_gloo_rehearsal(world):
     env = dict(os.environ, TT_REHEARSE_GLOO="1", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29517", "bench.py", "--gpus", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(29517 + world), "bench.py", "--gpus", str(world),
            "--workload", "config2", "--steps", "4", "--warmup", "2", "--batches", "8", "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
-    assert d["n_gpus"] == 2 and d["steps"] == 4 and d["value"] > 0
+    assert d["n_gpus"] == world and d["steps"] == 4 and d["value"] > 0
     sh = d["config"]["sharded"]
     assert sh["mode"] == "eager" and sh["capacity"] >= sh["capacity_needed"]
     assert d["roofline"]["alg_bytes_per_step"] > 0 and d["loss"] == d["loss"]  # finite
