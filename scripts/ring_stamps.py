@@ -61,7 +61,7 @@ for it in range(6):
     if it < 2:
         continue
     if st.ring_tail:
-        n_ins, dd = 64, int(os.environ.get("K3_DD", "576"))
+        n_ins, dd = 32, int(os.environ.get("K3_DD", "576"))
         show("tail", base[4096:6144], [("insert", 0, n_ins), ("tiles", n_ins, n_ins + ntile),
                                        ("bias", n_ins + ntile, n_ins + ntile + nbias),
                                        ("hot", n_ins + ntile + nbias, n_ins + ntile + nbias + 64),

@@ -1754,17 +1754,103 @@ __global__ void __launch_bounds__(256) tower_update_dedup_resolve_kernel(UpdateA
 // than once. The three roles read only what T1 (or the previous step) wrote; T3 follows as its own
 // launch (it needs every T2 slab: in-launch, that hand-off across the 8 XCDs' L2s cost more than
 // the launch boundary it saves — DESIGN.md section 5).
-// the NEXT batch's lookups, one per thread, inserted completely (probing in place)
-__device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, int blk) {
-  const int64_t i = (int64_t)blk * 256 + threadIdx.x;
-  if (i >= 2 * ins.B) return;
-  const int t = i >= ins.B;
-  const int64_t m = i - (t ? ins.B : 0);
-  const int64_t id = load_id(t ? ins.col[1] : ins.col[0], ins.id_dtype, m);
-  const uint64_t key = id != 0 ? (((uint64_t)(t ? ins.tab[1] : ins.tab[0]) << DD_TABLE_SHIFT) |
-                                  (uint64_t)py_mod64(id, t ? ins.mod[1] : ins.mod[0]))
-                               : DD_EMPTY;
-  dd_insert(ins.dd, key, (int32_t)i);
+// the NEXT batch's lookups, INS_PT per thread, inserted completely (probing in place). The
+// workgroup's repeated keys are merged in LDS first: one leader per key claims or joins the key's
+// slot with the group's count in ONE global atomic and hands each member its position (base +
+// rank in the group) — at skewed ids a hot row costs one atomic per workgroup, not one per lookup
+// (the update sums a row's lookups in lookup order whatever the positions: the same results).
+constexpr int INS_PT = 2;     // lookups per thread: 512 per workgroup
+constexpr int INS_HS = 1024;  // LDS hash slots per 512 lookups
+static_assert(INS_HS * (8 + 3 * 4) <= T2_SMEM, "the insert role's LDS hash fits the tail's LDS");
+__device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, int blk, char* smem) {
+  unsigned long long* hk = reinterpret_cast<unsigned long long*>(smem);  // [INS_HS] keys
+  int* hc = reinterpret_cast<int*>(smem + 8 * INS_HS);                   // [INS_HS] group counts
+  int* hb = hc + INS_HS;                                                 // [INS_HS] group base position
+  int* hg = hb + INS_HS;                                                 // [INS_HS] global slot
+  const DedupWs& ws = ins.dd;
+  for (int q = threadIdx.x; q < INS_HS; q += 256) {
+    hk[q] = DD_EMPTY;
+    hc[q] = 0;
+  }
+  int64_t iv[INS_PT];
+  uint64_t key[INS_PT];
+#pragma unroll
+  for (int u = 0; u < INS_PT; ++u) {
+    const int64_t i = ((int64_t)blk * INS_PT + u) * 256 + threadIdx.x;
+    iv[u] = i;
+    key[u] = DD_EMPTY;
+    if (i < 2 * ins.B) {
+      const int t = i >= ins.B;
+      const int64_t m = i - (t ? ins.B : 0);
+      const int64_t id = load_id(t ? ins.col[1] : ins.col[0], ins.id_dtype, m);
+      if (id != 0)
+        key[u] = ((uint64_t)(t ? ins.tab[1] : ins.tab[0]) << DD_TABLE_SHIFT) |
+                 (uint64_t)py_mod64(id, t ? ins.mod[1] : ins.mod[0]);
+      ws.lkey[i] = key[u];
+    }
+  }
+  __syncthreads();
+  int hl[INS_PT], rank[INS_PT];
+#pragma unroll
+  for (int u = 0; u < INS_PT; ++u) {
+    hl[u] = -1;
+    rank[u] = 0;
+    if (key[u] != DD_EMPTY) {
+      unsigned h = (unsigned)dd_mix64(key[u]) & (INS_HS - 1);
+      while (true) {
+        const unsigned long long prev = atomicCAS(&hk[h], (unsigned long long)DD_EMPTY, (unsigned long long)key[u]);
+        if (prev == DD_EMPTY || prev == key[u]) break;
+        h = (h + 1) & (INS_HS - 1);
+      }
+      hl[u] = (int)h;
+      rank[u] = atomicAdd(&hc[h], 1);
+    }
+  }
+  __syncthreads();
+  // each group's leader: one claiming CAS (with the group's count) or one add of it
+  const uint64_t mask = (uint64_t)ws.cap - 1;
+#pragma unroll
+  for (int u = 0; u < INS_PT; ++u) {
+    if (hl[u] >= 0 && rank[u] == 0) {
+      const uint64_t c = (uint64_t)hc[hl[u]];
+      uint64_t g = dd_mix64(key[u]) & mask;
+      int base;
+      while (true) {
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(&ws.slots[g].word);
+        const unsigned long long prev =
+            atomicCAS(w, (unsigned long long)DD_EMPTY, (unsigned long long)((key[u] << DD_CNT_BITS) | c));
+        if (prev == DD_EMPTY) {
+          base = 0;
+          break;
+        }
+        if ((prev >> DD_CNT_BITS) == key[u]) {
+          base = (int)(atomicAdd(w, (unsigned long long)c) & DD_CNT_MASK);
+          break;
+        }
+        g = (g + 1) & mask;
+      }
+      hb[hl[u]] = base;
+      hg[hl[u]] = (int)g;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < INS_PT; ++u) {
+    const int64_t i = iv[u];
+    if (i >= 2 * ins.B) continue;
+    if (hl[u] < 0) {
+      ws.claim[i] = -1;
+      continue;
+    }
+    const int k = hb[hl[u]] + rank[u], h = hg[hl[u]];
+    ws.claim[i] = k == 0 ? h : -1;
+    if (k < DD_INL) {
+      ws.slots[h].item[k] = (int32_t)i;
+    } else if (k == DD_INL) {
+      const int q = atomicAdd(&ws.ctr[0], 1);
+      if (q < ws.hot_cap) ws.hot[q] = h;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256) tower_tail_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
@@ -1774,7 +1860,7 @@ __global__ void __launch_bounds__(256) tower_tail_kernel(WgradArgs a2, const Wgr
   int b = (int)blockIdx.x;
   RING_STAMP(stamps, 0);
   if (b < n_ins)
-    insert_next_full_block(ins, b);
+    insert_next_full_block(ins, b, smem);
   else if ((b -= n_ins) < n_t2)
     wgrad_block(a2, tiles, b, smem);  // n_ins % 8 == 0: b keeps the XCD placement of wgrad_block
   else
@@ -2772,7 +2858,7 @@ int tt_tower_wgrad_pre_insert_rowwise_adagrad(const tt_tower_shape_t* shape, int
                          dedup_max_lookups, d, &dd_grid);
   if (rc) return rc;
   d.skip_single = 1;
-  const int64_t n_ins = ceil_div(ceil_div(2 * B, 256), 8) * 8;  // one lookup per thread; % 8 == 0
+  const int64_t n_ins = ceil_div(ceil_div(2 * B, 256 * INS_PT), 8) * 8;  // INS_PT lookups per thread; % 8 == 0
   int64_t* stamps = getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
   if (stamps && L.nwg > 256) stamps = nullptr;
   tower_tail_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
