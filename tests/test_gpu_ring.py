@@ -74,3 +74,60 @@ def test_ring_mixed_graph_sizes(device):
     assert a.ring_cursor == 0
     assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
     assert torch.equal(a.params, b.params) and float(a.loss) == float(b.loss)
+
+
+def test_ring_extreme_skew(device):
+    """Every item lookup of a batch on ONE row (8192 lookups: a hot row split over a team of
+    workgroups, its insert merged in LDS per workgroup), a few hundred distinct rows in another
+    batch (rows of 2..30 and > 30 lookups), user ids uniform: the ring equals the classic step bit
+    for bit over 4 steps in graphs."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N, B = [3_000_000, 5_000_000], 8192
+    g = torch.Generator().manual_seed(11)
+    batches = []
+    for s in range(4):
+        cols = [torch.randint(1, N[0], (B,), generator=g), torch.randint(1, N[1], (B,), generator=g)]
+        if s % 2 == 0:
+            cols[1][:] = 4_242_424 + s             # one row, B lookups
+        else:
+            cols[1] = torch.randint(1, 300, (B,), generator=g)  # ~300 rows, ~27 lookups each
+        lab = torch.randint(0, 2, (B,), generator=g).to(torch.int32)
+        batches.append(([c.to(device) for c in cols], lab.to(device)))
+    a = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=3)
+    b = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=3)
+    a.capture_ring(batches, steps_per_graph=2)
+    a.run(4)
+    for cols, lab in batches:
+        b.load_batch(cols, lab)
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
+    assert torch.equal(a.params, b.params) and float(a.loss) == float(b.loss)
+
+
+def test_ring_one_row_batch_vs_formula(device):
+    """A batch whose 8192 item lookups all hit ONE row: the row's row-wise Adagrad step (gradient =
+    the sum of the 8192 dX rows T1 left in gpooled, summed by a team of workgroups) against the
+    formula in float64 on the host (rtol 1e-4: the team's summation order is not the host's)."""
+    import numpy as np
+
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N, B, D, lr, row = [3_000_000, 5_000_000], 8192, 128, 0.01, 4_242_424
+    g = torch.Generator().manual_seed(12)
+    batches = []
+    for s in range(2):
+        cols = [torch.randint(1, N[0], (B,), generator=g), torch.full((B,), row + s, dtype=torch.int64)]
+        batches.append(([c.to(device) for c in cols], torch.randint(0, 2, (B,), generator=g).to(torch.int32).to(device)))
+    st = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=4, lr_emb=lr)
+    w0 = st.tables.table_view(1)[row].double().cpu().clone()
+    s0 = float(st.tables.state_view(1)[row])
+    st.capture_ring(batches, steps_per_graph=2)
+    st.run(1)
+    torch.cuda.synchronize()
+    G = st.gpooled[:, D:2 * D].double().cpu().sum(0)
+    s1 = s0 + float((G * G).mean())
+    w1 = w0 - lr * G / (np.sqrt(s1) + 1e-10)
+    np.testing.assert_allclose(float(st.tables.state_view(1)[row]), s1, rtol=1e-4)
+    np.testing.assert_allclose(st.tables.table_view(1)[row].double().cpu().numpy(), w1.numpy(), rtol=1e-4, atol=1e-7)
