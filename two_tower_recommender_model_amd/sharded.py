@@ -34,6 +34,7 @@ all-reduced over the ranks).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -709,6 +710,8 @@ class FusedShardedTwoTowerStep:
                 with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     for i in idx:
                         self.step_pipelined(staged[i][1], i % 2, staged[(i + 2) % n][0])
+                        if os.environ.get("TT_TEST_CAPTURE_FAIL") == "1":  # test hook: the eager fallback
+                            raise _lib.TTError("capture refused (TT_TEST_CAPTURE_FAIL)")
             torch.cuda.current_stream(self.device).wait_stream(s)
             _lib.graph_upload(g, self.device)  # no upload inside the first (timed) launch
             return g
