@@ -38,6 +38,7 @@ CFLAGS = [
     f"-I{CSRC}",
     "-Wall",
     "-Wno-unused-function",
+    *os.environ.get("TT_EXTRA_CFLAGS", "").split(),  # experiments only (e.g. -DDD_HOT_STAMPS=1)
 ]
 
 

@@ -232,6 +232,9 @@ __device__ __forceinline__ int dd_bitonic(int v) {
 constexpr int DD_HOT_PT = 16;                // lookups per thread per scan pass (4096 a pass)
 constexpr int DD_HOT_CH = 256 * DD_HOT_PT;  // lookups scanned per pass of a hot workgroup (LDS list)
 constexpr int DD_HOT_TEAM = 8;              // at most this many workgroups share one hot row
+#ifndef DD_HOT_STAMPS
+#define DD_HOT_STAMPS 0  // EXPERIMENT (scripts/hot_stamps.py; build with TT_EXTRA_CFLAGS=-DDD_HOT_STAMPS=1)
+#endif
 // LDS of the hot role (list + wave totals + group partials), provided by the launching kernel so a
 // combined launch can overlay it on its other roles' LDS
 constexpr int DD_SMEM_HOT = DD_HOT_CH * 4 + 16 + 8 * 32 * 16;
@@ -312,6 +315,9 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
       }
       if (lane == 63) wtot[wid] = inc;
       __syncthreads();
+#if DD_HOT_STAMPS
+      if (p == k) DD_STAMP(4);  // first pass: keys matched, scanned
+#endif
       int base = 0, total = 0;
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
@@ -339,6 +345,9 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
     }
     part[grp][hl] = acc;
     __syncthreads();
+#if DD_HOT_STAMPS
+    DD_STAMP(5);  // the member's passes summed
+#endif
     if (wid == 0) {
       f32x4v g = part[0][hl];
 #pragma unroll
@@ -355,6 +364,9 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
         if (lane == 0) prev = __hip_atomic_fetch_add(&ws.hcnt[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         prev = __shfl(prev, 0, 64);
         last = prev == K - 1;
+#if DD_HOT_STAMPS
+        DD_STAMP(6);  // partial published, counter added
+#endif
         if (last) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
           const float* all = ws.hotp + (int64_t)j * DD_HOT_TEAM * 128 + hl * 4;
@@ -388,6 +400,9 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
             *srow = snew;
             ws.slots[h].word = DD_EMPTY;
           }
+#if DD_HOT_STAMPS
+          DD_STAMP(7);  // row update issued
+#endif
         }
       }
     }
