@@ -68,6 +68,11 @@ def parse():
                     help="multi-hot workloads: group each batch inside its own step instead of one step ahead")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
+    ap.add_argument("--plan", default="auto", choices=["auto", "tw", "rw"],
+                    help="N > 1 sharding plan of the two tables: tw = table-wise (users on rank 0, items on rank "
+                         "1), rw = row-wise over all ranks; auto = tw at N = 2 (the same per-rank load as rw), rw "
+                         "from N = 4 (tw would leave N - 2 ranks without a table and give the two owners N / 2 x "
+                         "the lookups of a row-wise owner; DESIGN.md section 6)")
     return ap.parse_args()
 
 
@@ -621,8 +626,8 @@ def run_multi(args, world, rank, local_rank):
     collectives inside (eager launches if capture is refused). Segment capacities are sized from the
     resident batches (max over batches and ranks), so no timed step can overflow; the sticky
     overflow / bad-key flags are all-reduced and checked before and after the timed region."""
-    from two_tower_recommender_model_amd.sharded import (FusedShardedTwoTowerStep, TorchComm, default_capacity,
-                                                         segment_counts)
+    from two_tower_recommender_model_amd.sharded import (FusedShardedTwoTowerStep, TorchComm,
+                                                         capture_pool_or_eager, default_capacity, segment_counts)
 
     num_users, num_items, D, B, layers = WORKLOADS[args.workload]
     N = [num_users, num_items]
@@ -631,33 +636,25 @@ def run_multi(args, world, rank, local_rank):
     k = args.steps_per_graph
     nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k
     batches = synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1 + rank)
-    blocks = [-(-n // world) for n in N]
+    plan = args.plan if args.plan != "auto" else ("tw" if world == 2 else "rw")
+    if plan == "tw" and world < 2:
+        plan = "rw"  # one rank holds everything either way
+    tw_owners = [0, 1 % world]
+    sharding = ["table_wise"] * 2 if plan == "tw" else ["row_wise"] * 2
+    blocks = [0, 0] if plan == "tw" else [-(-n // world) for n in N]
+    owners = tw_owners if plan == "tw" else [0, 0]
     need = torch.zeros(1, dtype=torch.int64)
     for cols, _ in batches:
-        need = torch.maximum(need, segment_counts(cols, N, blocks, [0, 0], world).max().reshape(1))
+        need = torch.maximum(need, segment_counts(cols, N, blocks, owners, world).max().reshape(1))
     need = need.to(dev)
     dist.all_reduce(need, op=dist.ReduceOp.MAX)
     cap = max(default_capacity(B, world), -(-int(need) // 8) * 8)
-    step = FusedShardedTwoTowerStep(comm, N, D, layers, B, dev, lr_emb=0.01, lr_dense=0.01, seed=0, capacity=cap)
+    step = FusedShardedTwoTowerStep(comm, N, D, layers, B, dev, sharding=sharding, tw_owners=tw_owners, lr_emb=0.01,
+                                    lr_dense=0.01, seed=0, capacity=cap)
     step.load_batch(*batches[0])
     step.step()  # creates the RCCL communicators before any capture
-    mode = "hipgraph"
-    ok = torch.ones(1, device=dev)
-    if os.environ.get("TT_REHEARSE_GLOO") == "1":
-        ok.zero_()  # gloo collectives are not capturable: eager steps
-    else:
-        try:
-            step.capture_pool(batches, steps_per_graph=k)
-        except Exception as e:  # noqa: BLE001 - fall back to eager launches, same work per step
-            print(f"rank {rank}: graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
-            ok.zero_()
-    torch.cuda.synchronize()
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
-    if float(ok) < 1:
-        mode = "eager"
-        step.release_graphs()
-        step.cursor = None
-        dist.barrier()
+    # gloo collectives (TT_REHEARSE_GLOO, testing only) are not capturable: eager steps
+    mode = capture_pool_or_eager(step, batches, k, allow_capture=os.environ.get("TT_REHEARSE_GLOO") != "1")
 
     def run(n):
         if mode == "eager":
@@ -692,7 +689,9 @@ def run_multi(args, world, rank, local_rank):
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_step": emb_bytes, "unique_rows": uniq,
                 "timing": "SURVEY 8(d) bytes per rank over the max-over-ranks step time (collectives included)"}
-    info = {"capacity": cap, "capacity_needed": int(need), "resident_batches": nb,
+    info = {"plan": {"tw": "table-wise (user_id -> rank 0, product_id -> rank 1)",
+                     "rw": f"row-wise (blocks of ceil(N / {world}) rows)"}[plan],
+            "capacity": cap, "capacity_needed": int(need), "resident_batches": nb,
             "exchange_A_bytes_sent": 4 * step.A_total,
             "exchange_B_bytes_sent": 2 * D * world * step.S[r],
             "collectives_per_step": 2, "mode": mode}
@@ -743,7 +742,7 @@ def main():
                                     device_id=torch.device("cuda", local_rank))
         value, ms, loss, sharded_info, roofline = run_multi(args, world, rank, local_rank)
         cpu, steps_run = None, args.steps
-        config["parallelism"] = (f"row-wise sharded tables + data-parallel towers x{world}: pipelined, 2 RCCL "
+        config["parallelism"] = (f"{sharded_info['plan']} sharded tables + data-parallel towers x{world}: pipelined, 2 RCCL "
                                  f"all-to-alls per step ([grad rows | tower grad | next ids], next rows), "
                                  f"{sharded_info['mode']}")
         config["sharded"] = sharded_info

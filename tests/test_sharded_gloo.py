@@ -250,7 +250,7 @@ def _pipe_worker(rank, world, port, out_q):
             orig = mod.forward
 
             def fwd(features, orig=orig, mod=mod):
-                staged.append(id(features) in mod._prefetched)
+                staged.append(any(k is features for k, _ in mod._prefetched))
                 return orig(features)
 
             mod.forward = fwd

@@ -361,12 +361,8 @@ class FusedShardedTwoTowerStep:
         # dedup workspaces: batch i inserts at gather(i), Adagrad(i) consumes: two in flight
         self.max_lookups = max(1, W * self.S[r])
         nbytes = _lib.load().tt_dedup_workspace_bytes(self.max_lookups)
-        self.dd_ws = []
-        for _ in range(2):
-            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-            check(_lib.load().tt_dedup_workspace_init(ptr(ws), nbytes, self.max_lookups, stream_handle(dev)),
-                  "dedup_workspace_init")
-            self.dd_ws.append(ws)
+        self.dd_ws = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self._init_dedup()
         # Adagrad over the received gradient rows: one pseudo-feature per source block
         self._fm_src = (FeatureMeta * W)()
         for s in range(W):
@@ -393,6 +389,22 @@ class FusedShardedTwoTowerStep:
         torch.cuda.synchronize(dev)
 
     # ------------------------------------------------------------------------------------------
+    def _init_dedup(self) -> None:
+        for ws in self.dd_ws:
+            check(_lib.load().tt_dedup_workspace_init(ptr(ws), ws.numel(), self.max_lookups,
+                                                      stream_handle(self.device)), "dedup_workspace_init")
+
+    def reset_pipeline(self) -> None:
+        """Drop the pipelined state (the staged rows of the batch at the cursor and the keys both
+        dedup tables hold for it and the next batch): the next pipelined run primes again. Needed
+        whenever the staged state is stale or was never consumed: a capture that was refused after
+        ``prime`` (its steps never ran), a ``load_state_dict`` in the middle of a run, a switch
+        between the synchronous and the pipelined step. A dedup table filed twice with the same keys
+        would join its own slots: those rows would never be updated."""
+        torch.cuda.synchronize(self.device)
+        self._init_dedup()
+        self.cursor = None
+
     def _layout(self) -> None:
         W, F, D, P = self.W, self.F, self.D, self.towers.num_params
         rup = lambda x, m: -(-x // m) * m  # noqa: E731
@@ -524,6 +536,8 @@ class FusedShardedTwoTowerStep:
         """One synchronous step on the batch in ``cols`` / ``labels`` (no later batch known: ids,
         rows, gradient rows and tower gradients each take an exchange)."""
         lib, tw = _lib.load(), self.towers
+        if self.cursor is not None:  # a pipelined run left batches staged in the dedup tables
+            self.reset_pipeline()
         self._route(self.cols, 0)
         self._exchange_a()
         self._gather(0)
@@ -542,7 +556,9 @@ class FusedShardedTwoTowerStep:
 
     def prime(self, cols: Sequence[torch.Tensor], parity: int, next_cols: Optional[Sequence[torch.Tensor]] = None) -> None:
         """Stage the rows of a batch (the pipelined loop's first step) and, with ``next_cols``, place
-        the following batch's keys (its route, parity ^ 1)."""
+        the following batch's keys (its route, parity ^ 1). Starts from empty dedup tables (a
+        second prime over staged state would file the same keys twice)."""
+        self.reset_pipeline()
         self._route(cols, parity)
         self._exchange_a()
         self._gather(parity)
@@ -639,6 +655,9 @@ class FusedShardedTwoTowerStep:
                 self.exp_avg_sq.zero_()
                 self.adam_state.zero_()
         self.towers.update(self.params, do_adam=False)
+        # rows staged before the load are stale, and the dedup tables were filed for them: the next
+        # pipelined run (graph replay or eager) primes again from the loaded weights
+        self.reset_pipeline()
 
     def check(self, collective: bool = True) -> None:
         """Raise if any step so far overflowed a segment or received a key outside its shard. With
@@ -710,8 +729,6 @@ class FusedShardedTwoTowerStep:
                 with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     for i in idx:
                         self.step_pipelined(staged[i][1], i % 2, staged[(i + 2) % n][0])
-                        if os.environ.get("TT_TEST_CAPTURE_FAIL") == "1":  # test hook: the eager fallback
-                            raise _lib.TTError("capture refused (TT_TEST_CAPTURE_FAIL)")
             torch.cuda.current_stream(self.device).wait_stream(s)
             _lib.graph_upload(g, self.device)  # no upload inside the first (timed) launch
             return g
@@ -722,7 +739,14 @@ class FusedShardedTwoTowerStep:
         torch.cuda.synchronize(self.device)
 
     def run(self, n: int) -> None:
-        """Replay n pipelined steps from the pool, continuing at the cursor."""
+        """Replay n pipelined steps from the pool, continuing at the cursor (re-primed at the pool's
+        first batch after ``reset_pipeline`` / ``load_state_dict``)."""
+        if not self.small_graphs:
+            raise _lib.TTError("run: no captured pool (capture_pool first)")
+        if self.cursor is None:
+            staged = self._pool_inputs[0]
+            self.prime(staged[0][0], 0, staged[1][0])
+            self.cursor = 0
         i, nb, k = self.cursor, len(self.small_graphs), self.pool_k
         while n > 0:
             if i % k == 0 and n >= k:
@@ -746,3 +770,32 @@ class FusedShardedTwoTowerStep:
             i = self.cursor
             self.step_pipelined(batches[i][1].to(torch.int32), i % 2, list(batches[(i + 2) % nb][0]))
             self.cursor = (i + 1) % nb
+
+
+def capture_pool_or_eager(step: FusedShardedTwoTowerStep, batches: Sequence, steps_per_graph: int,
+                          allow_capture: bool = True) -> str:
+    """Collective (every rank): capture the pipelined pool into HIP graphs, or fall back to eager
+    steps on EVERY rank when any rank's capture is refused (or ``allow_capture`` is off, e.g. gloo
+    collectives). The fallback drops the graphs and the staged state the capture primed, so the
+    eager run starts from clean dedup tables. Returns "hipgraph" or "eager"."""
+    ok = torch.ones(1, device=step.device)
+    if allow_capture:
+        try:
+            step.capture_pool(batches, steps_per_graph=steps_per_graph)
+        except Exception as e:  # noqa: BLE001 - the same work per step runs eagerly
+            import sys
+
+            print(f"rank {step.rank}: graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
+            ok.zero_()
+    else:
+        ok.zero_()
+    torch.cuda.synchronize(step.device)
+    if dist.is_initialized():
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
+    if float(ok) >= 1:
+        return "hipgraph"
+    step.release_graphs()
+    step.reset_pipeline()
+    if dist.is_initialized():
+        dist.barrier()
+    return "eager"

@@ -209,7 +209,9 @@ class ShardedEmbeddingBagCollection(nn.Module):
         self._f_table = f_table
         self._ts_cache: Dict[Tuple[str, int], object] = {}
         self._grad_anchor = nn.Parameter(torch.zeros(0, device=self._device))
-        self._prefetched: Dict[int, dict] = {}
+        # input_dist results staged by TrainPipelineSparseDist: [(kjt, dist ctx)], newest last, matched
+        # by the KJT object's identity (not id(): a freed KJT's id is reused), at most two kept
+        self._prefetched: List[Tuple[KeyedJaggedTensor, dict]] = []
         self._shard_of = {t: (lo, n) for (t, lo, n) in local_tables}
         self._register_state_dict_hook(_sharded_state_dict_hook)
         self._register_load_state_dict_pre_hook(_sharded_load_pre_hook, with_module=True)
@@ -248,7 +250,12 @@ class ShardedEmbeddingBagCollection(nn.Module):
 
     # -- forward
     def forward(self, features: KeyedJaggedTensor) -> KeyedTensor:
-        d = self._prefetched.pop(id(features), None)
+        d = None
+        for i, (k, staged) in enumerate(self._prefetched):
+            if k is features:
+                d = staged
+                del self._prefetched[i]
+                break
         if d is None:
             d = self.input_dist(features)
         elif d["stream"] is not None:  # staged by TrainPipelineSparseDist on its data-dist stream
@@ -268,7 +275,13 @@ class ShardedEmbeddingBagCollection(nn.Module):
             d["stream"] = s
             d["event"] = torch.cuda.Event()
             d["event"].record(s)
-        self._prefetched[id(features)] = d
+        self._prefetched.append((features, d))
+        del self._prefetched[:-2]  # a batch whose forward never ran (an exception, a derived KJT)
+
+    def accepts(self, features: KeyedJaggedTensor) -> bool:
+        """Whether ``features`` carries every feature of this collection (what prefetch needs)."""
+        keys = set(features.keys())
+        return all(f in keys for f in self._feature_names)
 
     def input_dist(self, features: KeyedJaggedTensor) -> dict:
         """torchrec input_dist: KJT permute to the EBC's feature order, TW keys grouped by owner, RW

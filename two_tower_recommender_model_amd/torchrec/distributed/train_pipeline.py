@@ -111,6 +111,9 @@ class TrainPipelineSparseDist(TrainPipelineBase):
         kjt = getattr(st.batch, "sparse_features", None)
         if kjt is None:
             return
+        # only modules the batch KJT feeds whole (torchrec traces which module receives the input;
+        # a module fed a derived KJT runs its own input_dist in forward)
+        mods = [m for m in mods if m.accepts(kjt)]
         if self._data_dist_stream is None:
             for m in mods:
                 m.prefetch(kjt)
