@@ -42,6 +42,18 @@ WORKLOADS = {
     "config5": (50_000_000, 100_000_000, 128, 16384, [128, 64]),
 }
 MULTIHOT = {"config5": 39}  # workload -> max bag length (KJT input, bags of 1..max ids)
+# sharded-only workloads: single-hot features, one table each, query features first;
+# they run the sharded step at every N (at N = 1 over a one-rank group)
+SIDE = 1_000_000
+SHARDED = {
+    # config 3: 8 table-wise features per tower (user_id 50M, product_id 100M, 14 side tables of 1M)
+    "config3": dict(N=[50_000_000] + [SIDE] * 7 + [100_000_000] + [SIDE] * 7, Fq=8, D=128, B=8192,
+                    layers=[128, 64], plan="tw", ids="uniform", seed=2),
+    # config 4: a 1B-row item table row-wise over the ranks (125M rows each at N = 8), the 50M-row
+    # user table table-wise (on the last rank), single-hot Zipf ids
+    "config4": dict(N=[50_000_000, 1_000_000_000], Fq=1, D=128, B=8192, layers=[128, 64], plan="config4",
+                    ids="zipf", seed=3),
+}
 
 
 def parse():
@@ -49,8 +61,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
-    ap.add_argument("--ids", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS) + sorted(SHARDED))
+    ap.add_argument("--ids", default=None, choices=["uniform", "zipf"],
+                    help="id distribution (default uniform; config4: zipf)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="table rows of the CPU sample (0: the workload's full tables when host RAM allows)")
@@ -68,6 +81,8 @@ def parse():
                     help="multi-hot workloads: group each batch inside its own step instead of one step ahead")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="sharded step: T2 inside launch U instead of on a parallel branch beside exchange A")
     ap.add_argument("--plan", default="auto", choices=["auto", "tw", "rw"],
                     help="N > 1 sharding plan of the two tables: tw = table-wise (users on rank 0, items on rank "
                          "1), rw = row-wise over all ranks; auto = tw at N = 2 (the same per-rank load as rw), rw "
@@ -76,22 +91,70 @@ def parse():
     return ap.parse_args()
 
 
-def synth_batches(num_users, num_items, B, n, device, ids, seed):
+def synth_cols(Ns, B, n, device, ids, seed):
+    """n batches of single-hot id columns (one per table of Ns) and Bernoulli(0.5) labels."""
     g = torch.Generator(device=device).manual_seed(seed)
     out = []
+
+    def zipf(N):  # Zipf-like (s ~ 1.05) over randomly permuted ranks: heavy hot rows
+        u01 = torch.rand(B, generator=g, device=device, dtype=torch.float64)
+        r = torch.floor(torch.exp(u01 * torch.log(torch.tensor(float(N), device=device, dtype=torch.float64))))
+        return (r.to(torch.int64) * 2654435761) % N
+
     for _ in range(n):
         if ids == "uniform":
-            u = torch.randint(0, num_users, (B,), generator=g, device=device, dtype=torch.int64)
-            it = torch.randint(0, num_items, (B,), generator=g, device=device, dtype=torch.int64)
-        else:  # Zipf-like (s ~ 1.05) over randomly permuted ranks: heavy hot rows
-            def zipf(N):
-                u01 = torch.rand(B, generator=g, device=device, dtype=torch.float64)
-                r = torch.floor(torch.exp(u01 * torch.log(torch.tensor(float(N), device=device, dtype=torch.float64))))
-                return ((r.to(torch.int64) * 2654435761) % N)
-            u, it = zipf(num_users), zipf(num_items)
+            cols = [torch.randint(0, N, (B,), generator=g, device=device, dtype=torch.int64) for N in Ns]
+        else:
+            cols = [zipf(N) for N in Ns]
         lab = torch.randint(0, 2, (B,), generator=g, device=device, dtype=torch.int32)
-        out.append(([u, it], lab))
+        out.append((cols, lab))
     return out
+
+
+def synth_batches(num_users, num_items, B, n, device, ids, seed):
+    return synth_cols([num_users, num_items], B, n, device, ids, seed)
+
+
+def tw_plan(Ns, W):
+    """Table-wise owners: tables by size, largest first, each to the rank holding the fewest tables
+    (every table brings the same B lookups per source), then the fewest bytes."""
+    owners = [0] * len(Ns)
+    cnt, byt = [0] * W, [0] * W
+    for f in sorted(range(len(Ns)), key=lambda f: -Ns[f]):
+        r = min(range(W), key=lambda r: (cnt[r], byt[r]))
+        owners[f] = r
+        cnt[r] += 1
+        byt[r] += Ns[f]
+    return owners
+
+
+def sharded_spec(args, world):
+    """(N list, Fq, D, B, layers, sharding, owners, ids, seed, plan description) of the sharded step."""
+    if args.workload in SHARDED:
+        sp = SHARDED[args.workload]
+        N, Fq, D, B, layers = sp["N"], sp["Fq"], sp["D"], sp["B"], sp["layers"]
+        ids = args.ids or sp["ids"]
+        if sp["plan"] == "tw":
+            owners = tw_plan(N, world)
+            return (N, Fq, D, B, layers, ["table_wise"] * len(N), owners, ids, sp["seed"],
+                    f"table-wise ({len(N)} tables over {world} ranks, greedy by table count then bytes: {owners})")
+        # config4: items row-wise, users table-wise on the last rank
+        per_rank = (N[1] // world + N[0] * (world == 1)) * (4 * D + 4)
+        if per_rank > 200 << 30:
+            raise SystemExit(f"config4 needs at least 4 GPUs (the 1B-row table is {N[1] * 4 * D / 2**30:.0f} GiB; "
+                             f"{per_rank / 2**30:.0f} GiB per rank at N = {world})")
+        return (N, Fq, D, B, layers, ["table_wise", "row_wise"], [world - 1, 0], ids, sp["seed"],
+                f"product_id row-wise (blocks of ceil(N / {world}) rows), user_id table-wise on rank {world - 1}")
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    N = [num_users, num_items]
+    plan = args.plan if args.plan != "auto" else ("tw" if world == 2 else "rw")
+    if plan == "tw" and world < 2:
+        plan = "rw"  # one rank holds everything either way
+    if plan == "tw":
+        return (N, 1, D, B, layers, ["table_wise"] * 2, [0, 1], args.ids or "uniform", 1,
+                "table-wise (user_id -> rank 0, product_id -> rank 1)")
+    return (N, 1, D, B, layers, ["row_wise"] * 2, [0, 0], args.ids or "uniform", 1,
+            f"row-wise (blocks of ceil(N / {world}) rows)")
 
 
 def time_kernel(fn, iters):
@@ -629,28 +692,24 @@ def run_multi(args, world, rank, local_rank):
     from two_tower_recommender_model_amd.sharded import (FusedShardedTwoTowerStep, TorchComm,
                                                          capture_pool_or_eager, default_capacity, segment_counts)
 
-    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
-    N = [num_users, num_items]
+    N, Fq, D, B, layers, sharding, owners, ids, seed, plan = sharded_spec(args, world)
+    F = len(N)
     dev = torch.device("cuda", local_rank % torch.cuda.device_count())  # (rehearsal: ranks may share one GPU)
     comm = TorchComm(always_collective=True)
     k = args.steps_per_graph
     nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k
-    batches = synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1 + rank)
-    plan = args.plan if args.plan != "auto" else ("tw" if world == 2 else "rw")
-    if plan == "tw" and world < 2:
-        plan = "rw"  # one rank holds everything either way
-    tw_owners = [0, 1 % world]
-    sharding = ["table_wise"] * 2 if plan == "tw" else ["row_wise"] * 2
-    blocks = [0, 0] if plan == "tw" else [-(-n // world) for n in N]
-    owners = tw_owners if plan == "tw" else [0, 0]
+    batches = synth_cols(N, B, nb, dev, ids, seed=seed * 1000 + 1 + rank)
+    blocks = [-(-n // world) if sh == "row_wise" else 0 for n, sh in zip(N, sharding)]
+    seg_owner = [o if sh == "table_wise" else 0 for o, sh in zip(owners, sharding)]
     need = torch.zeros(1, dtype=torch.int64)
     for cols, _ in batches:
-        need = torch.maximum(need, segment_counts(cols, N, blocks, owners, world).max().reshape(1))
+        need = torch.maximum(need, segment_counts(cols, N, blocks, seg_owner, world).max().reshape(1))
     need = need.to(dev)
     dist.all_reduce(need, op=dist.ReduceOp.MAX)
     cap = max(default_capacity(B, world), -(-int(need) // 8) * 8)
-    step = FusedShardedTwoTowerStep(comm, N, D, layers, B, dev, sharding=sharding, tw_owners=tw_owners, lr_emb=0.01,
-                                    lr_dense=0.01, seed=0, capacity=cap)
+    step = FusedShardedTwoTowerStep(comm, N, D, layers, B, dev, sharding=sharding, tw_owners=owners, lr_emb=0.01,
+                                    lr_dense=0.01, seed=0, capacity=cap, num_query_features=Fq,
+                                    overlap=not args.no_overlap)
     step.load_batch(*batches[0])
     step.step()  # creates the RCCL communicators before any capture
     # gloo collectives (TT_REHEARSE_GLOO, testing only) are not capturable: eager steps
@@ -680,8 +739,8 @@ def run_multi(args, world, rank, local_rank):
     # SURVEY 8(d) embedding-path bytes per rank and step over the whole step's time (no per-launch
     # timing in this mode): every rank routes B x F lookups and owns ~B x F of the W x B x F lookups
     # for the update; U counted on this rank's resident batches (distinct (table, row) per batch)
-    FB = 2 * B
-    uniq = sum(int(torch.unique(torch.cat([c[0][c[0] != 0] % N[0], c[1][c[1] != 0] % N[1] + (1 << 40)])).numel())
+    FB = F * B
+    uniq = sum(int(torch.unique(torch.cat([c[f][c[f] != 0] % N[f] + (f << 40) for f in range(F)])).numel())
                for c, _ in batches) // len(batches)
     emb_bytes = FB * (16 + 4 * D) + FB * (4 + 8 * D) + uniq * (8 * D + 8)
     ach = emb_bytes / (dt / args.steps) / 1e9
@@ -689,12 +748,13 @@ def run_multi(args, world, rank, local_rank):
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_step": emb_bytes, "unique_rows": uniq,
                 "timing": "SURVEY 8(d) bytes per rank over the max-over-ranks step time (collectives included)"}
-    info = {"plan": {"tw": "table-wise (user_id -> rank 0, product_id -> rank 1)",
-                     "rw": f"row-wise (blocks of ceil(N / {world}) rows)"}[plan],
+    info = {"plan": plan, "features": F, "query_features": Fq, "ids": ids,
             "capacity": cap, "capacity_needed": int(need), "resident_batches": nb,
             "exchange_A_bytes_sent": 4 * step.A_total,
             "exchange_B_bytes_sent": 2 * D * world * step.S[r],
-            "collectives_per_step": 2, "mode": mode}
+            "collectives_per_step": 2, "mode": mode,
+            "overlap": "T2 (tower weight gradients) on a parallel graph branch beside exchange A + the owner's "
+                       "update" if step.overlap else "none (one stream)"}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
 
 
@@ -703,12 +763,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
-    hot = f"multi-hot (bags of 1..{MULTIHOT[args.workload]})" if args.workload in MULTIHOT else "single-hot"
-    config = {"workload": f"{args.workload}: {num_items // 1_000_000}M items x {num_users // 1_000_000}M users, "
-                          f"emb_dim {D}, towers {layers}, {hot} {args.ids} ids",
-              "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D, "tower_dtype": "bf16 (MFMA, fp32 acc)",
-              "parallelism": "single-gpu hipgraph"}
+    if args.ids is None:
+        args.ids = SHARDED[args.workload]["ids"] if args.workload in SHARDED else "uniform"
+    if args.workload in SHARDED:
+        sp = SHARDED[args.workload]
+        D, B, layers = sp["D"], sp["B"], sp["layers"]
+        desc = {"config3": "16 single-hot tables, 8 features per tower (user_id 50M, product_id 100M, 14 x 1M)",
+                "config4": "1B-row product_id table (row-wise) x 50M-row user_id table (table-wise)"}[args.workload]
+        config = {"workload": f"{args.workload}: {desc}, emb_dim {D}, towers {layers}, {args.ids} ids",
+                  "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D,
+                  "tower_dtype": "bf16 (MFMA, fp32 acc)"}
+    else:
+        num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+        hot = f"multi-hot (bags of 1..{MULTIHOT[args.workload]})" if args.workload in MULTIHOT else "single-hot"
+        config = {"workload": f"{args.workload}: {num_items // 1_000_000}M items x {num_users // 1_000_000}M users, "
+                              f"emb_dim {D}, towers {layers}, {hot} {args.ids} ids",
+                  "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D, "tower_dtype": "bf16 (MFMA, fp32 acc)",
+                  "parallelism": "single-gpu hipgraph"}
     sharded_info = None
     if args.workload in MULTIHOT:
         if world != 1 or args.sharded:
@@ -720,7 +791,7 @@ def main():
         roofline, cpu = None, None
         config["parallelism"] = "single-gpu, host-fed: pinned staging + async H2D (copy stream) + hipgraph replay"
         config["note"] = "PCIe-inclusive rate (inputs handed over in host memory); the resident-input line is the metric"
-    elif world == 1 and not args.sharded:
+    elif world == 1 and not args.sharded and args.workload not in SHARDED:
         value, ms, loss, roofline, cpu, steps_run = run_single(args)
     else:
         # TT_REHEARSE_GLOO=1 (testing only, never a bench line): gloo collectives and ranks sharing the
@@ -750,7 +821,7 @@ def main():
         out = {"metric": f"training pairs/sec at batch {B} (per GPU)", "value": round(value, 1), "unit": "pairs/s",
                "n_gpus": world, "steps": steps_run, "warmup": args.warmup, "ms_per_step": round(ms, 5),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-               "data": "synthetic (uniform ids, Bernoulli labels), random-init weights", "config": config,
+               "data": f"synthetic ({args.ids} ids, Bernoulli labels), random-init weights", "config": config,
                "loss": loss, "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

@@ -507,6 +507,18 @@ int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, con
                                    float* const* grad_rows_out, const float* params, const void* labels,
                                    int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
                                    void* stream);
+/* T1 of the pipelined sharded step with SEVERAL single-hot features per tower (BASELINE configs 3
+ * and 4: 8 table-wise features per tower, 1024-wide tower inputs; TorchRec KeyedTensor slices
+ * concatenated per tower, 03_model_training.py:420-436, generalised as in
+ * ray_tune_optuna_tuning_alex_test.py:270-306): features are numbered query first
+ * (f < in_dim[0] / D), then candidate; column k of tower t is column k % D of bf16 row
+ * pos_in[f * B + m] of rows_in (f = tower t's first feature + k / D; -1 -> zeros, a dropped id),
+ * and its dX column goes to column k % D of row pos_out[f * B + m] of grad_rows_out (-1: none).
+ * Any tower width the general T1 takes (inputs up to 1024); D in {16, 32, 64, 128}. */
+int tt_tower_fwd_bwd_indexed_multi_bf16(const tt_tower_shape_t* shape, int64_t B, int D, const int32_t* pos_in,
+                                        const int32_t* pos_out, const void* rows_in, float* grad_rows_out,
+                                        const float* params, const void* labels, int label_dtype, float grad_scale,
+                                        float* logits, void* workspace, size_t ws_bytes, void* stream);
 /* T3 without Adam: the reduced tower gradient, times `scale`, written at base + offsets[q] for
  * q < copies <= 16 (offsets: host array, floats) — the tower region of every destination block of
  * exchange A: DDP's mean all-reduce becomes a fixed-order sum on the receivers. */
@@ -542,6 +554,19 @@ int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, in
                                                const float* emb_grad, int64_t ldg, float* weights, float* state,
                                                float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
                                                int64_t dedup_max_lookups, void* stream);
+/* Launch U without T2 (the step graph runs T2 = tt_tower_wgrad_pre on a parallel branch, beside
+ * exchange A: the tower weight gradients overlap the gradient all-to-all, as the dense backward
+ * overlaps TorchRec's output_dist backward): the owner's row-wise Adagrad over the received gradient
+ * rows + the count pass of a later batch's route; arguments as in the launch above. */
+int tt_shard_route_count_rowwise_adagrad(int F, int64_t B, const void* const* cols, int id_dtype,
+                                         const int64_t* num_embeddings, const int64_t* block_sizes,
+                                         const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                         int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                         size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
+                                         const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
+                                         const float* emb_grad, int64_t ldg, float* weights, float* state,
+                                         float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                         int64_t dedup_max_lookups, void* stream);
 /* Launch G: the tower gradient x scale into `copies` destinations (as tt_tower_grads_replicated) +
  * the place pass of the route counted by launch U + the owner's gather of the next batch's rows
  * (arguments as tt_shard_gather_segs_bf16). */

@@ -40,7 +40,7 @@ import pytest
 import torch
 
 from oracle import ref
-from tower_emul import check_towers, emulate_bounds, split_params
+from tower_emul import check_adagrad, check_towers, emulate_bounds, split_params
 
 pytestmark = pytest.mark.gpu
 
@@ -129,34 +129,14 @@ def _check_adam(prm_before, grads, m0, v0, step0, params_after, exp_avg_after, e
 
 
 def _check_rowwise_adagrad(table_view, state_view, u, w_before, s_before, lookup_rows, dx_want, dx_bound):
-    """The embedding update against the oracle on the touched rows only, fed the EMULATED gradient
-    rows: ``u`` (device) = unique rows, ``lookup_rows`` (CPU) = row of every kept lookup in lookup
-    order, ``dx_want`` / ``dx_bound`` = the emulation's dX row of that lookup and its element-wise
-    bound. The tolerance is the dX bound carried through the update: a row's G = sum of its
-    lookups' dX (bound e_G = sum of theirs), s' = s + mean(G^2) (e_s = mean(2 |G| e_G + e_G^2)),
-    w' = w - lr G / (sqrt(s') + eps) (e_w = lr (e_G / r_lo + |G| (1 / r_lo - 1 / r)), r_lo from s' - e_s),
-    plus the fp32 arithmetic of the update (rtol 1e-5)."""
-    w_want, s_want = w_before.clone(), s_before.clone()
+    """The embedding update on the touched rows only (``u`` device, unique rows; ``lookup_rows``
+    CPU, the row of every kept lookup in lookup order) against the oracle fed the EMULATED dX rows,
+    tolerance from their bounds (tower_emul.check_adagrad)."""
     inv = torch.searchsorted(u.cpu(), lookup_rows)
-    ref.rowwise_adagrad_from_lookups(w_want, s_want, inv, dx_want.float(), LR, 1e-10)
-    n = u.numel()
-    G = torch.zeros(n, dx_want.shape[1], dtype=torch.float64).index_add_(0, inv, dx_want.double())
-    eG = torch.zeros_like(G).index_add_(0, inv, dx_bound.double())
-    s_new = s_before.double() + (G * G).mean(1)
-    e_s = (2 * G.abs() * eG + eG * eG).mean(1)
-    r = s_new.sqrt() + 1e-10
-    r_lo = (s_new - e_s).clamp_min(0).sqrt() + 1e-10
-    e_w = LR * (eG / r_lo[:, None] + G.abs() * (1 / r_lo - 1 / r)[:, None])
     w_got = table_view[u].cpu()
-    s_got = state_view[u].cpu()
-    tol_s = e_s + 1e-5 * s_new.abs() + 1e-12
-    assert bool(((s_got.double() - s_want.double()).abs() <= tol_s).all()), "row-wise Adagrad state outside the bound"
-    tol_w = e_w + 1e-5 * w_want.double().abs() + 1e-5 * LR * (G.abs() / r[:, None])
-    bad = ~((w_got.double() - w_want.double()).abs() <= tol_w)
-    assert not bool(bad.any()), f"{int(bad.sum())} table elements outside the bound"
+    rel = check_adagrad(w_got, state_view[u].cpu(), w_before, s_before, inv, dx_want, dx_bound, LR, 1e-10, "adagrad")
     assert not torch.equal(w_got, w_before)  # the update happened
-    rel = (e_w / (LR * G.abs() / r[:, None]).clamp_min(1e-30)).median()
-    print(f"adagrad check: median tolerance / step {float(rel):.3g}")
+    print(f"adagrad check: median tolerance / step {rel:.3g}")
 
 
 @pytest.mark.parametrize("case,ids", [("northstar", "uniform"), ("northstar", "zipf"), ("config2", "uniform")])

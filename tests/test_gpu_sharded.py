@@ -104,112 +104,183 @@ def test_sharded_w1_equals_fused_single_gpu_step(device):
     assert float(sh.loss) == float(ref_step.loss)
 
 
-@pytest.mark.parametrize("W,sharding", [(2, ("row_wise", "row_wise")), (3, ("table_wise", "row_wise")),
-                                        (4, ("row_wise", "table_wise")), (8, ("row_wise", "row_wise")),
-                                        (2, ("table_wise", "table_wise")), (4, ("table_wise", "table_wise"))])
-def test_sharded_threads_vs_oracle(device, W, sharding):
-    """W ranks as threads: (a) the rows each rank's towers read are the oracle tables' rows; (b) each
-    rank's gradient rows dX and its tower gradient (sent x 1/W) match the fp64 emulation of the bf16
-    towers on ITS OWN batch and mean loss (the loss scale TorchRec's sharded EBC gives: the sum over
-    ranks of the per-rank mean-loss gradients); (c) every shard equals the oracle's row-wise Adagrad
-    over the union of the kernels' gradient rows (ascending (rank, bag) order); (d) the towers equal
-    the oracle's Adam fed the fixed-order sum of the ranks' tower gradients x 1/W (DDP's mean
-    all-reduce) and are identical on every rank."""
-    from tower_emul import check_towers, emulate_bounds, split_params
+def _threads_vs_oracle(device, W, N, Fq, sharding, tw_owners, B, D, lr, layers, nsteps=3, seed=0, small=True):
+    """W ranks as threads of one process over ThreadComm, F = len(N) single-hot features (0 .. Fq-1
+    query, the rest candidate). Per step, against the state read from the shards before it: (a) the
+    rows each rank's towers read are the table rows its ids name (bf16, bit for bit); (b) each
+    rank's gradient rows dX, logits and tower gradient (sent x 1/W) against the fp64 emulation of
+    the bf16 towers on ITS OWN batch and mean loss, element-wise (tower_emul.check_towers; the loss
+    scale TorchRec's sharded EBC gives: the sum over ranks of the per-rank mean-loss gradients);
+    (c) every touched row against the oracle's row-wise Adagrad over the union of the EMULATED
+    gradient rows (ascending (rank, bag) order), tolerance from their bounds; (d) the towers
+    against the oracle's Adam fed the fixed-order sum of the ranks' tower gradients x 1/W (DDP's
+    mean all-reduce), identical on every rank. ``small``: tables initialised from one CPU copy and
+    every untouched row checked unchanged (off for BASELINE-size tables: each rank draws its own
+    shard and only the touched rows are read back)."""
+    from tower_emul import check_adagrad, check_towers, emulate_bounds, split_params
 
     from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, ThreadComm
 
-    B, D, N, lr, layers = 1024, 64, [9_000, 12_345], 0.02, [128, 64]
-    gen = torch.Generator().manual_seed(W)
-    full = [torch.empty(n, D).uniform_(-0.05, 0.05, generator=gen) for n in N]
-    states = [torch.zeros(n) for n in N]
+    F = len(N)
+    gen = torch.Generator().manual_seed(100 * W + F + seed)
+    full = [torch.empty(n, D).uniform_(-0.05, 0.05, generator=gen) for n in N] if small else None
     comms = ThreadComm.group(W)
-    steps = [None] * W
+    ranks = [None] * W
 
     def build(r):
         torch.cuda.set_device(device)
-        steps[r] = FusedShardedTwoTowerStep(comms[r], N, D, layers, B, device, sharding=sharding,
-                                            tw_owners=[W - 1, 0], full_tables=full, lr_emb=lr, seed=3)
+        ranks[r] = FusedShardedTwoTowerStep(comms[r], N, D, layers, B, device, sharding=sharding,
+                                            tw_owners=tw_owners, full_tables=full, lr_emb=lr, seed=3,
+                                            num_query_features=Fq)
 
     _run_ranks([lambda r=r: build(r) for r in range(W)])
-    P = steps[0].towers.num_params
+    in_dims = ranks[0].in_dims
+    P = ranks[0].towers.num_params
     m_ref, v_ref = [torch.zeros(P)], [torch.zeros(P)]
-    for s in range(3):
+
+    def read_rows(f, u):
+        """(weights, state) of global rows u (CPU, sorted) of table f, from the shards that hold them."""
+        w = torch.empty(u.numel(), D)
+        st_ = torch.empty(u.numel())
+        for r in range(W):
+            st = ranks[r]
+            lo, n = st.row_lo[f], st.local_rows[f]
+            sel = (u >= lo) & (u < lo + n)
+            if bool(sel.any()):
+                idx = (u[sel] - lo).to(device)
+                w[sel] = st.tables.table_view(f)[idx].cpu()
+                st_[sel] = st.tables.state_view(f)[idx].cpu()
+        return w, st_
+
+    def snapshot():
+        return [[(st.tables.table_view(f)[:st.local_rows[f]].cpu().clone(),
+                  st.tables.state_view(f)[:st.local_rows[f]].cpu().clone()) for f in range(F)] for st in ranks]
+
+    for s in range(nsteps):
         batches = []
-        params0 = steps[0].params.cpu().clone()
+        params0 = ranks[0].params.cpu().clone()
         for r in range(W):
             cols = [torch.randint(0, 2 * n, (B,), generator=gen) for n in N]
             cols[0][torch.rand(B, generator=gen) < 0.05] = 0
-            cols[1][:30] = 4242  # hot on one rank
+            cols[F - 1][:30] = 4242 % N[F - 1] + N[F - 1]  # hot on one rank (and past N: id % N)
             lab = torch.randint(0, 2, (B,), generator=gen).to(torch.int32)
             batches.append((cols, lab))
-            steps[r].load_batch([c.to(device) for c in cols], lab.to(device))
+            ranks[r].load_batch([c.to(device) for c in cols], lab.to(device))
+        uniq = []
+        for f in range(F):
+            ids = torch.cat([c[f][c[f] != 0] for c, _ in batches])
+            uniq.append(torch.unique(torch.remainder(ids, N[f])))
+        before = [read_rows(f, uniq[f]) for f in range(F)]
+        snap = snapshot() if small else None
         torch.cuda.synchronize()
 
         def run(r):
             torch.cuda.set_device(device)
-            steps[r].step()
+            ranks[r].step()
             torch.cuda.synchronize()
 
         _run_ranks([lambda r=r: run(r) for r in range(W)])
-        _run_ranks([lambda r=r: steps[r].check() for r in range(W)])
-        rows_all, grads_all = [[] for _ in N], [[] for _ in N]
+        _run_ranks([lambda r=r: ranks[r].check() for r in range(W)])
+        rows_all, dx_all, eb_all = [[] for _ in N], [[] for _ in N], [[] for _ in N]
         tower_sum = torch.zeros(P)
         for r in range(W):
-            st = steps[r]
+            st = ranks[r]
             cols, lab = batches[r]
             rin = st.rows_for(0).cpu()     # [F*B, D] bf16 rows T1 read
             gout = st.grad_rows(0).cpu()   # [F*B, D] the dX rows it sent
             pos = st.pos_in[0].cpu().numpy()
-            for f in range(2):
+            keep = []
+            for f in range(F):
                 kept = pos[f * B:(f + 1) * B] >= 0
                 assert np.array_equal(kept, cols[f].numpy() != 0)
-                ids = np.mod(cols[f].numpy()[kept], N[f])
+                keep.append(kept)
+                ids = torch.remainder(cols[f][torch.from_numpy(kept)], N[f])
                 got = rin[f * B:(f + 1) * B][torch.from_numpy(kept)]
-                want = full[f][torch.from_numpy(ids)].to(torch.bfloat16)
-                # (a) initial tables: bit for bit (after the same bf16 rounding); updated rows: the
-                # row-wise mean of G^2 is reduced in another order -> one bf16 ulp
-                if s == 0:
-                    assert torch.equal(got, want), (r, f)
-                else:
-                    np.testing.assert_allclose(got.float().numpy(), want.float().numpy(), rtol=1e-2, atol=1e-7)
-                rows_all[f].append(torch.from_numpy(ids))
-                grads_all[f].append(gout[f * B:(f + 1) * B][torch.from_numpy(kept)])
-            # (b) this rank's dX and tower gradient vs the emulation on its own batch
+                want = before[f][0][torch.searchsorted(uniq[f], ids)].to(torch.bfloat16)
+                assert torch.equal(got, want), (r, f)  # (a) bit for bit (the same bf16 rounding)
+                rows_all[f].append(ids)
+            # (b) this rank's logits, dX and tower gradient vs the emulation on its own batch
             x = rin.float()
-            prm = split_params(params0, [D, D], layers)
-            lg, loss, dxs, gw, amb = emulate_bounds(x[:B], x[B:], prm, layers, lab)
-            keepm = [(cols[f] != 0).double()[:, None] for f in range(2)]  # dropped lookups send no row
-            dxs = [(dxs[f][0] * keepm[f], dxs[f][1] * keepm[f]) for f in range(2)]
+            xq = torch.cat([x[f * B:(f + 1) * B] for f in range(Fq)], 1)
+            xc = torch.cat([x[f * B:(f + 1) * B] for f in range(Fq, F)], 1)
+            prm = split_params(params0, in_dims, layers)
+            lg, loss, dxs, gw, amb = emulate_bounds(xq, xc, prm, layers, lab)
+            dx_f, eb_f = [], []
+            for f in range(F):
+                t, j = (0, f) if f < Fq else (1, f - Fq)
+                m = torch.from_numpy(keep[f]).double()[:, None]  # dropped lookups send no row
+                dx_f.append(dxs[t][0][:, j * D:(j + 1) * D] * m)
+                eb_f.append(dxs[t][1][:, j * D:(j + 1) * D] * m)
+            dxs2 = [(torch.cat(dx_f[:Fq], 1), torch.cat(eb_f[:Fq], 1)),
+                    (torch.cat(dx_f[Fq:], 1), torch.cat(eb_f[Fq:], 1))]
+            got_dx = [torch.cat([gout[f * B:(f + 1) * B] for f in range(Fq)], 1),
+                      torch.cat([gout[f * B:(f + 1) * B] for f in range(Fq, F)], 1)]
             sent = st.tower_grad_sent().cpu()
             glist, o = [], 0
-            for p in prm:
-                glist.append(sent[o:o + p.numel()].reshape(p.shape) * W)
-                o += p.numel()
-            check_towers((lg, loss, dxs, gw, amb), st.logits.cpu(), [gout[:B], gout[B:]], glist, f"rank {r}")
+            for p_ in prm:
+                glist.append(sent[o:o + p_.numel()].reshape(p_.shape) * W)
+                o += p_.numel()
+            check_towers((lg, loss, dxs2, gw, amb), st.logits.cpu(), got_dx, glist, f"rank {r}")
+            for f in range(F):
+                k = torch.from_numpy(keep[f])
+                dx_all[f].append(dx_f[f][k])
+                eb_all[f].append(eb_f[f][k])
             tower_sum += sent  # fixed rank order, as the receivers sum
-        # (c) oracle update from the union of the gradient rows, rank-major
-        for f in range(2):
-            ref.rowwise_adagrad_from_lookups(full[f], states[f], torch.cat(rows_all[f]), torch.cat(grads_all[f]),
-                                             lr, 1e-10)
-        for r in range(W):
-            st = steps[r]
-            for f in range(2):
-                n = st.local_rows[f]
-                lo = st.row_lo[f]
-                np.testing.assert_allclose(st.tables.table_view(f)[:n].cpu().numpy(), full[f][lo:lo + n].numpy(),
-                                           rtol=1e-5, atol=1e-7)
-                np.testing.assert_allclose(st.tables.state_view(f)[:n].cpu().numpy(), states[f][lo:lo + n].numpy(),
-                                           rtol=1e-5, atol=1e-10)
+        # (c) every touched row vs the oracle fed the union of the emulated gradient rows, rank-major
+        for f in range(F):
+            inv = torch.searchsorted(uniq[f], torch.cat(rows_all[f]))
+            w_got, s_got = read_rows(f, uniq[f])
+            check_adagrad(w_got, s_got, before[f][0], before[f][1], inv, torch.cat(dx_all[f]), torch.cat(eb_all[f]),
+                          lr, 1e-10, f"feature {f}")
+        if small:  # untouched rows never move
+            for r in range(W):
+                st = ranks[r]
+                for f in range(F):
+                    lo, n = st.row_lo[f], st.local_rows[f]
+                    untouched = torch.ones(n, dtype=torch.bool)
+                    u = uniq[f]
+                    untouched[(u[(u >= lo) & (u < lo + n)] - lo)] = False
+                    w0, s0 = snap[r][f]
+                    assert torch.equal(st.tables.table_view(f)[:n].cpu()[untouched], w0[untouched])
+                    assert torch.equal(st.tables.state_view(f)[:n].cpu()[untouched], s0[untouched])
         # (d) Adam on the summed (mean) tower gradient; identical replicas
         p_ref = [params0.clone()]
         ref.adam(p_ref, [tower_sum], m_ref, v_ref, s + 1, 0.01)
-        np.testing.assert_allclose(steps[0].params.cpu().numpy(), p_ref[0].numpy(), rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(ranks[0].params.cpu().numpy(), p_ref[0].numpy(), rtol=1e-5, atol=1e-7)
         for r in range(1, W):
-            assert torch.equal(steps[r].params, steps[0].params)
+            assert torch.equal(ranks[r].params, ranks[0].params)
     # every row held exactly once
-    for f in range(2):
-        assert sum(steps[r].local_rows[f] for r in range(W)) == N[f]
+    for f in range(F):
+        assert sum(ranks[r].local_rows[f] for r in range(W)) == N[f]
+    return ranks
+
+
+@pytest.mark.parametrize("W,sharding", [(2, ("row_wise", "row_wise")), (3, ("table_wise", "row_wise")),
+                                        (4, ("row_wise", "table_wise")), (8, ("row_wise", "row_wise")),
+                                        (2, ("table_wise", "table_wise")), (4, ("table_wise", "table_wise"))])
+def test_sharded_threads_vs_oracle(device, W, sharding):
+    """The reference's two features (user / item towers), W ranks as threads (_threads_vs_oracle)."""
+    _threads_vs_oracle(device, W, [9_000, 12_345], 1, list(sharding), [W - 1, 0], 1024, 64, 0.02, [128, 64])
+
+
+@pytest.mark.parametrize("W,F,Fq,plan", [(1, 4, 2, "rw"), (2, 6, 3, "mix"), (3, 4, 2, "tw"), (8, 16, 8, "tw"),
+                                         (4, 2, 1, "config4")])
+def test_sharded_multifeature_threads_vs_oracle(device, W, F, Fq, plan):
+    """Several single-hot features per tower through the general T1 (BASELINE config 3's shape at
+    small table sizes: 8 table-wise features per tower at W = 8; config 4's plan: the item table
+    row-wise, the user table table-wise), W ranks as threads (_threads_vs_oracle)."""
+    N = [5_000 + 1_000 * f for f in range(F)]
+    if plan == "rw":
+        sharding, owners = ["row_wise"] * F, [0] * F
+    elif plan == "tw":
+        sharding, owners = ["table_wise"] * F, [(f * 5) % W for f in range(F)]
+    elif plan == "config4":
+        sharding, owners = ["table_wise", "row_wise"], [W - 1, 0]
+    else:
+        sharding = ["row_wise" if f % 2 else "table_wise" for f in range(F)]
+        owners = [f % W for f in range(F)]
+    layers = [128, 64] if F * 32 <= 1024 else [64, 32]
+    _threads_vs_oracle(device, W, N, Fq, sharding, owners, 512, 32 if F > 8 else 64, 0.02, layers, nsteps=2, seed=F)
 
 
 @pytest.mark.parametrize("W", [2, 3])
@@ -385,3 +456,23 @@ def test_sharded_pipeline_state_resets(device):
     r = subprocess.run([sys.executable, os.path.join(here, "sharded_pipeline_state_check.py")], capture_output=True,
                        text=True, timeout=300, cwd=os.path.dirname(here))
     assert r.returncode == 0 and "PIPELINE-STATE-OK" in r.stdout, (r.returncode, r.stdout[-1500:], r.stderr[-3000:])
+
+
+def test_sharded_config3_w8_baseline_size(device):
+    """BASELINE config 3 at its size on one MI355X: 8 ranks as threads, 16 single-hot tables (user_id
+    50M, product_id 100M, 14 x 1M rows; 84 GB of fp32 tables), 8 features per tower, D 128, B 8192
+    per rank, bf16 towers over 1024-wide inputs, every table table-wise (bench.tw_plan: two tables
+    per rank) — against the oracle on the touched rows (_threads_vs_oracle, 2 steps)."""
+    import bench
+
+    N = bench.SHARDED["config3"]["N"]
+    W = 8
+    owners = bench.tw_plan(N, W)
+    ranks = _threads_vs_oracle(device, W, N, 8, ["table_wise"] * len(N), owners, 8192, 128, 0.01, [128, 64],
+                               nsteps=2, seed=33, small=False)
+    assert ranks[0].in_dims == [1024, 1024]
+    del ranks
+    import gc
+
+    gc.collect()
+    torch.cuda.empty_cache()

@@ -273,6 +273,37 @@ def check_towers(emu, logits, dx, grads, what: str = "") -> dict:
     return out
 
 
+def check_adagrad(w_got, s_got, w_before, s_before, inv, dx_want, dx_bound, lr: float, eps: float = 1e-10,
+                  what: str = "") -> float:
+    """The row-wise Adagrad update (03_model_training.py:791-795) of U touched rows against the
+    oracle (oracle.ref.rowwise_adagrad_from_lookups) fed the EMULATED gradient rows: lookup j adds
+    dx_want[j] (element-wise bound dx_bound[j]) to touched row inv[j]. The tolerance is that bound
+    carried through the update: G = sum of a row's lookups (e_G = sum of their bounds),
+    s' = s + mean(G^2) (e_s = mean(2 |G| e_G + e_G^2)), w' = w - lr G / (sqrt(s') + eps)
+    (e_w = lr (e_G / r_lo + |G| (1 / r_lo - 1 / r)), r_lo from s' - e_s), plus the update's own fp32
+    arithmetic (1e-5 relative). w_* [U, D] and s_* [U] are CPU tensors. Returns the median
+    tolerance relative to the step (for logs)."""
+    from oracle import ref
+
+    w_want, s_want = w_before.clone(), s_before.clone()
+    ref.rowwise_adagrad_from_lookups(w_want, s_want, inv, dx_want.float(), lr, eps)
+    n = w_before.shape[0]
+    G = torch.zeros(n, dx_want.shape[1], dtype=torch.float64).index_add_(0, inv, dx_want.double())
+    eG = torch.zeros_like(G).index_add_(0, inv, dx_bound.double())
+    s_new = s_before.double() + (G * G).mean(1)
+    e_s = (2 * G.abs() * eG + eG * eG).mean(1)
+    r = s_new.sqrt() + eps
+    r_lo = (s_new - e_s).clamp_min(0).sqrt() + eps
+    e_w = lr * (eG / r_lo[:, None] + G.abs() * (1 / r_lo - 1 / r)[:, None])
+    tol_s = e_s + 1e-5 * s_new.abs() + 1e-12
+    bad = ~((s_got.double() - s_want.double()).abs() <= tol_s)
+    assert not bool(bad.any()), f"{what}: {int(bad.sum())} row-wise Adagrad states outside the bound"
+    tol_w = e_w + 1e-5 * w_want.double().abs() + 1e-5 * lr * (G.abs() / r[:, None])
+    bad = ~((w_got.double() - w_want.double()).abs() <= tol_w)
+    assert not bool(bad.any()), f"{what}: {int(bad.sum())} table elements outside the bound"
+    return float((e_w / (lr * G.abs() / r[:, None]).clamp_min(1e-30)).median())
+
+
 def rel_err(got: torch.Tensor, want: torch.Tensor) -> float:
     got, want = got.double().reshape(-1), want.double().reshape(-1)
     return float((got - want).norm() / (want.norm() + 1e-30))

@@ -243,6 +243,15 @@ SIGNATURES = {
         _int,
         [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp],
     ),
+    "tt_shard_route_count_rowwise_adagrad": (
+        _int,
+        [_int, _i64, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _ptm, _int, _pfm, _int,
+         _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
+    ),
+    "tt_tower_fwd_bwd_indexed_multi_bf16": (
+        _int,
+        [_psh, _i64, _int, _vp, _vp, _vp, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
+    ),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -299,6 +308,8 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_wgrad_route_count_rowwise_adagrad",
     "tt_tower_grads_replicated_route_place_gather",
     "tt_tower_adam_pre_grads_sum",
+    "tt_tower_fwd_bwd_indexed_multi_bf16",
+    "tt_shard_route_count_rowwise_adagrad",
 ]
 
 _lib = None

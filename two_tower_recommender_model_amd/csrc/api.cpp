@@ -56,6 +56,6 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_wgrad_pre_insert_rowwise_adagrad, tt_tower_wgrad_route_count_rowwise_adagrad,
 // tt_tower_grads_replicated_route_place_gather, tt_tower_adam_pre_grads_sum
 // tt_tower_fwd_bwd_kjt
-int tt_num_entry_points(void) { return 53; }
+int tt_num_entry_points(void) { return 55; }
 
 }  // extern "C"

@@ -110,6 +110,16 @@ struct TowerArgs {
   // rows: an id >= gmod[t] reads row 0, never out of bounds)
   const void* mval;
   const int32_t* moff[2];
+  // multi-feature indexed rows (sharded step with several single-hot features per tower,
+  // tt_tower_fwd_bwd_indexed_multi_bf16; the general kernel): input column k of tower t is column
+  // k % iD of bf16 row ipos[(ifeat0[t] + k / iD) * B + m] of isrc (-1 -> zeros), and dX column k
+  // goes to column k % iD of row ipos_out[same] of idst (-1: not written)
+  const int32_t* ipos;
+  const int32_t* ipos_out;
+  const __bf16* isrc;
+  float* idst;
+  int ifeat0[2];
+  int iD;
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
 };
@@ -196,10 +206,17 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
           for (int e = threadIdx.x; e < TR * (kc / 4); e += 256) {
             const int row = e / (kc / 4), c4 = (e % (kc / 4)) * 4;
             const int64_t gm = m0 + row;
-            f32x4 v = (f32x4)(0.f);
-            if (gm < B) v = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + k0 + c4);
             bf16x4 bv;
-            bv[0] = (__bf16)v[0]; bv[1] = (__bf16)v[1]; bv[2] = (__bf16)v[2]; bv[3] = (__bf16)v[3];
+            if (a.ipos) {  // the feature's row as returned by its owner (bf16, what T1 computes on)
+              const int kk = k0 + c4, f = a.ifeat0[t] + kk / a.iD;
+              const int32_t p = gm < B ? a.ipos[(int64_t)f * B + gm] : -1;
+              bv = p >= 0 ? *reinterpret_cast<const bf16x4*>(a.isrc + (int64_t)p * a.iD + kk % a.iD)
+                          : (bf16x4)(__bf16)0.f;
+            } else {
+              f32x4 v = (f32x4)(0.f);
+              if (gm < B) v = *reinterpret_cast<const f32x4*>(a.pooled + gm * a.ldp + a.s.in_col[t] + k0 + c4);
+              bv[0] = (__bf16)v[0]; bv[1] = (__bf16)v[1]; bv[2] = (__bf16)v[2]; bv[3] = (__bf16)v[3];
+            }
             *reinterpret_cast<bf16x4*>(xs + row * LSTR + c4) = bv;
           }
           __syncthreads();
@@ -373,6 +390,16 @@ __global__ void __launch_bounds__(256) tower_fwd_bwd_kernel(TowerArgs a) {
         for (int j = 0; j < 2; ++j) {
           if (!(j == 0 ? h0 : h1)) continue;
           const int col = c0 + (wid + 4 * j) * 16 + r16;
+          if (a.ipos) {  // dX column -> the lookup's gradient row in the exchange buffer
+            const int f = a.ifeat0[t] + col / a.iD, cc = col % a.iD;
+            for (int i = 0; i < 2; ++i)
+              for (int rr = 0; rr < 4; ++rr) {
+                const int64_t gm = m0 + i * 16 + q4 * 4 + rr;
+                const int32_t p = gm < B ? a.ipos_out[(int64_t)f * B + gm] : -1;
+                if (p >= 0) a.idst[(int64_t)p * a.iD + cc] = acc[i][j][rr];
+              }
+            continue;
+          }
           for (int i = 0; i < 2; ++i)
             for (int rr = 0; rr < 4; ++rr) {
               const int64_t gm = m0 + i * 16 + q4 * 4 + rr;
@@ -2052,7 +2079,8 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if ((!pooled && !a.gcol[0] && !a.gpos[0] && !a.mval) || (!gpooled && !a.gpos[0]) || !params || !labels || !logits)
+  if ((!pooled && !a.gcol[0] && !a.gpos[0] && !a.mval && !a.ipos) || (!gpooled && !a.gpos[0] && !a.ipos) || !params ||
+      !labels || !logits)
     return fail(TT_EINVAL, "tower: null pointer");
   if (label_dtype != TT_I32 && label_dtype != TT_I64 && label_dtype != TT_F32)
     return fail(TT_EINVAL, "tower: labels must be int32/int64/float32");
@@ -2097,6 +2125,10 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
   if ((a.gcol[0] || a.gpos[0]) && !two)
     return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
+  if (a.ipos) {  // several features per tower: the general kernel (any width, chunks of 128 columns)
+    tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
+    return check_launch("tower_fwd_bwd_indexed_multi");
+  }
   if (a.mval) {  // multi-hot EBC forward fused in: compile-time shapes only
     if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
       tower_l2_kernel<128, 128, 64, false, false, true><<<g, b512, 0, as_stream(stream)>>>(a);
@@ -2683,6 +2715,34 @@ int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, in
   return check_launch("tower_wgrad_route_count_rowwise_adagrad");
 }
 
+int tt_shard_route_count_rowwise_adagrad(int F, int64_t B, const void* const* cols, int id_dtype,
+                                         const int64_t* num_embeddings, const int64_t* block_sizes,
+                                         const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                         int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                         size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
+                                         const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
+                                         const float* emb_grad, int64_t ldg, float* weights, float* state,
+                                         float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                         int64_t dedup_max_lookups, void* stream) {
+  // launch U of the pipelined sharded step without its T2 tiles (those run on a parallel branch of
+  // the step graph, beside exchange A): the owner's update workgroups first, then the route count
+  RouteArgs r{};
+  int rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
+                           overflow, route_ws, route_ws_bytes, r);
+  if (rc) return rc;
+  DdUpdateArgs d{};
+  int64_t dd_grid = 0;
+  rc = dedup_update_args(tables, T, features, Fsrc, emb_B, emb_grad, ldg, weights, state, emb_lr, emb_eps, dedup_ws,
+                         dedup_ws_bytes, dedup_max_lookups, d, &dd_grid);
+  if (rc) return rc;
+  const int64_t n_cnt = (int64_t)r.nblk * F;
+  if (n_cnt + dd_grid > INT32_MAX) return fail(TT_EINVAL, "shard_route_count_rowwise_adagrad: grid too large");
+  WgradArgs a{};
+  tower_wgrad_route_rowwise_kernel<<<dim3((unsigned)(n_cnt + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
+      a, nullptr, r, d, 0, (int)n_cnt, (int)dd_grid);
+  return check_launch("shard_route_count_rowwise_adagrad");
+}
+
 int tt_tower_grads_replicated_route_place_gather(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
                                                  int copies, const int64_t* offsets, float scale, void* workspace,
                                                  size_t ws_bytes, int F, const void* const* cols, int id_dtype,
@@ -2864,6 +2924,32 @@ int tt_tower_wgrad_pre_insert_rowwise_adagrad(const tt_tower_shape_t* shape, int
   tower_tail_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
       a2, reinterpret_cast<const WgradTile*>(ws + a2.tiles_off), ins, d, (int)n_ins, (int)wgs, stamps);
   return check_launch("tower_wgrad_pre_insert_rowwise_adagrad");
+}
+
+int tt_tower_fwd_bwd_indexed_multi_bf16(const tt_tower_shape_t* shape, int64_t B, int D, const int32_t* pos_in,
+                                        const int32_t* pos_out, const void* rows_in, float* grad_rows_out,
+                                        const float* params, const void* labels, int label_dtype, float grad_scale,
+                                        float* logits, void* workspace, size_t ws_bytes, void* stream) {
+  if (!shape || !pos_in || !pos_out || !rows_in || !grad_rows_out)
+    return fail(TT_EINVAL, "tower_indexed_multi: null pointer");
+  if (D < 16 || D > 128 || D % 16 || XCH % D)
+    return fail(TT_EINVAL, "tower_indexed_multi: feature dim must be 16..128, a multiple of 16 dividing 128");
+  for (int t = 0; t < 2; ++t)
+    if (shape->in_dim[t] % D) return fail(TT_EINVAL, "tower_indexed_multi: tower input not a multiple of D");
+  if (shape->in_col[0] != 0 || shape->in_col[1] != shape->in_dim[0])
+    return fail(TT_EINVAL, "tower_indexed_multi: query features first, then candidate features");
+  if ((reinterpret_cast<uintptr_t>(rows_in) & 7) || (reinterpret_cast<uintptr_t>(grad_rows_out) & 3))
+    return fail(TT_EINVAL, "tower_indexed_multi: rows not aligned");
+  TowerArgs a{};
+  a.ipos = pos_in;
+  a.ipos_out = pos_out;
+  a.isrc = reinterpret_cast<const __bf16*>(rows_in);
+  a.idst = grad_rows_out;
+  a.ifeat0[0] = 0;
+  a.ifeat0[1] = shape->in_dim[0] / D;
+  a.iD = D;
+  return launch_t1(shape, B, a, nullptr, shape->in_dim[0] + shape->in_dim[1], nullptr, params, labels, label_dtype,
+                   grad_scale, logits, workspace, ws_bytes, stream);
 }
 
 int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,

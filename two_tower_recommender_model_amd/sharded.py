@@ -249,19 +249,33 @@ class FusedShardedTwoTowerStep:
                  batch_size: int, device: torch.device, sharding: Optional[Sequence[str]] = None,
                  tw_owners: Optional[Sequence[int]] = None, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
-                 capacity=None, full_tables: Optional[Sequence[torch.Tensor]] = None):
-        """Two features (query, candidate), one table each, single-hot. ``sharding[f]`` is
+                 capacity=None, full_tables: Optional[Sequence[torch.Tensor]] = None,
+                 num_query_features: Optional[int] = None, overlap: bool = True):
+        """Single-hot features, one table each: features 0 .. Fq-1 feed the query tower (their rows
+        concatenated in that order: torch.cat([kt[f] for f in query features]),
+        03_model_training.py:420-425), features Fq .. F-1 the candidate tower; ``num_query_features``
+        = Fq (default 1 with two features: the reference's user / item towers). ``sharding[f]`` is
         "row_wise" (default) or "table_wise" (owner ``tw_owners[f]``). ``capacity``: slots per
         (owner, row-wise feature) segment — an int, a per-feature list, or None (default_capacity);
         a table-wise feature's owner segment holds B. ``full_tables`` (CPU, optional) give the
         initial weights; otherwise each rank draws its shard from U(-sqrt(1/N), sqrt(1/N)) (torchrec
         EBC init). Tower parameters are initialised from ``seed`` identically on every rank (what
-        DDP's initial broadcast guarantees)."""
+        DDP's initial broadcast guarantees). Two features run T1 in its fused 2-layer form
+        (tt_tower_fwd_bwd_indexed2_bf16); more features per tower (BASELINE configs 3 and 4) run the
+        general T1 over the concatenated rows (tt_tower_fwd_bwd_indexed_multi_bf16). ``overlap``: the
+        pipelined step runs the towers' weight gradients (T2) on a parallel stream beside exchange A
+        and the owner's update (else inside launch U, one stream)."""
         self.comm = comm
         self.W, self.rank = comm.world, comm.rank
         self.device = torch.device(device)
         dev = self.device
-        self.F = 2
+        self.F = len(num_embeddings)
+        if self.F < 2 or self.F > _lib.TT_MAX_FEATURES:
+            raise _lib.TTError("sharded step: 2..64 features")
+        self.Fq = int(num_query_features) if num_query_features is not None else (1 if self.F == 2 else 0)
+        if not 1 <= self.Fq < self.F:
+            raise _lib.TTError("sharded step: num_query_features must leave both towers at least one feature")
+        self.multi = not (self.F == 2 and self.Fq == 1)
         self.B = int(batch_size)
         self.D = int(embedding_dim)
         self.N = [int(n) for n in num_embeddings]
@@ -270,10 +284,14 @@ class FusedShardedTwoTowerStep:
         self.id_dtype = id_dtype
         sharding = list(sharding or ["row_wise"] * self.F)
         tw_owners = list(tw_owners or [f % self.W for f in range(self.F)])
+        if len(sharding) != self.F or len(tw_owners) != self.F:
+            raise _lib.TTError("sharded step: one sharding / owner per feature")
         self.sharding = sharding
         W, r, F, B, D = self.W, self.rank, self.F, self.B, self.D
-        if D % 4 or D > 128:
-            raise _lib.TTError("sharded step: D % 4 == 0 and D <= 128")
+        if D % 4 or D > 128 or (self.multi and (D % 16 or 128 % D)):
+            raise _lib.TTError("sharded step: D % 4 == 0 and D <= 128 (several features per tower: D in 16, 32, "
+                               "64, 128)")
+        self.in_dims = [self.Fq * D, (F - self.Fq) * D]
         # ---- shards
         self.block, self.owner, local_rows, self.row_lo = [], [], [], []
         for f in range(F):
@@ -306,9 +324,12 @@ class FusedShardedTwoTowerStep:
                 a = (1.0 / self.N[f]) ** 0.5
                 view.uniform_(-a, a, generator=torch.Generator(device=dev).manual_seed(seed * 1000 + 17 * r + f))
         # ---- towers (data-parallel replicas)
-        if not ops.FusedTowers.supported([D, D], self.layer_sizes, [0, D], B) or len(self.layer_sizes) != 2:
-            raise _lib.TTError("sharded step: towers must be 2 layers (fused T1 indexed mode)")
-        self.towers = ops.FusedTowers([D, D], self.layer_sizes, [0, D], B, dev)
+        in_cols = [0, self.in_dims[0]]
+        if not ops.FusedTowers.supported(self.in_dims, self.layer_sizes, in_cols, B) or \
+                (not self.multi and len(self.layer_sizes) != 2):
+            raise _lib.TTError("sharded step: unsupported tower shape (two features: 2 layers, fused T1; inputs up "
+                               "to 1024 wide, widths 32..128)")
+        self.towers = ops.FusedTowers(self.in_dims, self.layer_sizes, in_cols, B, dev)
         P = self.towers.num_params
         self.params = torch.empty(P, dtype=torch.float32, device=dev)
         self.grads = torch.zeros(P, dtype=torch.float32, device=dev)
@@ -317,8 +338,8 @@ class FusedShardedTwoTowerStep:
         self.adam_state = torch.zeros(2, dtype=torch.int64, device=dev)
         g = torch.Generator().manual_seed(seed + 1)
         chunks = []
-        for _ in range(2):
-            i = D
+        for t in range(2):
+            i = self.in_dims[t]
             for out in self.layer_sizes:
                 bound = 1.0 / i ** 0.5
                 chunks += [torch.empty(out, i).uniform_(-bound, bound, generator=g).flatten(),
@@ -383,6 +404,8 @@ class FusedShardedTwoTowerStep:
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
         self.logits = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
+        self.overlap = bool(overlap)
+        self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         self.pool_graphs: list = []
         self.small_graphs: list = []
         self.cursor = None  # pipelined pool: index of the batch whose rows are staged in rows_in
@@ -431,9 +454,9 @@ class FusedShardedTwoTowerStep:
 
     def layer_views(self):
         """[(W, b)] per tower (query, candidate) as views of the flat parameter buffer."""
-        out, o, D = [], 0, self.D
-        for _ in range(2):
-            layers, i = [], D
+        out, o = [], 0
+        for t in range(2):
+            layers, i = [], self.in_dims[t]
             for n in self.layer_sizes:
                 w = self.params[o:o + n * i].view(n, i)
                 o += n * i
@@ -500,6 +523,12 @@ class FusedShardedTwoTowerStep:
     def _t1(self, parity: int, labels: torch.Tensor) -> None:
         lib, tw, B = _lib.load(), self.towers, self.B
         pin, pout = self.pos_in[parity], self.pos_out[parity]
+        if self.multi:
+            check(lib.tt_tower_fwd_bwd_indexed_multi_bf16(
+                C.byref(tw.shape), B, self.D, ptr(pin), ptr(pout), ptr(self.rows_in), ptr(self.sendA),
+                ptr(self.params), ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), ptr(tw.ws), tw.nbytes,
+                stream_handle(self.device)), "tower_fwd_bwd_indexed_multi")
+            return
         check(lib.tt_tower_fwd_bwd_indexed2_bf16(
             C.byref(tw.shape), B, ptr_array([pin[:B], pin[B:]]), ptr_array([pout[:B], pout[B:]]),
             ptr_array([self.rows_in, self.rows_in]), ptr_array([self.sendA, self.sendA]), ptr(self.params),
@@ -571,14 +600,31 @@ class FusedShardedTwoTowerStep:
         staging batch i+1's rows and routing ``next2_cols`` (batch i+2, same parity)."""
         lib, tw, ts, r, B, dev = _lib.load(), self.towers, self.tables, self.rank, self.B, self.device
         self._t1(parity, labels)
-        self._exchange_a()
         route = self._route_args(next2_cols, parity)
         ws = self.dd_ws[parity]
-        check(lib.tt_tower_wgrad_route_count_rowwise_adagrad(
-            C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
-            0.999, *route, ts._tm, ts.T, self._fm_src, self.W,
-            self.S[r], ptr(self.recvA), self.D, ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws),
-            ws.numel(), self.max_lookups, stream_handle(dev)), "tower_wgrad_route_count_rowwise_adagrad")
+        main = torch.cuda.current_stream(dev)
+        if self.overlap:
+            # T2 (weight gradients + Adam's step scalars) on a parallel branch: it reads only T1's
+            # operand strips, so it overlaps exchange A and the owner's update; launch G (which
+            # reduces T2's slabs into exchange B) joins it
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                check(lib.tt_tower_wgrad_pre(C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes,
+                                             ptr(self.adam_state), self.lr_dense, 0.9, 0.999, None, 0, 0,
+                                             stream_handle(dev)), "tower_wgrad_pre")
+            self._exchange_a()
+            check(lib.tt_shard_route_count_rowwise_adagrad(
+                route[0], B, *route[1:], ts._tm, ts.T, self._fm_src, self.W, self.S[r], ptr(self.recvA), self.D, ptr(ts.weights),
+                ptr(ts.state), self.lr_emb, self.eps, ptr(ws), ws.numel(), self.max_lookups, stream_handle(dev)),
+                "shard_route_count_rowwise_adagrad")
+            main.wait_stream(self.side)
+        else:
+            self._exchange_a()
+            check(lib.tt_tower_wgrad_route_count_rowwise_adagrad(
+                C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
+                0.999, *route, ts._tm, ts.T, self._fm_src, self.W,
+                self.S[r], ptr(self.recvA), self.D, ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws),
+                ws.numel(), self.max_lookups, stream_handle(dev)), "tower_wgrad_route_count_rowwise_adagrad")
         g = self._gather_args(parity ^ 1)
         g = g[:3] + g[5:]  # the combined launch takes F and W from the route's arguments
         check(lib.tt_tower_grads_replicated_route_place_gather(
@@ -600,7 +646,14 @@ class FusedShardedTwoTowerStep:
                 out.append((0, self.N[f] if self.owner[f] == r else 0))
         return out
 
-    def gathered_state_dict(self, feature_names: Sequence[str] = ("user_id", "product_id"),
+    def _names(self, feature_names):
+        names = list(feature_names) if feature_names is not None else (
+            ["user_id", "product_id"] if self.F == 2 else [f"f{i}" for i in range(self.F)])
+        if len(names) != self.F:
+            raise _lib.TTError("one feature name per feature")
+        return names
+
+    def gathered_state_dict(self, feature_names: Optional[Sequence[str]] = None,
                             prefix: str = "two_tower.", optimizer: bool = False) -> Dict[str, torch.Tensor]:
         """Collective: rank 0 returns the full state dict the reference's gather_and_get_state_dict
         writes (full tables + towers), other ranks {}. ``optimizer``: also the row-wise Adagrad state
@@ -609,7 +662,7 @@ class FusedShardedTwoTowerStep:
         from .lifecycle import _dense_items, _tower_views
 
         sd = {}
-        for f, name in enumerate(feature_names):
+        for f, name in enumerate(self._names(feature_names)):
             full = self.comm.gather_rows(self.tables.table_view(f), self.spans(f), self.N[f])
             if self.rank == 0:
                 sd[f"{prefix}ebc.embedding_bags.t_{name}.weight"] = full
@@ -618,7 +671,7 @@ class FusedShardedTwoTowerStep:
                 if self.rank == 0:
                     sd[f"optim.ebc.t_{name}.rowwise_adagrad_state"] = st[:, 0].clone()
         if self.rank == 0:
-            towers = _tower_views(self.params, [self.D, self.D], self.layer_sizes)
+            towers = _tower_views(self.params, self.in_dims, self.layer_sizes)
             sd.update({k: v.clone() for k, v in _dense_items(towers, prefix).items()})
             if optimizer:
                 sd["optim.towers.exp_avg"] = self.exp_avg.clone()
@@ -626,14 +679,14 @@ class FusedShardedTwoTowerStep:
                 sd["optim.towers.step"] = self.adam_state[:1].clone()
         return sd
 
-    def load_state_dict(self, sd: Dict[str, torch.Tensor], feature_names: Sequence[str] = ("user_id", "product_id"),
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], feature_names: Optional[Sequence[str]] = None,
                         prefix: str = "two_tower.") -> None:
         """Every rank takes its blocks of the full tables and the towers from a gathered dict (and
         the optimizer state when the dict holds ``optim.*`` keys; otherwise it is reset)."""
         from .lifecycle import _dense_items, _tower_views
 
         with torch.no_grad():
-            for f, name in enumerate(feature_names):
+            for f, name in enumerate(self._names(feature_names)):
                 lo, n = self.spans(f)[self.rank]
                 if n:
                     self.tables.table_view(f)[:n].copy_(sd[f"{prefix}ebc.embedding_bags.t_{name}.weight"][lo:lo + n])
@@ -642,7 +695,7 @@ class FusedShardedTwoTowerStep:
                         self.tables.state_view(f)[:n].copy_(sd[key][lo:lo + n])
                     else:
                         self.tables.state_view(f).zero_()
-            towers = _tower_views(self.params, [self.D, self.D], self.layer_sizes)
+            towers = _tower_views(self.params, self.in_dims, self.layer_sizes)
             for k, v in _dense_items(towers, prefix).items():
                 v.copy_(sd[k])
             if "optim.towers.exp_avg" in sd:
