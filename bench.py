@@ -81,8 +81,9 @@ def parse():
                     help="multi-hot workloads: group each batch inside its own step instead of one step ahead")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="sharded step: T2 inside launch U instead of on a parallel branch beside exchange A")
+    ap.add_argument("--overlap", action="store_true",
+                    help="sharded step: T2 on a parallel graph branch beside exchange A (default: inside launch U, "
+                         "one stream; the branch measured slower at world 1, DESIGN.md section 6)")
     ap.add_argument("--plan", default="auto", choices=["auto", "tw", "rw"],
                     help="N > 1 sharding plan of the two tables: tw = table-wise (users on rank 0, items on rank "
                          "1), rw = row-wise over all ranks; auto = tw at N = 2 (the same per-rank load as rw), rw "
@@ -667,7 +668,7 @@ def run_host_fed(args):
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
     host = synthetic_host_batches([num_users, num_items], B, args.batches, seed=1)
-    pipe = HostFedPipeline(step, group=args.steps_per_graph, depth=3)
+    pipe = HostFedPipeline(step, group=args.steps_per_graph, depth=3, trace=True)
     src = itertools.cycle(host)
     # whole groups, and enough of them that the pipeline's fill (two groups copied before the first
     # replay) and drain do not dominate: at least 64 groups timed
@@ -675,11 +676,15 @@ def run_host_fed(args):
     steps = max(64 * g, -(-args.steps // g) * g)
     pipe.run(src, max_steps=max(args.warmup, 4 * g))
     torch.cuda.synchronize()
+    pipe.trace.clear()
     t0 = time.perf_counter()
     n = pipe.run(src, max_steps=steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return n * B / dt, dt / n * 1e3, float(step.loss), n
+    info = pipe.summary()
+    info.update(graphs="production ring" if pipe.ring else "classic pool", steps_per_group=g,
+                host_cpus=len(os.sched_getaffinity(0)), torch_threads=torch.get_num_threads())
+    return n * B / dt, dt / n * 1e3, float(step.loss), n, info
 
 
 def run_multi(args, world, rank, local_rank):
@@ -709,7 +714,7 @@ def run_multi(args, world, rank, local_rank):
     cap = max(default_capacity(B, world), -(-int(need) // 8) * 8)
     step = FusedShardedTwoTowerStep(comm, N, D, layers, B, dev, sharding=sharding, tw_owners=owners, lr_emb=0.01,
                                     lr_dense=0.01, seed=0, capacity=cap, num_query_features=Fq,
-                                    overlap=not args.no_overlap)
+                                    overlap=args.overlap)
     step.load_batch(*batches[0])
     step.step()  # creates the RCCL communicators before any capture
     # gloo collectives (TT_REHEARSE_GLOO, testing only) are not capturable: eager steps
@@ -787,8 +792,9 @@ def main():
         value, ms, loss, roofline, cpu, steps_run = run_multihot(args)
         config["parallelism"] = "single-gpu hipgraph, KJT input"
     elif world == 1 and args.host_fed:
-        value, ms, loss, steps_run = run_host_fed(args)
+        value, ms, loss, steps_run, hf = run_host_fed(args)
         roofline, cpu = None, None
+        config["host_fed"] = hf
         config["parallelism"] = "single-gpu, host-fed: pinned staging + async H2D (copy stream) + hipgraph replay"
         config["note"] = "PCIe-inclusive rate (inputs handed over in host memory); the resident-input line is the metric"
     elif world == 1 and not args.sharded and args.workload not in SHARDED:

@@ -255,8 +255,11 @@ typedef struct {
   int32_t width[4];
   int32_t in_dim[2];
   int32_t in_col[2];
-  int32_t _pad;
+  int32_t flags; /* TT_TOWER_GENERAL_T1: T1 is always the general kernel (several features per tower,
+                    tt_tower_fwd_bwd_indexed_multi_bf16), so T3 keeps its plain bf16 weight copies
+                    even for 2-layer shapes <= 128 wide; 0 otherwise */
 } tt_tower_shape_t;
+#define TT_TOWER_GENERAL_T1 1
 
 int64_t tt_tower_num_params(const tt_tower_shape_t* shape);
 size_t tt_tower_workspace_bytes(const tt_tower_shape_t* shape, int64_t B);

@@ -8,8 +8,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("group,n", [(2, 7), (4, 16)])
-def test_host_fed_pipeline_equals_eager_steps(device, group, n):
+@pytest.mark.parametrize("group,n,ring", [(2, 7, True), (4, 16, True), (4, 10, False)])
+def test_host_fed_pipeline_equals_eager_steps(device, group, n, ring):
+    """ring: the production ring's graphs (the default), else the classic per-step graphs."""
     from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
     from two_tower_recommender_model_amd.host_pipeline import HostFedPipeline, synthetic_host_batches
 
@@ -17,9 +18,11 @@ def test_host_fed_pipeline_equals_eager_steps(device, group, n):
     host = synthetic_host_batches([2 * x for x in N], B, n, seed=group, zero_frac=0.02)  # ids past N: id % N
     a = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=3)
     b = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=3)
-    pipe = HostFedPipeline(a, group=group, depth=3)
+    pipe = HostFedPipeline(a, group=group, depth=3, ring=ring)
+    assert pipe.ring == ring
     a.reset_optimizer_state()
-    steps = pipe.run(host)
+    steps = pipe.run(host[:n // 2])  # two runs: the second restarts the ring (reset + prime)
+    steps += pipe.run(host[n // 2:])
     assert steps == n
     for cols, lab in host:
         b.load_batch([torch.from_numpy(c).to(device) for c in cols], torch.from_numpy(lab).to(device))

@@ -113,7 +113,7 @@ def _relu_bf(v):
 
 
 def emulate_bounds(xq: torch.Tensor, xc: torch.Tensor, params: Sequence[torch.Tensor], widths: Sequence[int],
-                   labels: torch.Tensor):
+                   labels: torch.Tensor, ex=None):
     """``emulate`` plus a per-element bound on how far the kernels' values may lie from it.
 
     The kernels and the emulation share every rounding point; they differ only in the order of the
@@ -125,6 +125,10 @@ def emulate_bounds(xq: torch.Tensor, xc: torch.Tensor, params: Sequence[torch.Te
     bound takes the whole value: the explicit mask for ReLU flips within error of 0). The last
     layer's sigmoid uses the hardware exp / reciprocal: 1e-6 absolute on sigma is allowed.
 
+    ``ex`` (optional) = [e_xq, e_xc]: element-wise bounds on how far the kernels' tower inputs may
+    lie from xq / xc (multi-hot bags: the pooled sums are fp32 sums in another order); by default
+    the inputs are the same values (single-hot rows).
+
     Returns (logits, e_logits), loss, [(dX, e_dX) per tower], [(g, e_g) in params order], all
     fp64, and ``ambiguous`` [B] bool: the rows with a ReLU unit (either tower, any layer) whose
     pre-activation lies within its bound of 0 (their mask may differ from the kernels').
@@ -135,9 +139,14 @@ def emulate_bounds(xq: torch.Tensor, xc: torch.Tensor, params: Sequence[torch.Te
     acts, zs, ezs, eacts, outs, eouts = [], [], [], [], [], []
     ambiguous = torch.zeros(B, dtype=torch.bool)
     i = 0
-    for x in (xq, xc):
-        h = bf(x)
-        eh = torch.zeros_like(h)
+    for t_in, x in enumerate((xq, xc)):
+        if ex is None:
+            h = bf(x)
+            eh = torch.zeros_like(h)
+        else:
+            x = x.double()
+            h = _bf32(x)
+            eh = _round_err(x, ex[t_in].double())
         a_t, ea_t, z_t, ez_t = [h], [eh], [], []
         for li in range(L):
             W, b = Ws[i], Ws[i + 1]
@@ -302,6 +311,30 @@ def check_adagrad(w_got, s_got, w_before, s_before, inv, dx_want, dx_bound, lr: 
     bad = ~((w_got.double() - w_want.double()).abs() <= tol_w)
     assert not bool(bad.any()), f"{what}: {int(bad.sum())} table elements outside the bound"
     return float((e_w / (lr * G.abs() / r[:, None]).clamp_min(1e-30)).median())
+
+
+def check_adam(p_before, m_before, v_before, step: int, g, e_g, p_got, m_got, v_got, lr: float,
+               betas=(0.9, 0.999), eps: float = 1e-8, what: str = "") -> None:
+    """torch.optim.Adam (KeyedOptimizerWrapper(Adam), 03_model_training.py:826-829) on flat fp32
+    parameters: step ``step`` (1-based) from (p, m, v)_before with the EMULATED gradient g, bound
+    e_g, against the kernels' (p, m, v) after. The bound is carried through m' = b1 m + (1 - b1) g,
+    v' = b2 v + (1 - b2) g^2 and the update lr m^ / (sqrt(v^) + eps), plus fp32 slack."""
+    b1, b2 = betas
+    g, e_g = g.double(), e_g.double()
+    m = b1 * m_before.double() + (1 - b1) * g
+    v = b2 * v_before.double() + (1 - b2) * g * g
+    e_m = (1 - b1) * e_g
+    e_v = (1 - b2) * (2 * g.abs() * e_g + e_g * e_g)
+    c1, c2 = 1 - b1 ** step, 1 - b2 ** step
+    mh, vh, e_mh, e_vh = m / c1, v / c2, e_m / c1, e_v / c2
+    den = vh.sqrt() + eps
+    den_lo = (vh - e_vh).clamp_min(0).sqrt() + eps
+    p = p_before.double() - lr * mh / den
+    e_p = lr * (e_mh / den_lo + mh.abs() * (1 / den_lo - 1 / den))
+    for name, got, want, e in (("exp_avg", m_got, m, e_m), ("exp_avg_sq", v_got, v, e_v), ("param", p_got, p, e_p)):
+        lim = e + 1e-5 * want.abs() + (1e-6 * lr if name == "param" else 1e-30)
+        bad = ~((got.double() - want).abs() <= lim)
+        assert not bool(bad.any()), f"{what} Adam {name}: {int(bad.sum())} of {want.numel()} outside the bound"
 
 
 def rel_err(got: torch.Tensor, want: torch.Tensor) -> float:

@@ -19,6 +19,7 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / "libtt_mi355x.so"
 TT_OK = 0
 TT_I32, TT_I64, TT_F32, TT_BF16 = 0, 1, 2, 3
 TT_POOL_SUM, TT_POOL_MEAN = 0, 1
+TT_TOWER_GENERAL_T1 = 1
 TT_MAX_FEATURES = 64
 TT_MAX_TABLES = 64
 
@@ -48,7 +49,7 @@ class TowerShape(C.Structure):
         ("width", C.c_int32 * 4),
         ("in_dim", C.c_int32 * 2),
         ("in_col", C.c_int32 * 2),
-        ("_pad", C.c_int32),
+        ("flags", C.c_int32),
     ]
 
 

@@ -2429,7 +2429,8 @@ static int t3_args(const tt_tower_shape_t* shape, int64_t B, float* params, floa
   a.wtbf = reinterpret_cast<__bf16*>(ws + L.o_wtbf);
   // the plain [out][in] / [in][out] bf16 copies are read only by tower_fwd_bwd_kernel, which
   // launch_t1 uses for shapes other than two layers over inputs <= 128 wide
-  a.skip_plain = shape->L == 2 && shape->in_dim[0] <= 128 && shape->in_dim[1] <= 128;
+  a.skip_plain = shape->L == 2 && shape->in_dim[0] <= 128 && shape->in_dim[1] <= 128 &&
+                 !(shape->flags & TT_TOWER_GENERAL_T1);
   a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.wd = weight_decay;
   a.step_state = step_state;
   a.do_adam = do_adam;
@@ -2940,6 +2941,9 @@ int tt_tower_fwd_bwd_indexed_multi_bf16(const tt_tower_shape_t* shape, int64_t B
     return fail(TT_EINVAL, "tower_indexed_multi: query features first, then candidate features");
   if ((reinterpret_cast<uintptr_t>(rows_in) & 7) || (reinterpret_cast<uintptr_t>(grad_rows_out) & 3))
     return fail(TT_EINVAL, "tower_indexed_multi: rows not aligned");
+  if (shape->L == 2 && shape->in_dim[0] <= 128 && shape->in_dim[1] <= 128 && !(shape->flags & TT_TOWER_GENERAL_T1))
+    return fail(TT_EINVAL, "tower_indexed_multi: set TT_TOWER_GENERAL_T1 in the shape (T3 must keep the general "
+                           "T1's weight copies)");
   TowerArgs a{};
   a.ipos = pos_in;
   a.ipos_out = pos_out;

@@ -15,6 +15,14 @@ step's kernels. Per group of ``group`` batches (one HIP graph of ``group`` steps
 
 ``depth`` device / pinned slots rotate (3: one computing, one landing, one being filled), so the
 host's memcpy and the PCIe copy of later groups overlap the graph of the current one.
+
+With ``ring`` (the default when the step supports it) the graphs are the PRODUCTION ring's
+(``FusedTwoTowerStep.capture_ring`` over the slots' batches: each step files the next batch's dedup
+table, rows looked up once are updated inside T1): group g's graph also reads the first batch of
+group g+1 (its last step files that batch), so group g starts after BOTH slots have landed; the
+first batch's table is primed when a run starts. ``trace`` records host timestamps per group
+(host copy, H2D issue, waits, replay issue) and device events around every replay, for
+``summary()``.
 """
 from __future__ import annotations
 
@@ -27,15 +35,17 @@ from . import _lib
 
 
 class HostFedPipeline:
-    def __init__(self, step, group: int = 8, depth: int = 3):
+    def __init__(self, step, group: int = 8, depth: int = 3, ring: Optional[bool] = None, trace: bool = False):
         """step: a FusedTwoTowerStep (single-hot columns). group: batches per graph replay."""
         if getattr(step, "kjt_input", False):
             raise _lib.TTError("HostFedPipeline: single-hot column input only")
         self.step = step
         self.group = int(group)
         self.depth = int(depth)
-        if self.group < 1 or self.depth < 2:
-            raise _lib.TTError("HostFedPipeline: group >= 1, depth >= 2")
+        self.ring = step.ring_supported() if ring is None else bool(ring)
+        if self.group < 1 or self.depth < (3 if self.ring else 2):
+            raise _lib.TTError("HostFedPipeline: group >= 1, depth >= 2 (3 with the ring)")
+        self.trace = [] if trace else None
         dev, B, F = step.device, step.B, step.F
         self.device = dev
         idt = step.id_dtype
@@ -56,14 +66,29 @@ class HostFedPipeline:
         for s in range(self.depth):
             for j in range(self.group):
                 batches.append(([self.dev_ids[s][j, f] for f in range(F)], self.dev_lab[s][j]))
-        step.capture_pool(batches, steps_per_graph=self.group)
-        self.graphs = list(step.pool_graphs)
+        self._batches = batches
+        if self.ring:
+            if (self.depth * self.group) % 2:
+                raise _lib.TTError("HostFedPipeline: the ring needs an even number of slot batches")
+            step.capture_ring(batches, steps_per_graph=self.group)
+            self.graphs = list(step.ring_graphs)
+            assert step.ring_offset == 0
+        else:
+            step.capture_pool(batches, steps_per_graph=self.group)
+            self.graphs = list(step.pool_graphs)
 
     # -- stage 1
+    def _t(self):
+        import time
+
+        return time.perf_counter()
+
     def _fill(self, slot: int, it: Iterator) -> int:
         """Host columns of up to `group` batches -> pinned slot -> async H2D. Returns the count."""
+        t0 = self._t() if self.trace is not None else 0.0
         if self.h2d_done[slot] is not None:
             self.h2d_done[slot].synchronize()  # the pinned buffer's previous copy has left
+        t1 = self._t() if self.trace is not None else 0.0
         n = 0
         for j in range(self.group):
             try:
@@ -75,6 +100,7 @@ class HostFedPipeline:
             self.pin_lab_np[slot][j] = np.asarray(labels)
             n += 1
         self.filled[slot] = n
+        t2 = self._t() if self.trace is not None else 0.0
         if n == 0:
             return 0
         with torch.cuda.stream(self.copy_stream):
@@ -85,15 +111,31 @@ class HostFedPipeline:
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
         self.h2d_done[slot] = ev
+        if self.trace is not None:
+            self.trace.append(("fill", slot, n, t0, t1, t2, self._t()))
         return n
 
     # -- stage 3
     def _compute(self, slot: int) -> None:
+        t0 = self._t() if self.trace is not None else 0.0
         main = torch.cuda.current_stream(self.device)
         main.wait_event(self.h2d_done[slot])
+        nxt = (slot + 1) % self.depth
+        if self.ring and self.filled[nxt] and self.h2d_done[nxt] is not None:
+            main.wait_event(self.h2d_done[nxt])  # the ring's last step files group g+1's first batch
         n = self.filled[slot]
+        if self.trace is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(main)
+        t1 = self._t() if self.trace is not None else 0.0
         if n == self.group:
             self.graphs[slot].replay()
+        elif self.ring:  # a final partial group: the production steps, eagerly
+            st, nb = self.step, len(self._batches)
+            for j in range(n):
+                i = slot * self.group + j
+                cols, lab = self._batches[i]
+                st.ring_step(cols, lab, i % 2, self._batches[(i + 1) % nb][0])
         else:  # a final partial group: the same kernels, eagerly
             st = self.step
             keep = st.cols, st.labels
@@ -104,9 +146,34 @@ class HostFedPipeline:
                     st.step()
             finally:
                 st.cols, st.labels = keep
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(enable_timing=self.trace is not None)
         ev.record(main)
         self.slot_free[slot] = ev
+        if self.trace is not None:
+            self.trace.append(("compute", slot, n, t0, t1, self._t(), (e0, ev)))
+
+    def summary(self) -> dict:
+        """From ``trace``: mean host milliseconds per group in each stage (fill: the wait for the
+        pinned slot's previous copy, the host memcpy, the H2D issue; compute: the wait / replay
+        issue) and the device milliseconds per group between the replay's start and end events, and
+        the host's total per group (the loop's period)."""
+        if not self.trace:
+            return {}
+        torch.cuda.synchronize(self.device)
+        fills = [e for e in self.trace if e[0] == "fill"]
+        comps = [e for e in self.trace if e[0] == "compute"]
+        ms = lambda a, b: (b - a) * 1e3  # noqa: E731
+        out = {
+            "groups": len(comps),
+            "host_ms_fill_wait_prev_copy": sum(ms(e[3], e[4]) for e in fills) / max(1, len(fills)),
+            "host_ms_fill_memcpy": sum(ms(e[4], e[5]) for e in fills) / max(1, len(fills)),
+            "host_ms_fill_h2d_issue": sum(ms(e[5], e[6]) for e in fills) / max(1, len(fills)),
+            "host_ms_compute_issue": sum(ms(e[3], e[5]) for e in comps) / max(1, len(comps)),
+            "device_ms_per_group": sum(e[6][0].elapsed_time(e[6][1]) for e in comps) / max(1, len(comps)),
+        }
+        if len(comps) > 1:
+            out["host_ms_period"] = ms(comps[0][3], comps[-1][3]) / (len(comps) - 1)
+        return out
 
     def run(self, host_batches: Iterable[Tuple[Sequence, object]], max_steps: Optional[int] = None) -> int:
         """Train on host batches ((id columns, labels) per batch: numpy arrays or CPU tensors of the
@@ -122,6 +189,13 @@ class HostFedPipeline:
         # prologue: groups 0 .. depth-2 in flight
         for g in range(D - 1):
             self._fill(g % D, it)
+        if self.ring and self.filled[0]:
+            # the first batch's dedup table, once its slot has landed (every later table is filed
+            # by the step before its batch); tables left over from a previous run are emptied
+            main = torch.cuda.current_stream(self.device)
+            main.wait_event(self.h2d_done[0])
+            self.step.ring_reset()
+            self.step.ring_prime(self._batches[0][0], 0)
         g = 0
         while True:
             slot = g % D

@@ -526,10 +526,13 @@ class FusedTowers:
                 and B % 8 == 0 and B >= 8)
 
     def __init__(self, in_dims: Sequence[int], widths: Sequence[int], in_cols: Sequence[int], B: int,
-                 device: torch.device):
+                 device: torch.device, flags: int = 0):
+        """flags: _lib.TT_TOWER_GENERAL_T1 when T1 always runs the general kernel (several features
+        per tower)."""
         self.device = torch.device(device)
         self.B = int(B)
         sh = _lib.TowerShape()
+        sh.flags = int(flags)
         sh.L = len(widths)
         for i, w in enumerate(widths):
             sh.width[i] = int(w)

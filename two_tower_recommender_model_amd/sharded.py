@@ -250,7 +250,7 @@ class FusedShardedTwoTowerStep:
                  tw_owners: Optional[Sequence[int]] = None, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
                  capacity=None, full_tables: Optional[Sequence[torch.Tensor]] = None,
-                 num_query_features: Optional[int] = None, overlap: bool = True):
+                 num_query_features: Optional[int] = None, overlap: bool = False):
         """Single-hot features, one table each: features 0 .. Fq-1 feed the query tower (their rows
         concatenated in that order: torch.cat([kt[f] for f in query features]),
         03_model_training.py:420-425), features Fq .. F-1 the candidate tower; ``num_query_features``
@@ -264,7 +264,8 @@ class FusedShardedTwoTowerStep:
         (tt_tower_fwd_bwd_indexed2_bf16); more features per tower (BASELINE configs 3 and 4) run the
         general T1 over the concatenated rows (tt_tower_fwd_bwd_indexed_multi_bf16). ``overlap``: the
         pipelined step runs the towers' weight gradients (T2) on a parallel stream beside exchange A
-        and the owner's update (else inside launch U, one stream)."""
+        and the owner's update (else inside launch U, one stream; the default: the parallel branch
+        measured 94.1 against 70.5 us per world-1 step, profiles/r03_bench_sharded_w1*.log)."""
         self.comm = comm
         self.W, self.rank = comm.world, comm.rank
         self.device = torch.device(device)
@@ -329,7 +330,8 @@ class FusedShardedTwoTowerStep:
                 (not self.multi and len(self.layer_sizes) != 2):
             raise _lib.TTError("sharded step: unsupported tower shape (two features: 2 layers, fused T1; inputs up "
                                "to 1024 wide, widths 32..128)")
-        self.towers = ops.FusedTowers(self.in_dims, self.layer_sizes, in_cols, B, dev)
+        self.towers = ops.FusedTowers(self.in_dims, self.layer_sizes, in_cols, B, dev,
+                                      flags=_lib.TT_TOWER_GENERAL_T1 if self.multi else 0)
         P = self.towers.num_params
         self.params = torch.empty(P, dtype=torch.float32, device=dev)
         self.grads = torch.zeros(P, dtype=torch.float32, device=dev)

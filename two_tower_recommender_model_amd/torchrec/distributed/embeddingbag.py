@@ -70,7 +70,14 @@ def _reduce_scatter_rows(out: torch.Tensor, inp: torch.Tensor, W: int, pg) -> No
 
 
 def _all_gather_rows(out: torch.Tensor, inp: torch.Tensor, pg) -> None:
-    dist.all_gather_into_tensor(out, inp.contiguous(), group=pg)
+    """out[W*B, D] = every rank's inp[B, D], rank-major (all-gather along dim 0)."""
+    if dist.get_backend(pg) == "gloo" and inp.is_cuda:
+        # gloo (the CPU tests and the one-GPU multi-process rehearsal): its all-to-all takes device
+        # tensors, so the all-gather is an all-to-all of the input repeated for every destination
+        W = dist.get_world_size(pg)
+        dist.all_to_all_single(out, inp.contiguous().repeat(W, 1), group=pg)
+    else:
+        dist.all_gather_into_tensor(out, inp.contiguous(), group=pg)
 
 
 class _ShardedLookup(torch.autograd.Function):
