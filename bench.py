@@ -668,7 +668,7 @@ def run_host_fed(args):
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
     host = synthetic_host_batches([num_users, num_items], B, args.batches, seed=1)
-    pipe = HostFedPipeline(step, group=args.steps_per_graph, depth=3, trace=True)
+    pipe = HostFedPipeline(step, group=args.steps_per_graph, depth=4, trace=True)
     src = itertools.cycle(host)
     # whole groups, and enough of them that the pipeline's fill (two groups copied before the first
     # replay) and drain do not dominate: at least 64 groups timed

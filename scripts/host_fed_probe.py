@@ -18,7 +18,7 @@ torch.cuda.set_device(dev)
 N, B, g = [50_000_000, 100_000_000], 8192, 8
 step = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, dev, lr_emb=0.01, lr_dense=0.01, seed=0)
 host = synthetic_host_batches(N, B, 64, seed=1)
-pipe = HostFedPipeline(step, group=g, depth=3)
+pipe = HostFedPipeline(step, group=g, depth=4)
 # (1) the pool graphs alone (data already in the device slots)
 for gr in pipe.graphs:
     gr.replay()

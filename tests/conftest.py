@@ -32,3 +32,20 @@ def device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _release_gpu_memory(request):
+    """After every GPU test: drop the caching allocator's free blocks, so tests that start child
+    processes (each needs tens of GB of tables) never meet memory an earlier test left cached."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+
+    import torch
+
+    gc.collect()
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()

@@ -18,7 +18,7 @@ def test_host_fed_pipeline_equals_eager_steps(device, group, n, ring):
     host = synthetic_host_batches([2 * x for x in N], B, n, seed=group, zero_frac=0.02)  # ids past N: id % N
     a = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=3)
     b = FusedTwoTowerStep(N, [D, D], [0], [1], [128, 64], B, device, seed=3)
-    pipe = HostFedPipeline(a, group=group, depth=3, ring=ring)
+    pipe = HostFedPipeline(a, group=group, depth=4, ring=ring)
     assert pipe.ring == ring
     a.reset_optimizer_state()
     steps = pipe.run(host[:n // 2])  # two runs: the second restarts the ring (reset + prime)

@@ -45,14 +45,20 @@ struct DedupWs {
                      // walks the claimers instead of all cap slots
   Ovf* ovf;          // [groups][64], key EMPTY between steps (the resolver clears what it filed)
   int32_t ovf_groups;
+#if TT_EXPERIMENTS
   int64_t* stamps;  // EXPERIMENT (TT_DD_STAMPS): [update workgroups][8] s_memrealtime per phase
+#endif
   // hot rows split over a team of workgroups (dd_hot_role): partial sums [hot_cap][DD_HOT_TEAM][128]
   // and per hot row the team's arrival counter (zero between launches: reset by the last arriver)
   float* hotp;
   int32_t* hcnt;
 };
+#if TT_EXPERIMENTS
 #define DD_STAMP(k) \
   do { if (ws.stamps && threadIdx.x == 0) ws.stamps[(int64_t)bid * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define DD_STAMP(k) do { } while (0)
+#endif
 
 __device__ __forceinline__ uint64_t dd_mix64(uint64_t x) {
   x ^= x >> 33;

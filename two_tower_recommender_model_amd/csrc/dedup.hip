@@ -55,7 +55,11 @@ size_t dedup_layout(void* base, int64_t L, DedupWs* w) {
   t.ovf_groups = (int32_t)((L + 63) / 64);
   t.ovf = reinterpret_cast<DedupWs::Ovf*>(take(sizeof(DedupWs::Ovf) * 64 * (size_t)t.ovf_groups));
   int64_t* dbg = reinterpret_cast<int64_t*>(take(sizeof(int64_t) * 8 * (L / (8 * DD_SPH) + 64)));
+#if TT_EXPERIMENTS
   t.stamps = getenv("TT_DD_STAMPS") ? dbg : nullptr;
+#else
+  (void)dbg;
+#endif
   const int64_t hot_cap = L / (DD_INL + 1) + 1;
   t.hotp = reinterpret_cast<float*>(take(sizeof(float) * 128 * DD_HOT_TEAM * hot_cap));
   t.hcnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * hot_cap));
@@ -142,7 +146,9 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
   // 64 hot workgroups: every one that finds no hot row still checks in, and at uniform ids (no hot
   // rows) 128 cost the ring's tail launch ~0.3 us on MI355X while halving the Zipf tail's hot rows
   int64_t hot_max = 64;
+#if TT_EXPERIMENTS
   if (const char* e = getenv("TT_DD_HOT_WGS")) hot_max = std::max(8, atoi(e));  // EXPERIMENT (A/B)
+#endif
   a.hot_wgs = (int)std::min<int64_t>(hot_max, std::max<int64_t>(1, max_lookups / (DD_INL + 1)));
   a.slot_hw = ceil_div(ceil_div(max_lookups, DD_SPH), 8) * 8;
   *grid = a.hot_wgs + a.slot_hw / 8;

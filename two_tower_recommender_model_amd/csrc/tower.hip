@@ -120,15 +120,27 @@ struct TowerArgs {
   float* idst;
   int ifeat0[2];
   int iD;
+#if TT_EXPERIMENTS
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
+#endif
 };
+#if TT_EXPERIMENTS
+#define TDBG(bit) ((a.dbg & (bit)) != 0)
+#else
+#define TDBG(bit) false
+#endif
 // EXPERIMENT (TT_T1_DEBUG bit 64 with 8): lane 0 of every wave at its arrival at barrier k (1..7),
 // at its start (0) and its end (8): [nwg][16][9] after the 8192 stamps of the other launches
+#if TT_EXPERIMENTS
 #define T1_WSTAMP(k) \
   do { if (a.stamps && (a.dbg & 64) && lane == 0) a.stamps[8192 + ((int64_t)blockIdx.x * 16 + (k)) * 9 + wid] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 #define T1_STAMP(k) \
   do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define T1_WSTAMP(k) do { } while (0)
+#define T1_STAMP(k) do { } while (0)
+#endif
 
 __device__ __forceinline__ float lbl(const void* p, int dt, int64_t i) {
   if (dt == TT_I32) return (float)reinterpret_cast<const int32_t*>(p)[i];
@@ -714,12 +726,12 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         pv[j] = p ? *reinterpret_cast<const uint32_t*>(p + (k % SEG) * 64) : 0u;
       }
     };
-    const bool late = (a.dbg & 256) != 0;  // experiment: prefetch after the last barrier
+    const bool late = TDBG(256);  // experiment: prefetch after the last barrier
     if (pref && !late) issue_prefetch();
     uint32_t touch = 0;
 #pragma unroll 1
     for (int k = 1; k < T1_BARRIERS; ++k) {
-      if (k == 5 && (a.dbg & 512) && r >= 0) {
+      if (k == 5 && TDBG(512) && r >= 0) {
         // experiment: re-touch this lookup's row and state (translation) ahead of the in-place update
         touch = *reinterpret_cast<const uint32_t*>((tq ? a.gtab[1] : a.gtab[0]) + r * IN_) ^
                 __float_as_uint((tq ? a.us[1] : a.us[0])[r]);
@@ -761,7 +773,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     __syncthreads();
     __syncthreads();
     if (a.dd_on) dd_insert_defer_finish(a.dd, p, (int32_t)(tq * a.B + gm), (int)blockIdx.x);
+#if TT_EXPERIMENTS
     if (a.stamps && lane == 0) a.stamps[(int64_t)blockIdx.x * 16 + 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll 1
     for (int k = 2; k < T1_BARRIERS; ++k) __syncthreads();
     return;
@@ -820,9 +834,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
             if (pin >= 0)
               src[i] = reinterpret_cast<const char*>(a.gsrc[t]) + ((int64_t)pin * in + c4) * (r16 ? 2 : 4);
           } else {
-            const int64_t id = (a.dbg & 32) ? 1 : load_id(a.gcol[t], a.gid_dtype, gm);
+            const int64_t id = TDBG(32) ? 1 : load_id(a.gcol[t], a.gid_dtype, gm);
             if (id != 0)
-              src[i] = reinterpret_cast<const char*>(a.gtab[t] + ((a.dbg & 4) ? 0 : py_mod64(id, a.gmod[t])) * in + c4);
+              src[i] = reinterpret_cast<const char*>(a.gtab[t] + (TDBG(4) ? 0 : py_mod64(id, a.gmod[t])) * in + c4);
           }
         }
       }
@@ -847,7 +861,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     }
   }
   Frags f0, f1, g1;
-  if (a.dbg & 16) {
+  if (TDBG(16)) {
     for (int s_ = 0; s_ < 4; ++s_) for (int j_ = 0; j_ < 2; ++j_) { f0.f[s_][j_] = (bf16x8)(__bf16)0.f; f1.f[s_][j_] = f0.f[s_][j_]; g1.f[s_][j_] = f0.f[s_][j_]; }
   } else {
   load_frags(f0, a.wbf + a.wcoff[t][0], in, in, W0, w4);      // W0 [W0][in]
@@ -896,7 +910,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   // columns 4 p .. 4 p + 3 of a 4-row block; lane i receives column i): lane i then holds rows
   // r0 .. r0 + 7 of column c0 + i, one 16-B strip store. Every lane executes the reads (full EXEC):
   // groups past the last block read block 0 and store nothing.
-  if (!(a.dbg & 1)) {
+  if (!TDBG(1)) {
     const int g16 = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
     const int nblk = (in / 16) * (TR / 8);  // blocks of 16 columns x 8 rows
     for (int b0 = w4 * 4; b0 < nblk; b0 += 16) {  // wave-uniform
@@ -940,7 +954,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         hs[t][row * LSTR + col] = pk[rr];
       }
       const int r0 = i * 16 + q4 * 4;
-      if (!(a.dbg & 1)) store_t4(act_tile + col * TR + r0, pk, r0, nval);
+      if (!TDBG(1)) store_t4(act_tile + col * TR + r0, pk, r0, nval);
     }
   }
   T1_WSTAMP(2);
@@ -1017,7 +1031,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     s += dpp_f<0x4E>(s);
     if ((tt & 3) == 0) db1[c] = s;
     __bf16* dst = dz1_tile + c * TR + rb;
-    if (a.dbg & 1) {
+    if (TDBG(1)) {
     } else if (rb + 8 <= nval) {
       *reinterpret_cast<bf16x8*>(dst) = v;
     } else {
@@ -1049,7 +1063,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         xs[t][row * LSTR + col] = pk[rr];
       }
       const int r0 = i * 16 + q4 * 4;
-      if (!(a.dbg & 1)) store_t4(dz0_tile + col * TR + r0, pk, r0, nval);
+      if (!TDBG(1)) store_t4(dz0_tile + col * TR + r0, pk, r0, nval);
     }
     s += __shfl_xor(s, 16, 64);
     s += __shfl_xor(s, 32, 64);
@@ -1133,7 +1147,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     for (int i = 0; i < 4; ++i) {
       if (i < nxv && ur[i] >= 0) {
         const int c4 = ((tt + 256 * i) % (in / 4)) * 4;
-        if (!(a.dbg & 128)) {
+        if (!TDBG(128)) {
           *reinterpret_cast<f32x4*>(a.uw[t] + ur[i] * in + c4) = rw_apply(xv[i], gq[i], step[i]);
           if (c4 == 0) a.us[t][ur[i]] = snew[i];
         }
@@ -1143,7 +1157,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (i < nxv && dstq[i] && !(a.dbg & 2)) *reinterpret_cast<f32x4*>(dstq[i]) = gq[i];
+    if (i < nxv && dstq[i] && !TDBG(2)) *reinterpret_cast<f32x4*>(dstq[i]) = gq[i];
   T1_WSTAMP(8);
   T1_STAMP(15);
 }
@@ -1189,12 +1203,18 @@ struct WgradArgs {
   // staged path (every K <= 128): tiles of T2_NT dW rows x the whole K, (t, l, n0) per tile
   int lds;
   int32_t t2_code[16];  // t | l << 4 | n0 << 8
+#if TT_EXPERIMENTS
   int64_t* stamps;      // EXPERIMENT (TT_T2_STAMPS): [workgroups][8] s_memrealtime per phase
+#endif
   DedupWs dd;           // tt_tower_wgrad_pre with a dedup workspace: the first n_res workgroups
   int n_res;            //   finish T1's deferred inserts (dd_resolve_block)
 };
+#if TT_EXPERIMENTS
 #define T2_STAMP(k) \
   do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define T2_STAMP(k) do { } while (0)
+#endif
 
 // staged T2 (wgrad_lds_block): a workgroup owns T2_NT rows x all K columns of one dW over a batch
 // slice. The slice is read in passes of T2_PF chunks of T2_MB rows; ALL loads of a pass are issued
@@ -1526,8 +1546,12 @@ __device__ __forceinline__ void insert_next_block(const InsertArgs& ins, int blk
 }
 
 // EXPERIMENT (TT_RING_STAMPS): s_memrealtime of wave 0 at the start / end of each workgroup's role
+#if TT_EXPERIMENTS
 #define RING_STAMP(p, k) \
   do { if ((p) && threadIdx.x == 0 && blockIdx.x < 1024) (p)[(int64_t)blockIdx.x * 2 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define RING_STAMP(p, k) do { (void)(p); } while (0)
+#endif
 
 __global__ void __launch_bounds__(256) tower_wgrad_insert_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
                                                                  InsertArgs ins, int n_t2, int64_t* stamps) {
@@ -1622,10 +1646,16 @@ struct UpdateArgs {
   float out_scale;
   int in_srcs;
   int64_t in_stride;
+#if TT_EXPERIMENTS
   int64_t* stamps;  // EXPERIMENT (TT_RING_STAMPS): [workgroups][4] s_memrealtime per phase
+#endif
 };
+#if TT_EXPERIMENTS
 #define T3_STAMP(k) \
   do { if (a.stamps && threadIdx.x == 0 && bid < 512) a.stamps[(int64_t)bid * 4 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define T3_STAMP(k) do { } while (0)
+#endif
 
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
   T3_STAMP(0);
@@ -2118,8 +2148,10 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   a.in_max = L.in_max;
   a.Bp = L.Bp;
   a.nwg = L.nwg;
+#if TT_EXPERIMENTS
   if (const char* e = getenv("TT_T1_DEBUG")) a.dbg = atoi(e);
   if (a.dbg & 8) a.stamps = reinterpret_cast<int64_t*>(ws + L.o_dbg);
+#endif
   const int i0 = shape->in_dim[0], i1 = shape->in_dim[1], w0 = shape->width[0], w1 = shape->width[1];
   const dim3 g(L.nwg), b512(T1_THREADS);
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
@@ -2199,7 +2231,9 @@ static int wgrad_args(const tt_tower_shape_t* shape, int64_t B, float* loss, voi
   a.loss = loss;
   a.nbias = nbias;
   a.tiles_off = (int64_t)L.o_tiles;
+#if TT_EXPERIMENTS
   if (getenv("TT_T2_STAMPS")) a.stamps = reinterpret_cast<int64_t*>(ws + L.o_dbg);
+#endif
   a.lds = L.lds;
   for (int i = 0; i < 16; ++i) {
     a.t2_code[i] = L.t2_code[i];
@@ -2463,11 +2497,14 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
     tower_update_dedup_kernel<<<dim3((unsigned)(dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(a, *dd, (int)dd_grid);
     return check_launch("tower_update_rowwise_adagrad");
   }
+#if TT_EXPERIMENTS
   if (getenv("TT_RING_STAMPS")) {  // workgroups [0, 512) stamp
     TowerLayout L;
     tower_layout(shape, B, &L);
     a.stamps = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 6144;
   }
+#endif
+
   tower_update_kernel<<<dim3((unsigned)g3), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("tower_update");
 }
@@ -2709,7 +2746,11 @@ int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, in
   if (rc) return rc;
   const int64_t n_cnt = (int64_t)r.nblk * F;
   if (wgs + n_cnt + dd_grid > INT32_MAX) return fail(TT_EINVAL, "tower_wgrad_route_rowwise: grid too large");
+#if TT_EXPERIMENTS
   static const bool dd_first = !getenv("TT_U_DD_FIRST") || atoi(getenv("TT_U_DD_FIRST")) != 0;  // A/B switch
+#else
+  constexpr bool dd_first = true;
+#endif
   tower_wgrad_route_rowwise_kernel<<<dim3((unsigned)(wgs + n_cnt + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
       a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), r, d, (int)wgs,
       (int)n_cnt, dd_first ? (int)dd_grid : 0);
@@ -2843,7 +2884,7 @@ int tt_tower_wgrad_pre_insert(const tt_tower_shape_t* shape, int64_t B, float* l
   rc = insert_args(B, next_cols, id_dtype, num_embeddings, dedup_tables, next_dedup_ws, dedup_max_lookups, ins);
   if (rc) return rc;
   const int64_t n_ins = ceil_div(ceil_div(2 * B, 64), 4);  // 4 waves of 64 lookups per workgroup
-  int64_t* stamps = getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 4096 : nullptr;
+  int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 4096 : nullptr;
   tower_wgrad_insert_kernel<<<dim3((unsigned)(wgs + n_ins)), dim3(256), 0, as_stream(stream)>>>(
       a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), ins, (int)wgs, stamps);
   return check_launch("tower_wgrad_pre_insert");
@@ -2876,7 +2917,7 @@ int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, i
   rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
                nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0, a, &g3);
   if (rc) return rc;
-  int64_t* stamps = getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 6144 : nullptr;
+  int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 6144 : nullptr;
   if (stamps && (K3_RES_WGS + dd_grid + g3 > 1024 || L.nwg > 256)) stamps = nullptr;
   tower_update_dedup_resolve_kernel<<<dim3((unsigned)(K3_RES_WGS + dd_grid + g3)), dim3(256), 0,
                                       as_stream(stream)>>>(a, d, next, (int)dd_grid, stamps);
@@ -2920,7 +2961,7 @@ int tt_tower_wgrad_pre_insert_rowwise_adagrad(const tt_tower_shape_t* shape, int
   if (rc) return rc;
   d.skip_single = 1;
   const int64_t n_ins = ceil_div(ceil_div(2 * B, 256 * INS_PT), 8) * 8;  // INS_PT lookups per thread; % 8 == 0
-  int64_t* stamps = getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
+  int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
   if (stamps && L.nwg > 256) stamps = nullptr;
   tower_tail_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
       a2, reinterpret_cast<const WgradTile*>(ws + a2.tiles_off), ins, d, (int)n_ins, (int)wgs, stamps);

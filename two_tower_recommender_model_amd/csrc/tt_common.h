@@ -7,6 +7,12 @@
 #include <string>
 #include "tt_mi355x.h"
 
+// Experiment hooks (environment switches, s_memrealtime phase stamps, T1 debug bits used by
+// scripts/*_stamps.py): compiled out of release builds; build with TT_EXTRA_CFLAGS=-DTT_EXPERIMENTS=1
+#ifndef TT_EXPERIMENTS
+#define TT_EXPERIMENTS 0
+#endif
+
 #define TT_WAVE 64
 
 typedef __attribute__((ext_vector_type(4))) float f32x4v;

@@ -13,8 +13,13 @@ step's kernels. Per group of ``group`` batches (one HIP graph of ``group`` steps
                     step has no separate input_dist: the KJT build is fused into T1
   stage 3  compute  graph replay of group g on the step's stream, after its H2D event
 
-``depth`` device / pinned slots rotate (3: one computing, one landing, one being filled), so the
-host's memcpy and the PCIe copy of later groups overlap the graph of the current one.
+``depth`` device / pinned slots rotate (4: one computing, one landed for the next group, one being
+filled, one whose graph may still be draining); the host fills group g+2 right after queuing group
+g's graph, into the slot of group g-2. The host waits for that slot's last graph itself (an event it
+almost never has to wait for) and then issues the H2D with no device-side dependency: on this ROCm
+stack a hipMemcpyAsync queued behind a cross-stream event wait blocked the calling thread until the
+event fired (measured: 222 us of host time per group for the 1 MB id copy, 0.5 ms per group in all,
+against 0.29 ms of device work; profiles/r03_bench_hostfed*.log), so the host never ran ahead.
 
 With ``ring`` (the default when the step supports it) the graphs are the PRODUCTION ring's
 (``FusedTwoTowerStep.capture_ring`` over the slots' batches: each step files the next batch's dedup
@@ -35,7 +40,7 @@ from . import _lib
 
 
 class HostFedPipeline:
-    def __init__(self, step, group: int = 8, depth: int = 3, ring: Optional[bool] = None, trace: bool = False):
+    def __init__(self, step, group: int = 8, depth: int = 4, ring: Optional[bool] = None, trace: bool = False):
         """step: a FusedTwoTowerStep (single-hot columns). group: batches per graph replay."""
         if getattr(step, "kjt_input", False):
             raise _lib.TTError("HostFedPipeline: single-hot column input only")
@@ -43,8 +48,8 @@ class HostFedPipeline:
         self.group = int(group)
         self.depth = int(depth)
         self.ring = step.ring_supported() if ring is None else bool(ring)
-        if self.group < 1 or self.depth < (3 if self.ring else 2):
-            raise _lib.TTError("HostFedPipeline: group >= 1, depth >= 2 (3 with the ring)")
+        if self.group < 1 or self.depth < 4:
+            raise _lib.TTError("HostFedPipeline: group >= 1, depth >= 4")
         self.trace = [] if trace else None
         dev, B, F = step.device, step.B, step.F
         self.device = dev
@@ -103,16 +108,20 @@ class HostFedPipeline:
         t2 = self._t() if self.trace is not None else 0.0
         if n == 0:
             return 0
+        tr = self.trace is not None
+        if self.slot_free[slot] is not None:
+            self.slot_free[slot].synchronize()  # the graph that last read this slot (two groups back)
         with torch.cuda.stream(self.copy_stream):
-            if self.slot_free[slot] is not None:
-                self.copy_stream.wait_event(self.slot_free[slot])
+            t3 = self._t() if tr else 0.0
             self.dev_ids[slot][:n].copy_(self.pin_ids[slot][:n], non_blocking=True)
+            t4 = self._t() if tr else 0.0
             self.dev_lab[slot][:n].copy_(self.pin_lab[slot][:n], non_blocking=True)
+            t5 = self._t() if tr else 0.0
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
         self.h2d_done[slot] = ev
-        if self.trace is not None:
-            self.trace.append(("fill", slot, n, t0, t1, t2, self._t()))
+        if tr:
+            self.trace.append(("fill", slot, n, t0, t1, t2, self._t(), (t3, t4, t5)))
         return n
 
     # -- stage 3
@@ -168,6 +177,10 @@ class HostFedPipeline:
             "host_ms_fill_wait_prev_copy": sum(ms(e[3], e[4]) for e in fills) / max(1, len(fills)),
             "host_ms_fill_memcpy": sum(ms(e[4], e[5]) for e in fills) / max(1, len(fills)),
             "host_ms_fill_h2d_issue": sum(ms(e[5], e[6]) for e in fills) / max(1, len(fills)),
+            "host_ms_fill_wait_event": sum(ms(e[5], e[7][0]) for e in fills) / max(1, len(fills)),
+            "host_ms_fill_copy_ids": sum(ms(e[7][0], e[7][1]) for e in fills) / max(1, len(fills)),
+            "host_ms_fill_copy_labels": sum(ms(e[7][1], e[7][2]) for e in fills) / max(1, len(fills)),
+            "host_ms_fill_record": sum(ms(e[7][2], e[6]) for e in fills) / max(1, len(fills)),
             "host_ms_compute_issue": sum(ms(e[3], e[5]) for e in comps) / max(1, len(comps)),
             "device_ms_per_group": sum(e[6][0].elapsed_time(e[6][1]) for e in comps) / max(1, len(comps)),
         }
@@ -186,8 +199,10 @@ class HostFedPipeline:
             it = itertools.islice(it, max_steps)
         D = self.depth
         steps = 0
-        # prologue: groups 0 .. depth-2 in flight
-        for g in range(D - 1):
+        for k in range(D):  # a previous run's slots are refilled from group 0
+            self.filled[k] = 0
+        # prologue: groups 0 and 1 in flight
+        for g in range(2):
             self._fill(g % D, it)
         if self.ring and self.filled[0]:
             # the first batch's dedup table, once its slot has landed (every later table is filed
@@ -203,8 +218,7 @@ class HostFedPipeline:
                 break
             self._compute(slot)
             steps += self.filled[slot]
-            nxt = (g + D - 1) % D
-            self._fill(nxt, it)
+            self._fill((g + 2) % D, it)  # the slot of group g - 2
             g += 1
         return steps
 
