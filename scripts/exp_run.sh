@@ -1,6 +1,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --ids zipf > gpurun_out/r02e_bench_zipf.log 2>&1 || exit $?
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --workload config2 > gpurun_out/r02e_bench_config2.log 2>&1 || exit $?
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --sharded > gpurun_out/r02e_bench_sharded_w1.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 50 --warmup 10 > gpurun_out/s_bench.log 2>&1 || exit $?
+TT_EXPERIMENT_LIB=1 timeout -k 10 300 python -u scripts/ring_stamps.py > gpurun_out/s_ring.log 2>&1 || exit $?
+tail -2 gpurun_out/s_ring.log
+timeout -k 10 300 python -u scripts/rows_stamps.py > gpurun_out/s_rows_stamps.log 2>&1 || exit $?
+cat gpurun_out/s_rows_stamps.log

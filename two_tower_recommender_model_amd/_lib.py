@@ -15,6 +15,9 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libtt_mi355x.so"
+# measurement scripts only: an experiment build (TT_EXPERIMENTS=1, built with
+# `python -m two_tower_recommender_model_amd.build --experiments`) sits beside the release library
+EXP_LIB_PATH = Path(__file__).resolve().parent / "lib_exp" / "libtt_mi355x.so"
 
 TT_OK = 0
 TT_I32, TT_I64, TT_F32, TT_BF16 = 0, 1, 2, 3
@@ -327,7 +330,7 @@ def load(path: os.PathLike | None = None):
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = Path(path) if path else LIB_PATH
+        p = Path(path) if path else (EXP_LIB_PATH if os.environ.get("TT_EXPERIMENT_LIB") == "1" else LIB_PATH)
         if not p.exists():
             raise TTError(
                 f"libtt_mi355x.so not found at {p}: build it with "

@@ -22,6 +22,9 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 BUILD = ROOT / "build" / "tt_mi355x"
 LIB = PKG / "lib" / "libtt_mi355x.so"
+# experiment build (stamps / debug bits compiled in; loaded only with TT_EXPERIMENT_LIB=1)
+BUILD_EXP = ROOT / "build" / "tt_mi355x_exp"
+LIB_EXP = PKG / "lib_exp" / "libtt_mi355x.so"
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -49,51 +52,53 @@ def _stale(target: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def _compile(src: Path, obj: Path) -> None:
-    lang = ["-x", "hip"] if src.suffix == ".hip" else ["-x", "hip"]
-    cmd = [HIPCC, *CFLAGS, *lang, "-c", str(src), "-o", str(obj)]
+def _compile(src: Path, obj: Path, extra=()) -> None:
+    cmd = [HIPCC, *CFLAGS, *extra, "-x", "hip", "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
-    LIB.parent.mkdir(parents=True, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, experiments: bool = False) -> Path:
+    bdir, lib_path = (BUILD_EXP, LIB_EXP) if experiments else (BUILD, LIB)
+    extra = ["-DTT_EXPERIMENTS=1"] if experiments else []
+    bdir.mkdir(parents=True, exist_ok=True)
+    lib_path.parent.mkdir(parents=True, exist_ok=True)
     objs = []
     jobs = []
     for s in SOURCES:
         src = CSRC / s
-        obj = BUILD / (src.stem + ".o")
+        obj = bdir / (src.stem + ".o")
         objs.append(obj)
         if force or _stale(obj, [src, *HEADERS]):
             jobs.append((src, obj))
     if jobs:
         workers = min(len(jobs), max(1, min(8, os.cpu_count() or 1)))
         with cf.ThreadPoolExecutor(workers) as ex:
-            futs = [ex.submit(_compile, s, o) for s, o in jobs]
+            futs = [ex.submit(_compile, s, o, extra) for s, o in jobs]
             for f in futs:
                 f.result()
         if verbose:
             print("compiled:", ", ".join(s.name for s, _ in jobs))
-    if force or jobs or _stale(LIB, objs):
-        tmp = LIB.with_suffix(".so.tmp")
+    if force or jobs or _stale(lib_path, objs):
+        tmp = lib_path.with_suffix(".so.tmp")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, LIB)
+        os.replace(tmp, lib_path)
         if verbose:
-            print("linked", LIB)
-    return LIB
+            print("linked", lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--experiments", action="store_true", help="stamps / debug bits compiled in (lib_exp/)")
     args = ap.parse_args()
     try:
-        build(force=args.force, verbose=True)
+        build(force=args.force, verbose=True, experiments=args.experiments)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -135,8 +135,15 @@ __device__ __forceinline__ void dd_insert(const DedupWs& ws, uint64_t key, int32
 // overflow entry for dd_resolve_block, which runs in a later launch. Every lane writes its entry
 // (EMPTY when there is nothing to resolve): no counts, no compaction. The wave's tail is then ONE
 // atomic round trip, not a probe chain (the slowest of 64 lanes decides when a wave ends).
+__device__ __forceinline__ void dd_insert_defer_finish_at(const DedupWs& ws, const DdPend& p, int32_t i, int group,
+                                                          int entry);
 __device__ __forceinline__ void dd_insert_defer_finish(const DedupWs& ws, const DdPend& p, int32_t i, int group) {
-  const int lane = threadIdx.x & 63;
+  dd_insert_defer_finish_at(ws, p, i, group, threadIdx.x & 63);
+}
+// the same with the entry (< 64) of the group given explicitly (the row-owned T1: 16 lookups per wave)
+__device__ __forceinline__ void dd_insert_defer_finish_at(const DedupWs& ws, const DdPend& p, int32_t i, int group,
+                                                          int entry) {
+  const int lane = entry;
   const bool live = p.key != DD_EMPTY;
   const bool claimed = live && p.prev == DD_EMPTY;
   if (claimed) ws.slots[p.h].item[0] = i;

@@ -120,6 +120,8 @@ struct TowerArgs {
   float* idst;
   int ifeat0[2];
   int iD;
+  // the row-owned T1 (tower_rows_kernel): both towers' bf16 weight image, the LDS layout (rk_off)
+  const char* wimg;
 #if TT_EXPERIMENTS
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
@@ -673,6 +675,18 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   // a.gtab[t], ... with scalar loads (a per-lane index into the kernarg arrays is a vector load from
   // the kernarg segment: one more dependent memory hop in front of the row gather)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the [128, 64] towers over 128-wide inputs write ROW-MAJOR operand strips ([Bp][features], as the
+  // row-owned T1 does; the tail reads them with wgrad_lds_block_rm): copies of the LDS tiles
+  constexpr bool RM = IN_ == 128 && W0_ == 128 && W1_ == 64;
+  auto rm_copy = [&](const __bf16* tile, __bf16* dst, int nchunk, int ld, int nval_) {
+    // tile: TR rows at LSTR; dst: row 0 of the tile in a [Bp][ld] strip; nchunk 16-B pieces per row
+    const int tt_ = threadIdx.x & 255;
+    for (int idx = tt_; idx < TR * nchunk; idx += 256) {
+      const int row = idx / nchunk, ch = idx % nchunk;
+      if (row < nval_)
+        *reinterpret_cast<bf16x8*>(dst + (int64_t)row * ld + ch * 8) = *reinterpret_cast<const bf16x8*>(tile + row * LSTR + ch * 8);
+    }
+  };
   if (UPD && wid == 8) {
     T1_WSTAMP(0);
     // ---- the dedup wave (UPD): for each of the 2 x TR lookups, is its row looked up once in this
@@ -697,7 +711,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
       }
     }
     const uint64_t word = cl >= 0 ? a.dd.slots[cl].word : DD_EMPTY;
-    const bool single = cl >= 0 && (word & DD_CNT_MASK) == 1;
+    const bool single = r >= 0 && cl >= 0 && (word & (uint32_t)DD_CNT_MASK) == 1u;
     urow[tq][row] = single ? r : -1;
     ustate[tq][row] = st;
     T1_WSTAMP(1);
@@ -910,7 +924,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   // columns 4 p .. 4 p + 3 of a 4-row block; lane i receives column i): lane i then holds rows
   // r0 .. r0 + 7 of column c0 + i, one 16-B strip store. Every lane executes the reads (full EXEC):
   // groups past the last block read block 0 and store nothing.
-  if (!TDBG(1)) {
+  if (RM) {
+    rm_copy(xs[t], a.xt + (int64_t)t * a.in_max * a.Bp + m0 * a.in_max, IN_ / 8, (int)a.in_max, nval);
+  } else if (!TDBG(1)) {
     const int g16 = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
     const int nblk = (in / 16) * (TR / 8);  // blocks of 16 columns x 8 rows
     for (int b0 = w4 * 4; b0 < nblk; b0 += 16) {  // wave-uniform
@@ -954,12 +970,13 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
         hs[t][row * LSTR + col] = pk[rr];
       }
       const int r0 = i * 16 + q4 * 4;
-      if (!TDBG(1)) store_t4(act_tile + col * TR + r0, pk, r0, nval);
+      if (!RM && !TDBG(1)) store_t4(act_tile + col * TR + r0, pk, r0, nval);
     }
   }
   T1_WSTAMP(2);
   __syncthreads();
   T1_STAMP(2);
+  if (RM) rm_copy(hs[t], a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m0 * MAXW, W0_ / 8, MAXW, nval);
   // ---- 2. layer 1: out = relu(h W1^T + b1) (fp32)
   mma_frags(acc, hs[t], f1, W0, W1, w4);
 #pragma unroll
@@ -1018,20 +1035,34 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   for (int c = tt >> 2; c < W1; c += 64) {
     const int rb = (tt & 3) * 8;
     bf16x8 v;
-    float s = 0.f;
+    float s = 0.f, zz[8];
     for (int j = 0; j < 8; ++j) {
       const int row = rb + j;
       float z = outf[t][row * FSTR + c] > 0.f ? dlog[row] * outf[1 - t][row * FSTR + c] : 0.f;
       if (row >= nval) z = 0.f;
+      zz[j] = z;
       s += z;
       v[j] = (__bf16)z;
       dzs[t][row * LSTR + c] = v[j];
     }
-    s += dpp_f<0xB1>(s);  // the 4 lanes of a column are one quad: xor 1, then xor 2
-    s += dpp_f<0x4E>(s);
+    if (RM) {
+      // the row-owned T1's tree (rk_colsum, then the two 16-row halves): rows paired at row bits
+      // 3 (the quad partner ^ 1), 2, 1, 0 (in thread), then the halves (quad partner ^ 2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zz[j] += dpp_f<0xB1>(zz[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zz[j] += zz[j + 4];
+      zz[0] += zz[2];
+      zz[1] += zz[3];
+      s = zz[0] + zz[1];
+      s += dpp_f<0x4E>(s);
+    } else {
+      s += dpp_f<0xB1>(s);  // the 4 lanes of a column are one quad: xor 1, then xor 2
+      s += dpp_f<0x4E>(s);
+    }
     if ((tt & 3) == 0) db1[c] = s;
     __bf16* dst = dz1_tile + c * TR + rb;
-    if (TDBG(1)) {
+    if (RM || TDBG(1)) {
     } else if (rb + 8 <= nval) {
       *reinterpret_cast<bf16x8*>(dst) = v;
     } else {
@@ -1042,6 +1073,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   T1_WSTAMP(5);
   __syncthreads();
   T1_STAMP(5);
+  if (RM) rm_copy(dzs[t], a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + m0 * MAXW, W1_ / 8, MAXW, nval);
   // ---- 5. dZ0 = (dZ1 W1) * (h > 0)  -> xs (X is no longer needed)
   mma_frags(acc, dzs[t], g1, W1, W0, w4);
   T1_WSTAMP(14);
@@ -1049,29 +1081,44 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   for (int j = 0; j < 2; ++j) {
     if (w4 + 4 * j >= W0 / 16) continue;
     const int col = (w4 + 4 * j) * 16 + r16;
-    float s = 0.f;
+    float s = 0.f, hsum[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       bf16x4 pk;
+      float zz[4];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = i * 16 + q4 * 4 + rr;
         float z = (float)hs[t][row * LSTR + col] > 0.f ? acc[i][j][rr] : 0.f;
         if (row >= nval) z = 0.f;
+        zz[rr] = z;
         s += z;
         pk[rr] = (__bf16)z;
         xs[t][row * LSTR + col] = pk[rr];
       }
+      if (RM) {
+        // the row-owned T1's tree over the 16-row half i: row bits 3 (lanes ^ 32), 2 (^ 16), 1, 0
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) zz[rr] += __shfl_xor(zz[rr], 32, 64);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) zz[rr] += __shfl_xor(zz[rr], 16, 64);
+        hsum[i] = (zz[0] + zz[2]) + (zz[1] + zz[3]);
+      }
       const int r0 = i * 16 + q4 * 4;
-      if (!TDBG(1)) store_t4(dz0_tile + col * TR + r0, pk, r0, nval);
+      if (!RM && !TDBG(1)) store_t4(dz0_tile + col * TR + r0, pk, r0, nval);
     }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    if (RM) {
+      s = hsum[0] + hsum[1];
+    } else {
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+    }
     if (q4 == 0) db0[col] = s;
   }
   T1_WSTAMP(6);
   __syncthreads();
   T1_STAMP(6);
+  if (RM) rm_copy(xs[t], a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m0 * MAXW, W0_ / 8, MAXW, nval);
   // ---- 6. dX = dZ0 W0 -> LDS (outf is free since phase 4) -> pooled gradient, whole rows
   mma_w0_tr(acc, xs[t], w0img[t], W0, in, w4);
 #pragma unroll
@@ -1163,6 +1210,471 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// T1, row-owned form (tower_rows_kernel): the production shape — both towers over 128-wide
+// single-hot rows gathered from the tables, layers [128, 64]. One workgroup of 4 waves per 32
+// batch rows; wave w runs tower t = w >> 1 over rows 16 (w & 1) .. + 15 of the tile through the
+// whole chain (gather, both layers, logit, dZ1, dZ0, dX, the in-place row-wise Adagrad) with every
+// activation in registers: three barriers (the weight image landed; the towers' outputs exchanged
+// for the logit; the workgroup's bias / loss partials combined), no LDS round trip between layers.
+//
+// Every product is computed transposed, Z^T = W A^T: the weights are the MFMA A operand (M = the
+// layer's output features, from an LDS image of both towers' bf16 weights, 96 KB, copied whole by
+// LDS-DMA), the wave's 16 batch rows are N. The M rows of every tile are PERMUTED (rk_perm): row
+// rho of M-tile mt is feature 32 (mt >> 1) + 8 (rho >> 2) + 4 (mt & 1) + (rho & 3), so a lane's
+// result values of the tile pair (2 s, 2 s + 1) are features 32 s + 8 q .. + 7 of its batch row n
+// (q = lane >> 4, n = lane & 15) — exactly the B operand of the next product's k-step s, and two
+// 16-B pieces of the row (the gathered fp32 row is loaded straight into that layout, and dX comes
+// out in it: the row-wise Adagrad updates the row from registers). Forward A fragments are one
+// ds_read_b128 per lane (W [out][in] image, conflict-free under rk_swz); backward ones (W^T) two
+// ds_read_b64_tr_b16 from the same image (2-way: the minimum with a fixed 8-B half per read).
+// The T1 -> T2 operand strips (tile-major, strip_at) go through a per-wave LDS transpose; the bias
+// partials are fp32 column sums (a DPP transpose-reduce over the wave's 16 rows, then the two row
+// halves in order): the tail launch and T3 read the same buffers as with tower_l2_kernel.
+constexpr int RK_IN = 128, RK_W0 = 128, RK_W1 = 64;
+constexpr int RK_IMG_T = (RK_W0 + RK_W1) * 256;  // bytes per tower: W0 [128][128], then W1 [64][128]
+constexpr int RK_IMG = 2 * RK_IMG_T;             // 98,304 B
+// 16-B chunk swizzle of image row `row` (256-B rows): b128 reads of 16 permuted rows x one chunk
+// and transposed reads of 8 rows x 4 chunks (two 16-lane groups) hit distinct banks
+__host__ __device__ __forceinline__ int rk_swz(int row) {
+  return (row & 3) | (((row & 1) | (((row >> 3) & 1) << 1)) << 2);
+}
+__host__ __device__ __forceinline__ int rk_off(int row, int col) {  // byte offset of bf16 element (row, col)
+  return row * 256 + (((col >> 3) ^ rk_swz(row)) << 4) + ((col & 7) << 1);
+}
+__device__ __forceinline__ int rk_perm(int mt, int rho) {
+  return 32 * (mt >> 1) + 8 * (rho >> 2) + 4 * (mt & 1) + (rho & 3);
+}
+// A fragment (M-tile mt, k-step s) of W from its image ([M][K] rows): lane (rho, q) holds
+// W[rk_perm(mt, rho)][32 s + 8 q .. + 7]
+__device__ __forceinline__ bf16x8 rk_afwd(const char* img, int mt, int s, int rho, int q) {
+  return *reinterpret_cast<const bf16x8*>(img + rk_off(rk_perm(mt, rho), 32 * s + 8 * q));
+}
+// A fragment (M-tile mt, k-step s) of W^T from the image of W ([K][M] rows): lane 4 q' + p of the
+// 16-lane group q addresses image row 32 s + 8 q + q' (+ 4) at the 4 contiguous features
+// rk_perm(mt, 4 p .. 4 p + 3); lane rho receives feature rk_perm(mt, rho) at those rows
+__device__ __forceinline__ bf16x8 rk_abwd(const char* img, int mt, int s, int lane) {
+  const int q = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+  const int row = 32 * s + 8 * q + qq;
+  const int col = 32 * (mt >> 1) + 8 * p + 4 * (mt & 1);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + rk_off(row, col)));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + rk_off(row + 4, col)));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 rk_pack(const f32x4& a, const f32x4& b) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = (__bf16)a[j];
+    v[4 + j] = (__bf16)b[j];
+  }
+  return v;
+}
+// acc[mt] (mt < MT) = sum over k-steps s < S of A(mt, s) x b[s]: the A fragments of k-step s + 1
+// are read (into the other of two register sets) before k-step s's MFMAs issue, so with one wave
+// per SIMD each k-step's LDS latency hides behind the previous step's MFMAs
+template <int MT, int S, bool BWD>
+__device__ __forceinline__ void rk_gemm(f32x4 (&acc)[8], const char* img, const bf16x8 (&b)[4], int lane) {
+  const int n = lane & 15, q = lane >> 4;
+  bf16x8 fa[2][MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    acc[mt] = (f32x4)(0.f);
+    fa[0][mt] = BWD ? rk_abwd(img, mt, 0, lane) : rk_afwd(img, mt, 0, n, q);
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s + 1 < S) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        fa[(s + 1) & 1][mt] = BWD ? rk_abwd(img, mt, s + 1, lane) : rk_afwd(img, mt, s + 1, n, q);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s & 1][mt], b[s], acc[mt], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+// lane value from lane ^ X of its 16-lane row (X in {1, 2, 4, 8}) by DPP
+template <int X>
+__device__ __forceinline__ float rk_xor(float v) {
+  if constexpr (X == 1) return dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  if constexpr (X == 2) return dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  if constexpr (X == 4) return dpp_f<0x1B>(dpp_f<0x141>(v));  // row_half_mirror, then quad reversal
+  return dpp_f<0x128>(v);                        // row_ror 8
+}
+// column sums over the 16 lanes of each 16-lane row: NV values per lane in, NV / 16 out; after it,
+// lane n holds the sums of values k = (NV / 16) n + i, i < NV / 16 (halving at lane bits 3, 2, 1, 0)
+template <int X, int H>  // the live values v[0, 2 H) -> v[0, H)
+__device__ __forceinline__ void rk_halve(float* v, int n) {
+  const bool up = (n & X) != 0;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const float keep = up ? v[H + i] : v[i], send = up ? v[i] : v[H + i];
+    v[i] = keep + rk_xor<X>(send);
+  }
+}
+template <int NV>
+__device__ __forceinline__ void rk_colsum(float (&v)[NV], int n) {
+  static_assert(NV == 32 || NV == 16, "column sum of 32 or 16 values per lane");
+  rk_halve<8, NV / 2>(v, n);
+  rk_halve<4, NV / 4>(v, n);
+  rk_halve<2, NV / 8>(v, n);
+  rk_halve<1, NV / 16>(v, n);
+}
+// row-major operand strip ([Bp][nf] bf16, what the tail's wgrad_lds_block_rm reads): lane (q, n)
+// stores its 16-B pieces (features 32 s + 8 q .. + 7) of batch row m; a wave instruction writes 16
+// whole 64-B row segments
+// (every row of the tile, dead rows of a ragged tile included: the strips hold Bp rows, the tail
+// reads the first B; no branch around the stores, which would make later load waits count
+// conservatively)
+template <int NS>
+__device__ __forceinline__ void rk_strip(const bf16x8 (&v)[4], __bf16* row, int q) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) *reinterpret_cast<bf16x8*>(row + 32 * s + 8 * q) = v[s];
+}
+
+// raw 4- or 8-byte element i of an id / label column: the conversion is left to the caller, so a
+// dtype branch does not put a wait for the load right behind it (the loads of a prologue all issue
+// before the first wait)
+struct RkRaw {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ RkRaw rk_raw(const void* p, bool wide, int64_t i) {
+  RkRaw r;
+  if (wide) {
+    const uint2 v = reinterpret_cast<const uint2*>(p)[i];
+    r.lo = v.x;
+    r.hi = v.y;
+  } else {
+    r.lo = reinterpret_cast<const uint32_t*>(p)[i];
+    r.hi = 0u;
+  }
+  return r;
+}
+__device__ __forceinline__ int64_t rk_id(RkRaw r, bool wide) {
+  return wide ? (int64_t)(((uint64_t)r.hi << 32) | r.lo) : (int64_t)(int32_t)r.lo;
+}
+__device__ __forceinline__ float rk_label(RkRaw r, int dt) {
+  if (dt == TT_I32) return (float)(int32_t)r.lo;
+  if (dt == TT_I64) return (float)(int64_t)(((uint64_t)r.hi << 32) | r.lo);
+  return __uint_as_float(r.lo);
+}
+// EXPERIMENT (TT_T1_DEBUG bit 8): lane 0 of each wave at point k: stamps[8192 + (wg * 16 + k) * 9 + wave]
+#if TT_EXPERIMENTS
+#define RK_STAMP(k) \
+  do { if (a.stamps && lane == 0) a.stamps[8192 + ((int64_t)blockIdx.x * 16 + (k)) * 9 + wid] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+// extra points in wave slots 4 .. 7
+#define RK_STAMP2(k) \
+  do { if (a.stamps && lane == 0) a.stamps[8192 + ((int64_t)blockIdx.x * 16 + (k)) * 9 + 4 + wid] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define RK_STAMP(k) do { } while (0)
+#define RK_STAMP2(k) do { } while (0)
+#endif
+template <bool UPD>
+__global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
+  __shared__ __attribute__((aligned(16))) char wimg[RK_IMG];         // both towers' W0, W1 (rk_off)
+  __shared__ __attribute__((aligned(16))) float xo[2][2][16 * 64];  // tower outputs per (tower, row half)
+  __shared__ float bsum[2][RK_W0 + RK_W1];                          // row half 1's bias partials
+  __shared__ float lrow[TR];                                        // row losses
+  __shared__ __attribute__((aligned(16))) float xr[4][16 * RK_IN];  // per wave: its 16 gathered rows
+                                                                    // (fp32, 16-B chunk c of row n at c ^ n)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = wid >> 1, h = wid & 1, q = lane >> 4, n = lane & 15;
+  const int64_t B = a.B, m0 = (int64_t)blockIdx.x * TR, m = m0 + 16 * h + n;
+  const bool live = m < B;
+  RK_STAMP(0);
+  // ---- 0. loads in dependency order (vmcnt retires in issue order: a wait for a load also waits
+  // for everything issued before it): the ids, the label, the biases (raw: no conversion between
+  // them); the weight image -> LDS (LDS-DMA, 1 KB per wave instruction); the row
+  const bool wide = a.gid_dtype == TT_I64;
+  const int64_t mc = live ? m : 0;  // dead rows of a ragged tile read row 0 of every column
+  const RkRaw id_raw = rk_raw(t ? a.gcol[1] : a.gcol[0], wide, mc);
+  const RkRaw lab_raw = rk_raw(a.labels, a.label_dtype == TT_I64, mc);
+  f32x4 b0v[8], b1v[4];
+  {
+    const float* b0p = a.params + a.boff[t][0];
+    const float* b1p = a.params + a.boff[t][1];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) b0v[mt] = *reinterpret_cast<const f32x4*>(b0p + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1));
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) b1v[mt] = *reinterpret_cast<const f32x4*>(b1p + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // the weight image (no dependency): 24 16-B loads per lane into registers, issued while the ids
+  // come back (plain loads: with an LDS-DMA in flight the compiler waits vmcnt(0) at the first use
+  // of any load, so the ids must land before the first DMA is issued), written to LDS below
+  bf16x8 wreg[RK_IMG / 1024 / 4];
+#pragma unroll
+  for (int k = 0; k < RK_IMG / 1024 / 4; ++k)
+    wreg[k] = *reinterpret_cast<const bf16x8*>(a.wimg + (wid + 4 * k) * 1024 + lane * 16);
+  __builtin_amdgcn_sched_barrier(0);
+  const int64_t id = live ? rk_id(id_raw, wide) : 0;
+  const int64_t r = id != 0 ? py_mod64(id, t ? a.gmod[1] : a.gmod[0]) : -1;
+  const float* tab = t ? a.gtab[1] : a.gtab[0];
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) void glb_void;
+  // the wave's 16 rows -> LDS by LDS-DMA, two whole 512-B rows per wave instruction (two TLB pages
+  // per instruction, full lines; a lane-per-row-piece register gather touches 16 rows per
+  // instruction): lane l of instruction i carries 16-B chunk (l & 31) ^ row of row 2 i + (l >> 5),
+  // so that the B-layout reads below are conflict-free; rows without an id read table row 0
+  // (ignored)
+  float* xw = xr[wid];
+  {
+    const int rr0 = lane >> 5, pc = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 2 * i + rr0;
+      const int64_t rid = __shfl((long long)r, row, 64);
+      const float* src = tab + (rid >= 0 ? rid : 0) * RK_IN + 4 * (pc ^ row);
+      __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(xw + i * 256), 16, 0, 0);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // the classic step's insert of this batch's lookups (T1 with a dedup workspace): the claiming
+  // CAS now, the deferred finish at the end (lane q == 0 of each row)
+  DdPend pend;
+  pend.key = DD_EMPTY;
+  const int32_t li = (int32_t)(t * B + m);
+  if (!UPD && a.dd_on && q == 0 && live) {
+    const uint64_t key = r >= 0 ? (((uint64_t)(t ? a.dd_table[1] : a.dd_table[0]) << DD_TABLE_SHIFT) | (uint64_t)r)
+                                : DD_EMPTY;
+    dd_insert_begin(a.dd, key, li, pend);
+  }
+  RK_STAMP(1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the rows (LDS-DMA) and the image registers
+  RK_STAMP(2);
+#pragma unroll
+  for (int k = 0; k < RK_IMG / 1024 / 4; ++k)
+    *reinterpret_cast<bf16x8*>(wimg + (wid + 4 * k) * 1024 + lane * 16) = wreg[k];
+  __syncthreads();
+  RK_STAMP(3);
+  // this lane's row in the B layout: xv[mt] = features 32 (mt >> 1) + 8 q + 4 (mt & 1) .. + 3 (fp32)
+  f32x4 xv[8];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xw + n * RK_IN + 4 * (c ^ n));
+    xv[mt] = r >= 0 ? v : (f32x4)(0.f);
+  }
+  // UPD, past barrier 1 (nothing waits on these until the row update): is the row looked up once in
+  // this step (claim -> slot word in this batch's completed dedup table), its state
+  // (unconditional loads at clamped indices: a branch around a load pulls its first use, and the
+  // wait for it, into the branch)
+  int32_t cl = -1;
+  float s_old = 0.f;
+  if (UPD) {
+    cl = a.dd.claim[live ? t * B + m : 0];
+    s_old = (t ? a.us[1] : a.us[0])[r >= 0 ? r : 0];  // speculative: used only for a single-lookup row
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const char* img0 = wimg + t * RK_IMG_T;
+  const char* img1 = img0 + RK_W0 * 256;
+  // ---- 1. layer 0: h^T = relu(W0 X^T + b0), 8 M-tiles x 4 k-steps
+  bf16x8 xb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) xb[s] = rk_pack(xv[2 * s], xv[2 * s + 1]);
+  f32x4 acc[8];
+  rk_gemm<8, 4, false>(acc, img0, xb, lane);
+  RK_STAMP(4);
+  bf16x8 hb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    f32x4 u0, u1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u0[j] = fmaxf(acc[2 * s][j] + b0v[2 * s][j], 0.f);
+      u1[j] = fmaxf(acc[2 * s + 1][j] + b0v[2 * s + 1][j], 0.f);
+    }
+    hb[s] = rk_pack(u0, u1);
+  }
+  // ---- 2. layer 1: out^T = relu(W1 h^T + b1) (fp32), 4 M-tiles x 4 k-steps; exchanged in LDS
+  f32x4 uo[4];
+  rk_gemm<4, 4, false>(acc, img1, hb, lane);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) uo[mt] = acc[mt];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) uo[mt][j] = fmaxf(uo[mt][j] + b1v[mt][j], 0.f);
+    const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);  // 16-B chunk of the 64-float row
+    *reinterpret_cast<f32x4*>(&xo[t][h][n * 64 + ((c ^ n) << 2)]) = uo[mt];
+  }
+  RK_STAMP(5);
+  // the slot word's low half holds the lookup count (little-endian; DD_CNT_BITS < 32)
+  const uint32_t word = UPD ? reinterpret_cast<const uint32_t*>(&a.dd.slots[cl >= 0 ? cl : 0].word)[0] : 0u;
+  // the T1 -> T2 strips of X and h (row-major): fire-and-forget stores
+  rk_strip<4>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);
+  rk_strip<4>(hb, a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
+  RK_STAMP(6);
+  __syncthreads();
+  RK_STAMP(7);
+  // ---- 3. logit (both towers compute it: the same products in the same order), BCE, dlogit
+  f32x4 vo[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);
+    vo[mt] = *reinterpret_cast<const f32x4*>(&xo[t ^ 1][h][n * 64 + ((c ^ n) << 2)]);
+  }
+  // the summation tree of tower_l2_kernel's logit (bit-identical logits): per group of 4 columns
+  // an fma chain from 0, groups g = 16 s' + ... combined at group bits 0 (in lane), 1 (lanes ^ 16),
+  // 2 (lanes ^ 32), 3 (in lane); uo[mt] holds group 8 (mt >> 1) + 2 q + (mt & 1)
+  float gs[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    float e = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e = fmaf(uo[mt][j], vo[mt][j], e);
+    gs[mt] = e;
+  }
+  float c0 = gs[0] + gs[1], c1 = gs[2] + gs[3];
+  c0 += __shfl_xor(c0, 16, 64);
+  c1 += __shfl_xor(c1, 16, 64);
+  c0 += __shfl_xor(c0, 32, 64);
+  c1 += __shfl_xor(c1, 32, 64);
+  const float d = c0 + c1;
+  float lo = 0.f, dl = 0.f;
+  if (live) {
+    const float x = d, y = rk_label(lab_raw, a.label_dtype);
+    const float e = __expf(-fabsf(x));
+    const float l1p = e < 1e-4f ? e * (1.f - 0.5f * e) : __logf(1.f + e);
+    const float lsig = fminf(x, 0.f) - l1p;
+    lo = (1.f - y) * x - lsig;
+    const float rc = __builtin_amdgcn_rcpf(1.f + e);
+    dl = ((x >= 0.f ? rc : e * rc) - y) * (a.grad_scale / (float)B);
+  }
+  if (t == 0 && q == 0) lrow[16 * h + n] = lo;
+  // ---- 4. dZ1 = dlogit * other * (self > 0) (fp32: bias sums; bf16: the next product, the strip)
+  float z1[16];
+  bf16x8 z1b[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) z1[4 * mt + j] = live && uo[mt][j] > 0.f ? dl * vo[mt][j] : 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)z1[8 * s + j];
+    z1b[s] = v;
+  }
+  // ---- 5. dZ0^T = (W1^T dZ1^T) * (h > 0): 8 M-tiles x 2 k-steps
+  RK_STAMP(8);
+  rk_gemm<8, 2, true>(acc, img1, z1b, lane);
+  float z0[32];
+  bf16x8 z0b[4];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      z0[4 * mt + j] = live && (float)hb[mt >> 1][4 * (mt & 1) + j] > 0.f ? acc[mt][j] : 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)z0[8 * s + j];
+    z0b[s] = v;
+  }
+  // ---- 6. dX^T = W0^T dZ0^T: 8 M-tiles x 4 k-steps; acc[mt] = dX features of xv[mt]
+  RK_STAMP(9);
+  rk_gemm<8, 4, true>(acc, img0, z0b, lane);
+  RK_STAMP(10);
+  // ---- 7. the row: UPD + looked up once -> row-wise Adagrad in place (the K3 update's arithmetic and
+  // summation tree: feature groups of 4 combined at group bits 4, 3 (in lane), 2, 1 (lanes ^ 32,
+  // ^ 16), 0 (in lane)); otherwise dX -> the pooled gradient (and the gathered row, pooled_out)
+  float* grow = live ? a.gpooled + m * a.ldp + a.s.in_col[t] : nullptr;
+  bool store_dx = live;
+  if (UPD) {
+    float e2[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const float s0 = rw_sq4(acc[0 + hh]), s1 = rw_sq4(acc[2 + hh]), s2 = rw_sq4(acc[4 + hh]), s3 = rw_sq4(acc[6 + hh]);
+      float c2 = (s0 + s2) + (s1 + s3);
+      c2 += __shfl_xor(c2, 32, 64);
+      c2 += __shfl_xor(c2, 16, 64);
+      e2[hh] = c2;
+    }
+    RK_STAMP2(0);
+    const float sq = e2[0] + e2[1];
+    const float snew = rw_state(s_old, sq, RK_IN);
+    const float step = rw_step(snew, a.ulr, a.ueps);
+    const bool single = r >= 0 && cl >= 0 && (word & (uint32_t)DD_CNT_MASK) == 1u;
+    // the updated rows go back through the wave's LDS rows (same chunk swizzle) and out as two
+    // whole rows per store instruction, as they came in
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);
+      *reinterpret_cast<f32x4*>(xw + n * RK_IN + 4 * (c ^ n)) = rw_apply(xv[mt], acc[mt], step);
+    }
+    RK_STAMP2(1);
+    asm volatile("" ::: "memory");  // LDS is in order per wave: only the compiler must not reorder
+    {
+      const int rr0 = lane >> 5, pc = lane & 31;
+      float* wtab = t ? a.uw[1] : a.uw[0];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = 2 * i + rr0;
+        const int64_t rid = __shfl((long long)r, row, 64);
+        const int sg = __shfl((int)single, row, 64);
+        const f32x4 w = *reinterpret_cast<const f32x4*>(xw + row * RK_IN + 4 * pc);
+        if (sg) *reinterpret_cast<f32x4*>(wtab + rid * RK_IN + 4 * (pc ^ row)) = w;
+      }
+    }
+    RK_STAMP2(2);
+    if (single) {
+      if (q == 0) (t ? a.us[1] : a.us[0])[r] = snew;
+      store_dx = a.pooled_out != nullptr;  // dX only for inspection
+    }
+  }
+  if (store_dx) {
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+      *reinterpret_cast<f32x4*>(grow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = acc[mt];
+  }
+  RK_STAMP2(3);
+  if (t == 0 && q == 0 && live) a.logits[m] = d;  // after the row update (see rk_strip)
+  if (a.pooled_out && live) {
+    float* prow = a.pooled_out + m * a.ldp + a.s.in_col[t];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) *reinterpret_cast<f32x4*>(prow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = xv[mt];
+  }
+  RK_STAMP(11);
+  // ---- 8. the dZ strips; bias partials (fp32 column sums over the wave's rows, then row half 0 +
+  // row half 1); the loss partial (the tile's 32 row losses in order)
+  rk_strip<2>(z1b, a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + m * MAXW, q);
+  rk_strip<4>(z0b, a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
+  RK_STAMP(12);
+  rk_colsum<32>(z0, n);  // lane n: k = 2 n + i, i < 2 (k = 4 mt + j)
+  rk_colsum<16>(z1, n);  // lane n: k = n
+  // feature of value k = 4 mt + j: 32 (mt >> 1) + 8 q + 4 (mt & 1) + j
+  auto feat = [&](int k) { return 32 * ((k >> 2) >> 1) + 8 * q + 4 * ((k >> 2) & 1) + (k & 3); };
+  if (h == 1) {
+    bsum[t][feat(2 * n)] = z0[0];
+    bsum[t][feat(2 * n + 1)] = z0[1];
+    bsum[t][RK_W0 + feat(n)] = z1[0];
+  }
+  RK_STAMP(13);
+  __syncthreads();
+  RK_STAMP(14);
+  if (h == 0) {
+    float* db0 = a.dbpart + (((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW;
+    float* db1 = a.dbpart + (((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW;
+    db0[feat(2 * n)] = z0[0] + bsum[t][feat(2 * n)];
+    db0[feat(2 * n + 1)] = z0[1] + bsum[t][feat(2 * n + 1)];
+    db1[feat(n)] = z1[0] + bsum[t][RK_W0 + feat(n)];
+    if (t == 0 && lane == 0) {
+      float p = 0.f;
+      for (int i = 0; i < TR; ++i) p += lrow[i];
+      a.loss_part[blockIdx.x] = p;
+    }
+  }
+  // every row's overflow entry is written (EMPTY for a dropped id or a dead row of a ragged tile):
+  // the resolver reads all 64 entries of the group
+  if (!UPD && a.dd_on && q == 0) dd_insert_defer_finish_at(a.dd, pend, li, (int)blockIdx.x, 16 * wid + n);
+  RK_STAMP(15);
+}
+
+// ---------------------------------------------------------------------------------------------
 // T2: dW_(t,l)[n][k] = sum_m dZ_(t,l)[m][n] * A_(t,l)[m][k], A = X (l=0) or act_(t,l-1)
 
 struct WgradTile {
@@ -1202,6 +1714,7 @@ struct WgradArgs {
   float lr, beta1, beta2;
   // staged path (every K <= 128): tiles of T2_NT dW rows x the whole K, (t, l, n0) per tile
   int lds;
+  int rm;  // row-major operand strips ([Bp][features], the row-owned T1's shape): wgrad_lds_block_rm
   int32_t t2_code[16];  // t | l << 4 | n0 << 8
 #if TT_EXPERIMENTS
   int64_t* stamps;      // EXPERIMENT (TT_T2_STAMPS): [workgroups][8] s_memrealtime per phase
@@ -1324,6 +1837,108 @@ __device__ __forceinline__ void wgrad_lds_block(const WgradArgs& a, int lb, char
   T2_STAMP(3);
 }
 
+// staged T2 over ROW-MAJOR operand strips ([Bp][features] bf16: what the row-owned T1 and the
+// fixed-shape tower_l2_kernel write for the [128, 64] towers over 128-wide inputs): a chunk of 32 batch
+// rows x [T2_NT dZ features | K layer-input features] goes to LDS as 32 rows at a 416-B stride
+// (whole 16-B pieces of rows, three loads per thread as in wgrad_lds_block), and the fragments are
+// transposed reads (ds_read_b64_tr_b16). K-slot (q, j) of every fragment is chunk row
+// 4 q + (j & 3) + 16 (j >> 2): the 32 lanes of a read then address 8 consecutive rows, which the
+// 416-B stride (= 160 mod 256) spreads over all 64 banks
+constexpr int T2R_STR = 208;  // bf16 per LDS row
+static_assert(2 * TR * T2R_STR * 2 <= T2_SMEM, "the row-major staged chunks fit the tail's LDS");
+__device__ __forceinline__ bf16x8 t2r_frag(const __bf16* d, int col0, int lane) {
+  const int q = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+  const __bf16* base = d + (4 * q + qq) * T2R_STR + col0 + 4 * p;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 16 * T2R_STR));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ void wgrad_lds_block_rm(const WgradArgs& a, int lb, char* smem) {
+  __bf16* buf = reinterpret_cast<__bf16*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int s = __builtin_amdgcn_readfirstlane(lb / a.ntiles), ti = __builtin_amdgcn_readfirstlane(lb % a.ntiles);
+  T2_STAMP(0);
+  const int code = a.t2_code[ti];
+  const int t = code & 15, l = (code >> 4) & 15, n0 = code >> 8;
+  const int K = a.K[t][l];
+  const int NT = min(T2_NT, a.width[l] - n0);
+  const int64_t B = a.B;
+  const __bf16* Z = a.dzt + ((int64_t)t * MAXL + l) * MAXW * a.Bp;  // [Bp][MAXW]
+  const __bf16* A = l == 0 ? a.xt + (int64_t)t * a.in_max * a.Bp : a.act + ((int64_t)t * MAXL + l - 1) * MAXW * a.Bp;
+  const int64_t anf = l == 0 ? a.in_max : MAXW;
+  const int64_t mb = (int64_t)s * a.mslice;
+  const int64_t me = min(mb + a.mslice, B);
+  // loader: piece 0 = dZ row tid >> 3, features n0 + 8 (tid & 7); pieces 1, 2 = layer-input row
+  // idx >> 4, features 8 (idx & 15), idx = tid + 256 (i - 1); LDS column of a piece: dZ at 0, layer
+  // input at T2_NT. Uniform block bases + 32-bit per-thread byte offsets (one address VGPR per load
+  // of the 24 in flight: the tail kernel's roles share its register allocation)
+  const char* zb = reinterpret_cast<const char*>(Z);
+  const char* ab = reinterpret_cast<const char*>(A);
+  const int prow0 = tid >> 3, prow1 = tid >> 4, prow2 = (tid + 256) >> 4;
+  const bool ok0 = 8 * (tid & 7) < NT, ok1 = 8 * (tid & 15) < K, ok2 = 8 * ((tid + 256) & 15) < K;
+  const uint32_t zstr = MAXW * 2, astr = (uint32_t)anf * 2;  // bytes per strip row
+  const uint32_t zo = (uint32_t)(mb + prow0) * zstr + (uint32_t)(n0 + 8 * (tid & 7)) * 2;
+  const uint32_t ao1 = (uint32_t)(mb + prow1) * astr + (uint32_t)(8 * (tid & 15)) * 2;
+  const uint32_t ao2 = (uint32_t)(mb + prow2) * astr + (uint32_t)(8 * ((tid + 256) & 15)) * 2;
+  const int lw0 = prow0 * T2R_STR + 8 * (tid & 7);
+  const int lw1 = prow1 * T2R_STR + T2_NT + 8 * (tid & 15);
+  const int lw2 = prow2 * T2R_STR + T2_NT + 8 * ((tid + 256) & 15);
+  const int nh = wid >> 1, kh = wid & 1;  // wave: dW rows [32 nh, +32) x columns [64 kh, +64)
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)(0.f);
+  for (int64_t p0 = mb; p0 < me; p0 += T2_PF * T2_MB) {
+    bf16x8 ld[T2_PF][3];
+    const uint32_t dr = (uint32_t)(p0 - mb);  // rows into the slice
+#pragma unroll
+    for (int c = 0; c < T2_PF; ++c) {
+      const uint32_t rc = dr + c * T2_MB;
+      const int64_t mrow = p0 + c * T2_MB;
+      ld[c][0] = ok0 && mrow + prow0 < me ? *reinterpret_cast<const bf16x8*>(zb + zo + rc * zstr) : (bf16x8)(__bf16)0.f;
+      ld[c][1] = ok1 && mrow + prow1 < me ? *reinterpret_cast<const bf16x8*>(ab + ao1 + rc * astr) : (bf16x8)(__bf16)0.f;
+      ld[c][2] = ok2 && mrow + prow2 < me ? *reinterpret_cast<const bf16x8*>(ab + ao2 + rc * astr) : (bf16x8)(__bf16)0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < T2_PF; ++c) {
+      if (p0 + c * T2_MB >= me) break;  // uniform: the slice's tail
+      __bf16* d = buf + (c & 1) * TR * T2R_STR;
+      if (ok0) *reinterpret_cast<bf16x8*>(d + lw0) = ld[c][0];
+      if (ok1) *reinterpret_cast<bf16x8*>(d + lw1) = ld[c][1];
+      if (ok2) *reinterpret_cast<bf16x8*>(d + lw2) = ld[c][2];
+      __syncthreads();  // one barrier per chunk: buffer c & 1 was last read two chunks ago
+      if (c == 0 && p0 == mb) T2_STAMP(1);
+      bf16x8 fa[2], fb[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = t2r_frag(d, nh * 32 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = t2r_frag(d, T2_NT + kh * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  T2_STAMP(2);
+  float* dst = a.slab + (int64_t)s * a.P + a.woff[t][l];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int n = n0 + nh * 32 + i * 16 + q * 4 + rr;
+          const int k = kh * 64 + j * 16 + r;
+          dst[(int64_t)n * K + k] = acc[i][j][rr];
+        }
+  T2_STAMP(3);
+}
+
 __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile* __restrict__ tiles, int bid,
                                             char* smem) {
   // workgroups [0, ntiles * S): one (32x32 tile of dW, batch slice) each, its 4 waves on 4
@@ -1388,6 +2003,10 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
   // XCD-aware placement: a contiguous 1/8 of the (slice, tile) list — whole slices, whose tiles
   // re-read the same operand strips — on one XCD and its L2
   const int lb = xcd_remap(bid, (int)nwg_tiles);
+  if (a.lds && a.rm) {
+    wgrad_lds_block_rm(a, lb, smem);
+    return;
+  }
   if (a.lds) {
     wgrad_lds_block(a, lb, smem);
     return;
@@ -1646,6 +2265,7 @@ struct UpdateArgs {
   float out_scale;
   int in_srcs;
   int64_t in_stride;
+  char* wimg;  // nullable: the row-owned T1's weight image (rk_off), written beside the other copies
 #if TT_EXPERIMENTS
   int64_t* stamps;  // EXPERIMENT (TT_RING_STAMPS): [workgroups][4] s_memrealtime per phase
 #endif
@@ -1677,7 +2297,7 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
     // loads and per-lane selects — a per-lane index into the kernarg arrays would be a chain of
     // dependent vector loads from the kernarg segment (several us per launch)
     int64_t soff = 0, swc = 0;
-    int sisw = 0, sk = 1, sn = 1;
+    int sisw = 0, sk = 1, sn = 1, st_ = 0, sl_ = 0;
 #pragma unroll
     for (int q = 0; q < 2 * 2 * MAXL; ++q) {
       if (q < a.nseg && i >= a.seg_off[q]) {
@@ -1686,6 +2306,8 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
         sk = a.seg_k[q];
         sn = a.seg_n[q];
         swc = a.seg_wc[q];
+        st_ = a.seg_t[q];
+        sl_ = a.seg_l[q];
       }
     }
     const int64_t e = i - soff;
@@ -1739,6 +2361,8 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
       }
       a.wbf[swc + frag_off((int)n, (int)k, K)] = (__bf16)p;   // W as [N][K]
       a.wtbf[swc + frag_off((int)k, (int)n, N)] = (__bf16)p;  // W^T as [K][N]
+      if (a.wimg)  // the row-owned T1's image: W [out][in], 256-B swizzled rows, W1 after W0
+        *reinterpret_cast<__bf16*>(a.wimg + st_ * RK_IMG_T + sl_ * (RK_W0 * 256) + rk_off((int)n, (int)k)) = (__bf16)p;
     }
     T3_STAMP(2);
   }
@@ -1910,7 +2534,7 @@ __device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, in
   }
 }
 
-__global__ void __launch_bounds__(256) tower_tail_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
+__global__ void __launch_bounds__(256, 3) tower_tail_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
                                                          InsertArgs ins, DdUpdateArgs d, int n_ins, int n_t2,
                                                          int64_t* stamps) {
   __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
@@ -1951,8 +2575,10 @@ struct TowerLayout {
   int ntiles;
   int lds;  // staged T2 (wgrad_lds_block)
   int32_t t2_code[16];
+  int rows;  // the row-owned T1 (tower_rows_kernel) serves this shape's single-hot gather launches
   // workspace carve (bytes)
-  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_tiles, o_dbg, total;
+  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_wimg, o_tiles, o_dbg,
+      total;
 };
 
 static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) {
@@ -2031,6 +2657,9 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.o_wtb = take((size_t)L.PW * 2);
   L.o_wbf = take((size_t)L.PW * 2);
   L.o_wtbf = take((size_t)L.PW * 2);
+  L.rows = s->L == 2 && s->in_dim[0] == RK_IN && s->in_dim[1] == RK_IN && s->width[0] == RK_W0 &&
+           s->width[1] == RK_W1 && !(s->flags & TT_TOWER_GENERAL_T1);
+  L.o_wimg = take(L.rows ? (size_t)RK_IMG : 0);
   L.o_tiles = take((size_t)nt * sizeof(WgradTile));
   L.o_dbg = take((size_t)(std::max<int64_t>(L.nwg * 2, 1024) * 8 + L.nwg * 16 * 9) * sizeof(int64_t));
   L.total = off;
@@ -2170,6 +2799,19 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
       return fail(TT_EINVAL, "tower_fwd_bwd_kjt: shapes in {64, 128} x [128, 64] only");
     return check_launch("tower_fwd_bwd_kjt");
   }
+  // single-hot rows gathered from the tables (not indexed / multi-hot / pooled input): the row-owned T1
+  bool rows_t1 = L.rows && a.gcol[0] && !a.gpos[0] && !a.ipos && !a.mval;
+#if TT_EXPERIMENTS
+  if (getenv("TT_T1_CLASSIC")) rows_t1 = false;  // EXPERIMENT (A/B): tower_l2_kernel instead
+#endif
+  if (rows_t1) {
+    a.wimg = ws + L.o_wimg;
+    if (a.uw[0])
+      tower_rows_kernel<true><<<g, dim3(256), 0, as_stream(stream)>>>(a);
+    else
+      tower_rows_kernel<false><<<g, dim3(256), 0, as_stream(stream)>>>(a);
+    return check_launch(a.uw[0] ? "tower_rows_gather_update" : "tower_rows_gather");
+  }
   if (a.uw[0]) {  // in-place update of single-lookup rows: compile-time shapes only
     if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)
       tower_l2_kernel<128, 128, 64, false, true><<<g, b512, 0, as_stream(stream)>>>(a);
@@ -2235,6 +2877,7 @@ static int wgrad_args(const tt_tower_shape_t* shape, int64_t B, float* loss, voi
   if (getenv("TT_T2_STAMPS")) a.stamps = reinterpret_cast<int64_t*>(ws + L.o_dbg);
 #endif
   a.lds = L.lds;
+  a.rm = L.rows;
   for (int i = 0; i < 16; ++i) {
     a.t2_code[i] = L.t2_code[i];
   }
@@ -2461,6 +3104,7 @@ static int t3_args(const tt_tower_shape_t* shape, int64_t B, float* params, floa
   a.wtb = reinterpret_cast<__bf16*>(ws + L.o_wtb);
   a.wbf = reinterpret_cast<__bf16*>(ws + L.o_wbf);
   a.wtbf = reinterpret_cast<__bf16*>(ws + L.o_wtbf);
+  a.wimg = L.rows ? ws + L.o_wimg : nullptr;
   // the plain [out][in] / [in][out] bf16 copies are read only by tower_fwd_bwd_kernel, which
   // launch_t1 uses for shapes other than two layers over inputs <= 128 wide
   a.skip_plain = shape->L == 2 && shape->in_dim[0] <= 128 && shape->in_dim[1] <= 128 &&
