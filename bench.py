@@ -321,8 +321,10 @@ def launch_bytes(step, nnz: int, uniq: int, once: int):
     k3_design = (F * B * (4 + 64) + (uniq - once) * (8 * D + 8) + multi * 4 * D + S * P * 4 + 6 * P * 4 + 4 * P)
     t1_alg = nnz * (8 + 4 * D) + F * B * (4 + 4 * D) + once * (8 + 4 * D + 8 * D + 8)
     k3_alg = multi * 8 + (F * B - once) * 4 * D + (uniq - once) * (8 * D + 8)
+    rows_t1 = uses_rows_t1(step)
     out = {"t1": {"alg_bytes": t1_alg, "design_bytes": t1_design, "flop": 8 * B * macs,
-                   "what": "tower_l2_kernel<UPD>: EBC gather + both towers fwd/bwd + row-wise Adagrad of the rows "
+                   "what": ("tower_rows_kernel<UPD> (row-owned waves, whole chain in registers)" if rows_t1 else
+                            "tower_l2_kernel<UPD>") + ": EBC gather + both towers fwd/bwd + row-wise Adagrad of the rows "
                            "looked up once"},
             "t2": {"alg_bytes": 0, "design_bytes": t2_design, "flop": 4 * B * macs,
                    "what": "tower_wgrad_insert_kernel: tower weight gradients + Adam scalars + next batch's dedup insert"},
@@ -368,6 +370,20 @@ def pmc_traffic(kernel_name: str, workload: str = "northstar"):
 
 KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_insert_kernel", "k3": "tower_update_dedup_resolve_kernel",
                 "tail": "tower_tail_kernel", "t3": "tower_update_kernel"}
+
+
+def uses_rows_t1(step) -> bool:
+    """The fused gather T1 of the [128, 64] towers over 128-wide rows is the row-owned kernel
+    (tower.hip launch_t1: tower_rows_kernel)."""
+    return bool(getattr(step, "gather", False)) and step.layer_sizes == [128, 64] and \
+        getattr(step, "in_q", 0) == 128 and getattr(step, "in_c", 0) == 128
+
+
+def kernel_names(step) -> dict:
+    names = dict(KERNEL_NAMES)
+    if uses_rows_t1(step):
+        names["t1"] = "tower_rows_kernel"
+    return names
 
 
 def synth_kjt_batches(num_users, num_items, B, maxlen, n, device, ids, seed):
@@ -530,11 +546,12 @@ def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northsta
     design bytes, flops and MFMA fractions beside it; the whole embedding path (8(d) bytes per step)
     over the step time and over the time of the two launches that carry it."""
     emb_path_bytes = kern.pop("_emb_path_bytes")
+    names = kernel_names(step)
     out = {}
     for name, k in kern.items():
         ms = timed.get(name) if timed else None
         e = dict(k)
-        e["kernel"] = KERNEL_NAMES[name]
+        e["kernel"] = names[name]
         if ms:
             e["ms"] = round(ms, 5)
             e["alg_GB/s"] = round(k["alg_bytes"] / ms / 1e6, 1)
@@ -542,7 +559,7 @@ def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northsta
             if k["flop"]:
                 e["TFLOP/s"] = round(k["flop"] / ms / 1e9, 1)
                 e["frac_of_bf16_peak"] = round(k["flop"] / ms / 1e9 / MFMA_BF16_PEAK_TFS, 4)
-        t, src = pmc_traffic(KERNEL_NAMES[name], workload)
+        t, src = pmc_traffic(names[name], workload)
         e["pmc_hbm_bytes"], e["pmc_source"] = t, src
         out[name] = e
     path = {"bytes_per_step": emb_path_bytes,
@@ -558,7 +575,7 @@ def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northsta
                  "frac_over_t1_k3": round(emb_path_bytes / emb_ms / 1e6 / HBM_PEAK_GBS, 4),
                  "note": "SURVEY 8(d) bytes per step: over the whole step, and over T1 + K3 or the tail launch (the launches that "
                          "carry the embedding work; both also run tower work)"})
-    return {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    return {"bound": "hbm", "kernel": names[dom], "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": out[dom]["pmc_hbm_bytes"],
             "traffic_source": out[dom]["pmc_source"], "alg_bytes_per_launch": out[dom]["alg_bytes"],
             "alg_bytes_rule": "SURVEY 8(d) share of T1: per kept lookup 8 B id + 4D row; per bag 4 B length + 4D "

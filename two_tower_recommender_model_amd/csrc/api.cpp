@@ -55,7 +55,7 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_update_pre_rowwise_adagrad_resolve
 // tt_tower_wgrad_pre_insert_rowwise_adagrad, tt_tower_wgrad_route_count_rowwise_adagrad,
 // tt_tower_grads_replicated_route_place_gather, tt_tower_adam_pre_grads_sum
-// tt_tower_fwd_bwd_kjt
+// tt_tower_fwd_bwd_kjt, tt_tower_fwd_bwd_indexed_multi_bf16, tt_shard_route_count_rowwise_adagrad
 int tt_num_entry_points(void) { return 55; }
 
 }  // extern "C"

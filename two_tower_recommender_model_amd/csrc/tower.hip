@@ -1371,7 +1371,10 @@ __device__ __forceinline__ float rk_label(RkRaw r, int dt) {
 #define RK_STAMP(k) do { } while (0)
 #define RK_STAMP2(k) do { } while (0)
 #endif
-template <bool UPD>
+// IDX: the sharded step's form (tt_tower_fwd_bwd_indexed2_bf16): tower t's input row m is bf16 row
+// gpos[t][m] of gsrc[t] (-1: zeros; the rows an owner returned, dense), its dX goes to fp32 row
+// gpos_out[t][m] of gdst[t]; no in-place update, no insert
+template <bool UPD, bool IDX = false>
 __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) char wimg[RK_IMG];         // both towers' W0, W1 (rk_off)
   __shared__ __attribute__((aligned(16))) float xo[2][2][16 * 64];  // tower outputs per (tower, row half)
@@ -1389,7 +1392,13 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   // them); the weight image -> LDS (LDS-DMA, 1 KB per wave instruction); the row
   const bool wide = a.gid_dtype == TT_I64;
   const int64_t mc = live ? m : 0;  // dead rows of a ragged tile read row 0 of every column
-  const RkRaw id_raw = rk_raw(t ? a.gcol[1] : a.gcol[0], wide, mc);
+  RkRaw id_raw{0u, 0u}, pout_raw{0u, 0u};
+  if (IDX) {
+    id_raw.lo = (uint32_t)(t ? a.gpos[1] : a.gpos[0])[mc];
+    pout_raw.lo = a.gpos_out[0] ? (uint32_t)(t ? a.gpos_out[1] : a.gpos_out[0])[mc] : id_raw.lo;
+  } else {
+    id_raw = rk_raw(t ? a.gcol[1] : a.gcol[0], wide, mc);
+  }
   const RkRaw lab_raw = rk_raw(a.labels, a.label_dtype == TT_I64, mc);
   f32x4 b0v[8], b1v[4];
   {
@@ -1409,8 +1418,13 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   for (int k = 0; k < RK_IMG / 1024 / 4; ++k)
     wreg[k] = *reinterpret_cast<const bf16x8*>(a.wimg + (wid + 4 * k) * 1024 + lane * 16);
   __builtin_amdgcn_sched_barrier(0);
-  const int64_t id = live ? rk_id(id_raw, wide) : 0;
-  const int64_t r = id != 0 ? py_mod64(id, t ? a.gmod[1] : a.gmod[0]) : -1;
+  int64_t r;  // the row's index in its source (table row / returned-rows buffer row), -1: zeros
+  if (IDX) {
+    r = live ? (int64_t)(int32_t)id_raw.lo : -1;
+  } else {
+    const int64_t id = live ? rk_id(id_raw, wide) : 0;
+    r = id != 0 ? py_mod64(id, t ? a.gmod[1] : a.gmod[0]) : -1;
+  }
   const float* tab = t ? a.gtab[1] : a.gtab[0];
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) void glb_void;
@@ -1420,7 +1434,19 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   // so that the B-layout reads below are conflict-free; rows without an id read table row 0
   // (ignored)
   float* xw = xr[wid];
-  {
+  if (IDX) {
+    // bf16 rows (256 B): four per wave instruction, lane l carries 16-B chunk (l & 15) ^ row of
+    // row 4 i + (l >> 4)
+    const int rr0 = lane >> 4, pc = lane & 15;
+    const char* src0 = reinterpret_cast<const char*>(t ? a.gsrc[1] : a.gsrc[0]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 4 * i + rr0;
+      const int64_t rid = __shfl((long long)r, row, 64);
+      const char* src = src0 + (rid >= 0 ? rid : 0) * (RK_IN * 2) + 16 * (pc ^ row);
+      __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(reinterpret_cast<char*>(xw) + i * 1024), 16, 0, 0);
+    }
+  } else {
     const int rr0 = lane >> 5, pc = lane & 31;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1451,11 +1477,23 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   RK_STAMP(3);
   // this lane's row in the B layout: xv[mt] = features 32 (mt >> 1) + 8 q + 4 (mt & 1) .. + 3 (fp32)
   f32x4 xv[8];
+  bf16x8 xb[4];
+  if (IDX) {  // the bf16 B operand straight from the returned rows
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
-    const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);
-    const f32x4 v = *reinterpret_cast<const f32x4*>(xw + n * RK_IN + 4 * (c ^ n));
-    xv[mt] = r >= 0 ? v : (f32x4)(0.f);
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(xw) + n * (RK_IN * 2) +
+                                                         16 * ((4 * s2 + q) ^ n));
+      xb[s2] = r >= 0 ? v : (bf16x8)(__bf16)0.f;
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xw + n * RK_IN + 4 * (c ^ n));
+      xv[mt] = r >= 0 ? v : (f32x4)(0.f);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) xb[s2] = rk_pack(xv[2 * s2], xv[2 * s2 + 1]);
   }
   // UPD, past barrier 1 (nothing waits on these until the row update): is the row looked up once in
   // this step (claim -> slot word in this batch's completed dedup table), its state
@@ -1471,9 +1509,6 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   const char* img0 = wimg + t * RK_IMG_T;
   const char* img1 = img0 + RK_W0 * 256;
   // ---- 1. layer 0: h^T = relu(W0 X^T + b0), 8 M-tiles x 4 k-steps
-  bf16x8 xb[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) xb[s] = rk_pack(xv[2 * s], xv[2 * s + 1]);
   f32x4 acc[8];
   rk_gemm<8, 4, false>(acc, img0, xb, lane);
   RK_STAMP(4);
@@ -1582,8 +1617,16 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   // ---- 7. the row: UPD + looked up once -> row-wise Adagrad in place (the K3 update's arithmetic and
   // summation tree: feature groups of 4 combined at group bits 4, 3 (in lane), 2, 1 (lanes ^ 32,
   // ^ 16), 0 (in lane)); otherwise dX -> the pooled gradient (and the gathered row, pooled_out)
-  float* grow = live ? a.gpooled + m * a.ldp + a.s.in_col[t] : nullptr;
-  bool store_dx = live;
+  float* grow;
+  bool store_dx;
+  if (IDX) {  // dX -> the requester's gradient row in the send buffer (none for a zero row)
+    const int32_t po = (int32_t)pout_raw.lo;
+    store_dx = r >= 0 && po >= 0;
+    grow = (t ? a.gdst[1] : a.gdst[0]) + (int64_t)(store_dx ? po : 0) * RK_IN;
+  } else {
+    grow = live ? a.gpooled + m * a.ldp + a.s.in_col[t] : nullptr;
+    store_dx = live;
+  }
   if (UPD) {
     float e2[2];
 #pragma unroll
@@ -1633,7 +1676,7 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   }
   RK_STAMP2(3);
   if (t == 0 && q == 0 && live) a.logits[m] = d;  // after the row update (see rk_strip)
-  if (a.pooled_out && live) {
+  if (!IDX && a.pooled_out && live) {
     float* prow = a.pooled_out + m * a.ldp + a.s.in_col[t];
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) *reinterpret_cast<f32x4*>(prow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = xv[mt];
@@ -2800,13 +2843,15 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
     return check_launch("tower_fwd_bwd_kjt");
   }
   // single-hot rows gathered from the tables (not indexed / multi-hot / pooled input): the row-owned T1
-  bool rows_t1 = L.rows && a.gcol[0] && !a.gpos[0] && !a.ipos && !a.mval;
+  bool rows_t1 = L.rows && !a.ipos && !a.mval && ((a.gcol[0] && !a.gpos[0]) || (a.gpos[0] && a.gsrc_bf16));
 #if TT_EXPERIMENTS
   if (getenv("TT_T1_CLASSIC")) rows_t1 = false;  // EXPERIMENT (A/B): tower_l2_kernel instead
 #endif
   if (rows_t1) {
     a.wimg = ws + L.o_wimg;
-    if (a.uw[0])
+    if (a.gpos[0])
+      tower_rows_kernel<false, true><<<g, dim3(256), 0, as_stream(stream)>>>(a);
+    else if (a.uw[0])
       tower_rows_kernel<true><<<g, dim3(256), 0, as_stream(stream)>>>(a);
     else
       tower_rows_kernel<false><<<g, dim3(256), 0, as_stream(stream)>>>(a);

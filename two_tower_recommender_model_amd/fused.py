@@ -163,8 +163,10 @@ class FusedTwoTowerStep:
         if self.dedup_single:
             self.tables.ensure_dedup_workspace(F * B)
         self.materialize_pooled = bool(materialize_pooled)
-        # ring: T1 touches the next batch's rows after its own gather (cache / TLB prefetch);
-        # TT_PREFETCH_NEXT=0 turns it off (A/B measurement)
+        # ring: tower_l2_kernel's dedup wave touches the next batch's rows after its own gather (cache
+        # / TLB prefetch); the row-owned T1 (128-wide rows) touches nothing (there the touches'
+        # TLB misses stall the workgroup's later stores, and beside T3 they cost T3 more than they
+        # save T1: DESIGN.md section 3); TT_PREFETCH_NEXT=0 turns it off (A/B measurement)
         self.prefetch_next = os.environ.get("TT_PREFETCH_NEXT", "1") != "0"
         # ring: T2 + complete next-batch insert + update of the rows looked up more than once in one
         # launch, then T3 alone; TT_RING_TAIL=0: T2 + deferred insert, then resolver + update + T3
