@@ -17,7 +17,18 @@ def pytest_configure(config):
 
 def load_golden(name: str) -> dict:
     with np.load(GOLDEN / name, allow_pickle=False) as z:
-        return {k: z[k] for k in z.files}
+        d = {k: z[k] for k in z.files}
+    # sparse_final fixtures (make_golden.py): dense final tables = initial tables with the changed
+    # rows replaced; Adagrad states are zero outside them
+    for k in [k for k in d if k.startswith("final_rows_")]:
+        t = k[len("final_rows_"):]
+        rows = d.pop(k)
+        fin = d[f"init_{t}"].copy()
+        fin[rows] = d.pop(f"final_vals_{t}")
+        st = np.zeros(fin.shape[0], np.float32)
+        st[rows] = d.pop(f"final_state_vals_{t}")
+        d[f"final_{t}"], d[f"final_state_{t}"] = fin, st
+    return d
 
 
 @pytest.fixture(scope="session")

@@ -84,8 +84,14 @@ def kjt_cases():
     print("kjt cases:", list(cases))
 
 
-def train_case(name, num_users, num_items, D, B, layers, steps, seed, zipf=False, lr=0.01):
-    """a4-a9 golden vectors: ``steps`` training steps of the reference TwoTowerTrainTask."""
+def train_case(name, num_users, num_items, D, B, layers, steps, seed, zipf=False, lr=0.01, survey_ids=False,
+               sparse_final=False):
+    """a4-a9 golden vectors: ``steps`` training steps of the reference TwoTowerTrainTask.
+
+    ``survey_ids``: SURVEY.md 8(d) config-1 ids (uniform in [1, N) plus 2 % zeros) instead of ids in
+    [0, 2N) with 5 % zeros. ``sparse_final``: store the final tables / Adagrad states as the rows that
+    differ from the initial ones (``final_rows_*`` / ``final_vals_*`` / ``final_state_vals_*``) to
+    keep full-size fixtures small; tests/conftest.py:load_golden rebuilds the dense arrays."""
     cat_cols = ["user_id", "product_id"]
     ns = load_reference_fragments(cat_cols)
     torch.manual_seed(seed)
@@ -120,9 +126,11 @@ def train_case(name, num_users, num_items, D, B, layers, steps, seed, zipf=False
             if zipf:
                 r = torch.distributions.Pareto(1.0, 0.35).sample((B,)).floor().to(torch.int64)
                 x = (r * 7919) % (emb_counts[ci] * 2)
+            elif survey_ids:
+                x = torch.randint(1, emb_counts[ci], (B,), generator=g, dtype=torch.int64)
             else:
                 x = torch.randint(0, emb_counts[ci] * 2, (B,), generator=g, dtype=torch.int64)
-            x[torch.rand(B, generator=g) < 0.05] = 0
+            x[torch.rand(B, generator=g) < (0.02 if survey_ids else 0.05)] = 0
             cols[c] = x
         cols["label"] = torch.randint(0, 2, (B,), generator=g, dtype=torch.int64)
         batch = ns["transform_to_torchrec_batch"](cols, num_embeddings_per_feature=emb_counts)
@@ -155,8 +163,15 @@ def train_case(name, num_users, num_items, D, B, layers, steps, seed, zipf=False
             f"s{s}_pooled": pooled.detach().numpy(), f"s{s}_pooled_grad": pooled.grad.numpy(),
         })
     for ti, cfg in enumerate(eb_configs):
-        rec[f"final_{cfg.name}"] = ebc.embedding_bags[cfg.name].weight.detach().numpy()
-        rec[f"final_state_{cfg.name}"] = states[ti].numpy()
+        fin = ebc.embedding_bags[cfg.name].weight.detach().numpy()
+        if sparse_final:
+            rows = np.nonzero((fin != rec[f"init_{cfg.name}"]).any(1) | (states[ti].numpy() != 0))[0]
+            rec[f"final_rows_{cfg.name}"] = rows.astype(np.int64)
+            rec[f"final_vals_{cfg.name}"] = fin[rows]
+            rec[f"final_state_vals_{cfg.name}"] = states[ti].numpy()[rows]
+        else:
+            rec[f"final_{cfg.name}"] = fin
+            rec[f"final_state_{cfg.name}"] = states[ti].numpy()
     for n, p in task.named_parameters():
         if "embedding_bags" not in n:
             rec["final_" + n] = p.detach().numpy()
@@ -260,8 +275,16 @@ if __name__ == "__main__":
         eval_case("limit", num_users=300, num_items=400, D=64, B=128, layers=[128, 64], n_batches=6, seed=22,
                   limit_batches=4)
         _sys.exit(0)
+    if len(_sys.argv) > 1 and _sys.argv[1] == "c1full":
+        train_case("c1full", num_users=10000, num_items=10000, D=16, B=256, layers=[128, 64], steps=3, seed=0,
+                   survey_ids=True, sparse_final=True)
+        _sys.exit(0)
     kjt_cases()
     # config-1 shape family (plumbing), shrunk to keep fixtures small
     train_case("c1", num_users=1000, num_items=1200, D=16, B=256, layers=[16, 8], steps=3, seed=0)
     train_case("zipf", num_users=500, num_items=800, D=32, B=128, layers=[32, 16], steps=3, seed=1, zipf=True)
     train_case("d128", num_users=300, num_items=400, D=128, B=64, layers=[128, 64], steps=2, seed=2)
+    # config 1 at its full SURVEY.md 8(d) size: 10k x 10k, D=16, B=256, the reference's default
+    # towers [128, 64] (03:62)
+    train_case("c1full", num_users=10000, num_items=10000, D=16, B=256, layers=[128, 64], steps=3, seed=0,
+               survey_ids=True, sparse_final=True)

@@ -32,7 +32,7 @@ def _layers(g):
     return [int(x) for x in g["layers"]]
 
 
-@pytest.mark.parametrize("case", ["c1", "zipf", "d128"])
+@pytest.mark.parametrize("case", ["c1", "c1full", "zipf", "d128"])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_fused_step_matches_reference_golden(device, case, precision):
     from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
@@ -83,7 +83,7 @@ def test_fused_step_matches_reference_golden(device, case, precision):
         check(st.cb[l].cpu().numpy(), g[f"final_two_tower.candidate_proj._mlp.{l}._linear.bias"], tol["mlp"])
 
 
-@pytest.mark.parametrize("case", ["c1", "d128"])
+@pytest.mark.parametrize("case", ["c1", "c1full", "d128"])
 def test_dropin_torchrec_api_matches_reference_golden(device, case):
     """The reference's main()/train() wiring on the torchrec-compatible API (world size 1)."""
     import two_tower_recommender_model_amd as tt

@@ -37,7 +37,7 @@ def _state_from_golden(g):
     return st, layers
 
 
-@pytest.mark.parametrize("case", ["c1", "zipf", "d128"])
+@pytest.mark.parametrize("case", ["c1", "c1full", "zipf", "d128"])
 @pytest.mark.parametrize("sparse_update", [True, False])
 def test_train_step_matches_reference_task(case, sparse_update):
     g = load_golden(f"train_{case}.npz")
