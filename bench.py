@@ -25,6 +25,8 @@ import platform
 import sys
 import time
 
+import numpy as np
+
 import torch
 import torch.distributed as dist
 
@@ -234,7 +236,7 @@ def cpu_rows(args, num_users, num_items, D):
 def cpu_baseline(args, num_users, num_items, D, B, layers):
     """The oracle (CPU restatement of TorchRec's unsharded CPU path, sparse touched-row update) on
     this host's cores, bounded sample: full B, D, towers, full tables when RAM allows; steps until
-    --cpu-seconds of CPU work (at least 5)."""
+    --cpu-seconds of CPU work (at least --cpu-steps); value = B / median step time."""
     from oracle import ref
 
     threads = cpu_threads()
@@ -250,22 +252,25 @@ def cpu_baseline(args, num_users, num_items, D, B, layers):
         lab = torch.randint(0, 2, (B,), generator=g)
         v, l, o = ref.kjt_build([c.numpy() for c in cols], list(rows))
         batches.append((torch.from_numpy(v), torch.from_numpy(o), lab))
-    for i in range(2):
+    for i in range(10):  # 10 warm-up steps, then the median of the timed ones
         v, o, lab = batches[i % 4]
         ref.train_step(st, v, o, B, lab, 0.01, 0.01)
     t0 = time.perf_counter()
-    n = 0
-    while n < args.cpu_steps or time.perf_counter() - t0 < args.cpu_seconds:
-        v, o, lab = batches[n % 4]
+    times = []
+    while len(times) < args.cpu_steps or time.perf_counter() - t0 < args.cpu_seconds:
+        v, o, lab = batches[len(times) % 4]
+        t = time.perf_counter()
         ref.train_step(st, v, o, B, lab, 0.01, 0.01)
-        n += 1
+        times.append(time.perf_counter() - t)
     dt = time.perf_counter() - t0
+    q10, q50, q90 = np.percentile(times, [10, 50, 90])
     return {
-        "value": round(n * B / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-        "sample": f"{n} steps ({dt:.1f} s) of the oracle train_step (torch CPU fp32: embedding_bag sum, towers "
-                  f"{layers}, BCE, sparse row-wise Adagrad, Adam) at B={B}, D={D}, {how} "
-                  f"({rows[0]}x{D} / {rows[1]}x{D}); {threads} threads of {len(os.sched_getaffinity(0))} in the "
-                  f"affinity mask; host CPU {cpu_model()}",
+        "value": round(float(B / q50), 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+        "sample": f"median of {len(times)} timed steps ({dt:.1f} s, after 10 warm-up) of the oracle train_step "
+                  f"(torch CPU fp32: embedding_bag sum, towers {layers}, BCE, sparse row-wise Adagrad, Adam) at "
+                  f"B={B}, D={D}, {how} ({rows[0]}x{D} / {rows[1]}x{D}); step p10/p50/p90 "
+                  f"{q10 * 1e3:.2f}/{q50 * 1e3:.2f}/{q90 * 1e3:.2f} ms; {threads} threads of "
+                  f"{len(os.sched_getaffinity(0))} in the affinity mask; host CPU {cpu_model()}",
     }
 
 
@@ -526,18 +531,22 @@ def cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen):
     st.tables = cpu_tables(rows, D, threads)
     st.states = [torch.zeros(n) for n in rows]
     bs = synth_kjt_batches(rows[0], rows[1], B, maxlen, 2, torch.device("cpu"), "uniform", seed=0)
-    ref.train_step(st, bs[0][0], bs[0][1], B, bs[0][2], 0.01, 0.01)
+    for i in range(4):
+        ref.train_step(st, bs[i % 2][0], bs[i % 2][1], B, bs[i % 2][2], 0.01, 0.01)
     t0 = time.perf_counter()
-    n = 0
-    while n < args.cpu_steps or time.perf_counter() - t0 < args.cpu_seconds:
-        v, o, lab = bs[n % 2]
+    times = []
+    while len(times) < args.cpu_steps or time.perf_counter() - t0 < args.cpu_seconds:
+        v, o, lab = bs[len(times) % 2]
+        t = time.perf_counter()
         ref.train_step(st, v, o, B, lab, 0.01, 0.01)
-        n += 1
+        times.append(time.perf_counter() - t)
     dt = time.perf_counter() - t0
-    return {"value": round(n * B / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} steps ({dt:.1f} s) of the oracle train_step on multi-hot bags (lengths U{{1..{maxlen}}}) "
-                      f"at B={B}, D={D}, towers {layers}, {how} ({rows[0]}x{D} / {rows[1]}x{D}); {threads} threads; "
-                      f"host CPU {cpu_model()}"}
+    q10, q50, q90 = np.percentile(times, [10, 50, 90])
+    return {"value": round(float(B / q50), 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"median of {len(times)} timed steps ({dt:.1f} s, after 4 warm-up) of the oracle train_step on "
+                      f"multi-hot bags (lengths U{{1..{maxlen}}}) at B={B}, D={D}, towers {layers}, {how} "
+                      f"({rows[0]}x{D} / {rows[1]}x{D}); step p10/p50/p90 {q10 * 1e3:.1f}/{q50 * 1e3:.1f}/"
+                      f"{q90 * 1e3:.1f} ms; {threads} threads; host CPU {cpu_model()}"}
 
 
 def roofline_report(kern, timed, nnz, uniq, step, B, ms_step, workload="northstar", once=None):
