@@ -38,6 +38,9 @@
  *                              <- both MLP towers (03:411-412, :420-436) + TwoTowerTrainTask
  *                                 (03:447-455) + loss.backward() through the towers + the dense
  *                                 Adam step (03:826-829), as three fused kernels
+ *   tt_launch (a launch plan)  <- the same backward work with several roles in one launch: the
+ *                                 weight gradients beside the embedding update / next-batch insert /
+ *                                 shard route and gather ("launch plans" below)
  */
 #ifndef TT_MI355X_H
 #define TT_MI355X_H
@@ -302,10 +305,11 @@ int tt_tower_fwd_bwd_kjt(const tt_tower_shape_t* shape, int64_t B, const void* v
                          const void* labels, int label_dtype, float grad_scale, float* logits,
                          void* workspace, size_t ws_bytes, void* stream);
 /* ---- the pipelined fused step: dedup one step ahead, single-lookup rows updated inside T1 ----------
- * Step i: T1 (gather + towers + in-place row-wise Adagrad of batch i's rows looked up ONCE, from
- * batch i's dedup table completed by step i-1) -> T2 (weight gradients + the insert of batch i+1
- * into the other table) -> K3 (deferred inserts of batch i+1 resolved, batch i's rows looked up more
- * than once updated from dX, T3). The first batch's table is built by tt_dedup_insert_cols. */
+ * Step i (the production ring): T1 (gather + towers + in-place row-wise Adagrad of batch i's rows
+ * looked up ONCE, from batch i's dedup table completed by step i-1) -> the tail (tt_launch roles
+ * WGRAD | INSERT | ADAGRAD: weight gradients + the complete insert of batch i+1 into the other
+ * table + the rows looked up more than once) -> T3 (tt_tower_update_pre). The first batch's table
+ * is built by tt_dedup_insert_cols. */
 /* T1 as tt_tower_fwd_bwd_gather, plus: a kept lookup (t, m) whose slot in dedup_ws (its claim, count
  * 1) says its row is looked up once in the step updates table_rows[t] / table_state[t] in place
  * (lr, eps: torchrec RowWiseAdagrad, 03_model_training.py:791-795); dX goes to gpooled for the
@@ -316,38 +320,6 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
                                    const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
                                    float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
                                    const void* const* next_cols, void* workspace, size_t ws_bytes, void* stream);
-/* tt_tower_wgrad_pre + the insert of the NEXT batch's lookups (i = t * B + m, key dedup_tables[t]
- * << 40 | id mod N) into next_dedup_ws (first CAS here, the rest deferred to the resolver of the
- * following tt_tower_update_pre_rowwise_adagrad_resolve). */
-int tt_tower_wgrad_pre_insert(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
-                              int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2,
-                              const void* const* next_cols, int id_dtype, const int64_t* num_embeddings,
-                              const int32_t* dedup_tables, void* next_dedup_ws, size_t dedup_ws_bytes,
-                              int64_t dedup_max_lookups, void* stream);
-/* tt_tower_update_pre_rowwise_adagrad over dedup_ws updating only the rows looked up MORE than once
- * (the others were updated by T1; their slots are freed), plus the resolver of next_dedup_ws's
- * deferred inserts (both workspaces: dedup_ws_bytes / dedup_max_lookups). */
-int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, int64_t B, float* params,
-                                                float* exp_avg, float* exp_avg_sq, float eps, float beta1,
-                                                float beta2, float weight_decay, float* grads_out, void* workspace,
-                                                size_t ws_bytes, const tt_table_meta_t* tables, int T,
-                                                const tt_feature_meta_t* features, int F, int64_t emb_B,
-                                                const float* grad, int64_t ldg, float* weights, float* state,
-                                                float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
-                                                size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
-/* The step's backward tail in one launch (the production ring; the two launches above are its
- * A/B variant): T2 (tt_tower_wgrad_pre: weight gradients, bias sums, loss, Adam scalars) + the
- * COMPLETE insert of next_cols into next_dedup_ws (no deferred entries, no resolver) + the
- * row-wise Adagrad of dedup_ws's rows looked up more than once, from grad (lr, emb_eps:
- * 03_model_training.py:791-795); T3 follows as tt_tower_update_pre. */
-int tt_tower_wgrad_pre_insert_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
-                                              size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
-                                              float adam_beta1, float adam_beta2, const void* const* next_cols,
-                                              int id_dtype, const int64_t* num_embeddings, const int32_t* dedup_tables,
-                                              const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
-                                              int F, const float* grad, int64_t ldg, float* weights, float* state,
-                                              float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
-                                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 /* T1 for the sharded step (row-wise / table-wise shards, single-hot): tower t's input row m is row
  * pos[t][m] of rows_in[t] ([*][in_dim[t]] fp32: the rows returned by the owners' all-to-all; -1
  * -> zeros, a dropped id), and its gradient row dX is written to row pos[t][m] of grad_rows_out[t]
@@ -367,38 +339,15 @@ int tt_tower_fwd_bwd_indexed_bf16(const tt_tower_shape_t* shape, int64_t B, cons
  * the mean BCE of the preceding T1 into loss[0] (nullable; fixed-order sum of T1's partials). */
 int tt_tower_wgrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
                    void* stream);
-/* T2 and the embedding backward in ONE launch: tt_tower_wgrad + tt_dedup_rowwise_adagrad (same
- * arguments as those two calls; emb_B = the dedup's lookups-per-feature B). One launch boundary after
- * T1 instead of two, no cross-stream join: the tile workgroups (MFMA / L2) and the row-update
- * workgroups (HBM) share the CUs. With adam_step_state (nullable) it also advances the Adam step
- * and precomputes the step's bias-correction scalars for tt_tower_update_pre. */
-int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
-                                   size_t ws_bytes, const tt_table_meta_t* tables, int T,
-                                   const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
-                                   int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
-                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, int64_t* adam_step_state,
-                                   float adam_lr, float adam_beta1, float adam_beta2, void* stream);
 /* T2 alone (tt_tower_wgrad) that also advances the Adam step and precomputes the step's
- * bias-correction scalars for tt_tower_update_pre / tt_tower_update_pre_rowwise_adagrad (the fused
+ * bias-correction scalars for tt_tower_update_pre (or a tt_launch plan's UPDATE role) (the fused
  * single-GPU step: T1 -> this -> T3 + embedding update). With dedup_ws (nullable) the same launch
  * finishes the dedup inserts T1 deferred (as tt_dedup_resolve). Replaces the towers' autograd
  * weight gradients (03_model_training.py:455) and the step-count part of Adam (:826-829). */
 int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
                        int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2, void* dedup_ws,
                        size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
-/* T3 (as tt_tower_update_pre) and the embedding backward + row-wise Adagrad (as
- * tt_dedup_rowwise_adagrad, emb_eps its eps) in ONE launch after tt_tower_wgrad_pre: the update's
- * slot workgroups and T3's parameter workgroups share one round of resident waves. Replaces Adam's
- * parameter update (03_model_training.py:826-829) and the fused TBE backward with RowWiseAdagrad
- * (:791-795). */
-int tt_tower_update_pre_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
-                                        float* exp_avg_sq, float eps, float beta1, float beta2, float weight_decay,
-                                        float* grads_out, void* workspace, size_t ws_bytes,
-                                        const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
-                                        int64_t emb_B, const float* grad, int64_t ldg, float* weights, float* state,
-                                        float lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                        int64_t dedup_max_lookups, void* stream);
-/* T3 after tt_tower_wgrad_rowwise_adagrad / tt_tower_wgrad_pre (adam_step_state != NULL): reduction
+/* T3 after tt_tower_wgrad_pre or a tt_launch WGRAD role (adam_step_state != NULL): reduction
  * + Adam with the precomputed scalars + bf16 copies. */
 int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
@@ -527,97 +476,155 @@ int tt_tower_fwd_bwd_indexed_multi_bf16(const tt_tower_shape_t* shape, int64_t B
  * exchange A: DDP's mean all-reduce becomes a fixed-order sum on the receivers. */
 int tt_tower_grads_replicated(const tt_tower_shape_t* shape, int64_t B, float* params, float* base, int copies,
                               const int64_t* offsets, float scale, void* workspace, size_t ws_bytes, void* stream);
-/* tt_tower_adam_grads_sum with the step scalars a preceding tt_tower_wgrad_pre (or launch U of
- * the pipelined sharded step) wrote into the workspace: no pow() per thread, no arrival ticket. */
+/* T3 with Adam on the gradient sum_{s < nsrc} grads[s * src_stride + i] (ascending s: identical on
+ * every rank) + the bf16 weight copies, with the step scalars a preceding WGRAD role (tt_tower_wgrad_pre,
+ * or launch U of the pipelined sharded step) wrote into the workspace: no pow() per thread. */
 int tt_tower_adam_pre_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
                                 int64_t src_stride, float* exp_avg, float* exp_avg_sq, float eps, float beta1,
                                 float beta2, float weight_decay, void* workspace, size_t ws_bytes, void* stream);
-/* T3 with Adam on the gradient sum_{s < nsrc} grads[s * src_stride + i] (ascending s: identical on
- * every rank) + the bf16 weight copies. */
-int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
-                            int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2,
-                            float eps, float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes,
-                            void* stream);
-
-/* The pipelined sharded step's launch U (after exchange A): T2 with Adam's step scalars
- * (tt_tower_wgrad_pre; adam_step_state advanced) + the count pass
- * of a later batch's route (arguments as tt_shard_route_segs) + the owner's row-wise Adagrad over
- * the received gradient rows (arguments as tt_dedup_rowwise_adagrad: Fsrc pseudo-features, B =
- * emb_B) — one launch, the tower weight gradients beside the embedding update (input_dist /
- * EBC backward + FBGEMM rowwise Adagrad and the dense backward of 03_model_training.py:417-455). */
-int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
-                                               size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
-                                               float adam_beta1, float adam_beta2, int F, const void* const* cols,
-                                               int id_dtype,
-                                               const int64_t* num_embeddings, const int64_t* block_sizes,
-                                               const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
-                                               int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                                               size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
-                                               const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
-                                               const float* emb_grad, int64_t ldg, float* weights, float* state,
-                                               float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                               int64_t dedup_max_lookups, void* stream);
-/* Launch U without T2 (the step graph runs T2 = tt_tower_wgrad_pre on a parallel branch, beside
- * exchange A: the tower weight gradients overlap the gradient all-to-all, as the dense backward
- * overlaps TorchRec's output_dist backward): the owner's row-wise Adagrad over the received gradient
- * rows + the count pass of a later batch's route; arguments as in the launch above. */
-int tt_shard_route_count_rowwise_adagrad(int F, int64_t B, const void* const* cols, int id_dtype,
-                                         const int64_t* num_embeddings, const int64_t* block_sizes,
-                                         const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
-                                         int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                                         size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
-                                         const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
-                                         const float* emb_grad, int64_t ldg, float* weights, float* state,
-                                         float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                         int64_t dedup_max_lookups, void* stream);
-/* Launch G: the tower gradient x scale into `copies` destinations (as tt_tower_grads_replicated) +
- * the place pass of the route counted by launch U + the owner's gather of the next batch's rows
- * (arguments as tt_shard_gather_segs_bf16). */
-int tt_tower_grads_replicated_route_place_gather(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
-                                                 int copies, const int64_t* offsets, float scale, void* workspace,
-                                                 size_t ws_bytes, int F, const void* const* cols, int id_dtype,
-                                                 const int64_t* num_embeddings, const int64_t* block_sizes,
-                                                 const int32_t* owners, int W, const tt_shard_seg_t* segs,
-                                                 int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow,
-                                                 void* route_ws, size_t route_ws_bytes, const float* weights,
-                                                 const tt_table_meta_t* tables, int T, const int64_t* recv,
-                                                 int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
-                                                 int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad,
-                                                 void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
-                                                 void* stream);
-/* T2 (tt_tower_wgrad) with the NEXT batch's route count pass (tt_shard_route_segs' first half: its
- * arguments, route_ws its workspace) as extra workgroups of the same launch. */
-int tt_tower_wgrad_route_count(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
-                               int F, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
-                               const int64_t* block_sizes, const int32_t* owners, int W, const tt_shard_seg_t* segs,
-                               int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                               size_t route_ws_bytes, void* stream);
-/* tt_tower_grads_replicated with the route's place pass (after tt_tower_wgrad_route_count on the same
- * arguments) as extra workgroups: together the two launches do what tt_shard_route_segs does. */
-int tt_tower_grads_replicated_route_place(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
-                                          int copies, const int64_t* offsets, float scale, void* workspace,
-                                          size_t ws_bytes, int F, const void* const* cols, int id_dtype,
-                                          const int64_t* num_embeddings, const int64_t* block_sizes,
-                                          const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
-                                          int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                                          size_t route_ws_bytes, void* stream);
-/* The owner's whole update of the pipelined sharded step in ONE launch: tt_tower_adam_grads_sum
- * (towers) and tt_dedup_rowwise_adagrad (emb_* arguments: the received gradient rows) share one
- * round of resident waves. */
-int tt_tower_adam_grads_sum_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
-                                            int nsrc, int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr,
-                                            float beta1, float beta2, float eps, float weight_decay,
-                                            int64_t* step_state, void* workspace, size_t ws_bytes,
-                                            const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
-                                            int F, int64_t emb_B, const float* emb_grad, int64_t ldg, float* weights,
-                                            float* state, float emb_lr, float emb_eps, void* dedup_ws,
-                                            size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 
 /* T3 with the gradient taken from `grads` (data-parallel towers: the all-reduced gradient) instead
  * of T2's partials: Adam + the bf16 weight copies. */
 int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
                         float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
                         float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- launch plans: the step's multi-role fused launches through ONE entry point ------------------
+ * A fused launch runs several ROLES side by side in one grid (each role a range of workgroups): the
+ * towers' weight gradients beside the embedding update, the next batch's dedup insert or route
+ * beside both, so the work after T1 shares the CUs behind one launch boundary. Instead of an export
+ * per combination the caller names the roles (tt_launch_plan_t.roles) and fills each named role's
+ * arguments; tt_launch checks the set against the fused launches the library implements:
+ *
+ *   roles                          the launch (reference work it replaces)
+ *   WGRAD | INSERT | ADAGRAD       single-GPU ring tail: T2 + the next batch's complete insert + the
+ *                                  rows looked up more than once (ADAGRAD.multi_only = 1); T1 updated
+ *                                  the others (03:455 backward + 03:791-795 RowWiseAdagrad)
+ *   WGRAD | INSERT                 T2 + the next batch's insert, first CAS only (the rest deferred
+ *                                  to the RESOLVE role of the following launch)
+ *   UPDATE | ADAGRAD | RESOLVE     T3 + rows looked up more than once (multi_only = 1) + the
+ *                                  deferred inserts of RESOLVE.dedup_ws (03:826-829, :791-795)
+ *   WGRAD | ADAGRAD                T2 + every row's update (multi_only = 0)
+ *   UPDATE | ADAGRAD               T3 + every row's update (multi_only = 0)
+ *   WGRAD | ROUTE_COUNT | ADAGRAD  sharded launch U: T2 + a later batch's route count pass + the
+ *                                  owner's update of the received gradient rows (multi_only = 0)
+ *   ROUTE_COUNT | ADAGRAD          launch U without T2 (T2 on a parallel graph branch)
+ *   UPDATE | ROUTE_PLACE | GATHER  sharded launch G: the tower gradient x scale into every
+ *                                  destination block (UPDATE.replicated = 1, no Adam) + the route's
+ *                                  place pass + the owner's gather of the next batch's rows (bf16)
+ *
+ * and fails with TT_EINVAL for any other set. A role's fields mean what the single-role entry
+ * point's arguments of the same name mean (tt_tower_wgrad_pre, tt_tower_update_pre /
+ * tt_tower_grads_replicated, tt_dedup_insert_cols, tt_dedup_resolve, tt_dedup_rowwise_adagrad,
+ * tt_shard_route_segs, tt_shard_gather_segs_bf16). The towers' shape / B / workspace are the plan's. */
+#define TT_ROLE_WGRAD 0x01u       /* T2: weight-gradient tiles, bias / loss sums, Adam step scalars */
+#define TT_ROLE_UPDATE 0x02u      /* T3: gradient reduction + Adam + bf16 weight copies */
+#define TT_ROLE_INSERT 0x04u      /* the next batch's dedup insert from its single-hot id columns */
+#define TT_ROLE_RESOLVE 0x08u     /* finish deferred dedup inserts */
+#define TT_ROLE_ADAGRAD 0x10u     /* row-wise Adagrad of the dedup workspace's rows */
+#define TT_ROLE_ROUTE_COUNT 0x20u /* sharded route, count pass (tt_shard_route_segs' first half) */
+#define TT_ROLE_ROUTE_PLACE 0x40u /* sharded route, place pass (its second half) */
+#define TT_ROLE_GATHER 0x80u      /* the owner's gather of the received keys' rows (bf16) */
+
+typedef struct {
+  float* loss;               /* nullable: mean BCE of the preceding T1 */
+  int64_t* adam_step_state;  /* advanced; the step scalars go to the workspace for UPDATE */
+  float adam_lr, adam_beta1, adam_beta2;
+} tt_wgrad_role_t;
+
+typedef struct {
+  float* params;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float eps, beta1, beta2, weight_decay;
+  float* grads_out;        /* nullable: the reduced gradient */
+  int32_t replicated;      /* 1: no Adam; gradient x scale to base + offsets[q], q < copies <= 16 */
+  int32_t copies;
+  float* base;
+  const int64_t* offsets;  /* host array, floats */
+  float scale;
+} tt_update_role_t;
+
+typedef struct {
+  const void* const* next_cols;  /* host array of 2 device id columns (towers 0, 1) */
+  int32_t id_dtype;
+  const int64_t* num_embeddings; /* host [2] */
+  const int32_t* dedup_tables;   /* host [2]: key table index of each tower */
+  void* next_dedup_ws;
+  size_t dedup_ws_bytes;
+  int64_t dedup_max_lookups;
+} tt_insert_role_t;
+
+typedef struct {
+  void* dedup_ws;  /* bytes / max lookups: the ADAGRAD role's */
+} tt_resolve_role_t;
+
+typedef struct {
+  const tt_table_meta_t* tables;
+  int32_t T;
+  int32_t F;
+  const tt_feature_meta_t* features;
+  int64_t B;               /* lookups per feature */
+  const float* grad;
+  int64_t ldg;
+  float* weights;
+  float* state;
+  float lr, eps;
+  void* dedup_ws;
+  size_t dedup_ws_bytes;
+  int64_t dedup_max_lookups;
+  int32_t multi_only;      /* 1: only rows looked up more than once (T1 updated the others) */
+} tt_adagrad_role_t;
+
+typedef struct {
+  int32_t F;
+  int32_t id_dtype;
+  const void* const* cols;
+  const int64_t* num_embeddings;
+  const int64_t* block_sizes;
+  const int32_t* owners;
+  int32_t W;
+  const tt_shard_seg_t* segs;
+  int64_t* send;
+  int32_t* pos_in;
+  int32_t* pos_out;
+  int32_t* overflow;
+  void* route_ws;
+  size_t route_ws_bytes;
+} tt_route_role_t;
+
+typedef struct {
+  const float* weights;
+  const tt_table_meta_t* tables;
+  int32_t T;
+  const int64_t* recv;
+  int64_t block_i64, counts_i64;
+  const int64_t* seg_off;
+  int64_t slots;
+  void* rows_out;
+  int64_t out_stride;
+  int32_t* bad;
+  void* dedup_ws;
+  size_t dedup_ws_bytes;
+  int64_t dedup_max_lookups;
+} tt_gather_role_t;
+
+typedef struct {
+  uint32_t roles;                 /* TT_ROLE_* bits */
+  const tt_tower_shape_t* shape;  /* the towers (WGRAD, UPDATE; the batch size B for the others) */
+  int64_t B;
+  void* workspace;
+  size_t ws_bytes;
+  tt_wgrad_role_t wgrad;
+  tt_update_role_t update;
+  tt_insert_role_t insert;
+  tt_resolve_role_t resolve;
+  tt_adagrad_role_t adagrad;
+  tt_route_role_t route;          /* ROUTE_COUNT / ROUTE_PLACE */
+  tt_gather_role_t gather;        /* F and W: the route's */
+} tt_launch_plan_t;
+
+int tt_launch(const tt_launch_plan_t* plan, void* stream);
 
 /* ---- a9: Adam on the flat dense-parameter buffer (torch.optim.Adam, amsgrad=False) ------------ */
 

@@ -34,9 +34,58 @@ def test_every_declared_symbol_exported(lib):
     assert declared, "header parse failed"
     missing = [d for d in declared if d not in exported]
     assert not missing, missing
+    extra = sorted(exported - set(declared))
+    assert not extra, f"exported but not declared in the header: {extra}"
     assert sorted(_lib.SIGNATURES) == declared
     assert lib.tt_num_entry_points() == len(_lib.COMPUTE_ENTRY_POINTS)
     assert lib.tt_abi_version() == 1
+
+
+def test_launch_plan_layout_matches_the_header(tmp_path):
+    """The ctypes mirror of tt_launch_plan_t (and its role structs) has the C compiler's layout:
+    sizes and field offsets from a C program built against include/tt_mi355x.h."""
+    import ctypes as C
+
+    from two_tower_recommender_model_amd import _lib
+
+    structs = {"tt_launch_plan_t": _lib.LaunchPlan, "tt_wgrad_role_t": _lib.WgradRole,
+               "tt_update_role_t": _lib.UpdateRole, "tt_insert_role_t": _lib.InsertRole,
+               "tt_resolve_role_t": _lib.ResolveRole, "tt_adagrad_role_t": _lib.AdagradRole,
+               "tt_route_role_t": _lib.RouteRole, "tt_gather_role_t": _lib.GatherRole}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "tt_mi355x.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'  printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        cname, fname, v = line.split()
+        got[(cname, fname)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == C.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
+
+
+def test_launch_rejects_unknown_role_sets(lib):
+    """tt_launch runs only the fused launches the library implements; another role set, or a role
+    flag that contradicts the launch, is a status code, not a launch."""
+    import ctypes as C
+
+    from two_tower_recommender_model_amd import _lib
+
+    plan = _lib.LaunchPlan(roles=_lib.ROLE_GATHER | _lib.ROLE_WGRAD)
+    assert lib.tt_launch(C.byref(plan), None) == 1001
+    assert b"set of roles" in lib.tt_last_error_string()
+    plan = _lib.LaunchPlan(roles=_lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD)  # ring tail: multi_only
+    assert lib.tt_launch(C.byref(plan), None) == 1001
+    assert b"multi_only" in lib.tt_last_error_string()
+    assert lib.tt_launch(None, None) == 1001
 
 
 def test_errors_are_status_codes(lib):

@@ -56,6 +56,69 @@ class TowerShape(C.Structure):
     ]
 
 
+# ---- launch plans (tt_launch): the multi-role fused launches -------------------------------------
+ROLE_WGRAD, ROLE_UPDATE, ROLE_INSERT, ROLE_RESOLVE = 0x01, 0x02, 0x04, 0x08
+ROLE_ADAGRAD, ROLE_ROUTE_COUNT, ROLE_ROUTE_PLACE, ROLE_GATHER = 0x10, 0x20, 0x40, 0x80
+
+
+class WgradRole(C.Structure):
+    _fields_ = [("loss", C.c_void_p), ("adam_step_state", C.c_void_p), ("adam_lr", C.c_float),
+                ("adam_beta1", C.c_float), ("adam_beta2", C.c_float)]
+
+
+class UpdateRole(C.Structure):
+    _fields_ = [("params", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p), ("eps", C.c_float),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("weight_decay", C.c_float), ("grads_out", C.c_void_p),
+                ("replicated", C.c_int32), ("copies", C.c_int32), ("base", C.c_void_p),
+                ("offsets", C.POINTER(C.c_int64)), ("scale", C.c_float)]
+
+
+class InsertRole(C.Structure):
+    _fields_ = [("next_cols", C.POINTER(C.c_void_p)), ("id_dtype", C.c_int32),
+                ("num_embeddings", C.POINTER(C.c_int64)), ("dedup_tables", C.POINTER(C.c_int32)),
+                ("next_dedup_ws", C.c_void_p), ("dedup_ws_bytes", C.c_size_t), ("dedup_max_lookups", C.c_int64)]
+
+
+class ResolveRole(C.Structure):
+    _fields_ = [("dedup_ws", C.c_void_p)]
+
+
+class AdagradRole(C.Structure):
+    _fields_ = [("tables", C.POINTER(TableMeta)), ("T", C.c_int32), ("F", C.c_int32),
+                ("features", C.POINTER(FeatureMeta)), ("B", C.c_int64), ("grad", C.c_void_p), ("ldg", C.c_int64),
+                ("weights", C.c_void_p), ("state", C.c_void_p), ("lr", C.c_float), ("eps", C.c_float),
+                ("dedup_ws", C.c_void_p), ("dedup_ws_bytes", C.c_size_t), ("dedup_max_lookups", C.c_int64),
+                ("multi_only", C.c_int32)]
+
+
+class RouteRole(C.Structure):
+    _fields_ = [("F", C.c_int32), ("id_dtype", C.c_int32), ("cols", C.POINTER(C.c_void_p)),
+                ("num_embeddings", C.POINTER(C.c_int64)), ("block_sizes", C.POINTER(C.c_int64)),
+                ("owners", C.POINTER(C.c_int32)), ("W", C.c_int32), ("segs", C.c_void_p), ("send", C.c_void_p),
+                ("pos_in", C.c_void_p), ("pos_out", C.c_void_p), ("overflow", C.c_void_p), ("route_ws", C.c_void_p),
+                ("route_ws_bytes", C.c_size_t)]
+
+
+class GatherRole(C.Structure):
+    _fields_ = [("weights", C.c_void_p), ("tables", C.POINTER(TableMeta)), ("T", C.c_int32), ("recv", C.c_void_p),
+                ("block_i64", C.c_int64), ("counts_i64", C.c_int64), ("seg_off", C.POINTER(C.c_int64)),
+                ("slots", C.c_int64), ("rows_out", C.c_void_p), ("out_stride", C.c_int64), ("bad", C.c_void_p),
+                ("dedup_ws", C.c_void_p), ("dedup_ws_bytes", C.c_size_t), ("dedup_max_lookups", C.c_int64)]
+
+
+class LaunchPlan(C.Structure):
+    _fields_ = [("roles", C.c_uint32), ("shape", C.POINTER(TowerShape)), ("B", C.c_int64),
+                ("workspace", C.c_void_p), ("ws_bytes", C.c_size_t), ("wgrad", WgradRole), ("update", UpdateRole),
+                ("insert", InsertRole), ("resolve", ResolveRole), ("adagrad", AdagradRole), ("route", RouteRole),
+                ("gather", GatherRole)]
+
+
+def launch(plan: LaunchPlan, stream: int, what: str = "launch") -> None:
+    """tt_launch(plan) on ``stream``; raises on a non-zero status. Keep every array the plan points
+    to alive until the call returns (the launch copies what it needs into kernel arguments)."""
+    check(load().tt_launch(C.byref(plan), stream), what)
+
+
 _vp = C.c_void_p
 _i32 = C.c_int32
 _i64 = C.c_int64
@@ -147,19 +210,9 @@ SIGNATURES = {
         _int,
         [_psh, _i64, _vp, _int, _vp, _pi64, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
     ),
-    "tt_tower_wgrad_rowwise_adagrad": (
-        _int,
-        [_psh, _i64, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64,
-         _vp, _f32, _f32, _f32, _vp],
-    ),
     "tt_tower_update_pre": (_int, [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp]),
     "tt_tower_wgrad_pre": (_int, [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _vp, _sz, _i64, _vp]),
     "tt_dedup_resolve": (_int, [_vp, _sz, _i64, _vp]),
-    "tt_tower_update_pre_rowwise_adagrad": (
-        _int,
-        [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64,
-         _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
-    ),
     "tt_shard_route_workspace_bytes": (_sz, [_int, _i64]),
     "tt_shard_route_cols": (
         _int,
@@ -196,66 +249,19 @@ SIGNATURES = {
         [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
     ),
     "tt_tower_grads_replicated": (_int, [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _vp]),
-    "tt_tower_adam_grads_sum_rowwise_adagrad": (
-        _int,
-        [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm,
-         _int, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
-    ),
-    "tt_tower_wgrad_route_count": (
-        _int,
-        [_psh, _i64, _vp, _vp, _sz, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
-         _vp],
-    ),
-    "tt_tower_grads_replicated_route_place": (
-        _int,
-        [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp,
-         _vp, _vp, _vp, _vp, _sz, _vp],
-    ),
     "tt_tower_fwd_bwd_gather_update": (
         _int,
         [_psh, _i64, _pvp, _int, _pi64, _pvp, _pvp, _vp, _i64, _vp, _vp, _vp, _int, _f32, _vp, _f32, _f32, _vp, _sz,
          _i64, _pvp, _vp, _sz, _vp],
     ),
-    "tt_tower_wgrad_pre_insert": (
-        _int,
-        [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _pvp, _int, _pi64, _pi32, _vp, _sz, _i64, _vp],
-    ),
-    "tt_tower_update_pre_rowwise_adagrad_resolve": (
-        _int,
-        [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64,
-         _vp, _vp, _f32, _f32, _vp, _vp, _sz, _i64, _vp],
-    ),
-    "tt_tower_wgrad_pre_insert_rowwise_adagrad": (
-        _int,
-        [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _pvp, _int, _pi64, _pi32, _ptm, _int, _pfm, _int, _vp, _i64,
-         _vp, _vp, _f32, _f32, _vp, _vp, _sz, _i64, _vp],
-    ),
     "tt_tower_adam_pre_grads_sum": (
         _int, [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _sz, _vp],
-    ),
-    "tt_tower_wgrad_route_count_rowwise_adagrad": (
-        _int,
-        [_psh, _i64, _vp, _vp, _sz, _vp, _f32, _f32, _f32, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp,
-         _vp, _f32, _f32, _vp, _sz, _i64, _vp],
-    ),
-    "tt_tower_grads_replicated_route_place_gather": (
-        _int,
-        [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _int, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _ptm, _int, _vp, _i64,
-         _i64, _pi64, _i64, _vp, _i64, _vp, _vp, _sz, _i64, _vp],
-    ),
-    "tt_tower_adam_grads_sum": (
-        _int,
-        [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp],
-    ),
-    "tt_shard_route_count_rowwise_adagrad": (
-        _int,
-        [_int, _i64, _pvp, _int, _pi64, _pi64, _pi32, _int, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _ptm, _int, _pfm, _int,
-         _i64, _vp, _i64, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _vp],
     ),
     "tt_tower_fwd_bwd_indexed_multi_bf16": (
         _int,
         [_psh, _i64, _int, _vp, _vp, _vp, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
     ),
+    "tt_launch": (_int, [C.c_void_p, _vp]),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -287,10 +293,8 @@ COMPUTE_ENTRY_POINTS = [
     "tt_dedup_insert_segments",
     "tt_dedup_rowwise_adagrad",
     "tt_tower_fwd_bwd_indexed",
-    "tt_tower_wgrad_rowwise_adagrad",
     "tt_tower_wgrad_pre",
     "tt_dedup_resolve",
-    "tt_tower_update_pre_rowwise_adagrad",
     "tt_shard_route_cols",
     "tt_shard_gather_rows",
     "tt_shard_gather_rows_bf16",
@@ -301,19 +305,10 @@ COMPUTE_ENTRY_POINTS = [
     "tt_shard_gather_segs_bf16",
     "tt_tower_fwd_bwd_indexed2_bf16",
     "tt_tower_grads_replicated",
-    "tt_tower_adam_grads_sum",
-    "tt_tower_adam_grads_sum_rowwise_adagrad",
-    "tt_tower_wgrad_route_count",
-    "tt_tower_grads_replicated_route_place",
     "tt_tower_fwd_bwd_gather_update",
-    "tt_tower_wgrad_pre_insert",
-    "tt_tower_update_pre_rowwise_adagrad_resolve",
-    "tt_tower_wgrad_pre_insert_rowwise_adagrad",
-    "tt_tower_wgrad_route_count_rowwise_adagrad",
-    "tt_tower_grads_replicated_route_place_gather",
     "tt_tower_adam_pre_grads_sum",
     "tt_tower_fwd_bwd_indexed_multi_bf16",
-    "tt_shard_route_count_rowwise_adagrad",
+    "tt_launch",
 ]
 
 _lib = None

@@ -47,15 +47,13 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_update
 // tt_pooled_fwd_cols, tt_bwd_prepare_cols
 // tt_dedup_workspace_init, tt_dedup_insert_cols, tt_dedup_insert_segments, tt_dedup_rowwise_adagrad
-// tt_tower_fwd_bwd_indexed, tt_tower_wgrad_rowwise_adagrad, tt_shard_route_cols, tt_shard_gather_rows,
-// tt_tower_adam_grads, tt_tower_update_pre
+// tt_tower_fwd_bwd_indexed, tt_shard_route_cols, tt_shard_gather_rows, tt_shard_gather_rows_bf16,
+// tt_tower_fwd_bwd_indexed_bf16, tt_tower_adam_grads, tt_tower_update_pre, tt_tower_wgrad_pre,
+// tt_dedup_resolve
 // tt_shard_route_segs, tt_shard_gather_segs_bf16, tt_tower_fwd_bwd_indexed2_bf16, tt_tower_grads_replicated,
-// tt_tower_adam_grads_sum, tt_tower_adam_grads_sum_rowwise_adagrad, tt_tower_wgrad_route_count,
-// tt_tower_grads_replicated_route_place, tt_tower_fwd_bwd_gather_update, tt_tower_wgrad_pre_insert,
-// tt_tower_update_pre_rowwise_adagrad_resolve
-// tt_tower_wgrad_pre_insert_rowwise_adagrad, tt_tower_wgrad_route_count_rowwise_adagrad,
-// tt_tower_grads_replicated_route_place_gather, tt_tower_adam_pre_grads_sum
-// tt_tower_fwd_bwd_kjt, tt_tower_fwd_bwd_indexed_multi_bf16, tt_shard_route_count_rowwise_adagrad
-int tt_num_entry_points(void) { return 55; }
+// tt_tower_fwd_bwd_gather_update, tt_tower_adam_pre_grads_sum
+// tt_tower_fwd_bwd_kjt, tt_tower_fwd_bwd_gather, tt_tower_fwd_bwd_indexed_multi_bf16
+// tt_launch (every multi-role fused launch, by plan)
+int tt_num_entry_points(void) { return 44; }
 
 }  // extern "C"

@@ -2226,20 +2226,6 @@ __global__ void __launch_bounds__(256) tower_wgrad_insert_kernel(WgradArgs a, co
   RING_STAMP(stamps, 1);
 }
 
-// Pipelined sharded step: the NEXT batch's route rides in the towers' launches as extra
-// workgroups (it depends only on that batch's ids): its count pass beside T2's tiles, its place
-// pass beside T3's parameter workgroups (tower_update_route_kernel below) — two launches fewer.
-__global__ void __launch_bounds__(256) tower_wgrad_route_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
-                                                                RouteArgs r, int n_t2) {
-  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
-  if ((int)blockIdx.x < n_t2) {
-    wgrad_block(a, tiles, (int)blockIdx.x, smem);
-  } else {
-    const int j = (int)blockIdx.x - n_t2;
-    route_count_block(r, j % r.nblk, j / r.nblk, reinterpret_cast<int (*)[RT_MAXW]>(smem));
-  }
-}
-
 // Pipelined sharded step, launch U (after exchange A brought the gradient rows of batch i and the
 // ids of batch i+1): T2 of batch i (weight-gradient tiles, bias sums, loss) beside the owner's
 // row-wise Adagrad of batch i's rows and the count pass of batch i+2's route — all three read only
@@ -2424,17 +2410,6 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
 }
 
 __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) { update_block(a, (int)blockIdx.x, (int)gridDim.x); }
-
-__global__ void __launch_bounds__(256) tower_update_route_kernel(UpdateArgs a, RouteArgs r, int n_upd) {
-  __shared__ int base[RT_MAXW];
-  __shared__ int wc[RT_BLOCK / 64][RT_MAXW];
-  if ((int)blockIdx.x < n_upd) {
-    update_block(a, (int)blockIdx.x, n_upd);
-  } else {
-    const int j = (int)blockIdx.x - n_upd;
-    route_place_block<true>(r, j % r.nblk, j / r.nblk, base, wc);
-  }
-}
 
 // Pipelined sharded step, launch G (after launch U updated this rank's rows): the owner's gather of
 // batch i+1's rows (bf16, into exchange B's row blocks, filing batch i+1's dedup table), the tower
@@ -3076,12 +3051,12 @@ int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, vo
   return check_launch("tower_wgrad_pre");
 }
 
-int tt_tower_wgrad_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
-                                   size_t ws_bytes, const tt_table_meta_t* tables, int T,
-                                   const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
-                                   int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
-                                   size_t dedup_ws_bytes, int64_t dedup_max_lookups, int64_t* adam_step_state,
-                                   float adam_lr, float adam_beta1, float adam_beta2, void* stream) {
+static int fused_wgrad_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                               size_t ws_bytes, const tt_table_meta_t* tables, int T,
+                               const tt_feature_meta_t* features, int F, int64_t emb_B, const float* grad,
+                               int64_t ldg, float* weights, float* state, float lr, float eps, void* dedup_ws,
+                               size_t dedup_ws_bytes, int64_t dedup_max_lookups, int64_t* adam_step_state,
+                               float adam_lr, float adam_beta1, float adam_beta2, void* stream) {
   WgradArgs a{};
   int64_t wgs = 0;
   int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
@@ -3217,13 +3192,13 @@ int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params,
                    nullptr, workspace, ws_bytes, stream, pre);
 }
 
-int tt_tower_update_pre_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
-                                        float* exp_avg_sq, float eps, float beta1, float beta2, float weight_decay,
-                                        float* grads_out, void* workspace, size_t ws_bytes,
-                                        const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
-                                        int64_t emb_B, const float* grad, int64_t ldg, float* weights, float* state,
-                                        float lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                        int64_t dedup_max_lookups, void* stream) {
+static int fused_update_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
+                                float* exp_avg_sq, float eps, float beta1, float beta2, float weight_decay,
+                                float* grads_out, void* workspace, size_t ws_bytes,
+                                const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
+                                int64_t emb_B, const float* grad, int64_t ldg, float* weights, float* state,
+                                float lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                int64_t dedup_max_lookups, void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
@@ -3262,18 +3237,6 @@ int tt_tower_grads_replicated(const tt_tower_shape_t* shape, int64_t B, float* p
                    workspace, ws_bytes, stream, nullptr, nullptr, 0, copies == 1 ? 2 : copies, off, scale);
 }
 
-int tt_tower_adam_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
-                            int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2,
-                            float eps, float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes,
-                            void* stream) {
-  TowerLayout L;
-  int rc = tower_layout(shape, B, &L);
-  if (rc) return rc;
-  if (!grads || nsrc < 1 || (nsrc > 1 && src_stride < L.P)) return fail(TT_EINVAL, "tower_adam_grads_sum: bad gradient");
-  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, 1,
-                   nullptr, grads, workspace, ws_bytes, stream, nullptr, nullptr, 0, 1, 0, 1.f, nsrc, src_stride);
-}
-
 int tt_tower_adam_pre_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
                                 int64_t src_stride, float* exp_avg, float* exp_avg_sq, float eps, float beta1,
                                 float beta2, float weight_decay, void* workspace, size_t ws_bytes, void* stream) {
@@ -3285,28 +3248,6 @@ int tt_tower_adam_pre_grads_sum(const tt_tower_shape_t* shape, int64_t B, float*
   const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
   return launch_t3(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, nullptr,
                    grads, workspace, ws_bytes, stream, pre, nullptr, 0, 1, nullptr, 1.f, nsrc, src_stride);
-}
-
-int tt_tower_adam_grads_sum_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads,
-                                            int nsrc, int64_t src_stride, float* exp_avg, float* exp_avg_sq, float lr,
-                                            float beta1, float beta2, float eps, float weight_decay,
-                                            int64_t* step_state, void* workspace, size_t ws_bytes,
-                                            const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
-                                            int F, int64_t emb_B, const float* emb_grad, int64_t ldg, float* weights,
-                                            float* state, float emb_lr, float emb_eps, void* dedup_ws,
-                                            size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
-  TowerLayout L;
-  int rc = tower_layout(shape, B, &L);
-  if (rc) return rc;
-  if (!grads || !step_state || nsrc < 1 || (nsrc > 1 && src_stride < L.P))
-    return fail(TT_EINVAL, "tower_adam_grads_sum_rowwise_adagrad: bad gradient");
-  DdUpdateArgs d{};
-  int64_t dd_grid = 0;
-  rc = dedup_update_args(tables, T, features, F, emb_B, emb_grad, ldg, weights, state, emb_lr, emb_eps, dedup_ws,
-                         dedup_ws_bytes, dedup_max_lookups, d, &dd_grid);
-  if (rc) return rc;
-  return launch_t3(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, 1, nullptr,
-                   grads, workspace, ws_bytes, stream, nullptr, &d, dd_grid, 1, nullptr, 1.f, nsrc, src_stride);
 }
 
 }  // extern "C"
@@ -3356,62 +3297,18 @@ static int route_segs_args(int F, int64_t B, const void* const* cols, int id_dty
 
 extern "C" {
 
-int tt_tower_wgrad_route_count(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
-                               int F, const void* const* cols, int id_dtype, const int64_t* num_embeddings,
-                               const int64_t* block_sizes, const int32_t* owners, int W, const tt_shard_seg_t* segs,
-                               int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                               size_t route_ws_bytes, void* stream) {
-  WgradArgs a{};
-  int64_t wgs = 0;
-  int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
-  if (rc) return rc;
-  RouteArgs r{};
-  rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
-                       overflow, route_ws, route_ws_bytes, r);
-  if (rc) return rc;
-  tower_wgrad_route_kernel<<<dim3((unsigned)(wgs + (int64_t)r.nblk * F)), dim3(256), 0, as_stream(stream)>>>(
-      a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), r, (int)wgs);
-  return check_launch("tower_wgrad_route_count");
-}
-
-int tt_tower_grads_replicated_route_place(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
-                                          int copies, const int64_t* offsets, float scale, void* workspace,
-                                          size_t ws_bytes, int F, const void* const* cols, int id_dtype,
-                                          const int64_t* num_embeddings, const int64_t* block_sizes,
-                                          const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
-                                          int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                                          size_t route_ws_bytes, void* stream) {
-  if (!params || !base || !offsets || copies < 1 || copies > 16) return fail(TT_EINVAL, "tower_grads_replicated: bad output");
-  RouteArgs r{};
-  int rc;
-  rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
-                       overflow, route_ws, route_ws_bytes, r);
-  if (rc) return rc;
-  int64_t off[16];
-  for (int q = 0; q < copies; ++q) off[q] = offsets[q];
-  if (copies == 1) off[1] = off[0];  // one copy takes the multi-copy path too (scale applied)
-  UpdateArgs a;
-  int64_t g3 = 0;
-  rc = t3_args(shape, B, params, nullptr, nullptr, 0.f, 0.9f, 0.999f, 1e-8f, 0.f, nullptr, 0, base, nullptr, workspace,
-               ws_bytes, nullptr, copies == 1 ? 2 : copies, off, scale, 1, 0, a, &g3);
-  if (rc) return rc;
-  tower_update_route_kernel<<<dim3((unsigned)(g3 + (int64_t)r.nblk * F)), dim3(256), 0, as_stream(stream)>>>(
-      a, r, (int)g3);
-  return check_launch("tower_grads_replicated_route_place");
-}
-
-int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
-                                               size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
-                                               float adam_beta1, float adam_beta2, int F, const void* const* cols,
-                                               int id_dtype,
-                                               const int64_t* num_embeddings, const int64_t* block_sizes,
-                                               const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
-                                               int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                                               size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
-                                               const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
-                                               const float* emb_grad, int64_t ldg, float* weights, float* state,
-                                               float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                               int64_t dedup_max_lookups, void* stream) {
+static int fused_wgrad_route_count_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                           size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
+                                           float adam_beta1, float adam_beta2, int F, const void* const* cols,
+                                           int id_dtype,
+                                           const int64_t* num_embeddings, const int64_t* block_sizes,
+                                           const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                           int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                           size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
+                                           const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
+                                           const float* emb_grad, int64_t ldg, float* weights, float* state,
+                                           float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                           int64_t dedup_max_lookups, void* stream) {
   if (!adam_step_state) return fail(TT_EINVAL, "tower_wgrad_route_rowwise: null Adam step state");
   WgradArgs a{};
   int64_t wgs = 0;
@@ -3446,15 +3343,15 @@ int tt_tower_wgrad_route_count_rowwise_adagrad(const tt_tower_shape_t* shape, in
   return check_launch("tower_wgrad_route_count_rowwise_adagrad");
 }
 
-int tt_shard_route_count_rowwise_adagrad(int F, int64_t B, const void* const* cols, int id_dtype,
-                                         const int64_t* num_embeddings, const int64_t* block_sizes,
-                                         const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
-                                         int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
-                                         size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
-                                         const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
-                                         const float* emb_grad, int64_t ldg, float* weights, float* state,
-                                         float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                         int64_t dedup_max_lookups, void* stream) {
+static int fused_route_count_adagrad(int F, int64_t B, const void* const* cols, int id_dtype,
+                                     const int64_t* num_embeddings, const int64_t* block_sizes,
+                                     const int32_t* owners, int W, const tt_shard_seg_t* segs, int64_t* send,
+                                     int32_t* pos_in, int32_t* pos_out, int32_t* overflow, void* route_ws,
+                                     size_t route_ws_bytes, const tt_table_meta_t* tables, int T,
+                                     const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
+                                     const float* emb_grad, int64_t ldg, float* weights, float* state,
+                                     float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
+                                     int64_t dedup_max_lookups, void* stream) {
   // launch U of the pipelined sharded step without its T2 tiles (those run on a parallel branch of
   // the step graph, beside exchange A): the owner's update workgroups first, then the route count
   RouteArgs r{};
@@ -3474,18 +3371,18 @@ int tt_shard_route_count_rowwise_adagrad(int F, int64_t B, const void* const* co
   return check_launch("shard_route_count_rowwise_adagrad");
 }
 
-int tt_tower_grads_replicated_route_place_gather(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
-                                                 int copies, const int64_t* offsets, float scale, void* workspace,
-                                                 size_t ws_bytes, int F, const void* const* cols, int id_dtype,
-                                                 const int64_t* num_embeddings, const int64_t* block_sizes,
-                                                 const int32_t* owners, int W, const tt_shard_seg_t* segs,
-                                                 int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow,
-                                                 void* route_ws, size_t route_ws_bytes, const float* weights,
-                                                 const tt_table_meta_t* tables, int T, const int64_t* recv,
-                                                 int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
-                                                 int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad,
-                                                 void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
-                                                 void* stream) {
+static int fused_grads_route_place_gather(const tt_tower_shape_t* shape, int64_t B, float* params, float* base,
+                                          int copies, const int64_t* offsets, float scale, void* workspace,
+                                          size_t ws_bytes, int F, const void* const* cols, int id_dtype,
+                                          const int64_t* num_embeddings, const int64_t* block_sizes,
+                                          const int32_t* owners, int W, const tt_shard_seg_t* segs,
+                                          int64_t* send, int32_t* pos_in, int32_t* pos_out, int32_t* overflow,
+                                          void* route_ws, size_t route_ws_bytes, const float* weights,
+                                          const tt_table_meta_t* tables, int T, const int64_t* recv,
+                                          int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
+                                          int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad,
+                                          void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
+                                          void* stream) {
   if (!params || !base || !offsets || copies < 1 || copies > 16) return fail(TT_EINVAL, "tower_grads_replicated: bad output");
   RouteArgs r{};
   int rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
@@ -3546,7 +3443,7 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
                    ws_bytes, stream);
 }
 
-int tt_tower_wgrad_pre_insert(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
+static int fused_wgrad_insert(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
                               int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2,
                               const void* const* next_cols, int id_dtype, const int64_t* num_embeddings,
                               const int32_t* dedup_tables, void* next_dedup_ws, size_t dedup_ws_bytes,
@@ -3579,14 +3476,14 @@ int tt_tower_wgrad_pre_insert(const tt_tower_shape_t* shape, int64_t B, float* l
   return check_launch("tower_wgrad_pre_insert");
 }
 
-int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, int64_t B, float* params,
-                                                float* exp_avg, float* exp_avg_sq, float eps, float beta1,
-                                                float beta2, float weight_decay, float* grads_out, void* workspace,
-                                                size_t ws_bytes, const tt_table_meta_t* tables, int T,
-                                                const tt_feature_meta_t* features, int F, int64_t emb_B,
-                                                const float* grad, int64_t ldg, float* weights, float* state,
-                                                float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
-                                                size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+static int fused_update_adagrad_resolve(const tt_tower_shape_t* shape, int64_t B, float* params,
+                                        float* exp_avg, float* exp_avg_sq, float eps, float beta1,
+                                        float beta2, float weight_decay, float* grads_out, void* workspace,
+                                        size_t ws_bytes, const tt_table_meta_t* tables, int T,
+                                        const tt_feature_meta_t* features, int F, int64_t emb_B,
+                                        const float* grad, int64_t ldg, float* weights, float* state,
+                                        float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
+                                        size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
   if (!next_dedup_ws || (reinterpret_cast<uintptr_t>(next_dedup_ws) & 63))
     return fail(TT_EINVAL, "tower_update_resolve: next dedup workspace null / misaligned");
   DdUpdateArgs d{};
@@ -3613,14 +3510,14 @@ int tt_tower_update_pre_rowwise_adagrad_resolve(const tt_tower_shape_t* shape, i
   return check_launch("tower_update_pre_rowwise_adagrad_resolve");
 }
 
-int tt_tower_wgrad_pre_insert_rowwise_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
-                                              size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
-                                              float adam_beta1, float adam_beta2, const void* const* next_cols,
-                                              int id_dtype, const int64_t* num_embeddings, const int32_t* dedup_tables,
-                                              const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
-                                              int F, const float* grad, int64_t ldg, float* weights, float* state,
-                                              float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
-                                              size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace,
+                                      size_t ws_bytes, int64_t* adam_step_state, float adam_lr,
+                                      float adam_beta1, float adam_beta2, const void* const* next_cols,
+                                      int id_dtype, const int64_t* num_embeddings, const int32_t* dedup_tables,
+                                      const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                                      int F, const float* grad, int64_t ldg, float* weights, float* state,
+                                      float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
+                                      size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
   if (!adam_step_state || !next_cols || !num_embeddings || !dedup_tables || !next_dedup_ws)
     return fail(TT_EINVAL, "tower_tail: null pointer");
   if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_tail: ids must be int32/int64");
@@ -3706,6 +3603,88 @@ int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, con
   return launch_t1(shape, B, a, nullptr,
                    std::max(shape->in_col[0] + shape->in_dim[0], shape->in_col[1] + shape->in_dim[1]), nullptr, params,
                    labels, label_dtype, grad_scale, logits, workspace, ws_bytes, stream);
+}
+
+// ---- launch plans (include/tt_mi355x.h): the multi-role fused launches behind one entry point ----
+int tt_launch(const tt_launch_plan_t* p, void* stream) {
+  if (!p) return fail(TT_EINVAL, "launch: null plan");
+  const tt_wgrad_role_t& w = p->wgrad;
+  const tt_update_role_t& u = p->update;
+  const tt_insert_role_t& in = p->insert;
+  const tt_adagrad_role_t& g = p->adagrad;
+  const tt_route_role_t& r = p->route;
+  const tt_gather_role_t& ga = p->gather;
+  const int64_t B = p->B;
+  auto need_multi = [&](int want) {
+    return g.multi_only == want ? TT_OK
+                                : fail(TT_EINVAL, want ? "launch: this plan updates only rows looked up more than once "
+                                                         "(adagrad.multi_only = 1)"
+                                                       : "launch: this plan updates every row (adagrad.multi_only = 0)");
+  };
+  auto adam_mode = [&]() {
+    return u.replicated ? fail(TT_EINVAL, "launch: this plan's UPDATE role runs Adam (update.replicated = 0)") : TT_OK;
+  };
+  int rc = TT_OK;
+  switch (p->roles) {
+    case TT_ROLE_WGRAD | TT_ROLE_INSERT | TT_ROLE_ADAGRAD:
+      if ((rc = need_multi(1))) return rc;
+      if ((in.dedup_ws_bytes && in.dedup_ws_bytes != g.dedup_ws_bytes) ||
+          (in.dedup_max_lookups && in.dedup_max_lookups != g.dedup_max_lookups))
+        return fail(TT_EINVAL, "launch: the ring's two dedup workspaces have one size (the ADAGRAD role's)");
+      return fused_wgrad_insert_adagrad(p->shape, B, w.loss, p->workspace, p->ws_bytes, w.adam_step_state, w.adam_lr,
+                                        w.adam_beta1, w.adam_beta2, in.next_cols, in.id_dtype, in.num_embeddings,
+                                        in.dedup_tables, g.tables, g.T, g.features, g.F, g.grad, g.ldg, g.weights,
+                                        g.state, g.lr, g.eps, g.dedup_ws, in.next_dedup_ws, g.dedup_ws_bytes,
+                                        g.dedup_max_lookups, stream);
+    case TT_ROLE_WGRAD | TT_ROLE_INSERT:
+      return fused_wgrad_insert(p->shape, B, w.loss, p->workspace, p->ws_bytes, w.adam_step_state, w.adam_lr,
+                                w.adam_beta1, w.adam_beta2, in.next_cols, in.id_dtype, in.num_embeddings,
+                                in.dedup_tables, in.next_dedup_ws, in.dedup_ws_bytes, in.dedup_max_lookups, stream);
+    case TT_ROLE_UPDATE | TT_ROLE_ADAGRAD | TT_ROLE_RESOLVE:
+      if ((rc = need_multi(1)) || (rc = adam_mode())) return rc;
+      return fused_update_adagrad_resolve(p->shape, B, u.params, u.exp_avg, u.exp_avg_sq, u.eps, u.beta1, u.beta2,
+                                          u.weight_decay, u.grads_out, p->workspace, p->ws_bytes, g.tables, g.T,
+                                          g.features, g.F, g.B, g.grad, g.ldg, g.weights, g.state, g.lr, g.eps,
+                                          g.dedup_ws, p->resolve.dedup_ws, g.dedup_ws_bytes, g.dedup_max_lookups,
+                                          stream);
+    case TT_ROLE_WGRAD | TT_ROLE_ADAGRAD:
+      if ((rc = need_multi(0))) return rc;
+      return fused_wgrad_adagrad(p->shape, B, w.loss, p->workspace, p->ws_bytes, g.tables, g.T, g.features, g.F, g.B,
+                                 g.grad, g.ldg, g.weights, g.state, g.lr, g.eps, g.dedup_ws, g.dedup_ws_bytes,
+                                 g.dedup_max_lookups, w.adam_step_state, w.adam_lr, w.adam_beta1, w.adam_beta2,
+                                 stream);
+    case TT_ROLE_UPDATE | TT_ROLE_ADAGRAD:
+      if ((rc = need_multi(0)) || (rc = adam_mode())) return rc;
+      return fused_update_adagrad(p->shape, B, u.params, u.exp_avg, u.exp_avg_sq, u.eps, u.beta1, u.beta2,
+                                  u.weight_decay, u.grads_out, p->workspace, p->ws_bytes, g.tables, g.T, g.features,
+                                  g.F, g.B, g.grad, g.ldg, g.weights, g.state, g.lr, g.eps, g.dedup_ws,
+                                  g.dedup_ws_bytes, g.dedup_max_lookups, stream);
+    case TT_ROLE_WGRAD | TT_ROLE_ROUTE_COUNT | TT_ROLE_ADAGRAD:
+      if ((rc = need_multi(0))) return rc;
+      return fused_wgrad_route_count_adagrad(p->shape, B, w.loss, p->workspace, p->ws_bytes, w.adam_step_state,
+                                             w.adam_lr, w.adam_beta1, w.adam_beta2, r.F, r.cols, r.id_dtype,
+                                             r.num_embeddings, r.block_sizes, r.owners, r.W, r.segs, r.send, r.pos_in,
+                                             r.pos_out, r.overflow, r.route_ws, r.route_ws_bytes, g.tables, g.T,
+                                             g.features, g.F, g.B, g.grad, g.ldg, g.weights, g.state, g.lr, g.eps,
+                                             g.dedup_ws, g.dedup_ws_bytes, g.dedup_max_lookups, stream);
+    case TT_ROLE_ROUTE_COUNT | TT_ROLE_ADAGRAD:
+      if ((rc = need_multi(0))) return rc;
+      return fused_route_count_adagrad(r.F, B, r.cols, r.id_dtype, r.num_embeddings, r.block_sizes, r.owners, r.W,
+                                       r.segs, r.send, r.pos_in, r.pos_out, r.overflow, r.route_ws, r.route_ws_bytes,
+                                       g.tables, g.T, g.features, g.F, g.B, g.grad, g.ldg, g.weights, g.state, g.lr,
+                                       g.eps, g.dedup_ws, g.dedup_ws_bytes, g.dedup_max_lookups, stream);
+    case TT_ROLE_UPDATE | TT_ROLE_ROUTE_PLACE | TT_ROLE_GATHER:
+      if (!u.replicated) return fail(TT_EINVAL, "launch: launch G's UPDATE role writes the replicated gradient "
+                                                "(update.replicated = 1)");
+      return fused_grads_route_place_gather(p->shape, B, u.params, u.base, u.copies, u.offsets, u.scale, p->workspace,
+                                            p->ws_bytes, r.F, r.cols, r.id_dtype, r.num_embeddings, r.block_sizes,
+                                            r.owners, r.W, r.segs, r.send, r.pos_in, r.pos_out, r.overflow, r.route_ws,
+                                            r.route_ws_bytes, ga.weights, ga.tables, ga.T, ga.recv, ga.block_i64,
+                                            ga.counts_i64, ga.seg_off, ga.slots, ga.rows_out, ga.out_stride, ga.bad,
+                                            ga.dedup_ws, ga.dedup_ws_bytes, ga.dedup_max_lookups, stream);
+    default:
+      return fail(TT_EINVAL, "launch: no fused launch runs this set of roles (see tt_launch_plan_t)");
+  }
 }
 
 }  // extern "C"

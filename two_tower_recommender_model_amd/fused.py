@@ -546,12 +546,13 @@ class FusedTwoTowerStep:
         self._mark("t1", 1)
         if self.ring_tail:
             self._mark("tail", 0)
-            check(lib.tt_tower_wgrad_pre_insert_rowwise_adagrad(
-                C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
-                0.999, ptr_array(list(next_cols)), id_dtype_code(next_cols[0].dtype), self._ring_ne, self._ring_tab,
-                ts._tm, ts.T, ts._fm, ts.F, ptr(self.gpooled), self.gpooled.stride(0), ptr(ts.weights), ptr(ts.state),
-                self.lr_emb, self.eps, ptr(ws), ptr(wsn), ws.numel(), ts._dd_cap, st),
-                "tower_wgrad_pre_insert_rowwise_adagrad")
+            # the tail: tower weight gradients (T2) + the next batch's complete insert + the rows
+            # looked up more than once (tt_launch roles WGRAD | INSERT | ADAGRAD)
+            plan = self._plan(_lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD, ws, multi_only=1)
+            plan.insert = _lib.InsertRole(next_cols=ptr_array(list(next_cols)),
+                                          id_dtype=id_dtype_code(next_cols[0].dtype), num_embeddings=self._ring_ne,
+                                          dedup_tables=self._ring_tab, next_dedup_ws=ptr(wsn))
+            _lib.launch(plan, st, "ring tail")
             self._mark("tail", 1)
             self._mark("t3", 0)
             check(lib.tt_tower_update_pre(C.byref(tw.shape), B, ptr(self.params), ptr(self.exp_avg),
@@ -560,18 +561,32 @@ class FusedTwoTowerStep:
             self._mark("t3", 1)
             return
         self._mark("t2", 0)
-        check(lib.tt_tower_wgrad_pre_insert(
-            C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
-            0.999, ptr_array(list(next_cols)), id_dtype_code(next_cols[0].dtype), self._ring_ne, self._ring_tab,
-            ptr(wsn), wsn.numel(), ts._dd_cap, st), "tower_wgrad_pre_insert")
+        plan = self._plan(_lib.ROLE_WGRAD | _lib.ROLE_INSERT, ws)
+        plan.insert = _lib.InsertRole(next_cols=ptr_array(list(next_cols)), id_dtype=id_dtype_code(next_cols[0].dtype),
+                                      num_embeddings=self._ring_ne, dedup_tables=self._ring_tab, next_dedup_ws=ptr(wsn),
+                                      dedup_ws_bytes=wsn.numel(), dedup_max_lookups=ts._dd_cap)
+        _lib.launch(plan, st, "wgrad_pre_insert")
         self._mark("t2", 1)
         self._mark("k3", 0)
-        check(lib.tt_tower_update_pre_rowwise_adagrad_resolve(
-            C.byref(tw.shape), B, ptr(self.params), ptr(self.exp_avg), ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0,
-            ptr(self.grads), ptr(tw.ws), tw.nbytes, ts._tm, ts.T, ts._fm, ts.F, B, ptr(self.gpooled),
-            self.gpooled.stride(0), ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws), ptr(wsn),
-            ws.numel(), ts._dd_cap, st), "tower_update_pre_rowwise_adagrad_resolve")
+        plan = self._plan(_lib.ROLE_UPDATE | _lib.ROLE_ADAGRAD | _lib.ROLE_RESOLVE, ws, multi_only=1)
+        plan.resolve = _lib.ResolveRole(dedup_ws=ptr(wsn))
+        _lib.launch(plan, st, "update_pre_rowwise_adagrad_resolve")
         self._mark("k3", 1)
+
+    def _plan(self, roles: int, ws: torch.Tensor, multi_only: int = 0) -> "_lib.LaunchPlan":
+        """A tt_launch plan over this step's towers, tables and dedup workspace ``ws`` with the
+        WGRAD / UPDATE / ADAGRAD roles filled (the caller adds the others)."""
+        tw, ts = self.towers, self.tables
+        return _lib.LaunchPlan(
+            roles=roles, shape=C.pointer(tw.shape), B=self.B, workspace=ptr(tw.ws), ws_bytes=tw.nbytes,
+            wgrad=_lib.WgradRole(loss=ptr(self.loss), adam_step_state=ptr(self.adam_state), adam_lr=self.lr_dense,
+                                 adam_beta1=0.9, adam_beta2=0.999),
+            update=_lib.UpdateRole(params=ptr(self.params), exp_avg=ptr(self.exp_avg), exp_avg_sq=ptr(self.exp_avg_sq),
+                                   eps=1e-8, beta1=0.9, beta2=0.999, weight_decay=0.0, grads_out=ptr(self.grads)),
+            adagrad=_lib.AdagradRole(tables=ts._tm, T=ts.T, F=ts.F, features=ts._fm, B=self.B, grad=ptr(self.gpooled),
+                                     ldg=self.gpooled.stride(0), weights=ptr(ts.weights), state=ptr(ts.state),
+                                     lr=self.lr_emb, eps=self.eps, dedup_ws=ptr(ws), dedup_ws_bytes=ws.numel(),
+                                     dedup_max_lookups=ts._dd_cap, multi_only=multi_only))
 
     def capture_ring(self, batches: Sequence, steps_per_graph: int = 1, keep_graph: bool = False) -> None:
         """Production HIP graphs over a cyclic pool of resident (cols, labels) batches (len even, a

@@ -358,6 +358,17 @@ class TableSet:
                                                ptr(self._dd_ws), self._dd_ws.numel(), self._dd_cap,
                                                stream_handle(self.device)), "dedup_rowwise_adagrad")
 
+    def _adagrad_role(self, fm, F: int, B: int, grad: torch.Tensor, lr: float, eps: float,
+                      multi_only: int = 0) -> "_lib.AdagradRole":
+        """The ADAGRAD role of a tt_launch plan over this set's tables and dedup workspace (the
+        arguments of ``dedup_rowwise_adagrad``)."""
+        if grad.dtype != torch.float32 or grad.stride(-1) != 1:
+            raise _lib.TTError("dedup_rowwise_adagrad: grad must be fp32 with unit column stride")
+        return _lib.AdagradRole(tables=self._tm, T=self.T, F=F, features=fm, B=int(B), grad=ptr(grad),
+                                ldg=grad.stride(0), weights=ptr(self.weights), state=ptr(self.state), lr=float(lr),
+                                eps=float(eps), dedup_ws=ptr(self._dd_ws), dedup_ws_bytes=self._dd_ws.numel(),
+                                dedup_max_lookups=self._dd_cap, multi_only=multi_only)
+
     def bwd_dense(self, grad_out: torch.Tensor, values: torch.Tensor, offsets: torch.Tensor, B: int,
                   grad_weights: torch.Tensor, pooling: int = TT_POOL_SUM) -> None:
         _dev(grad_out, grad_weights)
@@ -643,13 +654,13 @@ class FusedTowers:
             F = 1
         else:
             fm, F = tables._fm, tables.F
-        check(_lib_().tt_tower_wgrad_rowwise_adagrad(C.byref(self.shape), self.B, ptr(loss), ptr(self.ws), self.nbytes,
-                                                     tables._tm, tables.T, fm, F, int(emb_B), ptr(grad),
-                                                     grad.stride(0), ptr(tables.weights), ptr(tables.state), float(lr),
-                                                     float(eps), ptr(tables._dd_ws), tables._dd_ws.numel(),
-                                                     tables._dd_cap, ptr(adam_step_state), float(adam_lr),
-                                                     float(adam_beta1), float(adam_beta2), stream_handle(self.device)),
-              "tower_wgrad_rowwise_adagrad")
+        _lib.launch(_lib.LaunchPlan(
+            roles=_lib.ROLE_WGRAD | _lib.ROLE_ADAGRAD, shape=C.pointer(self.shape), B=self.B, workspace=ptr(self.ws),
+            ws_bytes=self.nbytes,
+            wgrad=_lib.WgradRole(loss=ptr(loss), adam_step_state=ptr(adam_step_state), adam_lr=float(adam_lr),
+                                 adam_beta1=float(adam_beta1), adam_beta2=float(adam_beta2)),
+            adagrad=tables._adagrad_role(fm, F, emb_B, grad, lr, eps)), stream_handle(self.device),
+            "tower_wgrad_rowwise_adagrad")
 
     def wgrad_pre(self, loss, adam_step_state, adam_lr: float = 0.01, adam_beta1: float = 0.9,
                   adam_beta2: float = 0.999, dedup: Optional["TableSet"] = None) -> None:
@@ -674,11 +685,13 @@ class FusedTowers:
             F = 1
         else:
             fm, F = tables._fm, tables.F
-        check(_lib_().tt_tower_update_pre_rowwise_adagrad(
-            C.byref(self.shape), self.B, ptr(params), ptr(exp_avg), ptr(exp_avg_sq), float(eps), float(beta1),
-            float(beta2), float(weight_decay), ptr(grads_out), ptr(self.ws), self.nbytes, tables._tm, tables.T, fm, F,
-            int(emb_B), ptr(grad), grad.stride(0), ptr(tables.weights), ptr(tables.state), float(lr), float(emb_eps),
-            ptr(tables._dd_ws), tables._dd_ws.numel(), tables._dd_cap, stream_handle(self.device)),
+        _lib.launch(_lib.LaunchPlan(
+            roles=_lib.ROLE_UPDATE | _lib.ROLE_ADAGRAD, shape=C.pointer(self.shape), B=self.B, workspace=ptr(self.ws),
+            ws_bytes=self.nbytes,
+            update=_lib.UpdateRole(params=ptr(params), exp_avg=ptr(exp_avg), exp_avg_sq=ptr(exp_avg_sq), eps=float(eps),
+                                   beta1=float(beta1), beta2=float(beta2), weight_decay=float(weight_decay),
+                                   grads_out=ptr(grads_out)),
+            adagrad=tables._adagrad_role(fm, F, emb_B, grad, lr, emb_eps)), stream_handle(self.device),
             "tower_update_pre_rowwise_adagrad")
 
     def update_pre(self, params, exp_avg, exp_avg_sq, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,

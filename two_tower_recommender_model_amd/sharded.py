@@ -557,6 +557,24 @@ class FusedShardedTwoTowerStep:
             ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
             "tower_adam_pre_grads_sum")
 
+    def _plan(self, roles: int, route, ws: torch.Tensor) -> "_lib.LaunchPlan":
+        """A tt_launch plan for the pipelined step's launches U / G: the towers, the WGRAD role, the
+        route of a later batch (``route`` = _route_args) and the owner's ADAGRAD role over the received
+        gradient rows (one pseudo-feature per source rank) in dedup workspace ``ws``."""
+        tw, ts, r = self.towers, self.tables, self.rank
+        return _lib.LaunchPlan(
+            roles=roles, shape=C.pointer(tw.shape), B=self.B, workspace=ptr(tw.ws), ws_bytes=tw.nbytes,
+            wgrad=_lib.WgradRole(loss=ptr(self.loss), adam_step_state=ptr(self.adam_state), adam_lr=self.lr_dense,
+                                 adam_beta1=0.9, adam_beta2=0.999),
+            route=_lib.RouteRole(F=route[0], cols=route[1], id_dtype=route[2], num_embeddings=route[3],
+                                 block_sizes=route[4], owners=route[5], W=route[6], segs=route[7], send=route[8],
+                                 pos_in=route[9], pos_out=route[10], overflow=route[11], route_ws=route[12],
+                                 route_ws_bytes=route[13]),
+            adagrad=_lib.AdagradRole(tables=ts._tm, T=ts.T, F=self.W, features=self._fm_src, B=self.S[r],
+                                     grad=ptr(self.recvA), ldg=self.D, weights=ptr(ts.weights), state=ptr(ts.state),
+                                     lr=self.lr_emb, eps=self.eps, dedup_ws=ptr(ws), dedup_ws_bytes=ws.numel(),
+                                     dedup_max_lookups=self.max_lookups, multi_only=0))
+
     def _route_args(self, cols: Sequence[torch.Tensor], parity: int):
         return (self.F, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ne, self._bs, self._ow, self.W,
                 ptr(self.segs), ptr(self.sendA), ptr(self.pos_in[parity]), ptr(self.pos_out[parity]),
@@ -615,23 +633,25 @@ class FusedShardedTwoTowerStep:
                                              ptr(self.adam_state), self.lr_dense, 0.9, 0.999, None, 0, 0,
                                              stream_handle(dev)), "tower_wgrad_pre")
             self._exchange_a()
-            check(lib.tt_shard_route_count_rowwise_adagrad(
-                route[0], B, *route[1:], ts._tm, ts.T, self._fm_src, self.W, self.S[r], ptr(self.recvA), self.D, ptr(ts.weights),
-                ptr(ts.state), self.lr_emb, self.eps, ptr(ws), ws.numel(), self.max_lookups, stream_handle(dev)),
-                "shard_route_count_rowwise_adagrad")
+            # launch U without T2: the owner's row-wise Adagrad + the count pass of batch i+2's route
+            _lib.launch(self._plan(_lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws), stream_handle(dev),
+                        "shard_route_count_rowwise_adagrad")
             main.wait_stream(self.side)
         else:
             self._exchange_a()
-            check(lib.tt_tower_wgrad_route_count_rowwise_adagrad(
-                C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes, ptr(self.adam_state), self.lr_dense, 0.9,
-                0.999, *route, ts._tm, ts.T, self._fm_src, self.W,
-                self.S[r], ptr(self.recvA), self.D, ptr(ts.weights), ptr(ts.state), self.lr_emb, self.eps, ptr(ws),
-                ws.numel(), self.max_lookups, stream_handle(dev)), "tower_wgrad_route_count_rowwise_adagrad")
+            # launch U: T2 + the count pass of batch i+2's route + the owner's row-wise Adagrad
+            _lib.launch(self._plan(_lib.ROLE_WGRAD | _lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws),
+                        stream_handle(dev), "tower_wgrad_route_count_rowwise_adagrad")
+        # launch G: the tower gradient x 1/W into every destination block + the route's place pass +
+        # the owner's gather of batch i+1's rows
+        plan = self._plan(_lib.ROLE_UPDATE | _lib.ROLE_ROUTE_PLACE | _lib.ROLE_GATHER, route, ws)
+        plan.update = _lib.UpdateRole(params=ptr(self.params), replicated=1, copies=self.W,
+                                      base=self.rows_out.data_ptr(), offsets=self._tw_off, scale=1.0 / self.W)
         g = self._gather_args(parity ^ 1)
-        g = g[:3] + g[5:]  # the combined launch takes F and W from the route's arguments
-        check(lib.tt_tower_grads_replicated_route_place_gather(
-            C.byref(tw.shape), B, ptr(self.params), self.rows_out.data_ptr(), self.W, self._tw_off, 1.0 / self.W,
-            ptr(tw.ws), tw.nbytes, *route, *g), "tower_grads_replicated_route_place_gather")
+        plan.gather = _lib.GatherRole(weights=g[0], tables=g[1], T=g[2], recv=g[5], block_i64=g[6], counts_i64=g[7],
+                                      seg_off=g[8], slots=g[9], rows_out=g[10], out_stride=g[11], bad=g[12],
+                                      dedup_ws=g[13], dedup_ws_bytes=g[14], dedup_max_lookups=g[15])
+        _lib.launch(plan, stream_handle(dev), "tower_grads_replicated_route_place_gather")
         self._exchange_b()
         self._adam()
 
