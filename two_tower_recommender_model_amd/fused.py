@@ -28,6 +28,10 @@ import torch
 from . import _lib, ops
 from ._lib import FeatureMeta, check, id_dtype_code, ptr, ptr_array, stream_handle
 
+# multi-hot pipelined step: the row update captured before the side branches (0: the previous
+# order, for same-box A/B measurements)
+_KJT_UPDATE_FIRST = os.environ.get("TT_KJT_UPDATE_FIRST", "1") != "0"
+
 
 class FusedTwoTowerStep:
     def __init__(self, num_embeddings: Sequence[int], embedding_dims: Sequence[int],
@@ -408,6 +412,23 @@ class FusedTwoTowerStep:
                                         self.params, self.labels, self.logits,
                                         pooled_out=self.pooled if self.materialize_pooled else None)
                 self._mark("t1", 1)
+                if defer_prepare and self.side2 is not None and _KJT_UPDATE_FIRST:
+                    # the row update (the step's critical path) enqueued right behind T1 on the
+                    # capture stream, the two side branches forked from T1's end after it: in the
+                    # graph the branches captured first started first, ~12 us apart, and the
+                    # update came third
+                    t1_done = torch.cuda.Event()
+                    t1_done.record(main)
+                    self._mark("upd", 0)
+                    self._emb_update()
+                    self._mark("upd", 1)
+                    for st, work in ((self.side, prepare), (self.side2, self._kjt_t2t3)):
+                        st.wait_event(t1_done)
+                        with torch.cuda.stream(st):
+                            work()
+                    main.wait_stream(self.side)
+                    main.wait_stream(self.side2)
+                    return
                 if defer_prepare:
                     launch_prepare()
             elif not self.gather:
@@ -418,11 +439,7 @@ class FusedTwoTowerStep:
             if self.side2 is not None:
                 self.side2.wait_stream(main)
             with torch.cuda.stream(s2):
-                self._mark("t2t3", 0)
-                self.towers.wgrad(self.loss)
-                self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
-                                   grads_out=self.grads)
-                self._mark("t2t3", 1)
+                self._kjt_t2t3()
             if self.side is not None and prepare is not None and not ahead:
                 main.wait_stream(self.side)
             self._mark("upd", 0)
@@ -444,6 +461,14 @@ class FusedTwoTowerStep:
         if ahead:
             main.wait_stream(self.side)
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.adam_state, self.lr_dense)
+
+    def _kjt_t2t3(self) -> None:
+        """T2 (weight gradients, loss) + T3 (Adam, bf16 weight copies) of the towers."""
+        self._mark("t2t3", 0)
+        self.towers.wgrad(self.loss)
+        self.towers.update(self.params, self.exp_avg, self.exp_avg_sq, self.adam_state, lr=self.lr_dense,
+                           grads_out=self.grads)
+        self._mark("t2t3", 1)
 
     def _mark(self, name: str, end: int) -> None:
         """Record the start (end=0) / end (end=1) HIP event of launch `name` of the current step
