@@ -78,10 +78,13 @@ def test_fused_step_matches_reference_golden(device, case, precision):
     else:
         # bf16 operands can flip a ReLU mask where a pre-activation is within bf16 error of 0;
         # each flip moves that unit's whole gradient. Require 99% of elements within tolerance
-        # and every element within 5x it.
+        # and every element within 5x it, or within 4 lr: the first row-wise Adagrad / Adam steps
+        # are normalised (lr g / rms(g)), so an element whose gradient a flip turns around moves
+        # by up to ~2 lr |g_i| / rms(g) (c1full, D = 16: 0.032 = 3.2 lr at one of 160k elements)
         def check(got, want, atol):
             err = np.abs(got - want)
-            assert np.mean(err <= atol) >= 0.99 and err.max() <= 5 * atol, (np.mean(err <= atol), err.max())
+            assert np.mean(err <= atol) >= 0.99 and err.max() <= max(5 * atol, 4 * lr), \
+                (np.mean(err <= atol), err.max())
     check(st.tables.table_view(0).cpu().numpy(), g["final_t_user_id"], tol["table"])
     check(st.tables.table_view(1).cpu().numpy(), g["final_t_product_id"], tol["table"])
     np.testing.assert_allclose(st.tables.state_view(0).cpu().numpy(), g["final_state_t_user_id"],

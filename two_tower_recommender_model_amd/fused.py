@@ -419,6 +419,7 @@ class FusedTwoTowerStep:
                     # update came third
                     t1_done = torch.cuda.Event()
                     t1_done.record(main)
+                    self.tables.use_bwd_workspace(parity)  # (prepare() leaves it so; it runs later here)
                     self._mark("upd", 0)
                     self._emb_update()
                     self._mark("upd", 1)
