@@ -1936,21 +1936,32 @@ __device__ __forceinline__ void wgrad_lds_block_rm(const WgradArgs& a, int lb, c
   for (int64_t p0 = mb; p0 < me; p0 += T2_PF * T2_MB) {
     bf16x8 ld[T2_PF][3];
     const uint32_t dr = (uint32_t)(p0 - mb);  // rows into the slice
+    // every load unconditional (an invalid piece reads the slice's first row and is zeroed after):
+    // loads behind branches make the compiler wait for ALL of them (vmcnt(0)) before chunk 0's
+    // LDS write; straight-line loads let chunk c wait for its own three only
+    bool okc[T2_PF][3];
 #pragma unroll
     for (int c = 0; c < T2_PF; ++c) {
       const uint32_t rc = dr + c * T2_MB;
       const int64_t mrow = p0 + c * T2_MB;
-      ld[c][0] = ok0 && mrow + prow0 < me ? *reinterpret_cast<const bf16x8*>(zb + zo + rc * zstr) : (bf16x8)(__bf16)0.f;
-      ld[c][1] = ok1 && mrow + prow1 < me ? *reinterpret_cast<const bf16x8*>(ab + ao1 + rc * astr) : (bf16x8)(__bf16)0.f;
-      ld[c][2] = ok2 && mrow + prow2 < me ? *reinterpret_cast<const bf16x8*>(ab + ao2 + rc * astr) : (bf16x8)(__bf16)0.f;
+      okc[c][0] = ok0 && mrow + prow0 < me;
+      okc[c][1] = ok1 && mrow + prow1 < me;
+      okc[c][2] = ok2 && mrow + prow2 < me;
+      ld[c][0] = *reinterpret_cast<const bf16x8*>(zb + zo + (okc[c][0] ? rc * zstr : 0u));
+      ld[c][1] = *reinterpret_cast<const bf16x8*>(ab + ao1 + (okc[c][1] ? rc * astr : 0u));
+      ld[c][2] = *reinterpret_cast<const bf16x8*>(ab + ao2 + (okc[c][2] ? rc * astr : 0u));
     }
 #pragma unroll
     for (int c = 0; c < T2_PF; ++c) {
       if (p0 + c * T2_MB >= me) break;  // uniform: the slice's tail
       __bf16* d = buf + (c & 1) * TR * T2R_STR;
-      if (ok0) *reinterpret_cast<bf16x8*>(d + lw0) = ld[c][0];
-      if (ok1) *reinterpret_cast<bf16x8*>(d + lw1) = ld[c][1];
-      if (ok2) *reinterpret_cast<bf16x8*>(d + lw2) = ld[c][2];
+      // pieces outside the tile's features land in LDS columns no fragment of this tile reads
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (!okc[c][i]) ld[c][i] = (bf16x8)(__bf16)0.f;
+      *reinterpret_cast<bf16x8*>(d + lw0) = ld[c][0];
+      *reinterpret_cast<bf16x8*>(d + lw1) = ld[c][1];
+      *reinterpret_cast<bf16x8*>(d + lw2) = ld[c][2];
       __syncthreads();  // one barrier per chunk: buffer c & 1 was last read two chunks ago
       if (c == 0 && p0 == mb) T2_STAMP(1);
       bf16x8 fa[2], fb[4];
