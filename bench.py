@@ -428,7 +428,9 @@ def run_multihot(args):
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01, lr_dense=0.01,
                              id_dtype=torch.int64, seed=0, max_lookups=cap)
     # pipelined grouping: batch i+1's tt_bwd_prepare runs on the side stream during step i
-    step.capture_pool_kjt(batches, ahead=not args.no_kjt_ahead)
+    ahead = not args.no_kjt_ahead
+    k = min(args.steps_per_graph, len(batches)) if ahead else 1  # several steps per graph: no gap between them
+    step.capture_pool_kjt(batches, ahead=ahead, steps_per_graph=k)
 
     def run(n):
         step.replay_pool(n)

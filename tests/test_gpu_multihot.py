@@ -137,13 +137,15 @@ def test_config3_shape_step_vs_oracle(device, precision):
             np.testing.assert_allclose(st.tables.table_view(f).cpu().numpy(), s0.tables[f].numpy(), rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("k", [1, 2], ids=["graph1", "graph2"])
 @pytest.mark.parametrize("hot", [False, True], ids=["uniform", "zipf"])
-def test_multihot_pipelined_grouping_bitwise(device, hot):
+def test_multihot_pipelined_grouping_bitwise(device, hot, k):
     """The pipelined pool (capture_pool_kjt(ahead=True): batch i+1's backward grouping built on the
     side stream during step i, two alternating workspaces) trains exactly like the unpipelined
     pool: 4 batches x 2 cycles of graph replays, tables / row-wise state / tower parameters / loss
     bitwise equal; then 3 eager pipelined steps (pool_step_eager) continue bitwise like 3 more
-    unpipelined graph replays. Zipf ids exercise the hot-row kernels."""
+    unpipelined graph replays. Zipf ids exercise the hot-row kernels; k = 2 replays graphs of two
+    pipelined steps where the cursor allows (replay_pool)."""
     from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
 
     rng = np.random.default_rng(23 if hot else 24)
@@ -160,7 +162,7 @@ def test_multihot_pipelined_grouping_bitwise(device, hot):
 
     ref_st, pipe = make(), make()
     ref_st.capture_pool_kjt(batches)
-    pipe.capture_pool_kjt(batches, ahead=True)
+    pipe.capture_pool_kjt(batches, ahead=True, steps_per_graph=k)  # k > 1: graphs of k steps too
     for i in range(8):
         ref_st.pool_graphs[i % 4].replay()
     pipe.replay_pool(8)

@@ -224,11 +224,16 @@ class FusedTwoTowerStep:
         self.offsets.copy_(offsets.to(torch.int32), non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
 
-    def capture_pool_kjt(self, batches: Sequence, keep_graph: bool = False, ahead: bool = False) -> None:
+    def capture_pool_kjt(self, batches: Sequence, keep_graph: bool = False, ahead: bool = False,
+                         steps_per_graph: int = 1) -> None:
         """One graph per resident multi-hot batch (values, offsets int32, labels), read in place.
         ahead: the pipelined form (``step(next_kjt=...)``): graph i groups batch i+1 of the pool
         while it trains on batch i, so the graphs must be replayed in pool order from the cursor
-        (``replay_pool``); the pool length must be even (the two grouping workspaces alternate)."""
+        (``replay_pool``); the pool length must be even (the two grouping workspaces alternate).
+        steps_per_graph k > 1 (ahead only; the pool length a multiple of k): also graphs of k
+        consecutive steps (``pool_graphs_k``), which ``replay_pool`` uses where the cursor allows —
+        between two graphs the stream idles ~20 us (the step's side branches join, the next graph
+        launches); inside one graph the next step's T1 follows the join directly."""
         staged = []
         for values, offsets, labels in batches:
             if values.dtype != self.id_dtype or offsets.dtype != torch.int32 or values.numel() > self.max_lookups \
@@ -236,25 +241,54 @@ class FusedTwoTowerStep:
                 raise _lib.TTError("capture_pool_kjt: batch does not match the step's dtype / capacity")
             staged.append((values.contiguous(), offsets.contiguous(), labels.to(torch.int32).contiguous()))
         n = len(staged)
+        k = int(steps_per_graph)
         if ahead and n % 2:
             raise _lib.TTError("capture_pool_kjt(ahead=True): the batch count must be even")
+        if k > 1 and (not ahead or n % k or k % 2):
+            raise _lib.TTError("capture_pool_kjt: steps_per_graph > 1 needs ahead=True, an even k dividing the pool")
         self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]
         keep = self.values, self.offsets, self.labels
         self.pool_graphs = []
+        self.pool_graphs_k = []
         self.pool_ahead = bool(ahead)
         self._kjt_pool = staged
         if ahead:
             self.kjt_ring_prime(staged[0][0], staged[0][1], 0)
+
+        def item(i):
+            v, o, lab = staged[i]
+            return v, o, lab, ((staged[(i + 1) % n][0], staged[(i + 1) % n][1]) if ahead else None), i % 2
+
         try:
-            for i, (v, o, lab) in enumerate(staged):
-                self.values, self.offsets, self.labels = v, o, lab
-                nxt = (staged[(i + 1) % n][0], staged[(i + 1) % n][1]) if ahead else None
-                self.capture(None, keep_graph=keep_graph, next_kjt=nxt, parity=i % 2)
-                self.pool_graphs.append(self.graph)
+            for i in range(n):
+                self.pool_graphs.append(self._capture_kjt_steps([item(i)], keep_graph))
+            if k > 1:
+                self.pool_graphs_k = [self._capture_kjt_steps([item(i) for i in range(j, j + k)], keep_graph)
+                                      for j in range(0, n, k)]
         finally:
             self.values, self.offsets, self.labels = keep
-        self.steps_per_graph = 1
+        self.graph = self.pool_graphs[-1]
+        self.steps_per_graph = k
         self.pool_cursor = 0
+
+    def _capture_kjt_steps(self, items, keep_graph: bool):
+        """One HIP graph of consecutive multi-hot steps; items: (values, offsets, labels, next_kjt,
+        parity) per step."""
+        self.sync_weights()
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph(keep_graph=keep_graph)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for v, o, lab, nxt, par in items:
+                    self.values, self.offsets, self.labels = v, o, lab
+                    self.step(next_kjt=nxt, parity=par)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        if not keep_graph:
+            _lib.graph_upload(g, self.device)
+        torch.cuda.synchronize(self.device)
+        return g
 
     def kjt_ring_prime(self, values: torch.Tensor, offsets: torch.Tensor, parity: int) -> None:
         """Group the first batch of a pipelined multi-hot sequence into workspace ``parity`` (every
@@ -268,9 +302,14 @@ class FusedTwoTowerStep:
         """Replay n pool graphs in pool order, continuing at the cursor (the pipelined pool needs
         the order: graph i expects batch i's grouping from graph i-1)."""
         i, nb = self.pool_cursor, len(self.pool_graphs)
-        for _ in range(n):
-            self.pool_graphs[i].replay()
-            i = (i + 1) % nb
+        k = getattr(self, "steps_per_graph", 1)
+        while n > 0:
+            if k > 1 and self.pool_graphs_k and i % k == 0 and n >= k:
+                self.pool_graphs_k[i // k].replay()
+                i, n = (i + k) % nb, n - k
+            else:
+                self.pool_graphs[i].replay()
+                i, n = (i + 1) % nb, n - 1
         self.pool_cursor = i
 
     def pool_step_eager(self) -> None:
