@@ -7,7 +7,7 @@ F=gpurun_out/final
 mkdir -p $F
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $F/smoke.log 2>&1 || exit $?
 OUT=gpurun_out/pmc bash scripts/pmc_traffic.sh > $F/pmc.log 2>&1 || exit $?
-cp gpurun_out/pmc/summary.json profiles/${TAG:-r03t}_pmc_traffic.json
+cp gpurun_out/pmc/summary.json profiles/${TAG:-r03u}_pmc_traffic.json
 timeout -k 10 600 python bench.py > $F/bench.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --ids zipf --no-cpu-baseline > $F/bench_zipf.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --workload config2 --no-cpu-baseline > $F/bench_config2.log 2>&1 || exit $?
