@@ -75,7 +75,8 @@ def parse():
                     help="resident synthetic batches cycled by the single-hot bench (64 x 16,384 rows x 512 B "
                          "= 537 MB touched: past the 256 MiB Infinity Cache)")
     ap.add_argument("--kernel-iters", type=int, default=50)
-    ap.add_argument("--steps-per-graph", type=int, default=8, choices=[1, 2, 4, 8])
+    ap.add_argument("--steps-per-graph", type=int, default=None, choices=[1, 2, 4, 8, 16, 32],
+                    help="steps per HIP graph (default 8)")
     ap.add_argument("--host-fed", action="store_true",
                     help="feed host batches through the 3-stage host pipeline (pinned staging, async H2D on a "
                          "copy stream, graph replay): the PCIe-inclusive rate, reported beside the resident one")
@@ -429,7 +430,7 @@ def run_multihot(args):
                              id_dtype=torch.int64, seed=0, max_lookups=cap)
     # pipelined grouping: batch i+1's tt_bwd_prepare runs on the side stream during step i
     ahead = not args.no_kjt_ahead
-    k = min(args.steps_per_graph, len(batches)) if ahead else 1  # several steps per graph: no gap between them
+    k = min(args.steps_per_graph or 8, len(batches)) if ahead else 1  # several steps per graph: no gap between them
     step.capture_pool_kjt(batches, ahead=ahead, steps_per_graph=k)
 
     def run(n):
@@ -604,12 +605,16 @@ def run_single(args):
     torch.cuda.set_device(dev)
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
-    nb = max(args.steps_per_graph, args.batches // args.steps_per_graph * args.steps_per_graph)
+    # 8 steps per graph by default: 32 measured 35.0 against 35.5-35.7 us/step in 96-step runs and
+    # 35.9 against 36.5 at the default 50, but no better at 20 steps (37.40 / 37.38 us, 38.35 / 38.06
+    # after 3 warm-up steps; profiles/r03_ring_steps_per_graph_ab*.log)
+    spg = args.steps_per_graph or 8
+    nb = max(spg, args.batches // spg * spg)
     batches = synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1)
     # the production ring: HIP graphs of k full steps over the resident batches (no input copies;
     # each step files the next batch's dedup table): a graph launch costs the host ~35-55 us, more
     # than a step's GPU time, so k > 1 keeps the GPU fed (single-step graphs for a remainder)
-    k = args.steps_per_graph
+    k = spg
     step.capture_ring(batches, steps_per_graph=k)
 
     def run(n):
@@ -696,11 +701,11 @@ def run_host_fed(args):
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01,
                              lr_dense=0.01, id_dtype=torch.int64, seed=0)
     host = synthetic_host_batches([num_users, num_items], B, args.batches, seed=1)
-    pipe = HostFedPipeline(step, group=args.steps_per_graph, depth=4, trace=True)
+    pipe = HostFedPipeline(step, group=args.steps_per_graph or 8, depth=4, trace=True)
     src = itertools.cycle(host)
     # whole groups, and enough of them that the pipeline's fill (two groups copied before the first
     # replay) and drain do not dominate: at least 64 groups timed
-    g = args.steps_per_graph
+    g = args.steps_per_graph or 8
     steps = max(64 * g, -(-args.steps // g) * g)
     pipe.run(src, max_steps=max(args.warmup, 4 * g))
     torch.cuda.synchronize()
@@ -729,7 +734,7 @@ def run_multi(args, world, rank, local_rank):
     F = len(N)
     dev = torch.device("cuda", local_rank % torch.cuda.device_count())  # (rehearsal: ranks may share one GPU)
     comm = TorchComm(always_collective=True)
-    k = args.steps_per_graph
+    k = args.steps_per_graph or 8
     nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k
     batches = synth_cols(N, B, nb, dev, ids, seed=seed * 1000 + 1 + rank)
     blocks = [-(-n // world) if sh == "row_wise" else 0 for n, sh in zip(N, sharding)]
