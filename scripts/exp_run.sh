@@ -2,9 +2,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python3 bench.py --no-cpu-baseline > gpurun_out/ab_k2.log 2>&1 || exit $?
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps-per-graph 8 >> gpurun_out/ab_k2.log 2>&1 || exit $?
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 20 --warmup 10 >> gpurun_out/ab_k2.log 2>&1 || exit $?
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 20 --warmup 10 --steps-per-graph 8 >> gpurun_out/ab_k2.log 2>&1 || exit $?
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 20 --warmup 3 >> gpurun_out/ab_k2.log 2>&1 || exit $?
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 20 --warmup 3 --steps-per-graph 8 >> gpurun_out/ab_k2.log 2>&1 || exit $?
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/gpu_suite_final.log 2>&1 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_final.log 2>&1 || exit $?
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/bench_driverlike.log 2>&1 || exit $?
