@@ -52,7 +52,8 @@
 extern "C" {
 #endif
 
-#define TT_ABI_VERSION 1
+/* 2: tt_tower_shape_t._pad became `flags`; the 12 role-combination exports became tt_launch */
+#define TT_ABI_VERSION 2
 
 /* status codes (besides hipError_t values, which are all < 1000) */
 #define TT_OK 0
@@ -260,7 +261,9 @@ typedef struct {
   int32_t in_col[2];
   int32_t flags; /* TT_TOWER_GENERAL_T1: T1 is always the general kernel (several features per tower,
                     tt_tower_fwd_bwd_indexed_multi_bf16), so T3 keeps its plain bf16 weight copies
-                    even for 2-layer shapes <= 128 wide; 0 otherwise */
+                    even for 2-layer shapes <= 128 wide; every other T1 entry point returns TT_EINVAL
+                    for such a shape. 0 otherwise; any other bit is TT_EINVAL. (ABI 2: this field
+                    was `_pad` in ABI 1 — zero it.) */
 } tt_tower_shape_t;
 #define TT_TOWER_GENERAL_T1 1
 
@@ -564,7 +567,7 @@ typedef struct {
   int32_t T;
   int32_t F;
   const tt_feature_meta_t* features;
-  int64_t B;               /* lookups per feature */
+  int64_t B;               /* lookups per feature (WGRAD | INSERT | ADAGRAD, the ring tail: 0 or the plan's B) */
   const float* grad;
   int64_t ldg;
   float* weights;

@@ -1,11 +1,14 @@
 """EXPERIMENT: phases of the hot-row role (dd_hot_role) inside the ring's tail launch at Zipf ids
-(TT_DD_STAMPS; library built with TT_EXTRA_CFLAGS=-DDD_HOT_STAMPS=1): per hot workgroup, s_memrealtime (100 MHz) at 4 first pass scanned, 5 passes summed,
+(TT_DD_STAMPS; experiment library: `TT_EXTRA_CFLAGS=-DDD_HOT_STAMPS=1 python -m
+two_tower_recommender_model_amd.build --experiments`, run with TT_EXPERIMENT_LIB=1): per hot
+workgroup, s_memrealtime (100 MHz) at 4 first pass scanned, 5 passes summed,
 6 partial published + counter added, 7 row update issued; us from the workgroup's start."""
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["TT_DD_STAMPS"] = "1"
+os.environ.setdefault("TT_EXPERIMENT_LIB", "1")
 import torch  # noqa: E402
 
 from two_tower_recommender_model_amd.fused import FusedTwoTowerStep  # noqa: E402

@@ -21,6 +21,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+from child_util import stage  # noqa: E402
 
 D, B, LR, LAYERS, STEPS = 128, 8192, 0.05, [128, 64], 3
 QUERY = ["user_id"] + [f"u_f{k}" for k in range(1, 8)]
@@ -32,6 +33,7 @@ ROWS.update({f: 1_000_000 for f in QUERY[1:] + CAND[1:]})
 def main():
     device = torch.device("cuda:0")
     torch.cuda.set_device(device)
+    stage("init_process_group")
     dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=device)
     import two_tower_recommender_model_amd as tt
     import two_tower_recommender_model_amd.torchrec.modules.mlp as mlp_mod
@@ -67,6 +69,7 @@ def main():
     planner = EmbeddingShardingPlanner(topology=Topology(world_size=1, compute_device="cuda"),
                                        constraints={c.name: ParameterConstraints(sharding_types=["table_wise"])
                                                     for c in cfgs})
+    stage("plan + DMP (allocates ~84 GB of tables)")
     plan = planner.collective_plan(task, get_default_sharders(), dist.group.WORLD)
     model = DistributedModelParallel(module=task, device=device, plan=plan)
     sebc = model.module.two_tower.ebc
@@ -75,6 +78,7 @@ def main():
     optimizer = KeyedOptimizerWrapper(dict(model.named_parameters()), lambda p: torch.optim.Adam(p, lr=0.01))
     pipeline = TrainPipelineSparseDist(model, optimizer, device)
 
+    stage("batches + compact oracle tables")
     # batches: single-hot, uniform ids in [0, N), ~1 % empty bags
     g = torch.Generator().manual_seed(33)
     host = []
@@ -120,6 +124,7 @@ def main():
     it = batches(host[:STEPS])
     pipeline._model.train()
     for s in range(STEPS):
+        stage(f"step {s}")
         loss, logits, _ = pipeline.progress(it)
         v, l, lab = host[s]
         offs = torch.from_numpy(ref.complete_cumsum(l.numpy()))
@@ -127,6 +132,7 @@ def main():
         np.testing.assert_allclose(float(loss), float(want_loss), rtol=1e-4)
         np.testing.assert_allclose(logits.cpu().numpy(), want_logits.numpy(), rtol=1e-4, atol=1e-5)
     torch.cuda.synchronize()
+    stage("final rows / states")
     for f, c in enumerate(cfgs):
         got = weights[f][rows[f].to(device)].cpu()
         # an Adagrad step moves an element by lr * G_d / rms(G): where G_d nearly cancels, the GPU
@@ -143,4 +149,6 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    from child_util import child_main
+
+    child_main(main)

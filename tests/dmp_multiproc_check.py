@@ -260,4 +260,6 @@ def check(wl, B, S, W, feats, allb, touched, snaps, got_outs):
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    from child_util import child_main
+
+    child_main(main)

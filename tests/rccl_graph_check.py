@@ -48,4 +48,6 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    from child_util import child_main
+
+    child_main(main)

@@ -38,7 +38,7 @@ def test_every_declared_symbol_exported(lib):
     assert not extra, f"exported but not declared in the header: {extra}"
     assert sorted(_lib.SIGNATURES) == declared
     assert lib.tt_num_entry_points() == len(_lib.COMPUTE_ENTRY_POINTS)
-    assert lib.tt_abi_version() == 1
+    assert lib.tt_abi_version() == 2
 
 
 def test_launch_plan_layout_matches_the_header(tmp_path):
@@ -85,6 +85,10 @@ def test_launch_rejects_unknown_role_sets(lib):
     plan = _lib.LaunchPlan(roles=_lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD)  # ring tail: multi_only
     assert lib.tt_launch(C.byref(plan), None) == 1001
     assert b"multi_only" in lib.tt_last_error_string()
+    plan = _lib.LaunchPlan(roles=_lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD, B=8192,
+                           adagrad=_lib.AdagradRole(multi_only=1, B=4096))
+    assert lib.tt_launch(C.byref(plan), None) == 1001
+    assert b"adagrad.B" in lib.tt_last_error_string()
     assert lib.tt_launch(None, None) == 1001
 
 
@@ -111,3 +115,27 @@ def test_product_path_has_no_cpu_fallback():
         ops.complete_cumsum(torch.zeros(4, dtype=torch.int32))
     src = "\n".join(p.read_text() for p in (ROOT / "two_tower_recommender_model_amd").rglob("*.py"))
     assert "import oracle" not in src and "from oracle" not in src
+
+
+def test_tower_shape_flags_validated(lib):
+    """tt_tower_shape_t.flags (ABI 2; `_pad` in ABI 1): unknown bits are TT_EINVAL, and a
+    TT_TOWER_GENERAL_T1 shape is refused by every T1 entry point except the indexed multi-feature
+    one (its strips are tile-major; the row-owned T1 and tower_l2_kernel write row-major ones)."""
+    import ctypes as C
+
+    from two_tower_recommender_model_amd import _lib
+
+    def shape(flags):
+        return _lib.TowerShape(L=2, width=(C.c_int32 * 4)(128, 64, 0, 0), in_dim=(C.c_int32 * 2)(128, 128),
+                               in_col=(C.c_int32 * 2)(0, 128), flags=flags)
+
+    B = 8192
+    assert lib.tt_tower_workspace_bytes(C.byref(shape(0)), B) > 0
+    assert lib.tt_tower_workspace_bytes(C.byref(shape(_lib.TT_TOWER_GENERAL_T1)), B) > 0
+    assert lib.tt_tower_workspace_bytes(C.byref(shape(4)), B) == 0
+    assert lib.tt_tower_num_params(C.byref(shape(0x100))) == -1
+    sh = shape(_lib.TT_TOWER_GENERAL_T1)
+    ws = lib.tt_tower_workspace_bytes(C.byref(sh), B)
+    fake = 1 << 20  # never dereferenced: the call must return before any launch
+    rc = lib.tt_tower_fwd_bwd(C.byref(sh), B, fake, 256, fake, fake, fake, _lib.TT_I32, 1.0, fake, fake, ws, None)
+    assert rc == 1001 and b"GENERAL_T1" in lib.tt_last_error_string()

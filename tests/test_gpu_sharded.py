@@ -433,29 +433,18 @@ def test_sharded_rccl_world1_graph_equals_eager(device):
     pipelined HIP graphs, at world size 1 with the collectives forced on: identical to eager
     synchronous steps over ThreadComm. Run in a child process (a process group and RCCL-in-graph
     state stay out of this test process)."""
-    import os
-    import subprocess
-    import sys
+    from child_util import run_child
 
-    here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, os.path.join(here, "rccl_graph_check.py")], capture_output=True, text=True,
-                       timeout=300, cwd=os.path.dirname(here))
-    assert r.returncode == 0 and "RCCL-GRAPH-OK" in r.stdout, (r.returncode, r.stdout[-1500:], r.stderr[:3000],
-                                                               r.stderr[-1500:])
+    run_child(["tests/rccl_graph_check.py"], "RCCL-GRAPH-OK", timeout=300)
 
 
 def test_sharded_pipeline_state_resets(device):
     """The pipelined state after a refused capture (the bench's eager fallback) and after a mid-run
     load_state_dict: both equal a clean eager run bit for bit (tests/sharded_pipeline_state_check.py,
     a child process over a one-rank RCCL group)."""
-    import os
-    import subprocess
-    import sys
+    from child_util import run_child
 
-    here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, os.path.join(here, "sharded_pipeline_state_check.py")], capture_output=True,
-                       text=True, timeout=300, cwd=os.path.dirname(here))
-    assert r.returncode == 0 and "PIPELINE-STATE-OK" in r.stdout, (r.returncode, r.stdout[-1500:], r.stderr[-3000:])
+    run_child(["tests/sharded_pipeline_state_check.py"], "PIPELINE-STATE-OK", timeout=300)
 
 
 def test_sharded_config3_w8_baseline_size(device):

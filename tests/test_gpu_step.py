@@ -53,11 +53,12 @@ def test_fused_step_matches_reference_golden(device, case, precision):
         st.cb[l].copy_(torch.from_numpy(g[f"init_two_tower.candidate_proj._mlp.{l}._linear.bias"]))
     st.capture()
     tol = TOL[precision]
-    # logit errors are measured against the largest logit of the run so far: the first Adam steps
-    # move every weight by ~lr whatever its gradient's size (lr g / sqrt(g^2)), so a bf16 gradient
-    # whose sign differs from the fp32 one moves that weight by ~2 lr, and where the run shrinks its
-    # logits (c1full: max|logit| 0.11 -> 0.017 -> 0.0013 over its 3 steps) the shift is large
-    # relative to the shrunken logits while staying ~0.5 % of the run's scale
+    # c1full only (bf16): logit errors are measured against the largest logit of the run so far. The
+    # first Adam steps move every weight by ~lr whatever its gradient's size (lr g / sqrt(g^2)), so a
+    # bf16 gradient whose sign differs from the fp32 one moves that weight by ~2 lr; this run shrinks
+    # its logits (max|logit| 0.11 -> 0.017 -> 0.0013 over its 3 steps), so the shift is large against
+    # the shrunken logits while staying ~0.5 % of the run's scale. Every other case: per step.
+    relaxed = precision == "bf16" and case == "c1full"
     lscale = 0.0
     for s in range(int(g["steps"])):
         cols = [torch.from_numpy(g[f"s{s}_user_id"]).to(device), torch.from_numpy(g[f"s{s}_product_id"]).to(device)]
@@ -69,7 +70,7 @@ def test_fused_step_matches_reference_golden(device, case, precision):
         np.testing.assert_allclose(st.pooled.cpu().numpy(), g[f"s{s}_pooled"], rtol=1e-6,
                                    atol=1e-7 if s == 0 or precision == "fp32" else tol["table"])
         lscale = max(lscale, float(np.abs(g[f"s{s}_logits"]).max()))
-        _logits_close(st.logits.cpu().numpy(), g[f"s{s}_logits"], tol["logit"], lscale)
+        _logits_close(st.logits.cpu().numpy(), g[f"s{s}_logits"], tol["logit"], lscale if relaxed else None)
         np.testing.assert_allclose(float(st.loss), float(g[f"s{s}_loss"]), rtol=tol["loss"])
         if precision == "fp32":
             np.testing.assert_allclose(st.gpooled.cpu().numpy(), g[f"s{s}_pooled_grad"], rtol=1e-3, atol=1e-7)
@@ -78,13 +79,14 @@ def test_fused_step_matches_reference_golden(device, case, precision):
     else:
         # bf16 operands can flip a ReLU mask where a pre-activation is within bf16 error of 0;
         # each flip moves that unit's whole gradient. Require 99% of elements within tolerance
-        # and every element within 5x it, or within 4 lr: the first row-wise Adagrad / Adam steps
-        # are normalised (lr g / rms(g)), so an element whose gradient a flip turns around moves
-        # by up to ~2 lr |g_i| / rms(g) (c1full, D = 16: 0.032 = 3.2 lr at one of 160k elements)
+        # and every element within 5x it. c1full only: within 4 lr — the first row-wise Adagrad /
+        # Adam steps are normalised (lr g / rms(g)), so an element whose gradient a flip turns
+        # around moves by up to ~2 lr |g_i| / rms(g) (D = 16: 0.032 = 3.2 lr at one of 160k elements)
+        cap = (lambda atol: max(5 * atol, 4 * lr)) if relaxed else (lambda atol: 5 * atol)
+
         def check(got, want, atol):
             err = np.abs(got - want)
-            assert np.mean(err <= atol) >= 0.99 and err.max() <= max(5 * atol, 4 * lr), \
-                (np.mean(err <= atol), err.max())
+            assert np.mean(err <= atol) >= 0.99 and err.max() <= cap(atol), (np.mean(err <= atol), err.max())
     check(st.tables.table_view(0).cpu().numpy(), g["final_t_user_id"], tol["table"])
     check(st.tables.table_view(1).cpu().numpy(), g["final_t_product_id"], tol["table"])
     np.testing.assert_allclose(st.tables.state_view(0).cpu().numpy(), g["final_state_t_user_id"],

@@ -41,8 +41,9 @@ CFLAGS = [
     f"-I{CSRC}",
     "-Wall",
     "-Wno-unused-function",
-    *os.environ.get("TT_EXTRA_CFLAGS", "").split(),  # experiments only (e.g. -DDD_HOT_STAMPS=1)
 ]
+# experiment-only extra flags (e.g. -DDD_HOT_STAMPS=1); applied to the --experiments build only
+EXTRA_EXP = os.environ.get("TT_EXTRA_CFLAGS", "").split()
 
 
 def _stale(target: Path, deps) -> bool:
@@ -61,7 +62,12 @@ def _compile(src: Path, obj: Path, extra=()) -> None:
 
 def build(force: bool = False, verbose: bool = False, experiments: bool = False) -> Path:
     bdir, lib_path = (BUILD_EXP, LIB_EXP) if experiments else (BUILD, LIB)
-    extra = ["-DTT_EXPERIMENTS=1"] if experiments else []
+    if EXTRA_EXP and not experiments:
+        raise RuntimeError("TT_EXTRA_CFLAGS is for the experiment build only: add --experiments "
+                           "(the release lib/ is always built from the tree as committed)")
+    extra = ["-DTT_EXPERIMENTS=1", *EXTRA_EXP] if experiments else []
+    if experiments and EXTRA_EXP:
+        force = True  # objects do not record their flags: rebuild when extra flags are given
     bdir.mkdir(parents=True, exist_ok=True)
     lib_path.parent.mkdir(parents=True, exist_ok=True)
     objs = []

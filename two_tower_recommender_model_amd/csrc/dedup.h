@@ -246,7 +246,12 @@ constexpr int DD_HOT_PT = 16;                // lookups per thread per scan pass
 constexpr int DD_HOT_CH = 256 * DD_HOT_PT;  // lookups scanned per pass of a hot workgroup (LDS list)
 constexpr int DD_HOT_TEAM = 8;              // at most this many workgroups share one hot row
 #ifndef DD_HOT_STAMPS
-#define DD_HOT_STAMPS 0  // EXPERIMENT (scripts/hot_stamps.py; build with TT_EXTRA_CFLAGS=-DDD_HOT_STAMPS=1)
+// EXPERIMENT (scripts/hot_stamps.py): TT_EXTRA_CFLAGS=-DDD_HOT_STAMPS=1 python -m
+// two_tower_recommender_model_amd.build --experiments, run with TT_EXPERIMENT_LIB=1
+#define DD_HOT_STAMPS 0
+#endif
+#if DD_HOT_STAMPS && !TT_EXPERIMENTS
+#error "DD_HOT_STAMPS needs the experiment build (DD_STAMP records nothing without TT_EXPERIMENTS): build --experiments"
 #endif
 // LDS of the hot role (list + wave totals + group partials), provided by the launching kernel so a
 // combined launch can overlay it on its other roles' LDS

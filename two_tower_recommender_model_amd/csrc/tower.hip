@@ -2614,6 +2614,7 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   if (!s) return fail(TT_EINVAL, "tower: null shape");
   if (s->L < 1 || s->L > MAXL) return fail(TT_EINVAL, "tower: 1..4 layers supported");
   if (B < 8 || B % 8) return fail(TT_EINVAL, "tower: B must be a positive multiple of 8");
+  if (s->flags & ~TT_TOWER_GENERAL_T1) return fail(TT_EINVAL, "tower: unknown shape flags");
   for (int l = 0; l < s->L; ++l)
     if (s->width[l] < 16 || s->width[l] > MAXW || s->width[l] % 32)
       return fail(TT_EINVAL, "tower: layer widths must be multiples of 32 in [32, 128]");
@@ -2815,6 +2816,11 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   const bool two = shape->L == 2 && i0 <= 128 && i1 <= 128;
   if ((a.gcol[0] || a.gpos[0]) && !two)
     return fail(TT_EINVAL, "tower: the fused gather needs 2 layers and inputs <= 128 wide");
+  // TT_TOWER_GENERAL_T1 shapes keep tile-major operand strips for T2 (a.rm = L.rows is false for
+  // them): only the general indexed kernel writes that layout for every shape, so every other T1
+  // entry point refuses the flag rather than hand T2 strips in a layout it does not read
+  if ((shape->flags & TT_TOWER_GENERAL_T1) && !a.ipos)
+    return fail(TT_EINVAL, "tower: TT_TOWER_GENERAL_T1 shapes run T1 through tt_tower_fwd_bwd_indexed_multi only");
   if (a.ipos) {  // several features per tower: the general kernel (any width, chunks of 128 columns)
     tower_fwd_bwd_kernel<<<dim3(L.nwg), dim3(256), 0, as_stream(stream)>>>(a);
     return check_launch("tower_fwd_bwd_indexed_multi");
@@ -3639,6 +3645,9 @@ int tt_launch(const tt_launch_plan_t* p, void* stream) {
   switch (p->roles) {
     case TT_ROLE_WGRAD | TT_ROLE_INSERT | TT_ROLE_ADAGRAD:
       if ((rc = need_multi(1))) return rc;
+      // the ring tail's lookups per feature are the plan's B (the tower batch): a different
+      // adagrad.B is a caller error, not something to ignore
+      if (g.B && g.B != B) return fail(TT_EINVAL, "launch: this plan's ADAGRAD role uses the plan's B (adagrad.B = 0 or B)");
       if ((in.dedup_ws_bytes && in.dedup_ws_bytes != g.dedup_ws_bytes) ||
           (in.dedup_max_lookups && in.dedup_max_lookups != g.dedup_max_lookups))
         return fail(TT_EINVAL, "launch: the ring's two dedup workspaces have one size (the ADAGRAD role's)");

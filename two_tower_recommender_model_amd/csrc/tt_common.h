@@ -8,7 +8,9 @@
 #include "tt_mi355x.h"
 
 // Experiment hooks (environment switches, s_memrealtime phase stamps, T1 debug bits used by
-// scripts/*_stamps.py): compiled out of release builds; build with TT_EXTRA_CFLAGS=-DTT_EXPERIMENTS=1
+// scripts/*_stamps.py): compiled out of release builds. The experiment library is built by
+// `python -m two_tower_recommender_model_amd.build --experiments` into lib_exp/ (never over the
+// release lib/) and loaded with TT_EXPERIMENT_LIB=1
 #ifndef TT_EXPERIMENTS
 #define TT_EXPERIMENTS 0
 #endif
