@@ -87,6 +87,12 @@ def parse():
     ap.add_argument("--overlap", action="store_true",
                     help="sharded step: T2 on a parallel graph branch beside exchange A (default: inside launch U, "
                          "one stream; the branch measured slower at world 1, DESIGN.md section 6)")
+    ap.add_argument("--path", default="fused", choices=["fused", "dropin"],
+                    help="dropin: the reference's own loop (DistributedModelParallel + TrainPipelineSparseDist."
+                         "progress + KeyedOptimizerWrapper(Adam) + RowWiseAdagrad in backward, 03_model_training.py:"
+                         "612-625, :770-829) on the torchrec shim, batches already device KJTs (the device KJT "
+                         "builder in place of the host transform); progress() dispatches to the fused ring "
+                         "(dropin.py). Also times the same loop with the dispatch off (the generic per-op path)")
     ap.add_argument("--plan", default="auto", choices=["auto", "tw", "rw"],
                     help="N > 1 sharding plan of the two tables: tw = table-wise (users on rank 0, items on rank "
                          "1), rw = row-wise over all ranks; auto = tw at N = 2 (the same per-rank load as rw), rw "
@@ -686,6 +692,87 @@ def run_single(args):
     return value, ms, loss, roofline, cpu, steps_run
 
 
+def run_dropin(args):
+    """The reference's loop through the torchrec shim: main()'s wiring (EBC on meta, TwoTower,
+    TwoTowerTrainTask, in-backward RowWiseAdagrad, DistributedModelParallel, KeyedOptimizerWrapper(Adam),
+    TrainPipelineSparseDist; 03_model_training.py:770-829) and train()'s ``pipeline.progress`` loop
+    (:612-625) over resident device KJT batches built by the device KJT builder (tt_kjt_build_mod_dropzero,
+    the reference's transform_to_torchrec_batch semantics). progress() dispatches to the fused ring
+    (dropin.py); K timed progress calls. Then the same model with the dispatch off (a fresh pipeline,
+    TT_DROPIN_FUSED=0: the generic per-op path on the same storage) for a few steps."""
+    import itertools
+
+    import two_tower_recommender_model_amd as tt
+    from two_tower_recommender_model_amd import ops
+
+    tt.install_torchrec_alias()
+    from torch.distributed.optim import _apply_optimizer_in_backward
+    from torchrec.datasets.utils import Batch
+    from torchrec.distributed import TrainPipelineSparseDist
+    from torchrec.distributed.model_parallel import DistributedModelParallel
+    from torchrec.modules.embedding_configs import EmbeddingBagConfig
+    from torchrec.modules.embedding_modules import EmbeddingBagCollection
+    from torchrec.optim.keyed import KeyedOptimizerWrapper
+    from torchrec.optim.rowwise_adagrad import RowWiseAdagrad
+    from torchrec.sparse.jagged_tensor import KeyedJaggedTensor
+
+    from two_tower_recommender_model_amd.task import TwoTower, TwoTowerTrainTask
+
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    cat_cols = ["user_id", "product_id"]
+    cfgs = [EmbeddingBagConfig(name=f"t_{f}", embedding_dim=D, num_embeddings=n, feature_names=[f])
+            for f, n in zip(cat_cols, (num_users, num_items))]
+    ebc = EmbeddingBagCollection(tables=cfgs, device=torch.device("meta"))
+    task = TwoTowerTrainTask(TwoTower(embedding_bag_collection=ebc, layer_sizes=layers, device=dev))
+    _apply_optimizer_in_backward(RowWiseAdagrad, task.two_tower.ebc.parameters(), {"lr": 0.01})
+    model = DistributedModelParallel(module=task, device=dev)
+    optimizer = KeyedOptimizerWrapper(dict(model.named_parameters()), lambda ps: torch.optim.Adam(ps, lr=0.01))
+    nb = max(2, args.batches)
+    batches = []
+    for cols, lab in synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1):
+        values, lengths, offsets, lpk = ops.kjt_build_mod_dropzero(cols, [num_users, num_items])
+        n = int(lpk.sum())
+        kjt = KeyedJaggedTensor(keys=cat_cols, values=values[:n], lengths=lengths, offsets=offsets,
+                                length_per_key=lpk.tolist())
+        batches.append(Batch(dense_features=torch.zeros(1, device=dev), sparse_features=kjt, labels=lab))
+    torch.cuda.synchronize()
+
+    def timed(pipeline, warmup, steps):
+        it = itertools.cycle(batches)
+        for _ in range(warmup):
+            pipeline.progress(it)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss, _, _ = pipeline.progress(it)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, float(loss)
+
+    pipeline = TrainPipelineSparseDist(model, optimizer, dev)
+    pipeline._model.train()
+    dt, loss = timed(pipeline, args.warmup, args.steps)
+    fd = pipeline._fused
+    info = {"dispatch": pipeline._fused_reason, "fused_steps": fd.steps_fused if fd else 0,
+            "generic_steps": fd.steps_generic if fd else args.warmup + args.steps,
+            "loop": "DistributedModelParallel + TrainPipelineSparseDist.progress + KeyedOptimizerWrapper(Adam) + "
+                    "RowWiseAdagrad in backward (03_model_training.py:612-625, :770-829); resident device KJTs"}
+    # the same loop with the dispatch off: the generic per-op path (pooled fwd, per-layer GEMMs, dot +
+    # BCE, autograd, dedup + Adagrad kernels, torch Adam) on the same storage
+    os.environ["TT_DROPIN_FUSED"] = "0"
+    try:
+        gp = TrainPipelineSparseDist(model, optimizer, dev)
+        gsteps = min(args.steps, 20)
+        gdt, _ = timed(gp, 3, gsteps)
+    finally:
+        os.environ.pop("TT_DROPIN_FUSED", None)
+    info["generic_path"] = {"ms_per_step": round(gdt / gsteps * 1e3, 4), "pairs/s": round(gsteps * B / gdt, 1),
+                            "steps": gsteps}
+    return args.steps * B / dt, dt / args.steps * 1e3, loss, args.steps, info
+
+
 def run_host_fed(args):
     """The fused step fed from HOST batches (host_pipeline.HostFedPipeline): numpy columns as the
     reference's loader yields them -> pinned staging -> async H2D on a copy stream -> k-step graph
@@ -824,6 +911,11 @@ def main():
             raise SystemExit(f"{args.workload}: the multi-hot workload runs at N = 1 (unsharded tables)")
         value, ms, loss, roofline, cpu, steps_run = run_multihot(args)
         config["parallelism"] = "single-gpu hipgraph, KJT input"
+    elif world == 1 and args.path == "dropin":
+        value, ms, loss, steps_run, di = run_dropin(args)
+        roofline, cpu = None, None
+        config["dropin"] = di
+        config["parallelism"] = "single-gpu: the reference's DMP + TrainPipelineSparseDist loop, dispatched to the fused ring"
     elif world == 1 and args.host_fed:
         value, ms, loss, steps_run, hf = run_host_fed(args)
         roofline, cpu = None, None

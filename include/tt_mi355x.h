@@ -114,6 +114,17 @@ int tt_kjt_build_mod_dropzero(int F, int64_t B, const void* const* cols, int id_
                               int64_t* length_per_key_out, void* workspace, size_t ws_bytes,
                               void* stream);
 
+/* Single-hot KJT (every bag 0 or 1 ids, e.g. the reference's transform_to_torchrec_batch output,
+ * 03_model_training.py:353-380) -> the F id columns the fused single-hot kernels take (the inverse
+ * of tt_kjt_build_mod_dropzero on its output): cols_out[f][b] = 0 for an empty bag, else its value
+ * v, or num_embeddings[f] for v == 0 (row 0 through the kernels' id mod N). offsets [F*B+1] int32;
+ * cols_out is a HOST array of F device pointers of dtype id_dtype (capacity B each). A bag of more
+ * than one id sets bit 0 of *err, a value outside [0, N) bit 1 (sticky: the caller zeroes it and
+ * checks it when it wants; such bags get column entry 0). Replaces nothing in TorchRec: the glue
+ * between TrainPipelineSparseDist's KJT batches and the fused step (dropin.py). */
+int tt_kjt_single_hot_cols(int F, int64_t B, const void* values, int id_dtype, const int32_t* offsets,
+                           const int64_t* num_embeddings, void* const* cols_out, int32_t* err, void* stream);
+
 size_t tt_complete_cumsum_workspace_bytes(int64_t n);
 /* offsets[0] = 0, offsets[i+1] = sum(lengths[0..i]); n may be 0. */
 int tt_complete_cumsum(const int32_t* lengths, int64_t n, int32_t* offsets, void* workspace,

@@ -59,6 +59,27 @@ def child_main(main) -> None:
     sys.exit(rc)
 
 
+def seed_all(default: int) -> int:
+    """Seed torch's global generators (model init: table uniform_, nn.Linear) from TT_TEST_SEED or
+    `default`, so a child's run is reproducible; returns the seed (printed by the child)."""
+    import torch
+
+    seed = int(os.environ.get("TT_TEST_SEED", default))
+    torch.manual_seed(seed)
+    print(f"[child seed] {seed}", flush=True)
+    return seed
+
+
+def margin(got, want, rtol: float, atol: float) -> float:
+    """max |got - want| / (atol + rtol |want|): <= 1 is what np.testing.assert_allclose accepts."""
+    import numpy as np
+
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    if got.size == 0:
+        return 0.0
+    return float(np.max(np.abs(got - want) / (atol + rtol * np.abs(want))))
+
+
 def parent_mem() -> str:
     return "parent: " + _mem_line()
 

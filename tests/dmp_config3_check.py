@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
-from child_util import stage  # noqa: E402
+from child_util import margin, seed_all, stage  # noqa: E402
 
 D, B, LR, LAYERS, STEPS = 128, 8192, 0.05, [128, 64], 3
 QUERY = ["user_id"] + [f"u_f{k}" for k in range(1, 8)]
@@ -33,6 +33,7 @@ ROWS.update({f: 1_000_000 for f in QUERY[1:] + CAND[1:]})
 def main():
     device = torch.device("cuda:0")
     torch.cuda.set_device(device)
+    seed_all(0)
     stage("init_process_group")
     dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=device)
     import two_tower_recommender_model_amd as tt
@@ -123,24 +124,30 @@ def main():
 
     it = batches(host[:STEPS])
     pipeline._model.train()
+    # margins: max error / allowed error per check (<= 1 passes); printed for every run so the
+    # distance from the tolerance is on record, then asserted
+    mg = {"loss": 0.0, "logits": 0.0, "rows": 0.0, "state": 0.0}
     for s in range(STEPS):
         stage(f"step {s}")
         loss, logits, _ = pipeline.progress(it)
         v, l, lab = host[s]
         offs = torch.from_numpy(ref.complete_cumsum(l.numpy()))
         want_loss, want_logits, _, _ = ref.train_step(st, compact(v, l), offs, B, lab, LR, 0.01)
-        np.testing.assert_allclose(float(loss), float(want_loss), rtol=1e-4)
-        np.testing.assert_allclose(logits.cpu().numpy(), want_logits.numpy(), rtol=1e-4, atol=1e-5)
+        mg["loss"] = max(mg["loss"], margin(float(loss), float(want_loss), 1e-4, 0.0))
+        mg["logits"] = max(mg["logits"], margin(logits.cpu().numpy(), want_logits.numpy(), 1e-4, 1e-5))
     torch.cuda.synchronize()
     stage("final rows / states")
     for f, c in enumerate(cfgs):
         got = weights[f][rows[f].to(device)].cpu()
         # an Adagrad step moves an element by lr * G_d / rms(G): where G_d nearly cancels, the GPU
         # and CPU fp32 towers' summation orders (dX rtol ~1e-6) show up at ~3e-4 of the step
-        np.testing.assert_allclose(got.numpy(), st.tables[f].numpy(), rtol=1e-5, atol=1e-3 * LR)
+        mg["rows"] = max(mg["rows"], margin(got.numpy(), st.tables[f].numpy(), 1e-5, 1e-3 * LR))
         i = sebc._local_index[f]
         got_s = sebc._ts.state_view(i)[rows[f].to(device)].cpu()
-        np.testing.assert_allclose(got_s.numpy(), st.states[f].numpy(), rtol=1e-4, atol=1e-10)
+        mg["state"] = max(mg["state"], margin(got_s.numpy(), st.states[f].numpy(), 1e-4, 1e-10))
+    print("MARGINS " + " ".join(f"{k}={v:.3g}" for k, v in mg.items()), flush=True)
+    bad = {k: v for k, v in mg.items() if not v <= 1.0}
+    assert not bad, f"outside tolerance (max error / allowed): {bad}"
     del pipeline, model
     torch.cuda.synchronize()
     dist.destroy_process_group()

@@ -57,6 +57,9 @@ def gather_and_get_state_dict(model):
 def main():
     device = torch.device("cuda:0")
     torch.cuda.set_device(device)
+    from child_util import seed_all
+
+    seed_all(0)
     dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=device)
     import two_tower_recommender_model_amd as tt
     import two_tower_recommender_model_amd.torchrec.modules.mlp as mlp_mod

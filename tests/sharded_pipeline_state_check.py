@@ -30,6 +30,9 @@ def same(a, b):
 def main():
     device = torch.device("cuda:0")
     torch.cuda.set_device(device)
+    from child_util import seed_all
+
+    seed_all(0)
     graph_safe_nccl_env()
     dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=device)
     B, D, N = 1024, 128, [20_000, 30_000]

@@ -54,6 +54,7 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_fwd_bwd_gather_update, tt_tower_adam_pre_grads_sum
 // tt_tower_fwd_bwd_kjt, tt_tower_fwd_bwd_gather, tt_tower_fwd_bwd_indexed_multi_bf16
 // tt_launch (every multi-role fused launch, by plan)
-int tt_num_entry_points(void) { return 44; }
+// tt_kjt_single_hot_cols
+int tt_num_entry_points(void) { return 45; }
 
 }  // extern "C"

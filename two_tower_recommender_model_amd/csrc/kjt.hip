@@ -253,6 +253,61 @@ int tt_kjt_build_mod_dropzero(int F, int64_t B, const void* const* cols, int id_
   return check_launch("kjt_build_mod_dropzero");
 }
 
+// ---- single-hot KJT -> id columns (the drop-in pipeline's input to the fused step) -----------
+// For key f, bag b of a KJT whose bags hold at most one id: col_f[b] = 0 for an empty bag (the
+// fused kernels' "dropped id"), else the bag's value v, or N_f for v == 0 (py_mod(N_f, N_f) = row 0:
+// the fused kernels read row py_mod(id, N) for every non-zero id). A bag with more than one id or
+// a value outside [0, N_f) sets bit 0 / bit 1 of the sticky err word (TorchRec's EBC would index
+// out of range there); its column entry is 0.
+}  // extern "C"
+
+namespace tt {
+__global__ void __launch_bounds__(256) kjt_single_hot_cols_kernel(KjtCols c, int id_dtype, int F, int64_t B,
+                                                                  const void* __restrict__ values,
+                                                                  const int32_t* __restrict__ offsets,
+                                                                  int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)F * B) return;
+  const int f = (int)(i / B);
+  const int64_t b = i - (int64_t)f * B;
+  const int32_t o0 = offsets[i], o1 = offsets[i + 1];
+  const int64_t N = c.num_emb[f];
+  int64_t out = 0;
+  int bad = 0;
+  if (o1 - o0 == 1) {
+    const int64_t v = id_dtype == TT_I64 ? reinterpret_cast<const int64_t*>(values)[o0]
+                                         : (int64_t)reinterpret_cast<const int32_t*>(values)[o0];
+    if (v < 0 || v >= N) bad = 2;
+    else out = v == 0 ? N : v;
+  } else if (o1 - o0 != 0) {
+    bad = 1;
+  }
+  if (bad) atomicOr(err, bad);
+  if (id_dtype == TT_I64) reinterpret_cast<int64_t*>(const_cast<void*>(c.col[f]))[b] = out;
+  else reinterpret_cast<int32_t*>(const_cast<void*>(c.col[f]))[b] = (int32_t)out;
+}
+}  // namespace tt
+
+extern "C" {
+int tt_kjt_single_hot_cols(int F, int64_t B, const void* values, int id_dtype, const int32_t* offsets,
+                           const int64_t* num_embeddings, void* const* cols_out, int32_t* err, void* stream) {
+  if (F < 1 || F > TT_MAX_FEATURES) return fail(TT_EINVAL, "kjt_single_hot_cols: F out of range [1,64]");
+  if (B < 1 || (int64_t)F * B > INT32_MAX) return fail(TT_EINVAL, "kjt_single_hot_cols: bad B");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "kjt_single_hot_cols: ids must be int32/int64");
+  if (!offsets || !num_embeddings || !cols_out || !err) return fail(TT_EINVAL, "kjt_single_hot_cols: null pointer");
+  KjtCols c{};
+  for (int f = 0; f < F; ++f) {
+    if (num_embeddings[f] < 1 || (id_dtype == TT_I32 && num_embeddings[f] > INT32_MAX))
+      return fail(TT_EINVAL, "kjt_single_hot_cols: num_embeddings out of range for the id dtype");
+    if (!cols_out[f]) return fail(TT_EINVAL, "kjt_single_hot_cols: null column");
+    c.col[f] = cols_out[f];
+    c.num_emb[f] = num_embeddings[f];
+  }
+  const int64_t n = (int64_t)F * B;
+  kjt_single_hot_cols_kernel<<<dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream)>>>(
+      c, id_dtype, F, B, values, offsets, err);
+  return check_launch("kjt_single_hot_cols");
+}
 }  // extern "C"
 
 // ---- permute_2D_sparse_data -------------------------------------------------------------------

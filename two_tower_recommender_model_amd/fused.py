@@ -41,7 +41,7 @@ class FusedTwoTowerStep:
                  overlap_prepare: bool = True, precision: str = "bf16", fused_towers: bool = True,
                  kjt_mode: str = "cols", overlap_towers: bool = True, fuse_gather: bool = True,
                  materialize_pooled: bool = False, dedup: str = "single", combined_bwd: bool = True,
-                 max_lookups: Optional[int] = None):
+                 max_lookups: Optional[int] = None, tables: Optional[ops.TableSet] = None):
         """One table per feature (feature f -> table f), features ordered as the KJT keys.
         precision: tower GEMM operands "bf16" (production) or "fp32" (parity mode).
         overlap_prepare / overlap_towers: run the dedup prepare / the towers' weight-gradient and
@@ -59,7 +59,10 @@ class FusedTwoTowerStep:
         max_lookups: multi-hot KJT input (config 5 bags): the step takes a KeyedJaggedTensor's
         values / offsets through ``load_kjt`` (ids already in range, as TorchRec's EBC takes them) with
         up to ``max_lookups`` ids per step, and runs the KJT-form kernels (tt_pooled_fwd, tiled
-        tt_bwd_prepare, tt_bwd_rowwise_adagrad) around the fused towers."""
+        tt_bwd_prepare, tt_bwd_rowwise_adagrad) around the fused towers.
+        tables: adopt an existing TableSet (table f = feature f's; e.g. an EmbeddingBagCollection's or
+        a one-rank ShardedEmbeddingBagCollection's storage): the step trains those weights and that
+        row-wise Adagrad state in place and initialises neither (dropin.py)."""
         self.device = torch.device(device)
         self.precision = precision
         if kjt_mode not in ("cols", "kjt"):
@@ -79,15 +82,23 @@ class FusedTwoTowerStep:
         self.lr_emb, self.lr_dense, self.eps = float(lr_emb), float(lr_dense), float(eps)
         self.id_dtype = id_dtype
         dev = self.device
-        # tables (one flat HBM buffer) + row-wise state
-        self.tables = ops.TableSet(self.num_embeddings, self.dims, list(range(self.F)), dev)
-        gen = torch.Generator(device=dev).manual_seed(seed)
-        self.tables.init_uniform_(gen)
         self.out_dim = sum(self.dims)
         col = [0]
         for d in self.dims:
             col.append(col[-1] + d)
         self.col = col
+        # tables (one flat HBM buffer) + row-wise state
+        self._adopted = tables is not None
+        if self._adopted:
+            if tables.T < self.F or [tables.rows[f] for f in range(self.F)] != self.num_embeddings or \
+                    [tables.dims[f] for f in range(self.F)] != self.dims or tables.device != dev:
+                raise _lib.TTError("fused step: the adopted TableSet's tables must be feature f -> table f with "
+                                   "the step's rows, dims and device")
+            self.tables = tables.remap(list(range(self.F)), col[:-1])
+        else:
+            self.tables = ops.TableSet(self.num_embeddings, self.dims, list(range(self.F)), dev)
+            gen = torch.Generator(device=dev).manual_seed(seed)
+            self.tables.init_uniform_(gen)
         # the reference's towers take the concatenation of their features; with the KJT key order
         # (query features, then candidate features) each tower input is one contiguous column slice
         self.q_lo, self.q_hi = col[min(self.qf)], col[max(self.qf) + 1]
@@ -201,7 +212,8 @@ class FusedTwoTowerStep:
 
     # ------------------------------------------------------------------------------------------
     def reset_optimizer_state(self) -> None:
-        self.tables.state.zero_()
+        if not self._adopted:  # an adopted TableSet keeps its owner's row-wise Adagrad state
+            self.tables.state.zero_()
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
         self.adam_state.zero_()

@@ -75,6 +75,31 @@ def kjt_build_mod_dropzero(cols: Sequence[torch.Tensor], num_embeddings: Sequenc
     return values_out, lengths_out, offsets_out, length_per_key_out
 
 
+def kjt_single_hot_cols(values: torch.Tensor, offsets: torch.Tensor, B: int, num_embeddings: Sequence[int],
+                        cols_out: Sequence[torch.Tensor], err: torch.Tensor) -> None:
+    """A single-hot KJT (bags of 0 or 1 ids, key-major, complete int32 offsets [F*B+1]) -> the fused
+    step's id columns (tt_kjt_single_hot_cols): 0 = empty bag, v = row v, N = row 0. ``err`` (int32 [1],
+    sticky) gets bit 0 for a bag of more than one id, bit 1 for a value outside [0, N)."""
+    F = len(cols_out)
+    dt = cols_out[0].dtype
+    _dev(offsets, err, *cols_out)
+    if offsets.dtype != torch.int32 or offsets.numel() != F * B + 1:
+        raise _lib.TTError("kjt_single_hot_cols: offsets must be int32 [F*B + 1]")
+    for c in cols_out:
+        if c.dtype != dt or c.numel() < B or not c.is_contiguous():
+            raise _lib.TTError("kjt_single_hot_cols: columns must be contiguous, one dtype, >= B ids")
+    if values.numel():
+        _dev(values)
+        if values.dtype != dt:
+            raise _lib.TTError("kjt_single_hot_cols: values must have the columns' id dtype")
+        vp = ptr(values)
+    else:  # every bag empty (the reference's all-zero batch gives an empty float tensor): never read
+        vp = ptr(cols_out[0])
+    ne = (C.c_int64 * F)(*[int(n) for n in num_embeddings])
+    check(_lib_().tt_kjt_single_hot_cols(F, B, vp, id_dtype_code(dt), ptr(offsets), ne, ptr_array(list(cols_out)),
+                                         ptr(err), stream_handle(offsets.device)), "kjt_single_hot_cols")
+
+
 def complete_cumsum(lengths: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _dev(lengths)
     if lengths.dtype != torch.int32:

@@ -14,6 +14,11 @@ Three stages over three streams, as torchrec's pipeline:
 Batch i's kernels are queued before batch i+1's input_dist starts, so the host-side waits of that
 input_dist (its split sizes) overlap batch i's device work. input_dist reads only ids, so running it
 before batch i's table update is exact. Without sharded modules the pipeline has two stages.
+
+Training ``progress`` on the reference's two-tower model (one rank, single-hot KJTs, bf16 towers)
+is dispatched to the fused production ring (``two_tower_recommender_model_amd.dropin``): the same
+step, in three fused launches per batch replayed as HIP graphs, on the model's own storage.
+``_fused_reason`` says why a pipeline did not dispatch; ``TT_DROPIN_FUSED=0`` turns it off.
 """
 from __future__ import annotations
 
@@ -41,6 +46,8 @@ class TrainPipelineBase:
         self._cur: Optional[_Staged] = None    # batch i (input_dist staged)
         self._next: Optional[_Staged] = None   # batch i+1 (copy issued)
         self._connected = False
+        self._fused = None          # dropin.FusedDropin once built (False: not applicable)
+        self._fused_reason = "not tried"
 
     def _sharded(self) -> List[Any]:
         return []
@@ -69,6 +76,16 @@ class TrainPipelineBase:
                 st.batch.record_stream(cur)
 
     def progress(self, dataloader_iter: Iterator) -> Any:
+        if self._model.training and self._cur is None:
+            if self._fused is None:
+                from ...dropin import FusedDropin
+
+                fd, self._fused_reason = FusedDropin.build(self)
+                self._fused = fd if fd is not None else False
+            if self._fused:
+                return self._fused.progress(dataloader_iter)
+        elif self._fused and self._fused.pending():
+            self._fused.drain_to(self)  # eval mid-chunk: the staged batches go the generic way
         if self._cur is None:
             # (re)fill: batch i copied and its input_dist staged, batch i+1's copy issued
             self._cur = self._fetch(dataloader_iter)
