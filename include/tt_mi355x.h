@@ -120,10 +120,12 @@ int tt_kjt_build_mod_dropzero(int F, int64_t B, const void* const* cols, int id_
  * v, or num_embeddings[f] for v == 0 (row 0 through the kernels' id mod N). offsets [F*B+1] int32;
  * cols_out is a HOST array of F device pointers of dtype id_dtype (capacity B each). A bag of more
  * than one id sets bit 0 of *err, a value outside [0, N) bit 1 (sticky: the caller zeroes it and
- * checks it when it wants; such bags get column entry 0). Replaces nothing in TorchRec: the glue
- * between TrainPipelineSparseDist's KJT batches and the fused step (dropin.py). */
+ * checks it when it wants; such bags get column entry 0). labels_out (nullable): the batch's B
+ * labels (int32 / int64, label_dtype) copied as int32 in the same launch. Replaces nothing in
+ * TorchRec: the glue between TrainPipelineSparseDist's KJT batches and the fused step (dropin.py). */
 int tt_kjt_single_hot_cols(int F, int64_t B, const void* values, int id_dtype, const int32_t* offsets,
-                           const int64_t* num_embeddings, void* const* cols_out, int32_t* err, void* stream);
+                           const int64_t* num_embeddings, void* const* cols_out, int32_t* err, const void* labels,
+                           int label_dtype, int32_t* labels_out, void* stream);
 
 size_t tt_complete_cumsum_workspace_bytes(int64_t n);
 /* offsets[0] = 0, offsets[i+1] = sum(lengths[0..i]); n may be 0. */

@@ -143,7 +143,7 @@ SIGNATURES = {
         _int,
         [_int, _i64, _pvp, _int, _pi64, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
     ),
-    "tt_kjt_single_hot_cols": (_int, [_int, _i64, _vp, _int, _vp, _pi64, _pvp, _vp, _vp]),
+    "tt_kjt_single_hot_cols": (_int, [_int, _i64, _vp, _int, _vp, _pi64, _pvp, _vp, _vp, _int, _vp, _vp]),
     "tt_complete_cumsum_workspace_bytes": (_sz, [_i64]),
     "tt_complete_cumsum": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "tt_kjt_permute": (

@@ -265,9 +265,13 @@ namespace tt {
 __global__ void __launch_bounds__(256) kjt_single_hot_cols_kernel(KjtCols c, int id_dtype, int F, int64_t B,
                                                                   const void* __restrict__ values,
                                                                   const int32_t* __restrict__ offsets,
-                                                                  int32_t* __restrict__ err) {
+                                                                  int32_t* __restrict__ err, const void* labels,
+                                                                  int label_dtype, int32_t* __restrict__ labels_out) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)F * B) return;
+  if (labels_out && i < B)
+    labels_out[i] = label_dtype == TT_I64 ? (int32_t)reinterpret_cast<const int64_t*>(labels)[i]
+                                          : reinterpret_cast<const int32_t*>(labels)[i];
   const int f = (int)(i / B);
   const int64_t b = i - (int64_t)f * B;
   const int32_t o0 = offsets[i], o1 = offsets[i + 1];
@@ -290,7 +294,10 @@ __global__ void __launch_bounds__(256) kjt_single_hot_cols_kernel(KjtCols c, int
 
 extern "C" {
 int tt_kjt_single_hot_cols(int F, int64_t B, const void* values, int id_dtype, const int32_t* offsets,
-                           const int64_t* num_embeddings, void* const* cols_out, int32_t* err, void* stream) {
+                           const int64_t* num_embeddings, void* const* cols_out, int32_t* err, const void* labels,
+                           int label_dtype, int32_t* labels_out, void* stream) {
+  if (labels_out && (!labels || (label_dtype != TT_I32 && label_dtype != TT_I64)))
+    return fail(TT_EINVAL, "kjt_single_hot_cols: labels must be int32/int64");
   if (F < 1 || F > TT_MAX_FEATURES) return fail(TT_EINVAL, "kjt_single_hot_cols: F out of range [1,64]");
   if (B < 1 || (int64_t)F * B > INT32_MAX) return fail(TT_EINVAL, "kjt_single_hot_cols: bad B");
   if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "kjt_single_hot_cols: ids must be int32/int64");
@@ -305,7 +312,7 @@ int tt_kjt_single_hot_cols(int F, int64_t B, const void* values, int id_dtype, c
   }
   const int64_t n = (int64_t)F * B;
   kjt_single_hot_cols_kernel<<<dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream)>>>(
-      c, id_dtype, F, B, values, offsets, err);
+      c, id_dtype, F, B, values, offsets, err, labels, label_dtype, labels_out);
   return check_launch("kjt_single_hot_cols");
 }
 }  // extern "C"

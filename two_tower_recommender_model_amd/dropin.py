@@ -36,7 +36,7 @@ from typing import Any, Iterator, List, Optional, Tuple
 import torch
 from torch import nn
 
-from . import _lib, ops
+from . import _lib
 
 
 def _named(obj, cls_name: str) -> bool:
@@ -167,12 +167,15 @@ class FusedDropin:
         return cls(pipeline, task, ebc, ts, cfg, towers, adam, feats, dims,
                    fresh_outputs=os.environ.get("TT_DROPIN_FRESH_OUTPUTS", "0") == "1"), "fused"
 
-    def _adam_lr(self) -> float:
-        ids = {id(self.towers[0]._mlp[0]._linear.weight)}
+    def _adam_group(self) -> dict:
+        w = self.towers[0]._mlp[0]._linear.weight
         for g in self.adam.param_groups:
-            if any(id(p) in ids for p in g["params"]):
-                return float(g["lr"])
+            if any(p is w for p in g["params"]):
+                return g
         raise _lib.TTError("dropin: tower parameters left the optimizer")
+
+    def _adam_lr(self) -> float:
+        return float(self._adam_group()["lr"])
 
     def fusable(self, batch) -> bool:
         kjt = getattr(batch, "sparse_features", None)
@@ -189,7 +192,8 @@ class FusedDropin:
         if self.step is not None and v.numel() and v.dtype != self.step.id_dtype:
             return False
         lab = batch.labels
-        return lab.numel() == B and lab.device == self.device and kjt.device() == self.device
+        return (lab.numel() == B and lab.dtype in (torch.int32, torch.int64) and lab.is_contiguous()
+                and lab.device == self.device and kjt.device() == self.device)
 
     # ---- the fused step, adopting the model's storage --------------------------------------------
     def _make_step(self, B: int, id_dtype: torch.dtype) -> None:
@@ -240,6 +244,14 @@ class FusedDropin:
         self.slot_logits = [torch.zeros(B, dtype=torch.float32, device=dev) for _ in range(D)]
         self.slot_loss = [torch.zeros((), dtype=torch.float32, device=dev) for _ in range(D)]
         self.zero_cols = [torch.zeros(B, dtype=idt, device=dev) for _ in range(2)]
+        # the per-batch conversion's ctypes arguments, built once
+        import ctypes as C
+
+        self._lib = _lib.load()
+        self._ne = (C.c_int64 * 2)(*st.num_embeddings)
+        self._slot_ptrs = [_lib.ptr_array(c) for c in self.slot_cols]
+        self._idt = _lib.id_dtype_code(idt)
+        self._group = self._adam_group()
         self._capture()
 
     def _ring_step(self, slot: int, parity: int, next_cols) -> None:
@@ -293,9 +305,15 @@ class FusedDropin:
         offs = kjt.offsets()
         if offs.dtype != torch.int32:
             offs = offs.to(torch.int32)
-        ops.kjt_single_hot_cols(v, offs, self.step.B, self.step.num_embeddings, self.slot_cols[slot], self.err)
-        self.slot_labels[slot].copy_(batch.labels, non_blocking=True)
-        return _Item(batch, slot, k % 2, batch.labels)
+        lab = batch.labels
+        # ids -> slot columns and labels -> slot labels in one launch (shapes / dtypes checked by
+        # fusable(); an empty values tensor is never read)
+        _lib.check(self._lib.tt_kjt_single_hot_cols(
+            2, self.step.B, v.data_ptr() if v.numel() else self.slot_cols[slot][0].data_ptr(), self._idt,
+            offs.data_ptr(), self._ne, self._slot_ptrs[slot], self.err.data_ptr(), lab.data_ptr(),
+            _lib.TT_I64 if lab.dtype == torch.int64 else _lib.TT_I32, self.slot_labels[slot].data_ptr(),
+            torch.cuda.current_stream(self.device).cuda_stream), "kjt_single_hot_cols")
+        return _Item(batch, slot, k % 2, lab)
 
     def check_errors(self) -> None:
         """Raise if any converted batch had a multi-id bag or an id out of range (one sync)."""
@@ -352,9 +370,9 @@ class FusedDropin:
 
     def _fused(self, cur: _Item, nxt: Optional[_Item]) -> Any:
         st = self.step
-        lr = self._adam_lr()
+        lr = self._group["lr"]
         if lr != self.lr_captured:  # the plan carries Adam's lr: re-capture after a change
-            st.lr_dense = lr
+            st.lr_dense = float(lr)
             self._capture()
         if not cur.primed:
             st.ring_prime(self.slot_cols[cur.slot], cur.parity)

@@ -76,10 +76,12 @@ def kjt_build_mod_dropzero(cols: Sequence[torch.Tensor], num_embeddings: Sequenc
 
 
 def kjt_single_hot_cols(values: torch.Tensor, offsets: torch.Tensor, B: int, num_embeddings: Sequence[int],
-                        cols_out: Sequence[torch.Tensor], err: torch.Tensor) -> None:
+                        cols_out: Sequence[torch.Tensor], err: torch.Tensor, labels: Optional[torch.Tensor] = None,
+                        labels_out: Optional[torch.Tensor] = None) -> None:
     """A single-hot KJT (bags of 0 or 1 ids, key-major, complete int32 offsets [F*B+1]) -> the fused
     step's id columns (tt_kjt_single_hot_cols): 0 = empty bag, v = row v, N = row 0. ``err`` (int32 [1],
-    sticky) gets bit 0 for a bag of more than one id, bit 1 for a value outside [0, N)."""
+    sticky) gets bit 0 for a bag of more than one id, bit 1 for a value outside [0, N). With
+    ``labels_out`` the B labels (int32 / int64) are copied to it as int32 in the same launch."""
     F = len(cols_out)
     dt = cols_out[0].dtype
     _dev(offsets, err, *cols_out)
@@ -96,8 +98,16 @@ def kjt_single_hot_cols(values: torch.Tensor, offsets: torch.Tensor, B: int, num
     else:  # every bag empty (the reference's all-zero batch gives an empty float tensor): never read
         vp = ptr(cols_out[0])
     ne = (C.c_int64 * F)(*[int(n) for n in num_embeddings])
+    ldt = TT_I32
+    if labels_out is not None:
+        _dev(labels, labels_out)
+        if labels.dtype not in (torch.int32, torch.int64) or labels.numel() < B or not labels.is_contiguous() or \
+                labels_out.dtype != torch.int32 or labels_out.numel() < B:
+            raise _lib.TTError("kjt_single_hot_cols: labels int32 / int64 [B] -> labels_out int32 [B]")
+        ldt = id_dtype_code(labels.dtype)
     check(_lib_().tt_kjt_single_hot_cols(F, B, vp, id_dtype_code(dt), ptr(offsets), ne, ptr_array(list(cols_out)),
-                                         ptr(err), stream_handle(offsets.device)), "kjt_single_hot_cols")
+                                         ptr(err), ptr(labels) if labels_out is not None else None, ldt,
+                                         ptr(labels_out), stream_handle(offsets.device)), "kjt_single_hot_cols")
 
 
 def complete_cumsum(lengths: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
