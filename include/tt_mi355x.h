@@ -505,6 +505,34 @@ int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params,
                         float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
                         float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- multi-hot sharded step (config 5, sharded_kjt.py): fixed-size exchanges ------------------------
+ * TorchRec's KJTAllToAll / PooledEmbeddingsAllToAll / reduce-scatter (torchrec/distributed/embeddingbag.py,
+ * reached from 03_model_training.py:812-815) exchange variable split sizes the host reads every batch;
+ * here every exchange block has a fixed size, so the step is capturable. Requester -> owner block d
+ * (int32, blk_stride elements): [lengths [F][B] of the ids d owns | those ids (row in d's shard) in
+ * (feature, bag, position) order, capacity cap]. A row-wise feature's owner is id / block_sizes[f]
+ * (block_sizes[f] > 0), a table-wise one's owners[f]. flags[0] (sticky): some destination got more
+ * than cap ids; flags[1]: an id outside [0, num_embeddings[f]) (skipped). W <= 16. */
+size_t tt_kjt_route_workspace_bytes(int F, int64_t B, int W);
+int tt_kjt_route(int F, int64_t B, const void* values, int id_dtype, const int32_t* offsets,
+                 const int64_t* num_embeddings, const int64_t* block_sizes, const int32_t* owners, int W, int64_t cap,
+                 int64_t blk_stride, int32_t* send, int32_t* flags, void* workspace, size_t ws_bytes, void* stream);
+/* Owner side: the W received blocks -> one KJT whose keys are (source s, served feature k) (feats[k],
+ * ascending; Fr of them): lengths_out [W*Fr*B], offsets_out [W*Fr*B + 1] (complete cumsum), the ids
+ * compacted into values_out (capacity W*cap). */
+size_t tt_kjt_unpack_workspace_bytes(int W, int Fr, int64_t B);
+int tt_kjt_unpack(int W, int F, int64_t B, const int32_t* recv, int64_t blk_stride, int64_t cap, const int32_t* feats,
+                  int Fr, int32_t* lengths_out, int32_t* offsets_out, int32_t* values_out, void* workspace,
+                  size_t ws_bytes, void* stream);
+/* Requester side of the pooled exchange: owner d's block (blk_stride floats) holds rows of ld_blk floats, bag b
+ * of feature f at row b, column owner_col[d*F + f] (-1: d does not serve f). partials_sum: out[b][f*D ..] =
+ * the sum over d (ascending) of those rows (row-wise: TorchRec's reduce-scatter; table-wise: one term).
+ * grad_pack: the inverse copy of the bag gradients grad[b][f*D ..] into every serving owner's block. */
+int tt_pooled_partials_sum(int W, int F, int64_t B, int D, const float* recv, int64_t blk_stride, int64_t ld_blk,
+                           const int32_t* owner_col, float* out, int64_t ldo, void* stream);
+int tt_pooled_grad_pack(int W, int F, int64_t B, int D, const float* grad, int64_t ldg, const int32_t* owner_col,
+                        float* send, int64_t blk_stride, int64_t ld_blk, void* stream);
+
 /* ---- launch plans: the step's multi-role fused launches through ONE entry point ------------------
  * A fused launch runs several ROLES side by side in one grid (each role a range of workgroups): the
  * towers' weight gradients beside the embedding update, the next batch's dedup insert or route

@@ -145,6 +145,12 @@ SIGNATURES = {
     ),
     "tt_kjt_single_hot_cols": (_int, [_int, _i64, _vp, _int, _vp, _pi64, _pvp, _vp, _vp, _int, _vp, _vp]),
     "tt_complete_cumsum_workspace_bytes": (_sz, [_i64]),
+    "tt_kjt_route_workspace_bytes": (_sz, [_int, _i64, _int]),
+    "tt_kjt_route": (_int, [_int, _i64, _vp, _int, _vp, _pi64, _pi64, _vp, _int, _i64, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "tt_kjt_unpack_workspace_bytes": (_sz, [_int, _int, _i64]),
+    "tt_kjt_unpack": (_int, [_int, _int, _i64, _vp, _i64, _i64, _vp, _int, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "tt_pooled_partials_sum": (_int, [_int, _int, _i64, _int, _vp, _i64, _i64, _vp, _vp, _i64, _vp]),
+    "tt_pooled_grad_pack": (_int, [_int, _int, _i64, _int, _vp, _i64, _vp, _vp, _i64, _i64, _vp]),
     "tt_complete_cumsum": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "tt_kjt_permute": (
         _int,
@@ -268,6 +274,10 @@ SIGNATURES = {
 COMPUTE_ENTRY_POINTS = [
     "tt_kjt_build_mod_dropzero",
     "tt_kjt_single_hot_cols",
+    "tt_kjt_route",
+    "tt_kjt_unpack",
+    "tt_pooled_partials_sum",
+    "tt_pooled_grad_pack",
     "tt_complete_cumsum",
     "tt_kjt_permute",
     "tt_block_bucketize",

@@ -55,6 +55,7 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_tower_fwd_bwd_kjt, tt_tower_fwd_bwd_gather, tt_tower_fwd_bwd_indexed_multi_bf16
 // tt_launch (every multi-role fused launch, by plan)
 // tt_kjt_single_hot_cols
-int tt_num_entry_points(void) { return 45; }
+// tt_kjt_route, tt_kjt_unpack, tt_pooled_partials_sum, tt_pooled_grad_pack
+int tt_num_entry_points(void) { return 49; }
 
 }  // extern "C"
