@@ -529,6 +529,78 @@ def run_multihot(args):
     return value, ms, loss, roofline, cpu, args.steps
 
 
+def run_multi_kjt(args, world, rank, local_rank):
+    """Config 5 over W ranks (or one rank with --sharded): the capturable multi-hot sharded step
+    (sharded_kjt.FusedShardedKJTStep: users table-wise on the last rank, items row-wise over all
+    ranks; three fixed-size all-to-alls per step, ids in, pooled rows out, bag gradients back, over
+    RCCL), one HIP graph per resident batch (eager under TT_REHEARSE_GLOO). B = 16,384 bags per
+    feature and rank, bags of Uniform{1..39} ids. Capacity: the most ids any rank's resident batch
+    sends to one destination (all-reduced)."""
+    from two_tower_recommender_model_amd.sharded import TorchComm
+    from two_tower_recommender_model_amd.sharded_kjt import FusedShardedKJTStep, route_counts
+
+    num_users, num_items, D, B, layers = WORKLOADS[args.workload]
+    maxlen = MULTIHOT[args.workload]
+    N = [num_users, num_items]
+    sharding, owners = ["table_wise", "row_wise"], [world - 1, 0]
+    dev = torch.device("cuda", local_rank % torch.cuda.device_count())
+    comm = TorchComm(always_collective=True)
+    batches = synth_kjt_batches(num_users, num_items, B, maxlen, 4, dev, args.ids, seed=4 * 1000 + 1 + rank)
+    need = torch.zeros(1, dtype=torch.int64)
+    for v, o, _ in batches:
+        need = torch.maximum(need, route_counts(v, o, B, N, sharding, owners, world).max().reshape(1))
+    need = need.to(dev)
+    dist.all_reduce(need, op=dist.ReduceOp.MAX)
+    cap = -(-int(need) // 8) * 8
+    step = FusedShardedKJTStep(comm, N, D, layers, B, dev, cap=cap, sharding=sharding, tw_owners=owners,
+                               lr_emb=0.01, lr_dense=0.01, seed=0)
+    graphs = os.environ.get("TT_REHEARSE_GLOO") != "1"
+    if graphs:
+        step.capture_pool(batches)
+        run = step.run
+    else:
+        step.warmup()
+        state = {"i": 0}
+
+        def run(n):
+            step.run_eager(batches, n, state["i"])
+            state["i"] += n
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    step.check()
+    dist.barrier()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], device=dev)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt)
+    step.check()
+    loss = float(step.loss)
+    step.release_graphs()
+    # SURVEY 8(d) embedding-path bytes per rank and step over the whole step (lookups of this rank's
+    # batch, unique rows counted on it): nnz (8 id fwd + 8 id bwd + 4D row) + F B (4 + 8D) + U (8D + 8)
+    nnz = sum(v.numel() for v, _, _ in batches) // len(batches)
+    uniq = 0
+    for v, o, _ in batches:
+        nb = int(o[B])
+        uniq += int(torch.unique(torch.cat([v[:nb], v[nb:] + (1 << 40)])).numel())
+    uniq //= len(batches)
+    emb_bytes = nnz * (16 + 4 * D) + 2 * B * (4 + 8 * D) + uniq * (8 * D + 8)
+    ach = emb_bytes / (dt / args.steps) / 1e9
+    roofline = {"bound": "hbm", "kernel": "whole sharded step (per rank)", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_step": emb_bytes, "lookups": nnz, "unique_rows": uniq,
+                "timing": "SURVEY 8(d) bytes per rank over the max-over-ranks step time (collectives included)"}
+    info = {"plan": f"users table-wise (rank {world - 1}) + items row-wise", "ids": args.ids, "capacity": cap,
+            "exchange_bytes_per_rank": {"A_ids": 4 * step.sendA.numel(), "B_pooled": 4 * step.sendB.numel(),
+                                        "C_grads": 4 * step.sendC.numel()},
+            "collectives_per_step": 3, "mode": "hipgraph" if graphs else "eager"}
+    return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
+
+
 def cpu_baseline_multihot(args, num_users, num_items, D, B, layers, maxlen):
     """The oracle train_step on multi-hot bags of the same shape (full tables when RAM allows)."""
     from oracle import ref
@@ -906,9 +978,7 @@ def main():
                   "global_batch": B * world, "per_gpu_batch": B, "emb_dim": D, "tower_dtype": "bf16 (MFMA, fp32 acc)",
                   "parallelism": "single-gpu hipgraph"}
     sharded_info = None
-    if args.workload in MULTIHOT:
-        if world != 1 or args.sharded:
-            raise SystemExit(f"{args.workload}: the multi-hot workload runs at N = 1 (unsharded tables)")
+    if args.workload in MULTIHOT and world == 1 and not args.sharded:
         value, ms, loss, roofline, cpu, steps_run = run_multihot(args)
         config["parallelism"] = "single-gpu hipgraph, KJT input"
     elif world == 1 and args.path == "dropin":
@@ -942,11 +1012,16 @@ def main():
         else:  # --sharded without a launcher (e.g. under rocprofv3): a one-rank group
             dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
                                     device_id=torch.device("cuda", local_rank))
-        value, ms, loss, sharded_info, roofline = run_multi(args, world, rank, local_rank)
+        if args.workload in MULTIHOT:
+            value, ms, loss, sharded_info, roofline = run_multi_kjt(args, world, rank, local_rank)
+            config["parallelism"] = (f"{sharded_info['plan']} + data-parallel towers x{world}: 3 fixed-size RCCL "
+                                     f"all-to-alls per step (ids, pooled rows, bag gradients), {sharded_info['mode']}")
+        else:
+            value, ms, loss, sharded_info, roofline = run_multi(args, world, rank, local_rank)
+            config["parallelism"] = (f"{sharded_info['plan']} sharded tables + data-parallel towers x{world}: pipelined, "
+                                     f"2 RCCL all-to-alls per step ([grad rows | tower grad | next ids], next rows), "
+                                     f"{sharded_info['mode']}")
         cpu, steps_run = None, args.steps
-        config["parallelism"] = (f"{sharded_info['plan']} sharded tables + data-parallel towers x{world}: pipelined, 2 RCCL "
-                                 f"all-to-alls per step ([grad rows | tower grad | next ids], next rows), "
-                                 f"{sharded_info['mode']}")
         config["sharded"] = sharded_info
     if rank == 0:
         out = {"metric": f"training pairs/sec at batch {B} (per GPU)", "value": round(value, 1), "unit": "pairs/s",

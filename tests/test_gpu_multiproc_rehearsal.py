@@ -30,3 +30,20 @@ def test_bench_multiprocess_gloo_rehearsal(world):
     assert sh["mode"] == "eager" and sh["capacity"] >= sh["capacity_needed"]
     assert d["roofline"]["alg_bytes_per_step"] > 0 and d["loss"] == d["loss"]  # finite
 
+
+
+@pytest.mark.parametrize("world", [2])
+def test_bench_config5_sharded_multiprocess_gloo_rehearsal(world):
+    """bench.py's config-5 N > 1 path (the capturable multi-hot sharded step: users table-wise on the
+    last rank, items row-wise, BASELINE table sizes and B = 16,384) as real processes over gloo
+    (eager collectives, ranks sharing the one GPU): capacities all-reduced, flags checked, the line."""
+    env = dict(os.environ, TT_REHEARSE_GLOO="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(29537 + world), "bench.py", "--gpus", str(world),
+           "--workload", "config5", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["n_gpus"] == world and d["steps"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
+    sh = d["config"]["sharded"]
+    assert sh["mode"] == "eager" and sh["collectives_per_step"] == 3
