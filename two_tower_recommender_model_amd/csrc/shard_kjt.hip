@@ -10,7 +10,6 @@
 namespace tt {
 
 constexpr int KR_MAXW = 16;
-constexpr int KR_SCAN_THREADS = 1024;
 
 struct KjtRouteArgs {
   const void* values;
@@ -23,7 +22,8 @@ struct KjtRouteArgs {
   int64_t B, cap, stride;  // ids per destination block, elements per destination block
   int32_t* send;           // [W][stride]: lengths [F*B] then ids [cap]
   int32_t* flags;          // {overflow, bad key}
-  int32_t* base;           // workspace [W][F*B]: exclusive scan of each destination's lengths
+  int32_t* lens;           // workspace [W][F*B]: the lengths, contiguous
+  int32_t* base;           // workspace [W*F*B + 1]: their complete cumsum (prefix within d = base - base[d*F*B])
 };
 
 __device__ __forceinline__ int64_t kr_id(const KjtRouteArgs& a, int64_t i) {
@@ -42,84 +42,69 @@ __device__ __forceinline__ int kr_owner(const KjtRouteArgs& a, int f, int64_t id
   return a.owner[f];
 }
 
-// pass 1 (thread per bag): ids per owner of the bag -> each destination's lengths region
+// the ids of bag i in chunks of KR_CHUNK loads issued together (a thread-per-bag loop of dependent
+// loads waited ~1 us per id): fn(k, id) for each id in bag order
+constexpr int KR_CHUNK = 8;
+template <typename Fn>
+__device__ __forceinline__ void kr_bag_ids(const KjtRouteArgs& a, int32_t o0, int32_t o1, Fn&& fn) {
+  for (int32_t k0 = o0; k0 < o1; k0 += KR_CHUNK) {
+    int64_t v[KR_CHUNK];
+#pragma unroll
+    for (int u = 0; u < KR_CHUNK; ++u) v[u] = k0 + u < o1 ? kr_id(a, k0 + u) : 0;
+#pragma unroll
+    for (int u = 0; u < KR_CHUNK; ++u)
+      if (k0 + u < o1) fn(k0 + u, v[u]);
+  }
+}
+
+// pass 1 (thread per bag): ids per owner of the bag -> each destination's lengths region and the
+// contiguous [W][F*B] copy the scan reads
 __global__ void __launch_bounds__(256) kjt_route_count_kernel(KjtRouteArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)a.F * a.B) return;
+  const int64_t n = (int64_t)a.F * a.B;
+  if (i >= n) return;
   const int f = (int)(i / a.B);
   const int32_t o0 = a.offsets[i], o1 = a.offsets[i + 1];
   int c[KR_MAXW];
 #pragma unroll
   for (int w = 0; w < KR_MAXW; ++w) c[w] = 0;
   int bad = 0;
-  for (int32_t k = o0; k < o1; ++k) {
-    const int64_t id = kr_id(a, k);
+  kr_bag_ids(a, o0, o1, [&](int32_t, int64_t id) {
     if (id < 0 || id >= a.num_emb[f]) {
       bad = 1;
-      continue;
+      return;
     }
     int64_t lr;
     const int d = kr_owner(a, f, id, lr);
 #pragma unroll
     for (int w = 0; w < KR_MAXW; ++w) c[w] += d == w;
-  }
+  });
   if (bad) a.flags[1] = 1;
 #pragma unroll
   for (int w = 0; w < KR_MAXW; ++w)
-    if (w < a.W) a.send[(int64_t)w * a.stride + i] = c[w];
+    if (w < a.W) {
+      a.send[(int64_t)w * a.stride + i] = c[w];
+      a.lens[(int64_t)w * n + i] = c[w];
+    }
 }
 
-// pass 2 (one workgroup per destination): exclusive scan of its F*B lengths; total > cap -> overflow
-__global__ void __launch_bounds__(KR_SCAN_THREADS) kjt_route_scan_kernel(KjtRouteArgs a) {
-  __shared__ int wsum[KR_SCAN_THREADS / 64];
-  __shared__ int carry;
-  const int d = blockIdx.x;
-  const int64_t n = (int64_t)a.F * a.B;
-  const int32_t* len = a.send + (int64_t)d * a.stride;
-  int32_t* out = a.base + (int64_t)d * n;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int64_t c0 = 0; c0 < n; c0 += KR_SCAN_THREADS) {
-    const int64_t i = c0 + threadIdx.x;
-    const int v = i < n ? len[i] : 0;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
-    int wb = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < KR_SCAN_THREADS / 64; ++w) {
-      const int s = wsum[w];
-      wb += w < wid ? s : 0;
-      tot += s;
-    }
-    const int cb = carry;
-    if (i < n) out[i] = cb + wb + incl - v;
-    __syncthreads();
-    if (threadIdx.x == 0) carry = cb + tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0 && carry > a.cap) a.flags[0] = 1;
-}
-
-// pass 3 (thread per bag): each kept id -> its destination's id region at base + rank in the bag
+// pass 3 (thread per bag): each kept id -> its destination's id region at (the destination's
+// exclusive prefix of its lengths) + rank in the bag; the block totals against cap (overflow flag)
 __global__ void __launch_bounds__(256) kjt_route_place_kernel(KjtRouteArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)a.F * a.B) return;
-  const int f = (int)(i / a.B);
   const int64_t n = (int64_t)a.F * a.B;
+  if (i < a.W) {
+    const int32_t tot = a.base[(i + 1) * n] - a.base[i * n];
+    if (tot > a.cap) a.flags[0] = 1;
+  }
+  if (i >= n) return;
+  const int f = (int)(i / a.B);
   const int32_t o0 = a.offsets[i], o1 = a.offsets[i + 1];
   int c[KR_MAXW];
 #pragma unroll
-  for (int w = 0; w < KR_MAXW; ++w) c[w] = w < a.W ? a.base[(int64_t)w * n + i] : 0;
-  for (int32_t k = o0; k < o1; ++k) {
-    const int64_t id = kr_id(a, k);
-    if (id < 0 || id >= a.num_emb[f]) continue;
+  for (int w = 0; w < KR_MAXW; ++w) c[w] = w < a.W ? a.base[(int64_t)w * n + i] - a.base[(int64_t)w * n] : 0;
+  kr_bag_ids(a, o0, o1, [&](int32_t, int64_t id) {
+    if (id < 0 || id >= a.num_emb[f]) return;
     int64_t lr;
     const int d = kr_owner(a, f, id, lr);
     int pos = 0;
@@ -127,7 +112,7 @@ __global__ void __launch_bounds__(256) kjt_route_place_kernel(KjtRouteArgs a) {
     for (int w = 0; w < KR_MAXW; ++w)
       if (d == w) pos = c[w]++;
     if (pos < a.cap) a.send[(int64_t)d * a.stride + n + pos] = (int32_t)lr;
-  }
+  });
 }
 
 // ---- owner side: received blocks -> one contiguous KJT over (source s, served feature k) keys ----
@@ -229,8 +214,13 @@ using namespace tt;
 
 extern "C" {
 
+int tt_complete_cumsum(const int32_t* lengths, int64_t n, int32_t* offsets, void* workspace, size_t ws_bytes,
+                       void* stream);
+size_t tt_complete_cumsum_workspace_bytes(int64_t n);
+
 size_t tt_kjt_route_workspace_bytes(int F, int64_t B, int W) {
-  return align_up((size_t)W * F * B * sizeof(int32_t), 256);
+  const int64_t n = (int64_t)W * F * B;
+  return align_up((size_t)n * 4, 256) + align_up((size_t)(n + 1) * 4, 256) + tt_complete_cumsum_workspace_bytes(n);
 }
 
 int tt_kjt_route(int F, int64_t B, const void* values, int id_dtype, const int32_t* offsets,
@@ -265,18 +255,21 @@ int tt_kjt_route(int F, int64_t B, const void* values, int id_dtype, const int32
   a.stride = blk_stride;
   a.send = send;
   a.flags = flags;
-  a.base = reinterpret_cast<int32_t*>(workspace);
+  const int64_t n = (int64_t)W * F * B;
+  char* ws = reinterpret_cast<char*>(workspace);
+  a.lens = reinterpret_cast<int32_t*>(ws);
+  a.base = reinterpret_cast<int32_t*>(ws + align_up((size_t)n * 4, 256));
+  char* cws = ws + align_up((size_t)n * 4, 256) + align_up((size_t)(n + 1) * 4, 256);
   hipStream_t st = as_stream(stream);
   const unsigned g = (unsigned)ceil_div((int64_t)F * B, 256);
   kjt_route_count_kernel<<<dim3(g), dim3(256), 0, st>>>(a);
-  kjt_route_scan_kernel<<<dim3(W), dim3(KR_SCAN_THREADS), 0, st>>>(a);
+  int rc = check_launch("kjt_route count");
+  if (rc) return rc;
+  rc = tt_complete_cumsum(a.lens, n, a.base, cws, tt_complete_cumsum_workspace_bytes(n), stream);
+  if (rc) return rc;
   kjt_route_place_kernel<<<dim3(g), dim3(256), 0, st>>>(a);
-  return check_launch("kjt_route");
+  return check_launch("kjt_route place");
 }
-
-int tt_complete_cumsum(const int32_t* lengths, int64_t n, int32_t* offsets, void* workspace, size_t ws_bytes,
-                       void* stream);
-size_t tt_complete_cumsum_workspace_bytes(int64_t n);
 
 size_t tt_kjt_unpack_workspace_bytes(int W, int Fr, int64_t B) {
   return tt_complete_cumsum_workspace_bytes((int64_t)W * Fr * B);
