@@ -368,6 +368,33 @@ int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, vo
 int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
                         size_t ws_bytes, void* stream);
+/* ---- the ring with T3 folded into the next step's T1 (two launches per step) -------------------
+ * A WGRAD role (tt_launch, tt_tower_wgrad_pre) marks the step's Adam update pending in the tower
+ * workspace; every T3 form that applies it clears the mark. tt_tower_fwd_bwd_gather_update_t3 is
+ * tt_tower_fwd_bwd_gather_update (without the next-batch prefetch) whose launch first applies a
+ * pending update exactly as tt_tower_update_pre would (same reduction order, same arithmetic, same
+ * copies), every workgroup waiting in-launch for all of them before reading the weights: the
+ * results are bit-identical to T3 followed by T1. It needs every workgroup resident at once
+ * (tt_tower_t3_fuse_supported: the row-owned T1 shape, <= 32 slabs, one workgroup per 32 rows
+ * within the device's residency) and fails with TT_EINVAL otherwise. After the last step of a run
+ * the update is still pending: tt_tower_update_lazy applies it if (and only if) it is, so the
+ * parameters / moments / copies are current before anything else reads them. Replaces the Adam
+ * step of KeyedOptimizerWrapper(Adam) (03_model_training.py:826-829), deferred into the next step. */
+int tt_tower_t3_fuse_supported(const tt_tower_shape_t* shape, int64_t B);
+int tt_tower_fwd_bwd_gather_update_t3(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
+                                      const int64_t* num_embeddings, float* const* table_rows,
+                                      float* const* table_state, float* pooled_out, int64_t ldp, float* gpooled,
+                                      float* params, float* exp_avg, float* exp_avg_sq, float adam_eps,
+                                      float beta1, float beta2, float weight_decay, float* grads_out,
+                                      const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
+                                      float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
+                                      void* workspace, size_t ws_bytes, void* stream);
+int tt_tower_update_lazy(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
+                         size_t ws_bytes, void* stream);
+/* Byte offset of the tower workspace's counter words (uint32): [2] update pending, [6] in-launch
+ * waits of tt_tower_fwd_bwd_gather_update_t3 that timed out (must stay 0); -1 for a bad shape. */
+int64_t tt_tower_counter_offset(const tt_tower_shape_t* shape, int64_t B);
 /* T3: fixed-order reduction of T2's partials, Adam (when do_adam; step_state as tt_adam_step),
  * and the bf16 weight copies for the next T1. grads_out (nullable) receives the gradient. */
 int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,

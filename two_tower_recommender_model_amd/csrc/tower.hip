@@ -1371,11 +1371,135 @@ __device__ __forceinline__ float rk_label(RkRaw r, int dt) {
 #define RK_STAMP(k) do { } while (0)
 #define RK_STAMP2(k) do { } while (0)
 #endif
+// ---------------------------------------------------------------------------------------------
+// T3: reduce + Adam + bf16 weight copies
+
+struct UpdateArgs {
+  float* params;
+  float* exp_avg;
+  float* exp_avg_sq;
+  const float* slab;
+  const float* dbpart;
+  int64_t P;
+  int S;
+  int nwg;
+  int nseg;
+  // segments of the flat parameter vector: W or b of (t, l)
+  int64_t seg_off[2 * 2 * MAXL + 1];
+  int32_t seg_t[2 * 2 * MAXL], seg_l[2 * 2 * MAXL], seg_isw[2 * 2 * MAXL], seg_n[2 * 2 * MAXL], seg_k[2 * 2 * MAXL];
+  int64_t seg_wc[2 * 2 * MAXL];  // bf16 copy offset for W segments
+  __bf16* wb;
+  __bf16* wtb;
+  __bf16* wbf;
+  __bf16* wtbf;
+  int skip_plain;  // wb / wtb unused by this shape's T1 (tower_l2_kernel): not written
+  float lr, beta1, beta2, eps, wd;
+  int64_t* step_state;
+  int do_adam;
+  float* grads_out;  // nullable: the reduced gradient (tests / inspection)
+  const float* grads_in;  // nullable: take the gradient from here (data-parallel: all-reduced)
+  const float* adam_pre;  // nullable: step size / sqrt(bias correction 2) precomputed by T2 (which
+                          // also advanced step_state): no pow() and no arrival ticket here
+  // data-parallel towers without an all-reduce launch (pipelined sharded step): grads_out is
+  // written out_copies times (stride out_stride, scaled by out_scale: one copy per destination
+  // rank of the exchange), and grads_in is the fixed-order sum of in_srcs vectors (stride in_stride)
+  int out_copies;
+  int64_t out_stride;
+  int64_t out_off[16];  // with out_copies > 1: element offset of copy q (explicit, out_stride unused)
+  float out_scale;
+  int in_srcs;
+  int64_t in_stride;
+  char* wimg;  // nullable: the row-owned T1's weight image (rk_off), written beside the other copies
+  int lazy;    // apply Adam only if T2 left the step pending (CW_PENDING), then clear it
+  int fuse_per;  // the T3 + T1 launch: parameters per workgroup (rounds of 256, <= 4096)
+#if TT_EXPERIMENTS
+  int64_t* stamps;  // EXPERIMENT (TT_RING_STAMPS): [workgroups][4] s_memrealtime per phase
+#endif
+};
+#if TT_EXPERIMENTS
+#define T3_STAMP(k) \
+  do { if (a.stamps && threadIdx.x == 0 && bid < 512) a.stamps[(int64_t)bid * 4 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define T3_STAMP(k) do { } while (0)
+#endif
+
+// one parameter's segment (W or b of tower t, layer l): a loop over the (wave-uniform) segment list
+// with scalar kernarg loads and per-lane selects — a per-lane index into the kernarg arrays would be
+// a chain of dependent vector loads from the kernarg segment (several us per launch)
+struct T3Seg {
+  int64_t soff = 0, swc = 0;
+  int sisw = 0, sk = 1, sn = 1, st_ = 0, sl_ = 0;
+};
+__device__ __forceinline__ T3Seg t3_seg(const UpdateArgs& a, int64_t i) {
+  T3Seg g;
+#pragma unroll
+  for (int q = 0; q < 2 * 2 * MAXL; ++q) {
+    if (q < a.nseg && i >= a.seg_off[q]) {
+      g.soff = a.seg_off[q];
+      g.sisw = a.seg_isw[q];
+      g.sk = a.seg_k[q];
+      g.sn = a.seg_n[q];
+      g.swc = a.seg_wc[q];
+      g.st_ = a.seg_t[q];
+      g.sl_ = a.seg_l[q];
+    }
+  }
+  return g;
+}
+
+// after the gradient g of parameter i (value p): gradient copies, Adam, the bf16 copies T1 reads
+__device__ __forceinline__ void t3_apply(const UpdateArgs& a, int64_t i, const T3Seg& sg, float p, float m,
+                                         float v0, float g, float step_size, float bc2_sqrt, bool adam) {
+  const int64_t e = i - sg.soff;
+  if (a.grads_out) {
+    if (a.out_copies <= 1) {
+      a.grads_out[i] = g;
+    } else {
+      const float gs = g * a.out_scale;
+      for (int q = 0; q < a.out_copies; ++q) a.grads_out[a.out_off[q] + i] = gs;
+    }
+  }
+  if (adam) {
+    if (a.wd != 0.f) g = g + a.wd * p;
+    m = m + (1.f - a.beta1) * (g - m);
+    const float v = v0 * a.beta2 + (1.f - a.beta2) * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+    p = p + (-step_size) * m / denom;
+    a.exp_avg[i] = m;
+    a.exp_avg_sq[i] = v;
+    a.params[i] = p;
+  }
+  if (sg.sisw) {
+    const int K = sg.sk, N = sg.sn;
+    const int64_t n = e / K, k = e - n * K;
+    if (!a.skip_plain) {
+      a.wb[sg.swc + e] = (__bf16)p;
+      a.wtb[sg.swc + k * N + n] = (__bf16)p;
+    }
+    a.wbf[sg.swc + frag_off((int)n, (int)k, K)] = (__bf16)p;   // W as [N][K]
+    a.wtbf[sg.swc + frag_off((int)k, (int)n, N)] = (__bf16)p;  // W^T as [K][N]
+    if (a.wimg)  // the row-owned T1's image: W [out][in], 256-B swizzled rows, W1 after W0
+      *reinterpret_cast<__bf16*>(a.wimg + sg.st_ * RK_IMG_T + sg.sl_ * (RK_W0 * 256) + rk_off((int)n, (int)k)) = (__bf16)p;
+  }
+}
+
+// words of the tower workspace's counter region (adam_pre = its first two floats; tt_tower_counter_offset):
+// [2] Adam step pending (set by T2 with adam_pre, cleared by the T3 that applies it), [3] the lazy
+// T3's arrivals, [4] / [5] the fused T3 + T1 launch's arrivals / passes, [6] its poll timeouts
+constexpr int CW_PENDING = 2, CW_LAZY_ARRIVE = 3, CW_FUSE_ARRIVE = 4, CW_FUSE_PASSED = 5, CW_FUSE_TIMEOUT = 6;
+
 // IDX: the sharded step's form (tt_tower_fwd_bwd_indexed2_bf16): tower t's input row m is bf16 row
 // gpos[t][m] of gsrc[t] (-1: zeros; the rows an owner returned, dense), its dX goes to fp32 row
 // gpos_out[t][m] of gdst[t]; no in-place update, no insert
-template <bool UPD, bool IDX = false>
-__global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
+// FUSE (the ring's T3 + T1 launch, tt_tower_fwd_bwd_gather_update_t3): the launch first applies the
+// Adam step the previous step's tail left pending (CW_PENDING): each workgroup takes u.fuse_per
+// parameters (one per thread: the slab sum, Adam, the bf16 copies T1 reads, the image), publishes
+// them (vmcnt(0), barrier, one agent-scope release, an arrival), and waits for every workgroup's
+// arrival before it reads the weight image and the biases. Every workgroup must be resident at
+// once (the host checks the occupancy); the wait is bounded (CW_FUSE_TIMEOUT records a miss).
+// The table rows are gathered while the update runs: they do not depend on it.
+template <bool UPD, bool IDX, bool FUSE>
+__device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const UpdateArgs& u) {
   __shared__ __attribute__((aligned(16))) char wimg[RK_IMG];         // both towers' W0, W1 (rk_off)
   __shared__ __attribute__((aligned(16))) float xo[2][2][16 * 64];  // tower outputs per (tower, row half)
   __shared__ float bsum[2][RK_W0 + RK_W1];                          // row half 1's bias partials
@@ -1401,22 +1525,52 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   }
   const RkRaw lab_raw = rk_raw(a.labels, a.label_dtype == TT_I64, mc);
   f32x4 b0v[8], b1v[4];
-  {
+  auto load_biases = [&]() {
     const float* b0p = a.params + a.boff[t][0];
     const float* b1p = a.params + a.boff[t][1];
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) b0v[mt] = *reinterpret_cast<const f32x4*>(b0p + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1));
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) b1v[mt] = *reinterpret_cast<const f32x4*>(b1p + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1));
-  }
-  __builtin_amdgcn_sched_barrier(0);
+  };
   // the weight image (no dependency): 24 16-B loads per lane into registers, issued while the ids
   // come back (plain loads: with an LDS-DMA in flight the compiler waits vmcnt(0) at the first use
   // of any load, so the ids must land before the first DMA is issued), written to LDS below
   bf16x8 wreg[RK_IMG / 1024 / 4];
+  auto load_image = [&]() {
 #pragma unroll
-  for (int k = 0; k < RK_IMG / 1024 / 4; ++k)
-    wreg[k] = *reinterpret_cast<const bf16x8*>(a.wimg + (wid + 4 * k) * 1024 + lane * 16);
+    for (int k = 0; k < RK_IMG / 1024 / 4; ++k)
+      wreg[k] = *reinterpret_cast<const bf16x8*>(a.wimg + (wid + 4 * k) * 1024 + lane * 16);
+  };
+  // FUSE: this workgroup's share of the pending Adam step, loads issued now (beside the ids)
+  uint32_t* cw = FUSE ? reinterpret_cast<uint32_t*>(const_cast<float*>(u.adam_pre)) : nullptr;
+  bool pending = false;
+  int64_t ui = 0;
+  bool uon = false;
+  T3Seg useg;
+  float up = 0.f, um = 0.f, uv = 0.f, ug = 0.f;
+  float uslab[32];
+  if (FUSE) {
+    pending = __builtin_amdgcn_readfirstlane(
+                  __hip_atomic_load(cw + CW_PENDING, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+    ui = (int64_t)blockIdx.x * u.fuse_per + threadIdx.x;
+    uon = pending && (int)threadIdx.x < u.fuse_per && ui < u.P;
+    const int64_t uc = uon ? ui : 0;
+    useg = t3_seg(u, uc);
+    if (pending) {
+      up = u.params[uc];
+      um = u.exp_avg[uc];
+      uv = u.exp_avg_sq[uc];
+      // one round of 32 slabs in flight (S <= 32: the host checks); bias parameters read slab 0 only
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        uslab[k] = k < u.S && (k == 0 || useg.sisw) ? u.slab[(int64_t)k * u.P + uc] : 0.f;
+    }
+  } else {
+    load_biases();
+    __builtin_amdgcn_sched_barrier(0);
+    load_image();
+  }
   __builtin_amdgcn_sched_barrier(0);
   int64_t r;  // the row's index in its source (table row / returned-rows buffer row), -1: zeros
   if (IDX) {
@@ -1468,6 +1622,60 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
     dd_insert_begin(a.dd, key, li, pend);
   }
   RK_STAMP(1);
+  if (FUSE) {
+    if (pending) {
+      // the slab sum in order s = 0, 1, ... (update_block's), Adam, the copies; then publish
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        if (k < u.S && (k == 0 || useg.sisw)) ug += uslab[k];
+      if (uon) t3_apply(u, ui, useg, up, um, uv, ug, u.adam_pre[0], u.adam_pre[1], true);
+      // small batches (few workgroups): further rounds of 256 parameters, one after another
+      for (int k = 256; k < u.fuse_per; k += 256) {
+        const int64_t i2 = ui + k;
+        const bool on2 = (int)threadIdx.x + k < u.fuse_per && i2 < u.P;
+        const int64_t c2 = on2 ? i2 : 0;
+        const T3Seg sg2 = t3_seg(u, c2);
+        const float p2 = u.params[c2], m2 = u.exp_avg[c2], v2 = u.exp_avg_sq[c2];
+#pragma unroll
+        for (int q2 = 0; q2 < 32; ++q2)
+          uslab[q2] = q2 < u.S && (q2 == 0 || sg2.sisw) ? u.slab[(int64_t)q2 * u.P + c2] : 0.f;
+        float g2 = 0.f;
+#pragma unroll
+        for (int q2 = 0; q2 < 32; ++q2)
+          if (q2 < u.S && (q2 == 0 || sg2.sisw)) g2 += uslab[q2];
+        if (on2) t3_apply(u, i2, sg2, p2, m2, v2, g2, u.adam_pre[0], u.adam_pre[1], true);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores (and the rows)
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(cw + CW_FUSE_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned nwg = gridDim.x;
+        int spin = 0;
+        while (__hip_atomic_load(cw + CW_FUSE_ARRIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg) {
+          if (++spin > (1 << 20)) {  // ~50 ms: a workgroup was not resident; recorded, not waited for
+            __hip_atomic_fetch_add(cw + CW_FUSE_TIMEOUT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(cw + CW_FUSE_PASSED, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == nwg - 1) {  // every workgroup is past the wait (and read CW_PENDING before it)
+          __hip_atomic_store(cw + CW_FUSE_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(cw + CW_FUSE_PASSED, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(cw + CW_PENDING, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      __syncthreads();
+    }
+    load_biases();
+    __builtin_amdgcn_sched_barrier(0);
+    load_image();
+    __builtin_amdgcn_sched_barrier(0);
+  }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the rows (LDS-DMA) and the image registers
   RK_STAMP(2);
 #pragma unroll
@@ -1715,6 +1923,14 @@ __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   // the resolver reads all 64 entries of the group
   if (!UPD && a.dd_on && q == 0) dd_insert_defer_finish_at(a.dd, pend, li, (int)blockIdx.x, 16 * wid + n);
   RK_STAMP(15);
+}
+template <bool UPD, bool IDX = false>
+__global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
+  const UpdateArgs u{};
+  tower_rows_body<UPD, IDX, false>(a, u);
+}
+__global__ void __launch_bounds__(256) tower_rows_t3_kernel(TowerArgs a, UpdateArgs u) {
+  tower_rows_body<true, false, true>(a, u);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2027,6 +2243,7 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
         const double bc2 = 1.0 - pow((double)a.beta2, (double)t_step);
         a.adam_pre[0] = (float)((double)a.lr / bc1);
         a.adam_pre[1] = (float)sqrt(bc2);
+        reinterpret_cast<uint32_t*>(a.adam_pre)[2] = 1u;  // CW_PENDING: the step's Adam is due
       }
       return;
     }
@@ -2267,59 +2484,12 @@ __global__ void __launch_bounds__(256) tower_wgrad_route_rowwise_kernel(WgradArg
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// T3: reduce + Adam + bf16 weight copies
-
-struct UpdateArgs {
-  float* params;
-  float* exp_avg;
-  float* exp_avg_sq;
-  const float* slab;
-  const float* dbpart;
-  int64_t P;
-  int S;
-  int nwg;
-  int nseg;
-  // segments of the flat parameter vector: W or b of (t, l)
-  int64_t seg_off[2 * 2 * MAXL + 1];
-  int32_t seg_t[2 * 2 * MAXL], seg_l[2 * 2 * MAXL], seg_isw[2 * 2 * MAXL], seg_n[2 * 2 * MAXL], seg_k[2 * 2 * MAXL];
-  int64_t seg_wc[2 * 2 * MAXL];  // bf16 copy offset for W segments
-  __bf16* wb;
-  __bf16* wtb;
-  __bf16* wbf;
-  __bf16* wtbf;
-  int skip_plain;  // wb / wtb unused by this shape's T1 (tower_l2_kernel): not written
-  float lr, beta1, beta2, eps, wd;
-  int64_t* step_state;
-  int do_adam;
-  float* grads_out;  // nullable: the reduced gradient (tests / inspection)
-  const float* grads_in;  // nullable: take the gradient from here (data-parallel: all-reduced)
-  const float* adam_pre;  // nullable: step size / sqrt(bias correction 2) precomputed by T2 (which
-                          // also advanced step_state): no pow() and no arrival ticket here
-  // data-parallel towers without an all-reduce launch (pipelined sharded step): grads_out is
-  // written out_copies times (stride out_stride, scaled by out_scale: one copy per destination
-  // rank of the exchange), and grads_in is the fixed-order sum of in_srcs vectors (stride in_stride)
-  int out_copies;
-  int64_t out_stride;
-  int64_t out_off[16];  // with out_copies > 1: element offset of copy q (explicit, out_stride unused)
-  float out_scale;
-  int in_srcs;
-  int64_t in_stride;
-  char* wimg;  // nullable: the row-owned T1's weight image (rk_off), written beside the other copies
-#if TT_EXPERIMENTS
-  int64_t* stamps;  // EXPERIMENT (TT_RING_STAMPS): [workgroups][4] s_memrealtime per phase
-#endif
-};
-#if TT_EXPERIMENTS
-#define T3_STAMP(k) \
-  do { if (a.stamps && threadIdx.x == 0 && bid < 512) a.stamps[(int64_t)bid * 4 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define T3_STAMP(k) do { } while (0)
-#endif
-
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
   T3_STAMP(0);
   const int64_t i = (int64_t)bid * 256 + threadIdx.x;
+  uint32_t* cw = a.adam_pre ? reinterpret_cast<uint32_t*>(const_cast<float*>(a.adam_pre)) : nullptr;
+  // lazy (the fused T3 + T1 ring's flush): apply the Adam step T2 left pending, if any
+  if (a.lazy && cw[CW_PENDING] == 0u) return;
   int64_t t_step = 0;
   float step_size = 0.f, bc2_sqrt = 1.f;
   if (a.do_adam && a.adam_pre) {
@@ -2333,31 +2503,15 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
     bc2_sqrt = (float)sqrt(bc2);
   }
   if (i < a.P) {
-    // this element's segment: a loop over the (wave-uniform) segment list with scalar kernarg
-    // loads and per-lane selects — a per-lane index into the kernarg arrays would be a chain of
-    // dependent vector loads from the kernarg segment (several us per launch)
-    int64_t soff = 0, swc = 0;
-    int sisw = 0, sk = 1, sn = 1, st_ = 0, sl_ = 0;
-#pragma unroll
-    for (int q = 0; q < 2 * 2 * MAXL; ++q) {
-      if (q < a.nseg && i >= a.seg_off[q]) {
-        soff = a.seg_off[q];
-        sisw = a.seg_isw[q];
-        sk = a.seg_k[q];
-        sn = a.seg_n[q];
-        swc = a.seg_wc[q];
-        st_ = a.seg_t[q];
-        sl_ = a.seg_l[q];
-      }
-    }
-    const int64_t e = i - soff;
-    float p = a.params[i];
+    const T3Seg sg = t3_seg(a, i);
+    const float p = a.params[i];
+    const float m = a.do_adam ? a.exp_avg[i] : 0.f, v = a.do_adam ? a.exp_avg_sq[i] : 0.f;
     float g = 0.f;
     if (a.grads_in) {
       g = a.grads_in[i];
       for (int q = 1; q < a.in_srcs; ++q) g += a.grads_in[(int64_t)q * a.in_stride + i];
     } else if (a.do_adam || a.grads_out) {
-      if (sisw) {
+      if (sg.sisw) {
         // a round's 32 slab loads all in flight (one memory latency per 32 slabs, not per load);
         // the sum keeps the sequential order s = 0, 1, ...
         for (int s0 = 0; s0 < a.S; s0 += 32) {
@@ -2371,40 +2525,22 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
       } else {
         g = a.slab[i];  // bias gradient, reduced over the T1 workgroups by T2's bias waves
       }
-      if (a.grads_out) {
-        if (a.out_copies <= 1) {
-          a.grads_out[i] = g;
-        } else {
-          const float gs = g * a.out_scale;
-          for (int q = 0; q < a.out_copies; ++q) a.grads_out[a.out_off[q] + i] = gs;
-        }
-      }
     }
     T3_STAMP(1);
-    if (a.do_adam) {
-      if (a.wd != 0.f) g = g + a.wd * p;
-      float m = a.exp_avg[i];
-      m = m + (1.f - a.beta1) * (g - m);
-      const float v = a.exp_avg_sq[i] * a.beta2 + (1.f - a.beta2) * g * g;
-      const float denom = sqrtf(v) / bc2_sqrt + a.eps;
-      p = p + (-step_size) * m / denom;
-      a.exp_avg[i] = m;
-      a.exp_avg_sq[i] = v;
-      a.params[i] = p;
-    }
-    if (sisw) {
-      const int K = sk, N = sn;
-      const int64_t n = e / K, k = e - n * K;
-      if (!a.skip_plain) {
-        a.wb[swc + e] = (__bf16)p;
-        a.wtb[swc + k * N + n] = (__bf16)p;
-      }
-      a.wbf[swc + frag_off((int)n, (int)k, K)] = (__bf16)p;   // W as [N][K]
-      a.wtbf[swc + frag_off((int)k, (int)n, N)] = (__bf16)p;  // W^T as [K][N]
-      if (a.wimg)  // the row-owned T1's image: W [out][in], 256-B swizzled rows, W1 after W0
-        *reinterpret_cast<__bf16*>(a.wimg + st_ * RK_IMG_T + sl_ * (RK_W0 * 256) + rk_off((int)n, (int)k)) = (__bf16)p;
-    }
+    t3_apply(a, i, sg, p, m, v, g, step_size, bc2_sqrt, a.do_adam);
     T3_STAMP(2);
+  }
+  if (a.lazy) {  // the last workgroup to finish clears the pending step (every one read it first)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(cw + CW_LAZY_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (unsigned)nblocks - 1) {
+        __hip_atomic_store(cw + CW_LAZY_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cw + CW_PENDING, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else if (a.do_adam && a.adam_pre && bid == 0 && threadIdx.x == 0) {
+    cw[CW_PENDING] = 0u;  // applied (no workgroup of this launch reads the word)
   }
   if (a.do_adam && !a.adam_pre) {
     __syncthreads();
@@ -2763,7 +2899,7 @@ namespace tt {
 // shared by tt_tower_fwd_bwd / tt_tower_fwd_bwd_gather: checks, T1 arguments, launch
 static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, const float* pooled, int64_t ldp,
                      float* gpooled, const float* params, const void* labels, int label_dtype, float grad_scale,
-                     float* logits, void* workspace, size_t ws_bytes, void* stream) {
+                     float* logits, void* workspace, size_t ws_bytes, void* stream, const UpdateArgs* fuse = nullptr) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
@@ -2839,8 +2975,14 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
 #if TT_EXPERIMENTS
   if (getenv("TT_T1_CLASSIC")) rows_t1 = false;  // EXPERIMENT (A/B): tower_l2_kernel instead
 #endif
+  if (fuse && !(rows_t1 && a.uw[0] && !a.gpos[0]))
+    return fail(TT_EINVAL, "tower: the T3 + T1 launch serves the ring's row-owned gather + update shape only");
   if (rows_t1) {
     a.wimg = ws + L.o_wimg;
+    if (fuse) {
+      tower_rows_t3_kernel<<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse);
+      return check_launch("tower_rows_gather_update_t3");
+    }
     if (a.gpos[0])
       tower_rows_kernel<false, true><<<g, dim3(256), 0, as_stream(stream)>>>(a);
     else if (a.uw[0])
@@ -3458,6 +3600,105 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
   dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
   return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
                    ws_bytes, stream);
+}
+
+// can every workgroup of the T3 + T1 launch (one per 32-row tile) be resident at once? (its
+// in-launch wait needs them all); cached per device
+static int t1f_capacity() {
+  static int cap[64];
+  static bool done[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!done[dev]) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(tower_rows_t3_kernel), 256,
+                                                     0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    cap[dev] = per_cu * cus;
+    done[dev] = true;
+  }
+  return cap[dev];
+}
+
+int tt_tower_t3_fuse_supported(const tt_tower_shape_t* shape, int64_t B) {
+  TowerLayout L;
+  if (tower_layout(shape, B, &L) != TT_OK) return 0;
+  if (!L.rows || L.S > 32 || ceil_div(L.P, (int64_t)L.nwg) > 4096) return 0;
+  return L.nwg <= t1f_capacity() ? 1 : 0;
+}
+
+int64_t tt_tower_counter_offset(const tt_tower_shape_t* shape, int64_t B) {
+  TowerLayout L;
+  if (tower_layout(shape, B, &L) != TT_OK) return -1;
+  return (int64_t)L.o_counter;
+}
+
+int tt_tower_fwd_bwd_gather_update_t3(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
+                                      const int64_t* num_embeddings, float* const* table_rows,
+                                      float* const* table_state, float* pooled_out, int64_t ldp, float* gpooled,
+                                      float* params, float* exp_avg, float* exp_avg_sq, float adam_eps,
+                                      float beta1, float beta2, float weight_decay, float* grads_out,
+                                      const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
+                                      float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
+                                      void* workspace, size_t ws_bytes, void* stream) {
+  if (!cols || !num_embeddings || !table_rows || !table_state || !dedup_ws)
+    return fail(TT_EINVAL, "tower_gather_update_t3: null pointer");
+  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_gather_update_t3: ids must be int32/int64");
+  if (dedup_max_lookups < 2 * B || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
+      dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) || (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
+    return fail(TT_ECAPACITY, "tower_gather_update_t3: dedup workspace too small / misaligned");
+  if (!tt_tower_t3_fuse_supported(shape, B))
+    return fail(TT_EINVAL, "tower_gather_update_t3: shape / batch not servable (row-owned T1, <= 32 slabs, <= 4096 "
+                           "parameters per workgroup, every workgroup resident)");
+  TowerArgs a{};
+  for (int t = 0; t < 2; ++t) {
+    if (!cols[t] || !table_rows[t] || !table_state[t] || num_embeddings[t] < 1)
+      return fail(TT_EINVAL, "tower_gather_update_t3: bad column");
+    if (reinterpret_cast<uintptr_t>(table_rows[t]) & 15)
+      return fail(TT_EINVAL, "tower_gather_update_t3: rows not 16-B aligned");
+    a.gcol[t] = cols[t];
+    a.gtab[t] = table_rows[t];
+    a.gmod[t] = num_embeddings[t];
+    a.uw[t] = table_rows[t];
+    a.us[t] = table_state[t];
+  }
+  a.gid_dtype = id_dtype;
+  a.pooled_out = pooled_out;
+  a.ulr = lr;
+  a.ueps = eps;
+  dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
+  UpdateArgs u;
+  int64_t g3 = 0;
+  rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, adam_eps, weight_decay, nullptr, 1, grads_out,
+               nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0, u, &g3);
+  if (rc) return rc;
+  u.fuse_per = (int)ceil_div(L.P, (int64_t)L.nwg);
+  return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
+                   ws_bytes, stream, &u);
+}
+
+int tt_tower_update_lazy(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
+                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
+  UpdateArgs u;
+  int64_t g3 = 0;
+  rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
+               nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0, u, &g3);
+  if (rc) return rc;
+  u.lazy = 1;
+  tower_update_kernel<<<dim3((unsigned)g3), dim3(256), 0, as_stream(stream)>>>(u);
+  return check_launch("tower_update_lazy");
 }
 
 static int fused_wgrad_insert(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,

@@ -548,6 +548,7 @@ class FusedTwoTowerStep:
         B = self.B
         if cols[0].numel() != B:
             raise _lib.TTError("eval_step: batch size differs from the step's")
+        self.flush()
         self.tables.pooled_fwd_cols(list(cols), self.num_embeddings, out=self.pooled)
         self._towers_fwd()
         L = len(self.layer_sizes)
@@ -560,7 +561,34 @@ class FusedTwoTowerStep:
         """Refresh the fused towers' bf16 weight copies after the fp32 parameters were changed
         outside step() (initialisation, loading a checkpoint)."""
         if self.towers is not None:
+            self.flush()
             self.towers.update(self.params, do_adam=False)
+
+    def t1_fuse(self) -> bool:
+        """Does the ring fold T3 into the next step's T1 (two launches per step)? The shape must be
+        the row-owned T1's with every T1 workgroup resident at once (tt_tower_t3_fuse_supported);
+        TT_T1_FUSE=0 turns it off."""
+        if getattr(self, "_t1f", None) is None:
+            self._t1f = bool(self.towers is not None and os.environ.get("TT_T1_FUSE", "1") != "0"
+                             and self.ring_supported()
+                             and _lib.load().tt_tower_t3_fuse_supported(C.byref(self.towers.shape), self.B) == 1)
+        return self._t1f
+
+    def flush(self) -> None:
+        """Apply the tower Adam update the last fused ring step left pending (a no-op launch when
+        none is): parameters, moments and weight copies are current afterwards. run() / run_eager()
+        end with it; call it after driving ring_step() directly, before reading the parameters."""
+        if self.towers is None or not getattr(self, "_t1f", None):
+            return
+        tw = self.towers
+        check(_lib.load().tt_tower_update_lazy(C.byref(tw.shape), self.B, ptr(self.params), ptr(self.exp_avg),
+                                               ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads),
+                                               ptr(tw.ws), tw.nbytes, stream_handle(self.device)), "tower_update_lazy")
+
+    def fuse_timeouts(self) -> int:
+        """In-launch waits of the fused T3 + T1 launch that gave up (must be 0; one sync)."""
+        off = _lib.load().tt_tower_counter_offset(C.byref(self.towers.shape), self.B)
+        return int(self.towers.ws[off + 24:off + 28].view(torch.int32).item())
 
     # ---- the pipelined ring (production): dedup one step ahead, single-lookup rows in T1 ---------
     def ring_supported(self) -> bool:
@@ -579,6 +607,7 @@ class FusedTwoTowerStep:
             check(lib.tt_dedup_workspace_init(ptr(ws1), ws1.numel(), ts._dd_cap, stream_handle(self.device)),
                   "dedup_workspace_init")
             self._ring = [ts._dd_ws, ws1]
+            self.t1_fuse()  # decided (a device query) before any capture
             self._ring_tab = (C.c_int32 * 2)(0, 1)
             self._ring_ne = (C.c_int64 * 2)(*self.num_embeddings)
         return self._ring
@@ -607,19 +636,32 @@ class FusedTwoTowerStep:
           tail  T2 (tower weight gradients, Adam scalars) + complete insert of the next batch +
                 update of the rows looked up more than once (from T1's dX)
           T3    slab reduction, Adam, bf16 weight copies
+        With t1_fuse() there are two: T3 runs at the start of the NEXT step's T1 launch (its
+        workgroups apply the pending update, wait for each other in-launch, then read the weights),
+        so after the last step the update is pending until flush() (run / run_eager call it).
         (ring_tail False: T2 + deferred insert of the next batch, then resolver + row update + T3)."""
         lib, tw, ts, B, dev = _lib.load(), self.towers, self.tables, self.B, self.device
         ring = self._ring_ws()
         ws, wsn = ring[parity], ring[parity ^ 1]
         st = stream_handle(dev)
+        fuse = self.ring_tail and self.t1_fuse()
         self._mark("t1", 0)
-        check(lib.tt_tower_fwd_bwd_gather_update(
-            C.byref(tw.shape), B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ring_ne,
-            ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
-            ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
-            ptr(self.params), ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws),
-            ws.numel(), ts._dd_cap, ptr_array(list(next_cols)) if self.prefetch_next else None, ptr(tw.ws), tw.nbytes,
-            st), "tower_fwd_bwd_gather_update")
+        if fuse:  # T1 with the previous step's pending T3 folded in (bit-identical to T3 then T1)
+            check(lib.tt_tower_fwd_bwd_gather_update_t3(
+                C.byref(tw.shape), B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ring_ne,
+                ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
+                ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
+                ptr(self.params), ptr(self.exp_avg), ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads),
+                ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws), ws.numel(),
+                ts._dd_cap, ptr(tw.ws), tw.nbytes, st), "tower_fwd_bwd_gather_update_t3")
+        else:
+            check(lib.tt_tower_fwd_bwd_gather_update(
+                C.byref(tw.shape), B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ring_ne,
+                ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
+                ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
+                ptr(self.params), ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws),
+                ws.numel(), ts._dd_cap, ptr_array(list(next_cols)) if self.prefetch_next else None, ptr(tw.ws),
+                tw.nbytes, st), "tower_fwd_bwd_gather_update")
         self._mark("t1", 1)
         if self.ring_tail:
             self._mark("tail", 0)
@@ -631,6 +673,8 @@ class FusedTwoTowerStep:
                                           dedup_tables=self._ring_tab, next_dedup_ws=ptr(wsn))
             _lib.launch(plan, st, "ring tail")
             self._mark("tail", 1)
+            if fuse:  # T3 runs in the next step's T1 (or flush())
+                return
             self._mark("t3", 0)
             check(lib.tt_tower_update_pre(C.byref(tw.shape), B, ptr(self.params), ptr(self.exp_avg),
                                           ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads), ptr(tw.ws),
@@ -746,6 +790,7 @@ class FusedTwoTowerStep:
                 (mid[sz][r // sz] if sz > 1 else self.ring_small[i]).replay()
             i, n = (i + sz) % nb, n - sz
         self.ring_cursor = i
+        self.flush()
 
     def timed_ring(self, n: int) -> dict:
         """n eager production steps (from the cursor) with a HIP event pair around every launch;
@@ -754,7 +799,8 @@ class FusedTwoTowerStep:
         try:
             for _ in range(n):
                 self._timing.append({})
-                self.run_eager(1)
+                self.run_eager(1, flush=False)
+            self.flush()
             torch.cuda.synchronize(self.device)
             acc = {}
             for m in self._timing:
@@ -764,7 +810,7 @@ class FusedTwoTowerStep:
             self._timing = None
         return {k: sum(v) / len(v) for k, v in acc.items()}
 
-    def run_eager(self, n: int) -> None:
+    def run_eager(self, n: int, flush: bool = True) -> None:
         """n production steps over the captured ring's batches without graphs (timing / tests)."""
         staged = self._ring_inputs
         nb = len(staged)
@@ -772,6 +818,8 @@ class FusedTwoTowerStep:
             i = self.ring_cursor
             self.ring_step(staged[i][0], staged[i][1], i % 2, staged[(i + 1) % nb][0])
             self.ring_cursor = (i + 1) % nb
+        if flush:
+            self.flush()
 
     # ------------------------------------------------------------------------------------------
     def capture(self, batches: Optional[Sequence] = None, keep_graph: bool = False,
