@@ -396,10 +396,10 @@ KERNEL_NAMES = {"t1": "tower_l2_kernel", "t2": "tower_wgrad_insert_kernel", "k3"
 
 
 def uses_rows_t1(step) -> bool:
-    """The fused gather T1 of the [128, 64] towers over 128-wide rows is the row-owned kernel
+    """The fused gather T1 of the [128, 64] towers over 128- or 64-wide rows is the row-owned kernel
     (tower.hip launch_t1: tower_rows_kernel)."""
     return bool(getattr(step, "gather", False)) and step.layer_sizes == [128, 64] and \
-        getattr(step, "in_q", 0) == 128 and getattr(step, "in_c", 0) == 128
+        getattr(step, "in_q", 0) == getattr(step, "in_c", 0) and getattr(step, "in_q", 0) in (64, 128)
 
 
 def kernel_names(step) -> dict:

@@ -377,7 +377,7 @@ int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params,
  * results are bit-identical to T3 followed by T1. It needs every workgroup resident at once
  * (tt_tower_t3_fuse_supported: the row-owned T1 shape, <= 32 slabs, one workgroup per 32 rows
  * within the device's residency) and fails with TT_EINVAL otherwise. After the last step of a run
- * the update is still pending: tt_tower_update_lazy applies it if (and only if) it is, so the
+ * the update is still pending: tt_tower_update_lazy (grads_in NULL: the slabs) applies it if (and only if) it is, so the
  * parameters / moments / copies are current before anything else reads them. Replaces the Adam
  * step of KeyedOptimizerWrapper(Adam) (03_model_training.py:826-829), deferred into the next step. */
 int tt_tower_t3_fuse_supported(const tt_tower_shape_t* shape, int64_t B);
@@ -390,8 +390,20 @@ int tt_tower_fwd_bwd_gather_update_t3(const tt_tower_shape_t* shape, int64_t B, 
                                       float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
                                       void* workspace, size_t ws_bytes, void* stream);
 int tt_tower_update_lazy(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
-                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
-                         size_t ws_bytes, void* stream);
+                         float eps, float beta1, float beta2, float weight_decay, float* grads_out,
+                         const float* grads_in, int nsrc, int64_t src_stride, void* workspace, size_t ws_bytes,
+                         void* stream);
+/* The sharded step's T1 (tt_tower_fwd_bwd_indexed2_bf16) whose launch first applies the pending
+ * update as tt_tower_adam_pre_grads_sum would: Adam on the fixed-order sum of the nsrc received
+ * tower gradients (grads_in + q * src_stride, q < nsrc <= 32). tt_tower_update_lazy with the same
+ * grads_in / nsrc / src_stride flushes the last step's. */
+int tt_tower_fwd_bwd_indexed2_bf16_t3(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
+                                      const int32_t* const* pos_out, const void* const* rows_in,
+                                      float* const* grad_rows_out, float* params, float* exp_avg, float* exp_avg_sq,
+                                      float adam_eps, float beta1, float beta2, float weight_decay,
+                                      const float* grads_in, int nsrc, int64_t src_stride, const void* labels,
+                                      int label_dtype, float grad_scale, float* logits, void* workspace,
+                                      size_t ws_bytes, void* stream);
 /* Byte offset of the tower workspace's counter words (uint32): [2] update pending, [6] in-launch
  * waits of tt_tower_fwd_bwd_gather_update_t3 that timed out (must stay 0); -1 for a bad shape. */
 int64_t tt_tower_counter_offset(const tt_tower_shape_t* shape, int64_t B);

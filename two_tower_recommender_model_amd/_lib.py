@@ -275,7 +275,13 @@ SIGNATURES = {
         [_psh, _i64, _pvp, _int, _pi64, _pvp, _pvp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp,
          _int, _f32, _vp, _f32, _f32, _vp, _sz, _i64, _vp, _sz, _vp],
     ),
-    "tt_tower_update_lazy": (_int, [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _sz, _vp]),
+    "tt_tower_update_lazy": (_int, [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _int, _i64, _vp, _sz,
+                                    _vp]),
+    "tt_tower_fwd_bwd_indexed2_bf16_t3": (
+        _int,
+        [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _int, _i64, _vp, _int, _f32,
+         _vp, _vp, _sz, _vp],
+    ),
     "tt_launch": (_int, [C.c_void_p, _vp]),
 }
 
@@ -330,6 +336,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_indexed_multi_bf16",
     "tt_tower_fwd_bwd_gather_update_t3",
     "tt_tower_update_lazy",
+    "tt_tower_fwd_bwd_indexed2_bf16_t3",
     "tt_launch",
 ]
 

@@ -675,9 +675,9 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   // a.gtab[t], ... with scalar loads (a per-lane index into the kernarg arrays is a vector load from
   // the kernarg segment: one more dependent memory hop in front of the row gather)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // the [128, 64] towers over 128-wide inputs write ROW-MAJOR operand strips ([Bp][features], as the
+  // the [128, 64] towers over 64- or 128-wide inputs write ROW-MAJOR operand strips ([Bp][features], as the
   // row-owned T1 does; the tail reads them with wgrad_lds_block_rm): copies of the LDS tiles
-  constexpr bool RM = IN_ == 128 && W0_ == 128 && W1_ == 64;
+  constexpr bool RM = (IN_ == 128 || IN_ == 64) && W0_ == 128 && W1_ == 64;
   auto rm_copy = [&](const __bf16* tile, __bf16* dst, int nchunk, int ld, int nval_) {
     // tile: TR rows at LSTR; dst: row 0 of the tile in a [Bp][ld] strip; nchunk 16-B pieces per row
     const int tt_ = threadIdx.x & 255;
@@ -1483,6 +1483,34 @@ __device__ __forceinline__ void t3_apply(const UpdateArgs& a, int64_t i, const T
   }
 }
 
+// the fused T3 share's gradient terms of parameter i, all loads issued at once (<= 32 terms: the
+// host checks S and in_srcs): the W received tower gradients (grads_in), or the weight's S slabs /
+// the bias's one reduced slab; t3_sum adds them in update_block's order
+__device__ __forceinline__ void t3_terms(const UpdateArgs& a, float (&v)[32], int64_t i, const T3Seg& sg) {
+  if (a.grads_in) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = k < a.in_srcs ? a.grads_in[(int64_t)k * a.in_stride + i] : 0.f;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = k < a.S && (k == 0 || sg.sisw) ? a.slab[(int64_t)k * a.P + i] : 0.f;
+  }
+}
+__device__ __forceinline__ float t3_sum(const UpdateArgs& a, const float (&v)[32], const T3Seg& sg) {
+  if (a.grads_in) {
+    float g = v[0];
+#pragma unroll
+    for (int k = 1; k < 32; ++k)
+      if (k < a.in_srcs) g += v[k];
+    return g;
+  }
+  if (!sg.sisw) return v[0];
+  float g = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    if (k < a.S) g += v[k];
+  return g;
+}
+
 // words of the tower workspace's counter region (adam_pre = its first two floats; tt_tower_counter_offset):
 // [2] Adam step pending (set by T2 with adam_pre, cleared by the T3 that applies it), [3] the lazy
 // T3's arrivals, [4] / [5] the fused T3 + T1 launch's arrivals / passes, [6] its poll timeouts
@@ -1498,13 +1526,18 @@ constexpr int CW_PENDING = 2, CW_LAZY_ARRIVE = 3, CW_FUSE_ARRIVE = 4, CW_FUSE_PA
 // arrival before it reads the weight image and the biases. Every workgroup must be resident at
 // once (the host checks the occupancy); the wait is bounded (CW_FUSE_TIMEOUT records a miss).
 // The table rows are gathered while the update runs: they do not depend on it.
-template <bool UPD, bool IDX, bool FUSE>
+// IN: the input width (128 or 64: config 2's D = 64; the first layer then has 2 k-steps and dX 4
+// M-tiles, the rows are 256 B)
+template <bool UPD, bool IDX, bool FUSE, int IN>
 __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const UpdateArgs& u) {
+  static_assert(IN == 128 || IN == 64, "row-owned T1: inputs of 128 or 64");
+  constexpr int NI = IN / 32;   // layer-0 k-steps (B-operand pieces xb[s], s < NI)
+  constexpr int MTI = IN / 16;  // dX M-tiles (row pieces xv[mt], mt < MTI)
   __shared__ __attribute__((aligned(16))) char wimg[RK_IMG];         // both towers' W0, W1 (rk_off)
   __shared__ __attribute__((aligned(16))) float xo[2][2][16 * 64];  // tower outputs per (tower, row half)
   __shared__ float bsum[2][RK_W0 + RK_W1];                          // row half 1's bias partials
   __shared__ float lrow[TR];                                        // row losses
-  __shared__ __attribute__((aligned(16))) float xr[4][16 * RK_IN];  // per wave: its 16 gathered rows
+  __shared__ __attribute__((aligned(16))) float xr[4][16 * IN];     // per wave: its 16 gathered rows
                                                                     // (fp32, 16-B chunk c of row n at c ^ n)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = wid >> 1, h = wid & 1, q = lane >> 4, n = lane & 15;
@@ -1561,10 +1594,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
       up = u.params[uc];
       um = u.exp_avg[uc];
       uv = u.exp_avg_sq[uc];
-      // one round of 32 slabs in flight (S <= 32: the host checks); bias parameters read slab 0 only
-#pragma unroll
-      for (int k = 0; k < 32; ++k)
-        uslab[k] = k < u.S && (k == 0 || useg.sisw) ? u.slab[(int64_t)k * u.P + uc] : 0.f;
+      t3_terms(u, uslab, uc, useg);
     }
   } else {
     load_biases();
@@ -1588,25 +1618,27 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   // so that the B-layout reads below are conflict-free; rows without an id read table row 0
   // (ignored)
   float* xw = xr[wid];
+  // (IN = 64: four 256-B rows per instruction)
+  constexpr int CPR = IDX ? IN / 8 : IN / 4;  // 16-B chunks per row (chunk swizzle: c ^ (row & (CPR - 1)))
+  constexpr int RPI = 64 / CPR;               // rows per wave instruction
   if (IDX) {
-    // bf16 rows (256 B): four per wave instruction, lane l carries 16-B chunk (l & 15) ^ row of
-    // row 4 i + (l >> 4)
-    const int rr0 = lane >> 4, pc = lane & 15;
+    // bf16 rows (2 IN bytes): lane l carries 16-B chunk (l % CPR) ^ row of row RPI i + l / CPR
+    const int rr0 = lane / CPR, pc = lane % CPR;
     const char* src0 = reinterpret_cast<const char*>(t ? a.gsrc[1] : a.gsrc[0]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 4 * i + rr0;
+    for (int i = 0; i < 16 / RPI; ++i) {
+      const int row = RPI * i + rr0;
       const int64_t rid = __shfl((long long)r, row, 64);
-      const char* src = src0 + (rid >= 0 ? rid : 0) * (RK_IN * 2) + 16 * (pc ^ row);
+      const char* src = src0 + (rid >= 0 ? rid : 0) * (IN * 2) + 16 * (pc ^ (row & (CPR - 1)));
       __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(reinterpret_cast<char*>(xw) + i * 1024), 16, 0, 0);
     }
   } else {
-    const int rr0 = lane >> 5, pc = lane & 31;
+    const int rr0 = lane / CPR, pc = lane % CPR;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = 2 * i + rr0;
+    for (int i = 0; i < 16 / RPI; ++i) {
+      const int row = RPI * i + rr0;
       const int64_t rid = __shfl((long long)r, row, 64);
-      const float* src = tab + (rid >= 0 ? rid : 0) * RK_IN + 4 * (pc ^ row);
+      const float* src = tab + (rid >= 0 ? rid : 0) * IN + 4 * (pc ^ row);
       __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(xw + i * 256), 16, 0, 0);
     }
   }
@@ -1624,10 +1656,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   RK_STAMP(1);
   if (FUSE) {
     if (pending) {
-      // the slab sum in order s = 0, 1, ... (update_block's), Adam, the copies; then publish
-#pragma unroll
-      for (int k = 0; k < 32; ++k)
-        if (k < u.S && (k == 0 || useg.sisw)) ug += uslab[k];
+      // the gradient summed as update_block sums it, Adam, the copies; then publish
+      ug = t3_sum(u, uslab, useg);
       if (uon) t3_apply(u, ui, useg, up, um, uv, ug, u.adam_pre[0], u.adam_pre[1], true);
       // small batches (few workgroups): further rounds of 256 parameters, one after another
       for (int k = 256; k < u.fuse_per; k += 256) {
@@ -1636,13 +1666,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
         const int64_t c2 = on2 ? i2 : 0;
         const T3Seg sg2 = t3_seg(u, c2);
         const float p2 = u.params[c2], m2 = u.exp_avg[c2], v2 = u.exp_avg_sq[c2];
-#pragma unroll
-        for (int q2 = 0; q2 < 32; ++q2)
-          uslab[q2] = q2 < u.S && (q2 == 0 || sg2.sisw) ? u.slab[(int64_t)q2 * u.P + c2] : 0.f;
-        float g2 = 0.f;
-#pragma unroll
-        for (int q2 = 0; q2 < 32; ++q2)
-          if (q2 < u.S && (q2 == 0 || sg2.sisw)) g2 += uslab[q2];
+        t3_terms(u, uslab, c2, sg2);
+        const float g2 = t3_sum(u, uslab, sg2);
         if (on2) t3_apply(u, i2, sg2, p2, m2, v2, g2, u.adam_pre[0], u.adam_pre[1], true);
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores (and the rows)
@@ -1688,20 +1713,20 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   bf16x8 xb[4];
   if (IDX) {  // the bf16 B operand straight from the returned rows
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(xw) + n * (RK_IN * 2) +
-                                                         16 * ((4 * s2 + q) ^ n));
+    for (int s2 = 0; s2 < NI; ++s2) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(xw) + n * (IN * 2) +
+                                                         16 * ((4 * s2 + q) ^ (n & (CPR - 1))));
       xb[s2] = r >= 0 ? v : (bf16x8)(__bf16)0.f;
     }
   } else {
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+    for (int mt = 0; mt < MTI; ++mt) {
       const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);
-      const f32x4 v = *reinterpret_cast<const f32x4*>(xw + n * RK_IN + 4 * (c ^ n));
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xw + n * IN + 4 * (c ^ n));
       xv[mt] = r >= 0 ? v : (f32x4)(0.f);
     }
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) xb[s2] = rk_pack(xv[2 * s2], xv[2 * s2 + 1]);
+    for (int s2 = 0; s2 < NI; ++s2) xb[s2] = rk_pack(xv[2 * s2], xv[2 * s2 + 1]);
   }
   // UPD, past barrier 1 (nothing waits on these until the row update): is the row looked up once in
   // this step (claim -> slot word in this batch's completed dedup table), its state
@@ -1718,7 +1743,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   const char* img1 = img0 + RK_W0 * 256;
   // ---- 1. layer 0: h^T = relu(W0 X^T + b0), 8 M-tiles x 4 k-steps
   f32x4 acc[8];
-  rk_gemm<8, 4, false>(acc, img0, xb, lane);
+  rk_gemm<8, NI, false>(acc, img0, xb, lane);
   RK_STAMP(4);
   bf16x8 hb[4];
 #pragma unroll
@@ -1747,7 +1772,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   // the slot word's low half holds the lookup count (little-endian; DD_CNT_BITS < 32)
   const uint32_t word = UPD ? reinterpret_cast<const uint32_t*>(&a.dd.slots[cl >= 0 ? cl : 0].word)[0] : 0u;
   // the T1 -> T2 strips of X and h (row-major): fire-and-forget stores
-  rk_strip<4>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);
+  rk_strip<NI>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);
   rk_strip<4>(hb, a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
   RK_STAMP(6);
   __syncthreads();
@@ -1820,7 +1845,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   }
   // ---- 6. dX^T = W0^T dZ0^T: 8 M-tiles x 4 k-steps; acc[mt] = dX features of xv[mt]
   RK_STAMP(9);
-  rk_gemm<8, 4, true>(acc, img0, z0b, lane);
+  rk_gemm<MTI, 4, true>(acc, img0, z0b, lane);
   RK_STAMP(10);
   // ---- 7. the row: UPD + looked up once -> row-wise Adagrad in place (the K3 update's arithmetic and
   // summation tree: feature groups of 4 combined at group bits 4, 3 (in lane), 2, 1 (lanes ^ 32,
@@ -1830,7 +1855,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   if (IDX) {  // dX -> the requester's gradient row in the send buffer (none for a zero row)
     const int32_t po = (int32_t)pout_raw.lo;
     store_dx = r >= 0 && po >= 0;
-    grow = (t ? a.gdst[1] : a.gdst[0]) + (int64_t)(store_dx ? po : 0) * RK_IN;
+    grow = (t ? a.gdst[1] : a.gdst[0]) + (int64_t)(store_dx ? po : 0) * IN;
   } else {
     grow = live ? a.gpooled + m * a.ldp + a.s.in_col[t] : nullptr;
     store_dx = live;
@@ -1839,36 +1864,43 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
     float e2[2];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const float s0 = rw_sq4(acc[0 + hh]), s1 = rw_sq4(acc[2 + hh]), s2 = rw_sq4(acc[4 + hh]), s3 = rw_sq4(acc[6 + hh]);
-      float c2 = (s0 + s2) + (s1 + s3);
+      // IN = 64: K3's first level (group bit 4) adds zeros, which is exact: only bit 3 remains
+      const float s0 = rw_sq4(acc[0 + hh]), s1 = rw_sq4(acc[2 + hh]);
+      float c2;
+      if constexpr (IN == 128) {
+        const float s2 = rw_sq4(acc[4 + hh]), s3 = rw_sq4(acc[6 + hh]);
+        c2 = (s0 + s2) + (s1 + s3);
+      } else {
+        c2 = s0 + s1;
+      }
       c2 += __shfl_xor(c2, 32, 64);
       c2 += __shfl_xor(c2, 16, 64);
       e2[hh] = c2;
     }
     RK_STAMP2(0);
     const float sq = e2[0] + e2[1];
-    const float snew = rw_state(s_old, sq, RK_IN);
+    const float snew = rw_state(s_old, sq, IN);
     const float step = rw_step(snew, a.ulr, a.ueps);
     const bool single = r >= 0 && cl >= 0 && (word & (uint32_t)DD_CNT_MASK) == 1u;
     // the updated rows go back through the wave's LDS rows (same chunk swizzle) and out as two
     // whole rows per store instruction, as they came in
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+    for (int mt = 0; mt < MTI; ++mt) {
       const int c = 8 * (mt >> 1) + 2 * q + (mt & 1);
-      *reinterpret_cast<f32x4*>(xw + n * RK_IN + 4 * (c ^ n)) = rw_apply(xv[mt], acc[mt], step);
+      *reinterpret_cast<f32x4*>(xw + n * IN + 4 * (c ^ n)) = rw_apply(xv[mt], acc[mt], step);
     }
     RK_STAMP2(1);
     asm volatile("" ::: "memory");  // LDS is in order per wave: only the compiler must not reorder
     {
-      const int rr0 = lane >> 5, pc = lane & 31;
+      const int rr0 = lane / CPR, pc = lane % CPR;
       float* wtab = t ? a.uw[1] : a.uw[0];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = 2 * i + rr0;
+      for (int i = 0; i < 16 / RPI; ++i) {
+        const int row = RPI * i + rr0;
         const int64_t rid = __shfl((long long)r, row, 64);
         const int sg = __shfl((int)single, row, 64);
-        const f32x4 w = *reinterpret_cast<const f32x4*>(xw + row * RK_IN + 4 * pc);
-        if (sg) *reinterpret_cast<f32x4*>(wtab + rid * RK_IN + 4 * (pc ^ row)) = w;
+        const f32x4 w = *reinterpret_cast<const f32x4*>(xw + row * IN + 4 * pc);
+        if (sg) *reinterpret_cast<f32x4*>(wtab + rid * IN + 4 * (pc ^ row)) = w;
       }
     }
     RK_STAMP2(2);
@@ -1879,7 +1911,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   }
   if (store_dx) {
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
+    for (int mt = 0; mt < MTI; ++mt)
       *reinterpret_cast<f32x4*>(grow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = acc[mt];
   }
   RK_STAMP2(3);
@@ -1887,7 +1919,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   if (!IDX && a.pooled_out && live) {
     float* prow = a.pooled_out + m * a.ldp + a.s.in_col[t];
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) *reinterpret_cast<f32x4*>(prow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = xv[mt];
+    for (int mt = 0; mt < MTI; ++mt) *reinterpret_cast<f32x4*>(prow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = xv[mt];
   }
   RK_STAMP(11);
   // ---- 8. the dZ strips; bias partials (fp32 column sums over the wave's rows, then row half 0 +
@@ -1924,13 +1956,14 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   if (!UPD && a.dd_on && q == 0) dd_insert_defer_finish_at(a.dd, pend, li, (int)blockIdx.x, 16 * wid + n);
   RK_STAMP(15);
 }
-template <bool UPD, bool IDX = false>
+template <bool UPD, bool IDX = false, int IN = 128>
 __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   const UpdateArgs u{};
-  tower_rows_body<UPD, IDX, false>(a, u);
+  tower_rows_body<UPD, IDX, false, IN>(a, u);
 }
+template <int IN = 128, bool IDX = false>
 __global__ void __launch_bounds__(256) tower_rows_t3_kernel(TowerArgs a, UpdateArgs u) {
-  tower_rows_body<true, false, true>(a, u);
+  tower_rows_body<!IDX, IDX, true, IN>(a, u);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2823,8 +2856,8 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.o_wtb = take((size_t)L.PW * 2);
   L.o_wbf = take((size_t)L.PW * 2);
   L.o_wtbf = take((size_t)L.PW * 2);
-  L.rows = s->L == 2 && s->in_dim[0] == RK_IN && s->in_dim[1] == RK_IN && s->width[0] == RK_W0 &&
-           s->width[1] == RK_W1 && !(s->flags & TT_TOWER_GENERAL_T1);
+  L.rows = s->L == 2 && s->in_dim[0] == s->in_dim[1] && (s->in_dim[0] == RK_IN || s->in_dim[0] == 64) &&
+           s->width[0] == RK_W0 && s->width[1] == RK_W1 && !(s->flags & TT_TOWER_GENERAL_T1);
   L.o_wimg = take(L.rows ? (size_t)RK_IMG : 0);
   L.o_tiles = take((size_t)nt * sizeof(WgradTile));
   L.o_dbg = take((size_t)(std::max<int64_t>(L.nwg * 2, 1024) * 8 + L.nwg * 16 * 9) * sizeof(int64_t));
@@ -2975,20 +3008,28 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
 #if TT_EXPERIMENTS
   if (getenv("TT_T1_CLASSIC")) rows_t1 = false;  // EXPERIMENT (A/B): tower_l2_kernel instead
 #endif
-  if (fuse && !(rows_t1 && a.uw[0] && !a.gpos[0]))
-    return fail(TT_EINVAL, "tower: the T3 + T1 launch serves the ring's row-owned gather + update shape only");
+  if (fuse && !(rows_t1 && ((a.uw[0] && !a.gpos[0]) || (a.gpos[0] && a.gsrc_bf16))))
+    return fail(TT_EINVAL, "tower: the T3 + T1 launch serves the row-owned gather + update and indexed bf16 forms only");
   if (rows_t1) {
     a.wimg = ws + L.o_wimg;
     if (fuse) {
-      tower_rows_t3_kernel<<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse);
+      if (a.gpos[0])
+        i0 == 64 ? tower_rows_t3_kernel<64, true><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse)
+                 : tower_rows_t3_kernel<128, true><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse);
+      else
+        i0 == 64 ? tower_rows_t3_kernel<64, false><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse)
+                 : tower_rows_t3_kernel<128, false><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse);
       return check_launch("tower_rows_gather_update_t3");
     }
     if (a.gpos[0])
-      tower_rows_kernel<false, true><<<g, dim3(256), 0, as_stream(stream)>>>(a);
+      i0 == 64 ? tower_rows_kernel<false, true, 64><<<g, dim3(256), 0, as_stream(stream)>>>(a)
+               : tower_rows_kernel<false, true, 128><<<g, dim3(256), 0, as_stream(stream)>>>(a);
     else if (a.uw[0])
-      tower_rows_kernel<true><<<g, dim3(256), 0, as_stream(stream)>>>(a);
+      i0 == 64 ? tower_rows_kernel<true, false, 64><<<g, dim3(256), 0, as_stream(stream)>>>(a)
+               : tower_rows_kernel<true, false, 128><<<g, dim3(256), 0, as_stream(stream)>>>(a);
     else
-      tower_rows_kernel<false><<<g, dim3(256), 0, as_stream(stream)>>>(a);
+      i0 == 64 ? tower_rows_kernel<false, false, 64><<<g, dim3(256), 0, as_stream(stream)>>>(a)
+               : tower_rows_kernel<false, false, 128><<<g, dim3(256), 0, as_stream(stream)>>>(a);
     return check_launch(a.uw[0] ? "tower_rows_gather_update" : "tower_rows_gather");
   }
   if (a.uw[0]) {  // in-place update of single-lookup rows: compile-time shapes only
@@ -3604,28 +3645,37 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
 
 // can every workgroup of the T3 + T1 launch (one per 32-row tile) be resident at once? (its
 // in-launch wait needs them all); cached per device
-static int t1f_capacity() {
-  static int cap[64];
-  static bool done[64];
+static int t1f_capacity(int in, bool idx) {
+  static int cap[64][4];
+  static bool done[64][4];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!done[dev]) {
+  const int w = (in == 64 ? 1 : 0) + (idx ? 2 : 0);
+  if (!done[dev][w]) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(tower_rows_t3_kernel), 256,
-                                                     0) != hipSuccess ||
+    const void* ks[4] = {reinterpret_cast<const void*>(tower_rows_t3_kernel<128, false>),
+                         reinterpret_cast<const void*>(tower_rows_t3_kernel<64, false>),
+                         reinterpret_cast<const void*>(tower_rows_t3_kernel<128, true>),
+                         reinterpret_cast<const void*>(tower_rows_t3_kernel<64, true>)};
+    const void* k = ks[w];
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return 0;
-    cap[dev] = per_cu * cus;
-    done[dev] = true;
+    cap[dev][w] = per_cu * cus;
+    done[dev][w] = true;
   }
-  return cap[dev];
+  return cap[dev][w];
 }
 
-int tt_tower_t3_fuse_supported(const tt_tower_shape_t* shape, int64_t B) {
+static int t3_fuse_ok(const tt_tower_shape_t* shape, int64_t B, bool idx) {
   TowerLayout L;
   if (tower_layout(shape, B, &L) != TT_OK) return 0;
   if (!L.rows || L.S > 32 || ceil_div(L.P, (int64_t)L.nwg) > 4096) return 0;
-  return L.nwg <= t1f_capacity() ? 1 : 0;
+  return L.nwg <= t1f_capacity(shape->in_dim[0], idx) ? 1 : 0;
+}
+
+int tt_tower_t3_fuse_supported(const tt_tower_shape_t* shape, int64_t B) {
+  return t3_fuse_ok(shape, B, false) && t3_fuse_ok(shape, B, true);
 }
 
 int64_t tt_tower_counter_offset(const tt_tower_shape_t* shape, int64_t B) {
@@ -3648,7 +3698,7 @@ int tt_tower_fwd_bwd_gather_update_t3(const tt_tower_shape_t* shape, int64_t B, 
   if (dedup_max_lookups < 2 * B || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
       dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) || (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
     return fail(TT_ECAPACITY, "tower_gather_update_t3: dedup workspace too small / misaligned");
-  if (!tt_tower_t3_fuse_supported(shape, B))
+  if (!t3_fuse_ok(shape, B, false))
     return fail(TT_EINVAL, "tower_gather_update_t3: shape / batch not servable (row-owned T1, <= 32 slabs, <= 4096 "
                            "parameters per workgroup, every workgroup resident)");
   TowerArgs a{};
@@ -3684,17 +3734,21 @@ int tt_tower_fwd_bwd_gather_update_t3(const tt_tower_shape_t* shape, int64_t B, 
 }
 
 int tt_tower_update_lazy(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
-                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
-                         size_t ws_bytes, void* stream) {
+                         float eps, float beta1, float beta2, float weight_decay, float* grads_out,
+                         const float* grads_in, int nsrc, int64_t src_stride, void* workspace, size_t ws_bytes,
+                         void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  if (grads_in && (nsrc < 1 || nsrc > 32 || (nsrc > 1 && src_stride < L.P)))
+    return fail(TT_EINVAL, "tower_update_lazy: bad gradient sources");
   const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
   UpdateArgs u;
   int64_t g3 = 0;
   rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
-               nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0, u, &g3);
+               grads_in, workspace, ws_bytes, pre, 1, nullptr, 1.f, grads_in ? nsrc : 1, grads_in ? src_stride : 0,
+               u, &g3);
   if (rc) return rc;
   u.lazy = 1;
   tower_update_kernel<<<dim3((unsigned)g3), dim3(256), 0, as_stream(stream)>>>(u);
@@ -3841,11 +3895,10 @@ int tt_tower_fwd_bwd_indexed_multi_bf16(const tt_tower_shape_t* shape, int64_t B
                    grad_scale, logits, workspace, ws_bytes, stream);
 }
 
-int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
-                                   const int32_t* const* pos_out, const void* const* rows_in,
-                                   float* const* grad_rows_out, const float* params, const void* labels,
-                                   int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
-                                   void* stream) {
+static int tower_indexed2(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
+                          const int32_t* const* pos_out, const void* const* rows_in, float* const* grad_rows_out,
+                          const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
+                          void* workspace, size_t ws_bytes, void* stream, const UpdateArgs* fuse) {
   if (!pos_in || !pos_out || !rows_in || !grad_rows_out) return fail(TT_EINVAL, "tower_indexed2: null pointer");
   TowerArgs a{};
   a.gsrc_bf16 = 1;
@@ -3860,7 +3913,43 @@ int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, con
   }
   return launch_t1(shape, B, a, nullptr,
                    std::max(shape->in_col[0] + shape->in_dim[0], shape->in_col[1] + shape->in_dim[1]), nullptr, params,
-                   labels, label_dtype, grad_scale, logits, workspace, ws_bytes, stream);
+                   labels, label_dtype, grad_scale, logits, workspace, ws_bytes, stream, fuse);
+}
+
+int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
+                                   const int32_t* const* pos_out, const void* const* rows_in,
+                                   float* const* grad_rows_out, const float* params, const void* labels,
+                                   int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+  return tower_indexed2(shape, B, pos_in, pos_out, rows_in, grad_rows_out, params, labels, label_dtype, grad_scale,
+                        logits, workspace, ws_bytes, stream, nullptr);
+}
+
+int tt_tower_fwd_bwd_indexed2_bf16_t3(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
+                                      const int32_t* const* pos_out, const void* const* rows_in,
+                                      float* const* grad_rows_out, float* params, float* exp_avg, float* exp_avg_sq,
+                                      float adam_eps, float beta1, float beta2, float weight_decay,
+                                      const float* grads_in, int nsrc, int64_t src_stride, const void* labels,
+                                      int label_dtype, float grad_scale, float* logits, void* workspace,
+                                      size_t ws_bytes, void* stream) {
+  TowerLayout L;
+  int rc = tower_layout(shape, B, &L);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
+  if (!grads_in || nsrc < 1 || nsrc > 32 || (nsrc > 1 && src_stride < L.P))
+    return fail(TT_EINVAL, "tower_indexed2_t3: bad gradient sources");
+  if (!t3_fuse_ok(shape, B, true))
+    return fail(TT_EINVAL, "tower_indexed2_t3: shape / batch not servable (row-owned T1, <= 4096 parameters per "
+                           "workgroup, every workgroup resident)");
+  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
+  UpdateArgs u;
+  int64_t g3 = 0;
+  rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, adam_eps, weight_decay, nullptr, 1, nullptr,
+               grads_in, workspace, ws_bytes, pre, 1, nullptr, 1.f, nsrc, src_stride, u, &g3);
+  if (rc) return rc;
+  u.fuse_per = (int)ceil_div(L.P, (int64_t)L.nwg);
+  return tower_indexed2(shape, B, pos_in, pos_out, rows_in, grad_rows_out, params, labels, label_dtype, grad_scale,
+                        logits, workspace, ws_bytes, stream, &u);
 }
 
 // ---- launch plans (include/tt_mi355x.h): the multi-role fused launches behind one entry point ----

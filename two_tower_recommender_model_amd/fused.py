@@ -582,8 +582,9 @@ class FusedTwoTowerStep:
             return
         tw = self.towers
         check(_lib.load().tt_tower_update_lazy(C.byref(tw.shape), self.B, ptr(self.params), ptr(self.exp_avg),
-                                               ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads),
-                                               ptr(tw.ws), tw.nbytes, stream_handle(self.device)), "tower_update_lazy")
+                                               ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads), None, 0,
+                                               0, ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
+              "tower_update_lazy")
 
     def fuse_timeouts(self) -> int:
         """In-launch waits of the fused T3 + T1 launch that gave up (must be 0; one sync)."""
