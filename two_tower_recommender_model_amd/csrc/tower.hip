@@ -1584,18 +1584,19 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   float up = 0.f, um = 0.f, uv = 0.f, ug = 0.f;
   float uslab[32];
   if (FUSE) {
+    // the share's loads are issued before the pending word is known (it almost always is: a
+    // branch on it would put a whole memory round trip in front of them)
+    ui = (int64_t)blockIdx.x * u.fuse_per + threadIdx.x;
+    const bool mine = (int)threadIdx.x < u.fuse_per && ui < u.P;
+    const int64_t uc = mine ? ui : 0;
+    useg = t3_seg(u, uc);
+    up = u.params[uc];
+    um = u.exp_avg[uc];
+    uv = u.exp_avg_sq[uc];
+    t3_terms(u, uslab, uc, useg);
     pending = __builtin_amdgcn_readfirstlane(
                   __hip_atomic_load(cw + CW_PENDING, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
-    ui = (int64_t)blockIdx.x * u.fuse_per + threadIdx.x;
-    uon = pending && (int)threadIdx.x < u.fuse_per && ui < u.P;
-    const int64_t uc = uon ? ui : 0;
-    useg = t3_seg(u, uc);
-    if (pending) {
-      up = u.params[uc];
-      um = u.exp_avg[uc];
-      uv = u.exp_avg_sq[uc];
-      t3_terms(u, uslab, uc, useg);
-    }
+    uon = pending && mine;
   } else {
     load_biases();
     __builtin_amdgcn_sched_barrier(0);
