@@ -1450,6 +1450,9 @@ __device__ __forceinline__ T3Seg t3_seg(const UpdateArgs& a, int64_t i) {
 // after the gradient g of parameter i (value p): gradient copies, Adam, the bf16 copies T1 reads
 __device__ __forceinline__ void t3_apply(const UpdateArgs& a, int64_t i, const T3Seg& sg, float p, float m,
                                          float v0, float g, float step_size, float bc2_sqrt, bool adam) {
+  // no fma contraction: the contraction choice would otherwise depend on the inlining context (T3,
+  // the fused T3 + T1 launch, the lazy flush), and every form must give the same bits
+#pragma clang fp contract(off)
   const int64_t e = i - sg.soff;
   if (a.grads_out) {
     if (a.out_copies <= 1) {
