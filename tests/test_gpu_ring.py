@@ -3,6 +3,8 @@ inside T1, the others by the tail launch from dX, then T3; or T2 + deferred inse
 update + T3): bit for bit the classic step (insert in T1, every row updated
 by K3), over resident batches with dropped ids, ids past N, repeated rows (2..30 lookups) and hot
 rows (> 30), through HIP graphs of several steps and eagerly."""
+import os
+
 import pytest
 import torch
 
@@ -150,7 +152,12 @@ def test_ring_t3_folded_into_t1_equals_three_launches(device, B):
     a = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=6)
     b = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=6)
     b._t1f = False
-    assert a.t1_fuse(), "the T3 + T1 launch should serve this shape on an MI355X"
+    a._t1f = None
+    os.environ["TT_T1_FUSE"] = "1"
+    try:
+        assert a.t1_fuse(), "the T3 + T1 launch should serve this shape on an MI355X"
+    finally:
+        del os.environ["TT_T1_FUSE"]
     for st in (a, b):
         st.capture_ring(batches, steps_per_graph=2)
         st.run(3)

@@ -5,6 +5,7 @@ in-process all-to-all (ThreadComm) against the oracle: the rows each rank's towe
 oracle tables bit for bit, every shard after each step equals the oracle's row-wise Adagrad over
 the union of the gradient rows the ranks produced (ascending (rank, bag) order), and the
 data-parallel towers stay identical on every rank."""
+import os
 import threading
 
 import numpy as np
@@ -493,12 +494,17 @@ def test_sharded_adam_folded_into_t1_equals_separate_launch(device, W):
         def build(r):
             torch.cuda.set_device(device)
             steps[r] = FusedShardedTwoTowerStep(comms[r], N, D, [128, 64], B, device, full_tables=full, seed=9)
-            if not fuse:
-                steps[r]._t1f = False
+            steps[r]._t1f = False
 
         _run_ranks([lambda r=r: build(r) for r in range(W)])
-        if fuse:
-            assert steps[0].t1_fuse(), "the fused Adam + T1 launch should serve this shape on an MI355X"
+        if fuse:  # opt-in (TT_T1_FUSE=1), decided per step object before its first step
+            os.environ["TT_T1_FUSE"] = "1"
+            try:
+                for st in steps:
+                    st._t1f = None
+                    assert st.t1_fuse(), "the fused Adam + T1 launch should serve this shape on an MI355X"
+            finally:
+                del os.environ["TT_T1_FUSE"]
 
         def go(r):
             torch.cuda.set_device(device)

@@ -1600,6 +1600,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
     pending = __builtin_amdgcn_readfirstlane(
                   __hip_atomic_load(cw + CW_PENDING, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
     uon = pending && mine;
+    RK_STAMP2(4);
   } else {
     load_biases();
     __builtin_amdgcn_sched_barrier(0);
@@ -1675,11 +1676,13 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
         if (on2) t3_apply(u, i2, sg2, p2, m2, v2, g2, u.adam_pre[0], u.adam_pre[1], true);
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores (and the rows)
+      RK_STAMP2(5);
       __syncthreads();
       if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(cw + CW_FUSE_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        RK_STAMP2(8);
         const unsigned nwg = gridDim.x;
         int spin = 0;
         while (__hip_atomic_load(cw + CW_FUSE_ARRIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg) {
@@ -1698,7 +1701,9 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
           __hip_atomic_store(cw + CW_PENDING, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+      RK_STAMP2(6);
       __syncthreads();
+      RK_STAMP2(7);
     }
     load_biases();
     __builtin_amdgcn_sched_barrier(0);

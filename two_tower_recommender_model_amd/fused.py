@@ -565,11 +565,13 @@ class FusedTwoTowerStep:
             self.towers.update(self.params, do_adam=False)
 
     def t1_fuse(self) -> bool:
-        """Does the ring fold T3 into the next step's T1 (two launches per step)? The shape must be
-        the row-owned T1's with every T1 workgroup resident at once (tt_tower_t3_fuse_supported);
-        TT_T1_FUSE=0 turns it off."""
+        """Does the ring fold T3 into the next step's T1 (two launches per step)? Opt-in
+        (TT_T1_FUSE=1): measured slower than the three-launch ring (the in-launch
+        wait for every workgroup's share costs more than the kernel boundary it removes). The shape
+        must be the row-owned T1's with every T1 workgroup resident at once
+        (tt_tower_t3_fuse_supported)."""
         if getattr(self, "_t1f", None) is None:
-            self._t1f = bool(self.towers is not None and os.environ.get("TT_T1_FUSE", "1") != "0"
+            self._t1f = bool(self.towers is not None and os.environ.get("TT_T1_FUSE", "0") == "1"
                              and self.ring_supported()
                              and _lib.load().tt_tower_t3_fuse_supported(C.byref(self.towers.shape), self.B) == 1)
         return self._t1f

@@ -435,7 +435,8 @@ class FusedShardedTwoTowerStep:
     def t1_fuse(self) -> bool:
         """Does the pipelined step apply the tower Adam update at the start of the NEXT step's T1
         launch (tt_tower_fwd_bwd_indexed2_bf16_t3) instead of its own launch? Single feature per
-        tower (the row-owned T1), every T1 workgroup resident, TT_T1_FUSE != 0."""
+        tower (the row-owned T1), every T1 workgroup resident; opt-in (TT_T1_FUSE=1: measured slower,
+        as for the single-GPU ring)."""
         if getattr(self, "_t1f", None) is None:
             # ranks sharing this GPU (thread ranks; processes of a one-GPU rehearsal) run their T1
             # launches concurrently: every one of their workgroups must be resident together, so
@@ -445,7 +446,7 @@ class FusedShardedTwoTowerStep:
             else:
                 local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
                 share = max(1, -(-local // max(1, torch.cuda.device_count())))
-            self._t1f = bool(not self.multi and os.environ.get("TT_T1_FUSE", "1") != "0" and self.W <= 32
+            self._t1f = bool(not self.multi and os.environ.get("TT_T1_FUSE", "0") == "1" and self.W <= 32
                              and _lib.load().tt_tower_t3_fuse_supported(C.byref(self.towers.shape),
                                                                         self.B * share) == 1)
         return self._t1f
