@@ -255,10 +255,7 @@ constexpr int DD_HOT_TEAM = 8;              // at most this many workgroups shar
 #endif
 // LDS of the hot role (list + wave totals + group partials), provided by the launching kernel so a
 // combined launch can overlay it on its other roles' LDS
-// up to DD_HOT_VAR hot rows, a row's team size follows its share of the hot lookups (team prefix
-// sums in LDS); beyond, every row gets the same team (dd_hot_team)
-constexpr int DD_HOT_VAR = 256;
-constexpr int DD_SMEM_HOT = DD_HOT_CH * 4 + 16 + 8 * 32 * 16 + (DD_HOT_VAR + 4) * 4;
+constexpr int DD_SMEM_HOT = DD_HOT_CH * 4 + 16 + 8 * 32 * 16;
 constexpr int DD_SMEM = DD_SMEM_HOT + (int)sizeof(DdMeta);  // + the per-workgroup meta copy
 
 // members per hot row: as many as the hot workgroups allow in one round (at least 1), at most one
@@ -268,18 +265,11 @@ __device__ __forceinline__ int dd_hot_team(int nh, int64_t n, int hot_wgs) {
   return max(1, min(min(DD_HOT_TEAM, npass), hot_wgs / max(1, nh)));
 }
 
-// every hot workgroup checks in once, after its last read of the hot rows' slots (their counts set
-// the teams); the last one frees those slots and resets the hot-row count and the ticket.
-// flag: one int of LDS. Called by the whole workgroup.
-__device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs, int* flag) {
-  __syncthreads();
-  if (threadIdx.x == 0) *flag = atomicAdd(&ws.ctr[1], 1) == hot_wgs - 1;
-  __syncthreads();
-  if (*flag) {
-    const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
-    for (int j = threadIdx.x; j < nh; j += blockDim.x) ws.slots[ws.hot[j]].word = DD_EMPTY;
-    __syncthreads();
-    if (threadIdx.x == 0) {
+// every hot workgroup checks in once; the last one resets the hot-row count and the ticket
+__device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs) {
+  if (threadIdx.x == 0) {
+    const int tk = atomicAdd(&ws.ctr[1], 1);
+    if (tk == hot_wgs - 1) {
       atomicExch(&ws.ctr[0], 0);
       atomicExch(&ws.ctr[1], 0);
     }
@@ -287,9 +277,7 @@ __device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs, in
 }
 
 // Rows looked up more than DD_INL times in the step. A row is split over a team of K workgroups
-// (up to DD_HOT_VAR hot rows: K_j = its share of the step's hot lookups x hot_wgs, clamped to
-// [1, min(DD_HOT_TEAM, passes)] — the Zipf head's rows get the big teams; beyond: dd_hot_team for
-// every row): member k scans passes k, k + K, ... of the step's keys (4096
+// (dd_hot_team): member k scans passes k, k + K, ... of the step's keys (4096
 // a pass, the next pass's keys in flight beside this pass's matching), its 8 groups add the pass's
 // matches at positions == group (mod 8) in ascending order (8 rows in flight), and the group sums
 // are added in group order: the member's partial. Members publish their partial write-through
@@ -303,65 +291,14 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
   f32x4v (*part)[32] = reinterpret_cast<f32x4v (*)[32]>(smem);       // [8][32], 16-B aligned
   int* list = reinterpret_cast<int*>(smem + 8 * 32 * 16);             // [DD_HOT_CH]
   int* wtot = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4);  // [4]
-  int* kpre = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4 + 16);  // [DD_HOT_VAR + 1]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = tid >> 5, hl = tid & 31;
   const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
   const int nn = (int)n;  // lookups < 2^18 (DD_CNT_BITS): 32-bit indices
   const int npass = (nn + DD_HOT_CH - 1) / DD_HOT_CH;
-  const int K0 = dd_hot_team(nh, n, hot_wgs);
-  const int kmax = min(DD_HOT_TEAM, npass);
-  const bool var = nh <= DD_HOT_VAR && kmax > 1;
-  int members = nh * K0;
-  if (var) {
-    // team sizes from the rows' lookup counts (every hot workgroup computes the same prefix)
-    if (wid == 0) {
-      uint32_t c[DD_HOT_VAR / 64];
-#pragma unroll
-      for (int i = 0; i < DD_HOT_VAR / 64; ++i) {
-        const int j = lane + 64 * i;
-        c[i] = j < nh ? (uint32_t)(ws.slots[ws.hot[j]].word & (uint64_t)DD_CNT_MASK) : 0u;
-      }
-      uint32_t tot = 0;
-#pragma unroll
-      for (int i = 0; i < DD_HOT_VAR / 64; ++i) tot += c[i];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-      int base = 0;
-#pragma unroll
-      for (int i = 0; i < DD_HOT_VAR / 64; ++i) {
-        const int j = lane + 64 * i;
-        const int kj = j < nh ? min(kmax, max(1, (int)((uint64_t)c[i] * (uint64_t)hot_wgs / max(1u, tot)))) : 0;
-        int inc = kj;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(inc, o, 64);
-          if (lane >= o) inc += y;
-        }
-        if (j < nh) kpre[j] = base + inc - kj;
-        base += __shfl(inc, 63, 64);
-      }
-      if (lane == 0) kpre[nh] = base;
-    }
-    __syncthreads();
-    members = kpre[nh];
-  }
-  for (int w = bid; w < members; w += hot_wgs) {
-    int j, k, K;
-    if (var) {  // the row whose team holds member w: largest j with kpre[j] <= w
-      int lo = 0, hi = nh;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (kpre[mid] <= w) lo = mid; else hi = mid;
-      }
-      j = lo;
-      k = w - kpre[j];
-      K = kpre[j + 1] - kpre[j];
-    } else {
-      j = w / K0;
-      k = w - j * K0;
-      K = K0;
-    }
+  const int K = dd_hot_team(nh, n, hot_wgs);
+  for (int w = bid; w < nh * K; w += hot_wgs) {
+    const int j = w / K, k = w - j * K;
     const int32_t h = ws.hot[j];
     const uint64_t key = ws.slots[h].word >> DD_CNT_BITS;
     const int t = (int)(key >> DD_TABLE_SHIFT);
@@ -477,7 +414,10 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
             *reinterpret_cast<f32x4v*>(wrow + hl * 4) =
                 rw_apply(*reinterpret_cast<const f32x4v*>(wrow + hl * 4), g, step);
           __builtin_amdgcn_wave_barrier();
-          if (lane == 0) *srow = snew;  // (the slot is freed by the last hot workgroup's ticket)
+          if (lane == 0) {
+            *srow = snew;
+            ws.slots[h].word = DD_EMPTY;
+          }
 #if DD_HOT_STAMPS
           DD_STAMP(7);  // row update issued
 #endif
@@ -486,7 +426,7 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
     }
     __syncthreads();
   }
-  dd_hot_ticket(ws, hot_wgs, wtot);
+  dd_hot_ticket(ws, hot_wgs);
 }
 
 // host: validate + fill the update launch's arguments; *grid = its workgroup count
@@ -509,10 +449,8 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     // a workgroup with no hot work item (most of them at uniform ids) only checks in: the ticket
     // that resets the hot-row count once every hot workgroup has read it
     const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
-    // an upper bound of the team members (dd_hot_role: at most nh x the largest team); the role's
-    // workgroups past the actual count only check in
-    if (bid >= nh * min(DD_HOT_TEAM, (int)((a.n + DD_HOT_CH - 1) / DD_HOT_CH))) {
-      dd_hot_ticket(ws, a.hot_wgs, reinterpret_cast<int*>(smem));
+    if (bid >= nh * dd_hot_team(nh, a.n, a.hot_wgs)) {
+      dd_hot_ticket(ws, a.hot_wgs);
       return;
     }
     dd_meta_fill(m, lm);
