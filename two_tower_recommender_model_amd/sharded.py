@@ -111,6 +111,13 @@ class TorchComm:
                     raise _lib.TTError("an eager collective did not complete before graph capture")
                 time.sleep(0.001)
         self._eager.clear()
+        # ProcessGroupNCCL's watchdog drops a completed work only on its next pass (every 100 ms) and
+        # queries its event until then; an event query racing the capture's first collective
+        # invalidated the capture on MI355X once in ~10 runs (hipErrorStreamCaptureInvalidated, then
+        # the watchdog aborting the process). Every eager work — these and the untracked synchronous
+        # ones (capacity / flag all-reduces) — is complete on the device now: let the watchdog
+        # retire them before the capture begins.
+        time.sleep(0.35)
 
     def all_reduce_max_(self, t: torch.Tensor) -> None:
         if self.world > 1 or self.always:
