@@ -282,6 +282,9 @@ SIGNATURES = {
         [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _int, _i64, _vp, _int, _f32,
          _vp, _vp, _sz, _vp],
     ),
+    "tt_bwd_rowwise_adagrad_part": (
+        _int, [_ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _int, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _int, _vp],
+    ),
     "tt_launch": (_int, [C.c_void_p, _vp]),
 }
 
@@ -337,6 +340,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_gather_update_t3",
     "tt_tower_update_lazy",
     "tt_tower_fwd_bwd_indexed2_bf16_t3",
+    "tt_bwd_rowwise_adagrad_part",
     "tt_launch",
 ]
 

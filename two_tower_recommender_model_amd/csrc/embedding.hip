@@ -1464,11 +1464,10 @@ int tt_bwd_prepare_cols(const tt_table_meta_t* tables, int T, const tt_feature_m
   return launch_scan_scatter(m, nullptr, w, st, gb);
 }
 
-int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
-                           int F, int64_t B, const float* grad_out, int64_t ldg,
-                           const int32_t* offsets, int pooling, float* weights, float* state,
-                           float lr, float eps, void* workspace, size_t ws_bytes,
-                           int64_t max_lookups, void* stream) {
+static int bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
+                               int64_t B, const float* grad_out, int64_t ldg, const int32_t* offsets, int pooling,
+                               float* weights, float* state, float lr, float eps, void* workspace, size_t ws_bytes,
+                               int64_t max_lookups, void* stream, int part) {
   EmbMeta m{};
   int rc = pack_meta(m, tables, T, features, F, B);
   if (rc) return rc;
@@ -1499,13 +1498,14 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
   bwd_layout(workspace, max_lookups, &w);
   hipStream_t st = as_stream(stream);
   const int64_t tiles = ceil_div((int64_t)F * B, TILE_BAGS);
-  if (offsets && F * B > 0 && tiles <= INT32_MAX) {  // once-looked-up rows of a KJT-form prepare (device flag)
+  if (part != 2 && offsets && F * B > 0 && tiles <= INT32_MAX) {  // once-looked-up rows of a KJT-form prepare
     if (narrow)
       bwd_adagrad_direct_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights,
                                                                             state, lr, eps, w);
     else
       bwd_single_fix_kernel<<<dim3((unsigned)tiles), dim3(256), 0, st>>>(m, offsets, w);
   }
+  if (part == 1) return check_launch("bwd_rowwise_adagrad_direct");
   if (narrow) {
     const int grid = (int)std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(max_lookups, 8)));
     bwd_adagrad_narrow_kernel<<<dim3(grid), dim3(256), 0, st>>>(m, grad_out, ldg, offsets, pooling, weights, state,
@@ -1523,6 +1523,25 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
     bwd_hot_final_kernel<<<dim3(fgrid), dim3(256), 0, st>>>(m, weights, state, lr, eps, w);
   }
   return check_launch("bwd_rowwise_adagrad");
+}
+
+int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
+                           int F, int64_t B, const float* grad_out, int64_t ldg,
+                           const int32_t* offsets, int pooling, float* weights, float* state,
+                           float lr, float eps, void* workspace, size_t ws_bytes,
+                           int64_t max_lookups, void* stream) {
+  return bwd_rowwise_adagrad(tables, T, features, F, B, grad_out, ldg, offsets, pooling, weights, state, lr, eps,
+                             workspace, ws_bytes, max_lookups, stream, 0);
+}
+
+int tt_bwd_rowwise_adagrad_part(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
+                                int64_t B, const float* grad_out, int64_t ldg, const int32_t* offsets, int pooling,
+                                float* weights, float* state, float lr, float eps, void* workspace, size_t ws_bytes,
+                                int64_t max_lookups, int part, void* stream) {
+  if (part < 0 || part > 2) return fail(TT_EINVAL, "bwd_rowwise_adagrad_part: part must be 0, 1 or 2");
+  if (part == 1 && !offsets) return fail(TT_EINVAL, "bwd_rowwise_adagrad_part: part 1 needs the KJT offsets");
+  return bwd_rowwise_adagrad(tables, T, features, F, B, grad_out, ldg, offsets, pooling, weights, state, lr, eps,
+                             workspace, ws_bytes, max_lookups, stream, part);
 }
 
 int tt_pooled_bwd_dense(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,

@@ -1531,9 +1531,12 @@ constexpr int CW_PENDING = 2, CW_LAZY_ARRIVE = 3, CW_FUSE_ARRIVE = 4, CW_FUSE_PA
 // The table rows are gathered while the update runs: they do not depend on it.
 // IN: the input width (128 or 64: config 2's D = 64; the first layer then has 2 k-steps and dX 4
 // M-tiles, the rows are 256 B)
-template <bool UPD, bool IDX, bool FUSE, int IN>
+// POOL: the input rows are the pooled matrix's (tower t's row m at a.pooled + m ldp + in_col[t]:
+// the multi-hot path's T1 after tt_pooled_fwd), no ids, no dedup
+template <bool UPD, bool IDX, bool FUSE, int IN, bool POOL = false>
 __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const UpdateArgs& u) {
   static_assert(IN == 128 || IN == 64, "row-owned T1: inputs of 128 or 64");
+  static_assert(!POOL || (!UPD && !IDX && !FUSE), "pooled input: the plain T1 only");
   constexpr int NI = IN / 32;   // layer-0 k-steps (B-operand pieces xb[s], s < NI)
   constexpr int MTI = IN / 16;  // dX M-tiles (row pieces xv[mt], mt < MTI)
   __shared__ __attribute__((aligned(16))) char wimg[RK_IMG];         // both towers' W0, W1 (rk_off)
@@ -1556,7 +1559,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   if (IDX) {
     id_raw.lo = (uint32_t)(t ? a.gpos[1] : a.gpos[0])[mc];
     pout_raw.lo = a.gpos_out[0] ? (uint32_t)(t ? a.gpos_out[1] : a.gpos_out[0])[mc] : id_raw.lo;
-  } else {
+  } else if (!POOL) {
     id_raw = rk_raw(t ? a.gcol[1] : a.gcol[0], wide, mc);
   }
   const RkRaw lab_raw = rk_raw(a.labels, a.label_dtype == TT_I64, mc);
@@ -1608,13 +1611,16 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   }
   __builtin_amdgcn_sched_barrier(0);
   int64_t r;  // the row's index in its source (table row / returned-rows buffer row), -1: zeros
-  if (IDX) {
+  if (POOL) {
+    r = live ? m : -1;
+  } else if (IDX) {
     r = live ? (int64_t)(int32_t)id_raw.lo : -1;
   } else {
     const int64_t id = live ? rk_id(id_raw, wide) : 0;
     r = id != 0 ? py_mod64(id, t ? a.gmod[1] : a.gmod[0]) : -1;
   }
-  const float* tab = t ? a.gtab[1] : a.gtab[0];
+  const float* tab = POOL ? a.pooled + a.s.in_col[t] : (t ? a.gtab[1] : a.gtab[0]);
+  const int64_t rstride = POOL ? a.ldp : IN;  // floats between consecutive source rows
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) void glb_void;
   // the wave's 16 rows -> LDS by LDS-DMA, two whole 512-B rows per wave instruction (two TLB pages
@@ -1643,7 +1649,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
     for (int i = 0; i < 16 / RPI; ++i) {
       const int row = RPI * i + rr0;
       const int64_t rid = __shfl((long long)r, row, 64);
-      const float* src = tab + (rid >= 0 ? rid : 0) * IN + 4 * (pc ^ row);
+      const float* src = tab + (rid >= 0 ? rid : 0) * rstride + 4 * (pc ^ row);
       __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(xw + i * 256), 16, 0, 0);
     }
   }
@@ -1925,7 +1931,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   }
   RK_STAMP2(3);
   if (t == 0 && q == 0 && live) a.logits[m] = d;  // after the row update (see rk_strip)
-  if (!IDX && a.pooled_out && live) {
+  if (!IDX && !POOL && a.pooled_out && live) {
     float* prow = a.pooled_out + m * a.ldp + a.s.in_col[t];
 #pragma unroll
     for (int mt = 0; mt < MTI; ++mt) *reinterpret_cast<f32x4*>(prow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = xv[mt];
@@ -1965,10 +1971,10 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   if (!UPD && a.dd_on && q == 0) dd_insert_defer_finish_at(a.dd, pend, li, (int)blockIdx.x, 16 * wid + n);
   RK_STAMP(15);
 }
-template <bool UPD, bool IDX = false, int IN = 128>
+template <bool UPD, bool IDX = false, int IN = 128, bool POOL = false>
 __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
   const UpdateArgs u{};
-  tower_rows_body<UPD, IDX, false, IN>(a, u);
+  tower_rows_body<UPD, IDX, false, IN, POOL>(a, u);
 }
 template <int IN = 128, bool IDX = false>
 __global__ void __launch_bounds__(256) tower_rows_t3_kernel(TowerArgs a, UpdateArgs u) {
@@ -3014,6 +3020,10 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   }
   // single-hot rows gathered from the tables (not indexed / multi-hot / pooled input): the row-owned T1
   bool rows_t1 = L.rows && !a.ipos && !a.mval && ((a.gcol[0] && !a.gpos[0]) || (a.gpos[0] && a.gsrc_bf16));
+  // pooled input (the multi-hot path after tt_pooled_fwd): the row-owned T1 reads the pooled rows
+  const bool rows_pool = L.rows && !a.ipos && !a.mval && !a.gcol[0] && !a.gpos[0] && pooled &&
+                         !(reinterpret_cast<uintptr_t>(pooled) & 15);
+  bool rows_pool_ok = true;
 #if TT_EXPERIMENTS
   if (getenv("TT_T1_CLASSIC")) rows_t1 = false;  // EXPERIMENT (A/B): tower_l2_kernel instead
 #endif
@@ -3040,6 +3050,15 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
       i0 == 64 ? tower_rows_kernel<false, false, 64><<<g, dim3(256), 0, as_stream(stream)>>>(a)
                : tower_rows_kernel<false, false, 128><<<g, dim3(256), 0, as_stream(stream)>>>(a);
     return check_launch(a.uw[0] ? "tower_rows_gather_update" : "tower_rows_gather");
+  }
+#if TT_EXPERIMENTS
+  if (getenv("TT_T1_CLASSIC")) rows_pool_ok = false;
+#endif
+  if (rows_pool && rows_pool_ok) {
+    a.wimg = ws + L.o_wimg;
+    i0 == 64 ? tower_rows_kernel<false, false, 64, true><<<g, dim3(256), 0, as_stream(stream)>>>(a)
+             : tower_rows_kernel<false, false, 128, true><<<g, dim3(256), 0, as_stream(stream)>>>(a);
+    return check_launch("tower_rows_pooled");
   }
   if (a.uw[0]) {  // in-place update of single-lookup rows: compile-time shapes only
     if (two && i0 == 128 && i1 == 128 && w0 == 128 && w1 == 64)

@@ -163,6 +163,11 @@ class FusedTwoTowerStep:
         self.dot_bce = ops.DotBCE(dev, B)
         self.tables.ensure_bwd_workspace(self.max_lookups)
         self.side = torch.cuda.Stream(device=dev) if overlap_prepare else None
+        # multi-hot step: the rows looked up more than once (tt_bwd_rowwise_adagrad_part 2) on their
+        # own stream beside the once-looked-up rows' update (part 1, the step's critical path);
+        # TT_KJT_SPLIT_UPDATE=0: one stream (A/B measurement)
+        self.side3 = (torch.cuda.Stream(device=dev)
+                      if overlap_prepare and os.environ.get("TT_KJT_SPLIT_UPDATE", "1") != "0" else None)
         # bf16 towers on the three fused kernels when the shape allows (else per-layer GEMMs)
         self.towers = None
         if precision == "bf16" and fused_towers and ops.FusedTowers.supported(
@@ -424,7 +429,7 @@ class FusedTwoTowerStep:
         # the next batch's grouping beside this step's embedding update rather than beside T1: T1's
         # workgroups each take a whole CU's LDS, so the grouping kernels' workgroups would hold CUs
         # T1 waits for
-        defer_prepare = ahead and self.gather_kjt
+        defer_prepare = ahead and self.kjt_mode == "kjt" and self.towers is not None and not self.gather
         if prepare is not None and not defer_prepare:
             launch_prepare()
         if self.gather:
@@ -456,12 +461,15 @@ class FusedTwoTowerStep:
             return
         if self.towers is not None:
             # T1 on the critical path; T2 + T3 (weight grads, Adam) beside the embedding update
-            if self.gather_kjt:
+            if self.gather_kjt or not self.gather:
                 self._mark("t1", 0)
-                self.towers.fwd_bwd_kjt(self.values, self.offsets,
-                                        [self.tables.table_view(0), self.tables.table_view(1)], self.gpooled,
-                                        self.params, self.labels, self.logits,
-                                        pooled_out=self.pooled if self.materialize_pooled else None)
+                if self.gather_kjt:
+                    self.towers.fwd_bwd_kjt(self.values, self.offsets,
+                                            [self.tables.table_view(0), self.tables.table_view(1)], self.gpooled,
+                                            self.params, self.labels, self.logits,
+                                            pooled_out=self.pooled if self.materialize_pooled else None)
+                else:  # tt_pooled_fwd above, then T1 on the pooled rows
+                    self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
                 self._mark("t1", 1)
                 if defer_prepare and self.side2 is not None and _KJT_UPDATE_FIRST:
                     # the row update (the step's critical path) enqueued right behind T1 on the
@@ -472,21 +480,26 @@ class FusedTwoTowerStep:
                     t1_done.record(main)
                     self.tables.use_bwd_workspace(parity)  # (prepare() leaves it so; it runs later here)
                     self._mark("upd", 0)
-                    self._emb_update()
+                    split = self.side3 is not None and self.offsets_used is not None
+                    if split:  # the once-looked-up rows here, the others beside them (disjoint rows)
+                        self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, self.B, self.lr_emb, self.eps,
+                                                        part=1)
+                    else:
+                        self._emb_update()
                     self._mark("upd", 1)
-                    for st, work in ((self.side, prepare), (self.side2, self._kjt_t2t3)):
+                    branches = [(self.side, prepare), (self.side2, self._kjt_t2t3)]
+                    if split:
+                        branches.append((self.side3, lambda: self.tables.bwd_rowwise_adagrad(
+                            self.gpooled, self.offsets_used, self.B, self.lr_emb, self.eps, part=2)))
+                    for st, work in branches:
                         st.wait_event(t1_done)
                         with torch.cuda.stream(st):
                             work()
-                    main.wait_stream(self.side)
-                    main.wait_stream(self.side2)
+                    for st, _ in branches:
+                        main.wait_stream(st)
                     return
                 if defer_prepare:
                     launch_prepare()
-            elif not self.gather:
-                self._mark("t1", 0)
-                self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
-                self._mark("t1", 1)
             s2 = self.side2 if self.side2 is not None else main
             if self.side2 is not None:
                 self.side2.wait_stream(main)

@@ -326,10 +326,19 @@ class TableSet:
                                           self._bwd_cap, stream_handle(self.device)), "bwd_prepare_cols")
 
     def bwd_rowwise_adagrad(self, grad_out: torch.Tensor, offsets: Optional[torch.Tensor], B: int, lr: float,
-                            eps: float, pooling: int = TT_POOL_SUM) -> None:
+                            eps: float, pooling: int = TT_POOL_SUM, part: int = 0) -> None:
+        """part 0: every touched row; 1: the rows looked up once (KJT form); 2: the others
+        (tt_bwd_rowwise_adagrad_part: the two parts touch disjoint rows, two streams may run them)."""
         _dev(grad_out)
         if grad_out.dtype != torch.float32 or grad_out.stride(1) != 1:
             raise _lib.TTError("bwd: grad_out must be fp32 with unit column stride")
+        if part:
+            check(_lib_().tt_bwd_rowwise_adagrad_part(self._tm, self.T, self._fm, self.F, B, ptr(grad_out),
+                                                      grad_out.stride(0), ptr(offsets), pooling, ptr(self.weights),
+                                                      ptr(self.state), float(lr), float(eps), ptr(self._bwd_ws),
+                                                      self._bwd_ws.numel(), self._bwd_cap, int(part),
+                                                      stream_handle(self.device)), "bwd_rowwise_adagrad_part")
+            return
         check(_lib_().tt_bwd_rowwise_adagrad(self._tm, self.T, self._fm, self.F, B, ptr(grad_out),
                                              grad_out.stride(0), ptr(offsets), pooling, ptr(self.weights),
                                              ptr(self.state), float(lr), float(eps), ptr(self._bwd_ws),
