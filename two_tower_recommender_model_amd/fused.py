@@ -168,6 +168,11 @@ class FusedTwoTowerStep:
         # TT_KJT_SPLIT_UPDATE=0: one stream (A/B measurement)
         self.side3 = (torch.cuda.Stream(device=dev)
                       if overlap_prepare and os.environ.get("TT_KJT_SPLIT_UPDATE", "1") != "0" else None)
+        # multi-hot pipelined step: the next batch's grouping is joined by the NEXT step's update
+        # (it may run on beside that step's T1) instead of at this step's end;
+        # TT_KJT_CROSS_STEP=0: joined at the end (A/B measurement)
+        self.cross_step_grouping = os.environ.get("TT_KJT_CROSS_STEP", "1") != "0"
+        self._prep_event = None
         # bf16 towers on the three fused kernels when the shape allows (else per-layer GEMMs)
         self.towers = None
         if precision == "bf16" and fused_towers and ops.FusedTowers.supported(
@@ -301,11 +306,21 @@ class FusedTwoTowerStep:
                 for v, o, lab, nxt, par in items:
                     self.values, self.offsets, self.labels = v, o, lab
                     self.step(next_kjt=nxt, parity=par)
+                self.kjt_join()  # every forked stream rejoins inside the graph
         torch.cuda.current_stream(self.device).wait_stream(s)
         if not keep_graph:
             _lib.graph_upload(g, self.device)
         torch.cuda.synchronize(self.device)
         return g
+
+    def kjt_join(self) -> None:
+        """Make the current stream wait for the next batch's grouping a pipelined multi-hot step left
+        running on the side stream (the following step joins it before its update; a captured graph
+        and any other use join it here)."""
+        ev = getattr(self, "_prep_event", None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            self._prep_event = None
 
     def kjt_ring_prime(self, values: torch.Tensor, offsets: torch.Tensor, parity: int) -> None:
         """Group the first batch of a pipelined multi-hot sequence into workspace ``parity`` (every
@@ -387,6 +402,8 @@ class FusedTwoTowerStep:
         B, F = self.B, self.F
         main = torch.cuda.current_stream(self.device)
         ahead = next_kjt is not None
+        if not ahead:
+            self.kjt_join()
         if ahead and not (self.kjt_input and self.side is not None):
             raise _lib.TTError("step(next_kjt): needs multi-hot input (max_lookups) and overlap_prepare")
         if self.kjt_mode == "kjt":
@@ -476,6 +493,9 @@ class FusedTwoTowerStep:
                     # capture stream, the two side branches forked from T1's end after it: in the
                     # graph the branches captured first started first, ~12 us apart, and the
                     # update came third
+                    # this batch's grouping (the previous step's side branch, joined here rather than at
+                    # that step's end: it may run on into this step's T1)
+                    self.kjt_join()
                     t1_done = torch.cuda.Event()
                     t1_done.record(main)
                     self.tables.use_bwd_workspace(parity)  # (prepare() leaves it so; it runs later here)
@@ -495,8 +515,13 @@ class FusedTwoTowerStep:
                         st.wait_event(t1_done)
                         with torch.cuda.stream(st):
                             work()
-                    for st, _ in branches:
+                    for st, _ in branches[1:]:
                         main.wait_stream(st)
+                    if self.cross_step_grouping:  # joined by the next step's update (kjt_join)
+                        self._prep_event = torch.cuda.Event()
+                        self._prep_event.record(self.side)
+                    else:
+                        main.wait_stream(self.side)
                     return
                 if defer_prepare:
                     launch_prepare()
