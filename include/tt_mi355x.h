@@ -216,7 +216,8 @@ int tt_bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_featur
                            int64_t max_lookups, void* stream);
 /* The same update in two parts that touch disjoint rows, for two streams: part 1 the rows looked up
  * once (KJT form: offsets required), part 2 every other row (2..32 lookups and the hot rows); part 0
- * is tt_bwd_rowwise_adagrad. Both parts read the same completed grouping and gradient. */
+ * is tt_bwd_rowwise_adagrad. Both parts read the same completed grouping and gradient. Parts 1 / 2
+ * need the narrow path (rows of D <= 128, 16-B aligned: TT_EINVAL otherwise). */
 int tt_bwd_rowwise_adagrad_part(const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features, int F,
                                 int64_t B, const float* grad_out, int64_t ldg, const int32_t* offsets, int pooling,
                                 float* weights, float* state, float lr, float eps, void* workspace, size_t ws_bytes,

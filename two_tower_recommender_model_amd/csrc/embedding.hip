@@ -1494,6 +1494,8 @@ static int bwd_rowwise_adagrad(const tt_table_meta_t* tables, int T, const tt_fe
     const int cap = v4 ? 1024 : (v2 ? 512 : 256);
     if (D > cap) return fail(TT_EINVAL, "bwd_rowwise_adagrad: unaligned dim > 256 unsupported");
   }
+  if (part && !narrow)  // the generic path's single-row fix feeds its update: one stream only
+    return fail(TT_EINVAL, "bwd_rowwise_adagrad_part: parts need 16-B aligned rows of D <= 128 (the narrow path)");
   BwdWs w;
   bwd_layout(workspace, max_lookups, &w);
   hipStream_t st = as_stream(stream);
