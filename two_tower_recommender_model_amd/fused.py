@@ -500,7 +500,8 @@ class FusedTwoTowerStep:
                     t1_done.record(main)
                     self.tables.use_bwd_workspace(parity)  # (prepare() leaves it so; it runs later here)
                     self._mark("upd", 0)
-                    split = self.side3 is not None and self.offsets_used is not None
+                    split = (self.side3 is not None and self.offsets_used is not None
+                             and all(d <= 128 and d % 4 == 0 for d in self.dims))  # the narrow path
                     if split:  # the once-looked-up rows here, the others beside them (disjoint rows)
                         self.tables.bwd_rowwise_adagrad(self.gpooled, self.offsets_used, self.B, self.lr_emb, self.eps,
                                                         part=1)
