@@ -71,6 +71,7 @@ struct TowerArgs {
   __bf16* dzt;          // [2][MAXL][MAXW][B]
   float* dbpart;        // [2][MAXL][nwg][MAXW]
   float* loss_part;     // [nwg]
+  uint32_t* sync;       // row-owned T1: zeroes the tail's completion counters (tail_t3_block)
   int64_t in_max;
   int64_t Bp;           // strip rows per block (B rounded up to 32)
   int nwg;
@@ -1518,6 +1519,7 @@ __device__ __forceinline__ float t3_sum(const UpdateArgs& a, const float (&v)[32
 // [2] Adam step pending (set by T2 with adam_pre, cleared by the T3 that applies it), [3] the lazy
 // T3's arrivals, [4] / [5] the fused T3 + T1 launch's arrivals / passes, [6] its poll timeouts
 constexpr int CW_PENDING = 2, CW_LAZY_ARRIVE = 3, CW_FUSE_ARRIVE = 4, CW_FUSE_PASSED = 5, CW_FUSE_TIMEOUT = 6;
+constexpr int SYNC_SPREAD = 8, SYNC_STRIDE = 32, CW_T3_TIMEOUT = 10;  // T3 in the tail (tail_t3_block)
 
 // IDX: the sharded step's form (tt_tower_fwd_bwd_indexed2_bf16): tower t's input row m is bf16 row
 // gpos[t][m] of gsrc[t] (-1: zeros; the rows an owner returned, dense), its dX goes to fp32 row
@@ -1547,6 +1549,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
                                                                     // (fp32, 16-B chunk c of row n at c ^ n)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = wid >> 1, h = wid & 1, q = lane >> 4, n = lane & 15;
+  // the completion counters of the tail launch that follows (T3 in the tail): zero at its start
+  if (blockIdx.x == 0 && threadIdx.x < SYNC_SPREAD) a.sync[threadIdx.x * SYNC_STRIDE] = 0u;
   const int64_t B = a.B, m0 = (int64_t)blockIdx.x * TR, m = m0 + 16 * h + n;
   const bool live = m < B;
   RK_STAMP(0);
@@ -2028,7 +2032,30 @@ struct WgradArgs {
 #endif
   DedupWs dd;           // tt_tower_wgrad_pre with a dedup workspace: the first n_res workgroups
   int n_res;            //   finish T1's deferred inserts (dd_resolve_block)
+  // T3 in the tail launch (tower_tail_t3_kernel): the slabs, bias sums and Adam scalars are stored
+  // write-through (sc1) and every T2 workgroup then adds one to a completion counter (MI355X_MICROARCH.md
+  // hand-off row 1: the T3 workgroups read them with sc1 loads once the count is complete)
+  int wt;
+  uint32_t* pub;          // completion counters (SYNC_SPREAD, SYNC_STRIDE apart; zeroed by T1)
+  uint32_t* pub_timeout;
 };
+
+// a write-through (sc1) 16-B store at byte offset off of the buffer that starts at base (< 4 GB)
+__device__ __forceinline__ void wt_store16(const void* base, uint32_t nbytes, uint32_t off, f32x4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes,
+                                                                      0x00020000);
+  typedef __attribute__((ext_vector_type(4))) unsigned u4;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, off, 0, 16 /* sc1 */);
+}
+// the T2 workgroup's hand-off to the T3 workgroups of the same launch: every wave's stores drained,
+// then one count (called by every thread of the workgroup)
+__device__ __forceinline__ void wgrad_publish(const WgradArgs& a) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.pub + (blockIdx.x % SYNC_SPREAD) * SYNC_STRIDE, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
 #if TT_EXPERIMENTS
 #define T2_STAMP(k) \
   do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
@@ -2243,17 +2270,43 @@ __device__ __forceinline__ void wgrad_lds_block_rm(const WgradArgs& a, int lb, c
   }
   T2_STAMP(2);
   float* dst = a.slab + (int64_t)s * a.P + a.woff[t][l];
+  if (a.wt) {
+    // 16-B write-through stores: a 4 x 4 transpose across the lanes r = 4 m .. 4 m + 3 of each
+    // 16-lane row gives lane 4 m + c row q * 4 + c, columns 4 m .. 4 m + 3 (contiguous in [n][K])
+    const int c = r & 3, m4 = r & ~3;
+    const uint32_t nbytes = (uint32_t)((int64_t)a.S * a.P * 4);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
+      for (int j = 0; j < 4; ++j)
+        if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K) {
+          f32x4 o;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int n = n0 + nh * 32 + i * 16 + q * 4 + rr;
-          const int k = kh * 64 + j * 16 + r;
-          dst[(int64_t)n * K + k] = acc[i][j][rr];
+          for (int d = 0; d < 4; ++d) {
+            const int src = (c - d) & 3;  // the component this lane sends in round d
+            const float send = src == 0 ? acc[i][j][0] : src == 1 ? acc[i][j][1] : src == 2 ? acc[i][j][2] : acc[i][j][3];
+            const float got = __shfl(send, (lane & ~3) + ((c + d) & 3), 64);
+            const int dc = (c + d) & 3;
+            if (dc == 0) o[0] = got; else if (dc == 1) o[1] = got; else if (dc == 2) o[2] = got; else o[3] = got;
+          }
+          const int n = n0 + nh * 32 + i * 16 + q * 4 + c;
+          const int k = kh * 64 + j * 16 + m4;
+          wt_store16(a.slab, nbytes, (uint32_t)(((int64_t)s * a.P + a.woff[t][l] + (int64_t)n * K + k) * 4), o);
         }
+    wgrad_publish(a);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int n = n0 + nh * 32 + i * 16 + q * 4 + rr;
+            const int k = kh * 64 + j * 16 + r;
+            dst[(int64_t)n * K + k] = acc[i][j][rr];
+          }
+  }
   T2_STAMP(3);
 }
 
@@ -2272,6 +2325,7 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
     // over workgroups, then a fixed butterfly -> slab[0]
     int64_t b = ((int64_t)bid - nwg_tiles) * 4 + wid;
     if (b == a.nbias) {  // the scalar loss: T1's per-workgroup partials in a fixed order
+      b = -1;            // (no bias output below)
       if (a.loss) {
         float s = 0.f;
         for (int w0 = 0; w0 < a.nwg; w0 += 512) {
@@ -2289,11 +2343,16 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
         a.step_state[0] = t_step;
         const double bc1 = 1.0 - pow((double)a.beta1, (double)t_step);
         const double bc2 = 1.0 - pow((double)a.beta2, (double)t_step);
-        a.adam_pre[0] = (float)((double)a.lr / bc1);
-        a.adam_pre[1] = (float)sqrt(bc2);
-        reinterpret_cast<uint32_t*>(a.adam_pre)[2] = 1u;  // CW_PENDING: the step's Adam is due
+        if (a.wt) {  // read by the T3 workgroups of this launch (sc1 loads)
+          __hip_atomic_store(a.adam_pre, (float)((double)a.lr / bc1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.adam_pre + 1, (float)sqrt(bc2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          a.adam_pre[0] = (float)((double)a.lr / bc1);
+          a.adam_pre[1] = (float)sqrt(bc2);
+        }
+        // CW_PENDING: the step's Adam is due (coherent: a T3 of this launch may clear it)
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(a.adam_pre) + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      return;
     }
     for (int t = 0; t < 2; ++t)
       for (int l = 0; l < a.L; ++l) {
@@ -2312,10 +2371,16 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
             for (int k = 0; k < 8; ++k) s += v[k];
           }
           s = wave_sum(s);
-          if (lane == 0) a.slab[a.boff[t][l] + b] = s;
+          if (lane == 0) {
+            if (a.wt)
+              __hip_atomic_store(a.slab + a.boff[t][l] + b, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              a.slab[a.boff[t][l] + b] = s;
+          }
         }
-        b -= a.width[l];
+        if (b >= 0) b -= a.width[l];
       }
+    if (a.wt) wgrad_publish(a);
     T2_STAMP(3);
     return;
   }
@@ -2486,7 +2551,7 @@ __device__ __forceinline__ void insert_next_block(const InsertArgs& ins, int blk
 // EXPERIMENT (TT_RING_STAMPS): s_memrealtime of wave 0 at the start / end of each workgroup's role
 #if TT_EXPERIMENTS
 #define RING_STAMP(p, k) \
-  do { if ((p) && threadIdx.x == 0 && blockIdx.x < 1024) (p)[(int64_t)blockIdx.x * 2 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+  do { if ((p) && threadIdx.x == 0 && blockIdx.x < 2048) (p)[(int64_t)blockIdx.x * 2 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define RING_STAMP(p, k) do { (void)(p); } while (0)
 #endif
@@ -2532,6 +2597,9 @@ __global__ void __launch_bounds__(256) tower_wgrad_route_rowwise_kernel(WgradArg
   }
 }
 
+// WT: T3 in the tail launch (tower_tail_t3_kernel): the slabs and the Adam scalars were stored
+// write-through by T2 workgroups of the same launch, so they are read with sc1 loads
+template <bool WT = false>
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
   T3_STAMP(0);
   const int64_t i = (int64_t)bid * 256 + threadIdx.x;
@@ -2541,8 +2609,13 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
   int64_t t_step = 0;
   float step_size = 0.f, bc2_sqrt = 1.f;
   if (a.do_adam && a.adam_pre) {
-    step_size = a.adam_pre[0];
-    bc2_sqrt = a.adam_pre[1];
+    if (WT) {
+      step_size = __hip_atomic_load(const_cast<float*>(a.adam_pre), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bc2_sqrt = __hip_atomic_load(const_cast<float*>(a.adam_pre) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      step_size = a.adam_pre[0];
+      bc2_sqrt = a.adam_pre[1];
+    }
   } else if (a.do_adam) {
     t_step = a.step_state[0] + 1;
     const double bc1 = 1.0 - pow((double)a.beta1, (double)t_step);
@@ -2565,13 +2638,19 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
         for (int s0 = 0; s0 < a.S; s0 += 32) {
           float v[32];
 #pragma unroll
-          for (int u = 0; u < 32; ++u) v[u] = s0 + u < a.S ? a.slab[(int64_t)(s0 + u) * a.P + i] : 0.f;
+          for (int u = 0; u < 32; ++u) {
+            const float* sp = a.slab + (int64_t)(s0 + u) * a.P + i;
+            v[u] = s0 + u < a.S ? (WT ? __hip_atomic_load(const_cast<float*>(sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : *sp)
+                                : 0.f;
+          }
 #pragma unroll
           for (int u = 0; u < 32; ++u)
             if (s0 + u < a.S) g += v[u];
         }
       } else {
-        g = a.slab[i];  // bias gradient, reduced over the T1 workgroups by T2's bias waves
+        // bias gradient, reduced over the T1 workgroups by T2's bias waves
+        g = WT ? __hip_atomic_load(const_cast<float*>(a.slab) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.slab[i];
       }
     }
     T3_STAMP(1);
@@ -2588,7 +2667,9 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
       }
     }
   } else if (a.do_adam && a.adam_pre && bid == 0 && threadIdx.x == 0) {
-    cw[CW_PENDING] = 0u;  // applied (no workgroup of this launch reads the word)
+    // applied (no workgroup of this launch reads the word; coherent: a WGRAD role of the same
+    // launch may have set it)
+    __hip_atomic_store(cw + CW_PENDING, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (a.do_adam && !a.adam_pre) {
     __syncthreads();
@@ -2605,6 +2686,38 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
 }
 
 __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) { update_block(a, (int)blockIdx.x, (int)gridDim.x); }
+
+// T3 in the tail: the T2 workgroups of a launch count their completion on 8 counters 128 B apart
+// (workgroup id mod 8: single-address atomics from every workgroup serialise), zeroed by the
+// row-owned T1 that precedes every tail. The waits that timed out are counted in the counter
+// region's word 10 (must stay 0).
+__device__ __forceinline__ void tail_t3_block(const UpdateArgs& u, const uint32_t* pub, uint32_t* timeout,
+                                              int n_t2, int bid, int g3, int64_t* stamps) {
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    int spin = 0;
+    for (;;) {
+      uint32_t v = 0;
+      if (lane < SYNC_SPREAD)
+        v = __hip_atomic_load(const_cast<uint32_t*>(pub) + lane * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int o = 4; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (__builtin_amdgcn_readfirstlane(v) >= (uint32_t)n_t2) break;
+      if (++spin > (1 << 22)) {  // ~200 ms: recorded, not waited for
+        if (lane == 0) __hip_atomic_fetch_add(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+#if TT_EXPERIMENTS  // the wait's end (in place of the start) in the stamps of T3 in the tail
+  if (stamps && threadIdx.x == 0 && blockIdx.x < 2048) stamps[(int64_t)blockIdx.x * 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#else
+  (void)stamps;
+#endif
+  update_block<true>(u, bid, g3);
+}
 
 // Pipelined sharded step, launch G (after launch U updated this rank's rows): the owner's gather of
 // batch i+1's rows (bf16, into exchange B's row blocks, filing batch i+1's dedup table), the tower
@@ -2747,6 +2860,24 @@ __device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, in
   }
 }
 
+__global__ void __launch_bounds__(256, 3) tower_tail_t3_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
+                                                            InsertArgs ins, DdUpdateArgs d, UpdateArgs u, int n_ins,
+                                                            int n_t2, int n_dd, int g3, int64_t* stamps) {
+  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
+  RING_STAMP(stamps, 0);
+  // the T3 workgroups last (they wait for every T2 workgroup: dispatched before them)
+  int b = (int)blockIdx.x;
+  if (b < n_ins)
+    insert_next_full_block(ins, b, smem);
+  else if ((b -= n_ins) < n_t2)
+    wgrad_block(a2, tiles, b, smem);
+  else if ((b -= n_t2) < n_dd)
+    dd_update_block(d, b, smem);
+  else
+    tail_t3_block(u, a2.pub, a2.pub_timeout, n_t2, b - n_dd, g3, stamps);
+  RING_STAMP(stamps, 1);
+}
+
 __global__ void __launch_bounds__(256, 3) tower_tail_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
                                                          InsertArgs ins, DdUpdateArgs d, int n_ins, int n_t2,
                                                          int64_t* stamps) {
@@ -2790,7 +2921,7 @@ struct TowerLayout {
   int32_t t2_code[16];
   int rows;  // the row-owned T1 (tower_rows_kernel) serves this shape's single-hot gather launches
   // workspace carve (bytes)
-  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_wimg, o_tiles, o_dbg,
+  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_wimg, o_tiles, o_dbg, o_sync,
       total;
 };
 
@@ -2876,6 +3007,7 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.o_wimg = take(L.rows ? (size_t)RK_IMG : 0);
   L.o_tiles = take((size_t)nt * sizeof(WgradTile));
   L.o_dbg = take((size_t)(std::max<int64_t>(L.nwg * 2, 1024) * 8 + L.nwg * 16 * 9) * sizeof(int64_t));
+  L.o_sync = take(SYNC_SPREAD * SYNC_STRIDE * 4);
   L.total = off;
   *lay = L;
   return TT_OK;
@@ -2988,6 +3120,7 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   a.dzt = reinterpret_cast<__bf16*>(ws + L.o_dzt);
   a.dbpart = reinterpret_cast<float*>(ws + L.o_dbpart);
   a.loss_part = reinterpret_cast<float*>(ws + L.o_losspart);
+  a.sync = reinterpret_cast<uint32_t*>(ws + L.o_sync);
   a.in_max = L.in_max;
   a.Bp = L.Bp;
   a.nwg = L.nwg;
@@ -3857,7 +3990,8 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
                                       const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
                                       int F, const float* grad, int64_t ldg, float* weights, float* state,
                                       float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
-                                      size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
+                                      size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream,
+                                      const tt_update_role_t* t3 = nullptr) {
   if (!adam_step_state || !next_cols || !num_embeddings || !dedup_tables || !next_dedup_ws)
     return fail(TT_EINVAL, "tower_tail: null pointer");
   if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_tail: ids must be int32/int64");
@@ -3887,6 +4021,25 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
   if (rc) return rc;
   d.skip_single = 1;
   const int64_t n_ins = ceil_div(ceil_div(2 * B, 256 * INS_PT), 8) * 8;  // INS_PT lookups per thread; % 8 == 0
+  if (t3) {  // + T3 in the same launch, its workgroups after every other role's
+    if (!(L.lds && L.rows)) return fail(TT_EINVAL, "tower_tail: T3 in the tail needs the row-owned shape");
+    UpdateArgs u;
+    int64_t g3 = 0;
+    const float* pre = reinterpret_cast<const float*>(ws + L.o_counter);
+    rc = t3_args(shape, B, t3->params, t3->exp_avg, t3->exp_avg_sq, 0.f, t3->beta1, t3->beta2, t3->eps,
+                 t3->weight_decay, nullptr, 1, t3->grads_out, nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0,
+                 u, &g3);
+    if (rc) return rc;
+    a2.wt = 1;
+    a2.pub = reinterpret_cast<uint32_t*>(ws + L.o_sync);  // zeroed by the row-owned T1 before
+    a2.pub_timeout = reinterpret_cast<uint32_t*>(ws + L.o_counter) + CW_T3_TIMEOUT;
+    if (n_ins + wgs + dd_grid + g3 > INT32_MAX) return fail(TT_EINVAL, "tower_tail: grid too large");
+    int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
+    tower_tail_t3_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(
+        a2, reinterpret_cast<const WgradTile*>(ws + a2.tiles_off), ins, d, u, (int)n_ins, (int)wgs, (int)dd_grid,
+        (int)g3, stamps);
+    return check_launch("tower_wgrad_pre_insert_rowwise_adagrad_update");
+  }
   int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
   if (stamps && L.nwg > 256) stamps = nullptr;
   tower_tail_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
@@ -4014,6 +4167,17 @@ int tt_launch(const tt_launch_plan_t* p, void* stream) {
                                         in.dedup_tables, g.tables, g.T, g.features, g.F, g.grad, g.ldg, g.weights,
                                         g.state, g.lr, g.eps, g.dedup_ws, in.next_dedup_ws, g.dedup_ws_bytes,
                                         g.dedup_max_lookups, stream);
+    case TT_ROLE_WGRAD | TT_ROLE_INSERT | TT_ROLE_ADAGRAD | TT_ROLE_UPDATE:
+      if ((rc = need_multi(1)) || (rc = adam_mode())) return rc;
+      if (g.B && g.B != B) return fail(TT_EINVAL, "launch: this plan's ADAGRAD role uses the plan's B (adagrad.B = 0 or B)");
+      if ((in.dedup_ws_bytes && in.dedup_ws_bytes != g.dedup_ws_bytes) ||
+          (in.dedup_max_lookups && in.dedup_max_lookups != g.dedup_max_lookups))
+        return fail(TT_EINVAL, "launch: the ring's two dedup workspaces have one size (the ADAGRAD role's)");
+      return fused_wgrad_insert_adagrad(p->shape, B, w.loss, p->workspace, p->ws_bytes, w.adam_step_state, w.adam_lr,
+                                        w.adam_beta1, w.adam_beta2, in.next_cols, in.id_dtype, in.num_embeddings,
+                                        in.dedup_tables, g.tables, g.T, g.features, g.F, g.grad, g.ldg, g.weights,
+                                        g.state, g.lr, g.eps, g.dedup_ws, in.next_dedup_ws, g.dedup_ws_bytes,
+                                        g.dedup_max_lookups, stream, &u);
     case TT_ROLE_WGRAD | TT_ROLE_INSERT:
       return fused_wgrad_insert(p->shape, B, w.loss, p->workspace, p->ws_bytes, w.adam_step_state, w.adam_lr,
                                 w.adam_beta1, w.adam_beta2, in.next_cols, in.id_dtype, in.num_embeddings,

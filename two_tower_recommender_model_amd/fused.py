@@ -615,6 +615,14 @@ class FusedTwoTowerStep:
                              and _lib.load().tt_tower_t3_fuse_supported(C.byref(self.towers.shape), self.B) == 1)
         return self._t1f
 
+    def t3_in_tail(self) -> bool:
+        """Does the ring run T3 inside the tail launch (two launches per step, nothing pending after
+        a step)? Its workgroups come last in the tail's grid and wait in-launch for every T2
+        workgroup's write-through slab rows (TT_T3_IN_TAIL=1)."""
+        if getattr(self, "_t3t", None) is None:
+            self._t3t = os.environ.get("TT_T3_IN_TAIL", "0") == "1"
+        return self._t3t
+
     def flush(self) -> None:
         """Apply the tower Adam update the last fused ring step left pending (a no-op launch when
         none is): parameters, moments and weight copies are current afterwards. run() / run_eager()
@@ -709,13 +717,16 @@ class FusedTwoTowerStep:
             self._mark("tail", 0)
             # the tail: tower weight gradients (T2) + the next batch's complete insert + the rows
             # looked up more than once (tt_launch roles WGRAD | INSERT | ADAGRAD)
-            plan = self._plan(_lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD, ws, multi_only=1)
+            # (+ UPDATE: T3 in the same launch, TT_T3_IN_TAIL=1)
+            t3_tail = not fuse and self.t3_in_tail()
+            roles = _lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD | (_lib.ROLE_UPDATE if t3_tail else 0)
+            plan = self._plan(roles, ws, multi_only=1)
             plan.insert = _lib.InsertRole(next_cols=ptr_array(list(next_cols)),
                                           id_dtype=id_dtype_code(next_cols[0].dtype), num_embeddings=self._ring_ne,
                                           dedup_tables=self._ring_tab, next_dedup_ws=ptr(wsn))
             _lib.launch(plan, st, "ring tail")
             self._mark("tail", 1)
-            if fuse:  # T3 runs in the next step's T1 (or flush())
+            if fuse or t3_tail:  # T3 runs in the next step's T1 (or flush()) / ran in the tail
                 return
             self._mark("t3", 0)
             check(lib.tt_tower_update_pre(C.byref(tw.shape), B, ptr(self.params), ptr(self.exp_avg),
