@@ -30,7 +30,7 @@ struct DedupWs {
   DSlot* slots;    // [cap], clean (key EMPTY, cnt 0) between steps
   uint64_t* lkey;  // [L] key of each lookup (DD_EMPTY: dropped / padding)
   int32_t* hot;    // [L / (DD_INL + 1) + 1] slots with cnt > DD_INL
-  int32_t* ctr;    // [4] {hot rows, hot-workgroup ticket, -, -}
+  int32_t* ctr;    // [4] {hot rows, hot-workgroup ticket, hot rows as the row-owned T1 found them, -}
   int64_t cap;
   int64_t L;
   int32_t hot_cap;  // entries of `hot` (a step inserts <= L lookups: <= L / 14 hot rows)
@@ -52,6 +52,12 @@ struct DedupWs {
   // and per hot row the team's arrival counter (zero between launches: reset by the last arriver)
   float* hotp;
   int32_t* hcnt;
+  // the ring's rows looked up 2..DD_INL times, listed by the row-owned T1 (which updates the rows
+  // looked up once and frees their slots): per T1 wave (segment) of 16 lookups, mcnt[seg] slots at
+  // multi[16 seg ..], written every step (no reset); the tail's list role updates them
+  int32_t* multi;  // [nseg * 16]
+  int32_t* mcnt;   // [nseg]
+  int32_t nseg;    // capacity in segments: ceil(L / 16)
 };
 #if TT_EXPERIMENTS
 #define DD_STAMP(k) \
@@ -187,6 +193,8 @@ struct DdUpdateArgs {
   int hot_wgs;         // workgroups of the hot role; the slot role has slot_hw / 8 more
   int64_t slot_hw;     // half-waves of the slot role: ceil(L / DD_SPH), a multiple of 8
   int skip_single;     // rows looked up once were updated by T1 (dd_mode 2): only free their slots
+  int multi_nseg;      // > 0: the slot role walks the T1 list of multi-lookup rows (DedupWs::multi, this
+                       // many segments) instead of every claiming lookup; T1 freed the single slots
 };
 
 // Per-lane table / feature meta from LDS: indexing the kernel-argument arrays by a per-lane value
@@ -285,15 +293,16 @@ __device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs) {
 // K - 1 reads the K partials (sc1 loads, after its add returned) and adds them in member order —
 // the same sum whichever member arrives last — then applies the row-wise Adagrad step. No member
 // waits on another (cdna_hip_programming.md Guideline 16: counter form, the last arriver combines).
+// nh: the step's hot rows; ticket: check in at the end (the last resets the count)
 __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
                                             float* __restrict__ weights, float* __restrict__ state, float lr,
-                                            float eps, const DedupWs& ws, int hot_wgs, int bid, char* smem) {
+                                            float eps, const DedupWs& ws, int hot_wgs, int bid, char* smem, int nh,
+                                            bool ticket) {
   f32x4v (*part)[32] = reinterpret_cast<f32x4v (*)[32]>(smem);       // [8][32], 16-B aligned
   int* list = reinterpret_cast<int*>(smem + 8 * 32 * 16);             // [DD_HOT_CH]
   int* wtot = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4);  // [4]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = tid >> 5, hl = tid & 31;
-  const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
   const int nn = (int)n;  // lookups < 2^18 (DD_CNT_BITS): 32-bit indices
   const int npass = (nn + DD_HOT_CH - 1) / DD_HOT_CH;
   const int K = dd_hot_team(nh, n, hot_wgs);
@@ -426,7 +435,7 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
     }
     __syncthreads();
   }
-  dd_hot_ticket(ws, hot_wgs);
+  if (ticket) dd_hot_ticket(ws, hot_wgs);
 }
 
 // host: validate + fill the update launch's arguments; *grid = its workgroup count
@@ -434,60 +443,21 @@ int dedup_update_args(const tt_table_meta_t* tables, int T, const tt_feature_met
                       const float* grad, int64_t ldg, float* weights, float* state, float lr, float eps,
                       void* workspace, size_t ws_bytes, int64_t max_lookups, DdUpdateArgs& a, int64_t* grid);
 
-// One workgroup (256 threads) of the update launch: bid < hot_wgs -> hot role, else 8 slots.
-// smem: DD_SMEM bytes of 16-B aligned LDS.
-__device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, char* smem) {
-  const EmbMeta& m = a.m;
+// the slot part of the update: DD_SPH slots per half-wave (sp, their first 128 B in dw, hq >= 0
+// for a slot to take), gradient rows summed in ascending lookup order, row-wise Adagrad, the slot
+// freed. spec: the claimer's key is lk[q] (its row, state and own gradient row loaded beside the slot)
+__device__ __forceinline__ void dd_slots_finish(const DdUpdateArgs& a, const GradMap& gm, const DdMeta* lm, bool spec,
+                                                const int (&hq)[DD_SPH], const uint64_t (&lk)[DD_SPH],
+                                                DSlot* const (&sp)[DD_SPH], const int (&dw)[DD_SPH], int64_t hw,
+                                                int64_t nhw, int bid) {
   const DedupWs& ws = a.ws;
+  (void)ws;
+  (void)bid;
   float* __restrict__ weights = a.weights;
   float* __restrict__ state = a.state;
   const float lr = a.lr, eps = a.eps;
-  DD_STAMP(0);
-  DdMeta* lm = reinterpret_cast<DdMeta*>(smem + DD_SMEM_HOT);
-  const GradMap gm{a.grad, a.ldg, (uint32_t)m.B, lm};
-  if (bid < a.hot_wgs) {
-    // a workgroup with no hot work item (most of them at uniform ids) only checks in: the ticket
-    // that resets the hot-row count once every hot workgroup has read it
-    const int nh = min(__hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ws.hot_cap);
-    if (bid >= nh * dd_hot_team(nh, a.n, a.hot_wgs)) {
-      dd_hot_ticket(ws, a.hot_wgs);
-      return;
-    }
-    dd_meta_fill(m, lm);
-    __syncthreads();
-    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem);
-    return;
-  }
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31, hb = lane & 32;
-  // DD_SPH claiming lookups per half-wave (i and i + nhw, ...), their dependent loads interleaved:
-  // the slot a lookup claimed (claim[i] >= 0) is updated by that lookup's half-wave; the grid covers
-  // the step's lookups (not the cap slots) in one round of resident waves
-  const int64_t hw = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
-  const int64_t nhw = a.slot_hw;
-  int hq[DD_SPH];
-  uint64_t lk[DD_SPH];
-  // spec (every mode but skip_single): the claiming lookup's own key is its slot's key, so its row,
-  // row state and own gradient row are loaded beside the slot (from lkey[i]) instead of after it —
-  // the update of a row looked up once (the common case) waits two dependent round trips, not three
-  const bool spec = !a.skip_single;
-#pragma unroll
-  for (int q = 0; q < DD_SPH; ++q) {
-    const int64_t i = hw + q * nhw;
-    hq[q] = i < a.n ? ws.claim[i] : -1;
-    lk[q] = spec && i < a.n ? ws.lkey[i] : DD_EMPTY;
-  }
-  DSlot* sp[DD_SPH];
-  int dw[DD_SPH];
-#pragma unroll
-  for (int q = 0; q < DD_SPH; ++q) {
-    sp[q] = ws.slots + (hq[q] >= 0 ? hq[q] : 0);
-    // an idle half-wave reads nothing and sees an EMPTY word
-    dw[q] = hq[q] >= 0 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : (hl < 2 ? -1 : 0);  // 32 lanes: 128 B
-  }
-  dd_meta_fill(m, lm);  // beside the slot loads
-  __syncthreads();
-  DD_STAMP(1);
   bool active[DD_SPH], col_ok[DD_SPH];
   int c[DD_SPH], cmax[DD_SPH], mine[DD_SPH], D[DD_SPH];
   float* wrow[DD_SPH];
@@ -580,6 +550,133 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     if (active[q] && hl == 0) sp[q]->word = DD_EMPTY;
   }
   DD_STAMP(3);
+}
+
+// the list role (DdUpdateArgs::multi_nseg): every workgroup scans the segment counts (thread t owns
+// segments t, t + 256, ...), takes the equal share [lb per, (lb + 1) per) of the listed slots in
+// that order (per <= 256: the host sizes nlb >= lookups / 512), gathers their slot indices into LDS
+// and updates those slots, DD_SPH per half-wave per round
+__device__ __forceinline__ void dd_multi_block(const DdUpdateArgs& a, const GradMap& gm, DdMeta* lm, int lb, int nlb,
+                                               char* smem, int bid) {
+  const DedupWs& ws = a.ws;
+  int* lst = reinterpret_cast<int*>(smem);  // [256]
+  int* wsum = lst + 256;                    // [4] wave totals
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nseg = a.multi_nseg;
+  constexpr int SPT = 8;  // segments per thread (nseg <= 2048)
+  int c[SPT];
+#pragma unroll
+  for (int k = 0; k < SPT; ++k) c[k] = tid + 256 * k < nseg ? ws.mcnt[tid + 256 * k] : 0;
+  dd_meta_fill(a.m, lm);
+  int mine = 0;
+#pragma unroll
+  for (int k = 0; k < SPT; ++k) mine += c[k];
+  int inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  int base = inc - mine, total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    base += w < wid ? wsum[w] : 0;
+    total += wsum[w];
+  }
+  const int per = (total + nlb - 1) / nlb;
+  const int r0 = lb * per, r1 = min(total, r0 + per);
+  int p = base;
+#pragma unroll
+  for (int k = 0; k < SPT; ++k) {
+    for (int e = 0; e < c[k]; ++e, ++p)
+      if (p >= r0 && p < r1) lst[p - r0] = ws.multi[(int64_t)(tid + 256 * k) * 16 + e];
+  }
+  __syncthreads();
+  const int len = max(0, r1 - r0);
+  const int hl = lane & 31;
+  const int hw = wid * 2 + ((lane & 32) >> 5);  // half-wave of the workgroup (8)
+  for (int j0 = 0; j0 < len; j0 += 8 * DD_SPH) {
+    int hq[DD_SPH];
+    uint64_t lk[DD_SPH];
+    DSlot* sp[DD_SPH];
+    int dw[DD_SPH];
+#pragma unroll
+    for (int q = 0; q < DD_SPH; ++q) {
+      const int j = j0 + hw + 8 * q;
+      hq[q] = j < len ? lst[j] : -1;
+      lk[q] = DD_EMPTY;
+      sp[q] = ws.slots + (hq[q] >= 0 ? hq[q] : 0);
+      dw[q] = hq[q] >= 0 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : (hl < 2 ? -1 : 0);
+    }
+    dd_slots_finish(a, gm, lm, false, hq, lk, sp, dw, 0, 0, bid);
+  }
+}
+
+// One workgroup (256 threads) of the update launch: bid < hot_wgs -> hot role, else 8 slots.
+// smem: DD_SMEM bytes of 16-B aligned LDS.
+__device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, char* smem) {
+  const EmbMeta& m = a.m;
+  const DedupWs& ws = a.ws;
+  float* __restrict__ weights = a.weights;
+  float* __restrict__ state = a.state;
+  const float lr = a.lr, eps = a.eps;
+  DD_STAMP(0);
+  DdMeta* lm = reinterpret_cast<DdMeta*>(smem + DD_SMEM_HOT);
+  const GradMap gm{a.grad, a.ldg, (uint32_t)m.B, lm};
+  if (bid < a.hot_wgs) {
+    // a workgroup with no hot work item (most of them at uniform ids) only checks in: the ticket
+    // that resets the hot-row count once every hot workgroup has read it. skip_single: the row-owned
+    // T1 moved the count to ctr[2] and zeroed ctr[0] (no ticket: 64 returning atomics on one word
+    // serialise, the last check-in ended the ring's tail ~3 us after its other roles)
+    const bool ticket = !a.skip_single;
+    const int nh = min(ticket ? __hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ws.ctr[2],
+                       ws.hot_cap);
+    if (bid >= nh * dd_hot_team(nh, a.n, a.hot_wgs)) {
+      if (ticket) dd_hot_ticket(ws, a.hot_wgs);
+      return;
+    }
+    dd_meta_fill(m, lm);
+    __syncthreads();
+    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem, nh, ticket);
+    return;
+  }
+  if (a.multi_nseg > 0) {
+    dd_multi_block(a, gm, lm, bid - a.hot_wgs, (int)(a.slot_hw / 8), smem, bid);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int hl = lane & 31, hb = lane & 32;
+  // DD_SPH claiming lookups per half-wave (i and i + nhw, ...), their dependent loads interleaved:
+  // the slot a lookup claimed (claim[i] >= 0) is updated by that lookup's half-wave; the grid covers
+  // the step's lookups (not the cap slots) in one round of resident waves
+  const int64_t hw = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
+  const int64_t nhw = a.slot_hw;
+  int hq[DD_SPH];
+  uint64_t lk[DD_SPH];
+  // spec (every mode but skip_single): the claiming lookup's own key is its slot's key, so its row,
+  // row state and own gradient row are loaded beside the slot (from lkey[i]) instead of after it —
+  // the update of a row looked up once (the common case) waits two dependent round trips, not three
+  const bool spec = !a.skip_single;
+#pragma unroll
+  for (int q = 0; q < DD_SPH; ++q) {
+    const int64_t i = hw + q * nhw;
+    hq[q] = i < a.n ? ws.claim[i] : -1;
+    lk[q] = spec && i < a.n ? ws.lkey[i] : DD_EMPTY;
+  }
+  DSlot* sp[DD_SPH];
+  int dw[DD_SPH];
+#pragma unroll
+  for (int q = 0; q < DD_SPH; ++q) {
+    sp[q] = ws.slots + (hq[q] >= 0 ? hq[q] : 0);
+    // an idle half-wave reads nothing and sees an EMPTY word
+    dw[q] = hq[q] >= 0 ? reinterpret_cast<const int32_t*>(sp[q])[hl] : (hl < 2 ? -1 : 0);  // 32 lanes: 128 B
+  }
+  dd_meta_fill(m, lm);  // beside the slot loads
+  __syncthreads();
+  DD_STAMP(1);
+  dd_slots_finish(a, gm, lm, spec, hq, lk, sp, dw, hw, nhw, bid);
 }
 
 

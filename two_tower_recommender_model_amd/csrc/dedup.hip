@@ -63,6 +63,9 @@ size_t dedup_layout(void* base, int64_t L, DedupWs* w) {
   const int64_t hot_cap = L / (DD_INL + 1) + 1;
   t.hotp = reinterpret_cast<float*>(take(sizeof(float) * 128 * DD_HOT_TEAM * hot_cap));
   t.hcnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * hot_cap));
+  t.nseg = (int32_t)((L + 15) / 16);
+  t.multi = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 16 * (size_t)t.nseg));
+  t.mcnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)t.nseg));
   t.cap = cap;
   t.L = L;
   t.hot_cap = (int32_t)(L / (DD_INL + 1) + 1);

@@ -715,6 +715,11 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     const bool single = r >= 0 && cl >= 0 && (word & (uint32_t)DD_CNT_MASK) == 1u;
     urow[tq][row] = single ? r : -1;
     ustate[tq][row] = st;
+    if (blockIdx.x == 0 && lane == 0) {  // the table's hot-row count for the update launch (dd_update_block)
+      const int32_t nh = a.dd.ctr[0];
+      a.dd.ctr[2] = nh;
+      a.dd.ctr[0] = 0;
+    }
     T1_WSTAMP(1);
     __syncthreads();
     // the next batch's rows of this tile, after the compute waves' gather has landed (barrier 1):
@@ -1754,6 +1759,11 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
   int32_t cl = -1;
   float s_old = 0.f;
   if (UPD) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the table's hot-row count for the tail (dd_update_block)
+      const int32_t nh = a.dd.ctr[0];
+      a.dd.ctr[2] = nh;
+      a.dd.ctr[0] = 0;
+    }
     cl = a.dd.claim[live ? t * B + m : 0];
     s_old = (t ? a.us[1] : a.us[0])[r >= 0 ? r : 0];  // speculative: used only for a single-lookup row
   }
@@ -1900,7 +1910,19 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
     const float sq = e2[0] + e2[1];
     const float snew = rw_state(s_old, sq, IN);
     const float step = rw_step(snew, a.ulr, a.ueps);
-    const bool single = r >= 0 && cl >= 0 && (word & (uint32_t)DD_CNT_MASK) == 1u;
+    const uint32_t cnt = word & (uint32_t)DD_CNT_MASK;
+    const bool single = r >= 0 && cl >= 0 && cnt == 1u;
+    {
+      // this wave's rows looked up 2..DD_INL times (their claiming lookups): the tail's list role
+      // updates them (segment = the wave; plain stores, the count written every step)
+      const bool mul = q == 0 && r >= 0 && cl >= 0 && cnt >= 2u && cnt <= (uint32_t)DD_INL;
+      const uint64_t bal = __ballot(mul);
+      const int seg = (int)blockIdx.x * 4 + wid;
+      if (seg < a.dd.nseg) {
+        if (mul) a.dd.multi[(int64_t)seg * 16 + __popcll(bal & ((1ull << lane) - 1))] = cl;
+        if (lane == 0) a.dd.mcnt[seg] = __popcll(bal);
+      }
+    }
     // the updated rows go back through the wave's LDS rows (same chunk swizzle) and out as two
     // whole rows per store instruction, as they came in
 #pragma unroll
@@ -1924,7 +1946,10 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
     }
     RK_STAMP2(2);
     if (single) {
-      if (q == 0) (t ? a.us[1] : a.us[0])[r] = snew;
+      if (q == 0) {
+        (t ? a.us[1] : a.us[0])[r] = snew;
+        a.dd.slots[cl].word = DD_EMPTY;  // free: nothing else of the step reads a single slot
+      }
       store_dx = a.pooled_out != nullptr;  // dX only for inspection
     }
   }
@@ -2969,7 +2994,11 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
         }
     // slices of whole passes (256 rows), at most 64 (the slab depth T3 reduces over)
     const int64_t pass = T2_PF * T2_MB;
-    const int64_t S = std::min<int64_t>(64, ceil_div(B, pass));
+    int64_t passes = 1;  // per slice
+#if TT_EXPERIMENTS
+    if (const char* e = getenv("TT_T2_SLICE_PASSES")) passes = std::max(1, atoi(e));  // EXPERIMENT
+#endif
+    const int64_t S = std::min<int64_t>(64, ceil_div(B, pass * passes));
     L.mslice = ceil_div(ceil_div(B, S), pass) * pass;
     L.S = (int)ceil_div(B, L.mslice);
   } else {
@@ -4020,6 +4049,15 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
                          dedup_max_lookups, d, &dd_grid);
   if (rc) return rc;
   d.skip_single = 1;
+  if (L.rows && L.lds && getenv("TT_MULTI_LIST")) {  // the row-owned T1 listed the multi-lookup rows
+    d.multi_nseg = (int)(L.nwg * 4);
+    if (d.multi_nseg > d.ws.nseg || d.multi_nseg > 2048)
+      return fail(TT_EINVAL, "tower_tail: the T1 list needs a dedup workspace of its batch and B <= 16384");
+    // a workgroup's share of the listed slots <= 256 (at most lookups / 2 slots are listed)
+    const int64_t nlb = std::max<int64_t>(8, ceil_div(2 * B, 512) * 4);
+    d.slot_hw = nlb * 8;
+    dd_grid = d.hot_wgs + nlb;
+  }
   const int64_t n_ins = ceil_div(ceil_div(2 * B, 256 * INS_PT), 8) * 8;  // INS_PT lookups per thread; % 8 == 0
   if (t3) {  // + T3 in the same launch, its workgroups after every other role's
     if (!(L.lds && L.rows)) return fail(TT_EINVAL, "tower_tail: T3 in the tail needs the row-owned shape");
