@@ -43,7 +43,7 @@ def show(name, seg, roles):
     s = seg.view(-1, 2).cpu().double()
     used = int((s[:, 0] != 0).sum())
     s = s[:used]
-    t0 = s[:, 0].min()
+    t0 = s[s[:, 0] != 0, 0].min()  # workgroups that returned before stamping hold 0
     rel = (s - t0) / 100.0
     out = [f"{name} grid {used} end max {float(rel[:, 1].max()):.2f}"]
     for rn, a, b in roles:
@@ -56,7 +56,10 @@ def show(name, seg, roles):
 
 for it in range(6):
     base[4096:].zero_()
-    st.run_eager(1)
+    if os.environ.get("GRAPH") == "1":  # the last tail of an 8-step graph replay
+        st.run(8)
+    else:
+        st.run_eager(1)
     torch.cuda.synchronize()
     if it < 2:
         continue

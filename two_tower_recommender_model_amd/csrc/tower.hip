@@ -4049,7 +4049,11 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
                          dedup_max_lookups, d, &dd_grid);
   if (rc) return rc;
   d.skip_single = 1;
-  if (L.rows && L.lds && getenv("TT_MULTI_LIST")) {  // the row-owned T1 listed the multi-lookup rows
+  bool list = L.rows && L.lds;  // the row-owned T1 listed the multi-lookup rows and freed the single slots
+#if TT_EXPERIMENTS
+  if (const char* e = getenv("TT_MULTI_LIST")) list = list && e[0] != '0';  // EXPERIMENT: A/B
+#endif
+  if (list) {
     d.multi_nseg = (int)(L.nwg * 4);
     if (d.multi_nseg > d.ws.nseg || d.multi_nseg > 2048)
       return fail(TT_EINVAL, "tower_tail: the T1 list needs a dedup workspace of its batch and B <= 16384");
