@@ -591,6 +591,9 @@ int tt_pooled_grad_pack(int W, int F, int64_t B, int D, const float* grad, int64
  *   WGRAD | INSERT | ADAGRAD       single-GPU ring tail: T2 + the next batch's complete insert + the
  *                                  rows looked up more than once (ADAGRAD.multi_only = 1); T1 updated
  *                                  the others (03:455 backward + 03:791-795 RowWiseAdagrad)
+ *   WGRAD | INSERT | ADAGRAD      the same + T3 in the same grid (its workgroups last, waiting for
+ *     | UPDATE                     every T2 workgroup's write-through slab rows); row-owned T1
+ *                                  shapes only; measured slower than the separate T3
  *   WGRAD | INSERT                 T2 + the next batch's insert, first CAS only (the rest deferred
  *                                  to the RESOLVE role of the following launch)
  *   UPDATE | ADAGRAD | RESOLVE     T3 + rows looked up more than once (multi_only = 1) + the
