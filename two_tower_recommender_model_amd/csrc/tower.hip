@@ -4052,6 +4052,7 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
   bool list = L.rows && L.lds;  // the row-owned T1 listed the multi-lookup rows and freed the single slots
 #if TT_EXPERIMENTS
   if (const char* e = getenv("TT_MULTI_LIST")) list = list && e[0] != '0';  // EXPERIMENT: A/B
+  if (getenv("TT_T1_CLASSIC")) list = false;  // EXPERIMENT: tower_l2_kernel T1 writes no list
 #endif
   if (list) {
     d.multi_nseg = (int)(L.nwg * 4);
