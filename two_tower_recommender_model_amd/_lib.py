@@ -358,7 +358,9 @@ def load(path: os.PathLike | None = None):
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = Path(path) if path else (EXP_LIB_PATH if os.environ.get("TT_EXPERIMENT_LIB") == "1" else LIB_PATH)
+        exp = os.environ.get("TT_EXPERIMENT_LIB", "")
+        # measurement scripts: "1" = the experiment build, or a path to another experiment .so (A/B)
+        p = Path(path) if path else (EXP_LIB_PATH if exp == "1" else Path(exp) if exp.endswith(".so") else LIB_PATH)
         if not p.exists():
             raise TTError(
                 f"libtt_mi355x.so not found at {p}: build it with "

@@ -20,6 +20,9 @@ constexpr int DD_CNT_BITS = 18;     // slot word = key << 18 | count; a step has
 constexpr uint64_t DD_CNT_MASK = (1ull << DD_CNT_BITS) - 1;
 constexpr int DD_INL = 30;          // lookups stored inline per slot (128-B slot: word + 30 items)
 constexpr int DD_SPH = 4;           // slots per half-wave in the update launch
+#ifndef DD_MR
+#define DD_MR 4                     // gradient rows of a multi-lookup slot in flight per half-wave
+#endif
 
 struct __attribute__((aligned(128))) DSlot {
   uint64_t word;  // DD_EMPTY when free, else key << 18 | lookups of this key in the step
@@ -195,6 +198,9 @@ struct DdUpdateArgs {
   int skip_single;     // rows looked up once were updated by T1 (dd_mode 2): only free their slots
   int multi_nseg;      // > 0: the slot role walks the T1 list of multi-lookup rows (DedupWs::multi, this
                        // many segments) instead of every claiming lookup; T1 freed the single slots
+#if TT_EXPERIMENTS
+  int exp_skip;        // EXPERIMENT (TT_EXP_SKIP, timing only, wrong results): 1 hot role, 2 slot role
+#endif
 };
 
 // Per-lane table / feature meta from LDS: indexing the kernel-argument arrays by a per-lane value
@@ -522,15 +528,17 @@ __device__ __forceinline__ void dd_slots_finish(const DdUpdateArgs& a, const Gra
 #pragma unroll
     for (int q = 0; q < DD_SPH; ++q) {
       if (cmax[q] > 1) mine[q] = dd_bitonic<32>(mine[q]);
-      for (int i = 0; i < cmax[q]; i += 4) {  // 4 gradient rows in flight, added in ascending order
-        f32x4v x[4];
+      // DD_MR gradient rows in flight, added in ascending order (12 measured: Zipf -0.8 / +0.5 µs
+      // in two A/Bs, uniform +0.3 — code-layout noise, not a gain; scripts/r04_mr.sh)
+      for (int i = 0; i < cmax[q]; i += DD_MR) {
+        f32x4v x[DD_MR];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < DD_MR; ++u) {
           const int b = __shfl(mine[q], hb + min(i + u, 31), 64);
           x[u] = col_ok[q] && i + u < c[q] ? *reinterpret_cast<const f32x4v*>(gm.row(b) + hl * 4) : (f32x4v)(0.f);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < DD_MR; ++u)
           if (i + u < c[q]) g[q] += x[u];
       }
     }
@@ -625,6 +633,10 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   DD_STAMP(0);
   DdMeta* lm = reinterpret_cast<DdMeta*>(smem + DD_SMEM_HOT);
   const GradMap gm{a.grad, a.ldg, (uint32_t)m.B, lm};
+#if TT_EXPERIMENTS
+  if ((a.exp_skip & 1) && bid < a.hot_wgs) return;
+  if ((a.exp_skip & 2) && bid >= a.hot_wgs) return;
+#endif
   if (bid < a.hot_wgs) {
     // a workgroup with no hot work item (most of them at uniform ids) only checks in: the ticket
     // that resets the hot-row count once every hot workgroup has read it. skip_single: the row-owned

@@ -4053,6 +4053,7 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
 #if TT_EXPERIMENTS
   if (const char* e = getenv("TT_MULTI_LIST")) list = list && e[0] != '0';  // EXPERIMENT: A/B
   if (getenv("TT_T1_CLASSIC")) list = false;  // EXPERIMENT: tower_l2_kernel T1 writes no list
+  if (const char* e = getenv("TT_EXP_SKIP")) d.exp_skip = atoi(e);
 #endif
   if (list) {
     d.multi_nseg = (int)(L.nwg * 4);
