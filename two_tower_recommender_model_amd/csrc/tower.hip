@@ -4060,7 +4060,10 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
     if (d.multi_nseg > d.ws.nseg || d.multi_nseg > 2048)
       return fail(TT_EINVAL, "tower_tail: the T1 list needs a dedup workspace of its batch and B <= 16384");
     // a workgroup's share of the listed slots <= 256 (at most lookups / 2 slots are listed)
-    const int64_t nlb = std::max<int64_t>(8, ceil_div(2 * B, 512) * 4);
+    int64_t nlb = std::max<int64_t>(8, ceil_div(2 * B, 512) * 4);
+#if TT_EXPERIMENTS
+    if (const char* e = getenv("TT_LIST_WGS")) nlb = std::max(nlb, (int64_t)atoi(e));  // EXPERIMENT
+#endif
     d.slot_hw = nlb * 8;
     dd_grid = d.hot_wgs + nlb;
   }
