@@ -2791,7 +2791,11 @@ __global__ void __launch_bounds__(256) tower_update_dedup_resolve_kernel(UpdateA
 // slot with the group's count in ONE global atomic and hands each member its position (base +
 // rank in the group) — at skewed ids a hot row costs one atomic per workgroup, not one per lookup
 // (the update sums a row's lookups in lookup order whatever the positions: the same results).
-constexpr int INS_PT = 2;     // lookups per thread: 512 per workgroup
+#ifndef TT_INS_PT
+#define TT_INS_PT 1
+#endif
+constexpr int INS_PT = TT_INS_PT;  // lookups per thread (1: 256 per workgroup, 64 workgroups at the
+                                   // north star; 2 measured 0.3-0.4 µs slower per step, scripts/r04_inspt.sh)
 constexpr int INS_HS = 1024;  // LDS hash slots per 512 lookups
 static_assert(INS_HS * (8 + 3 * 4) <= T2_SMEM, "the insert role's LDS hash fits the tail's LDS");
 __device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, int blk, char* smem) {
