@@ -337,7 +337,11 @@ int tt_tower_fwd_bwd_kjt(const tt_tower_shape_t* shape, int64_t B, const void* v
 /* T1 as tt_tower_fwd_bwd_gather, plus: a kept lookup (t, m) whose slot in dedup_ws (its claim, count
  * 1) says its row is looked up once in the step updates table_rows[t] / table_state[t] in place
  * (lr, eps: torchrec RowWiseAdagrad, 03_model_training.py:791-795); dX goes to gpooled for the
- * others (for every lookup with pooled_out). Shapes: in_dim in {64, 128}, widths [128, 64]. */
+ * others (for every lookup with pooled_out). Shapes: in_dim in {64, 128}, widths [128, 64].
+ * It also hands dedup_ws over to the update that follows (a role with ADAGRAD.multi_only = 1): the
+ * table's hot-row count moves to the update's word (the insert count is zeroed for the table's next
+ * fill), and with the row-owned T1 (the default for these shapes) the slots of the rows it updated
+ * are freed and the slots of rows looked up 2..30 times are listed per wave for the tail. */
 int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
                                    const int64_t* num_embeddings, float* const* table_rows, float* const* table_state,
                                    float* pooled_out, int64_t ldp, float* gpooled, const float* params,
