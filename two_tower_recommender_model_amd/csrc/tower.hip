@@ -2627,7 +2627,7 @@ __global__ void __launch_bounds__(256) tower_wgrad_route_rowwise_kernel(WgradArg
 template <bool WT = false>
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
   T3_STAMP(0);
-  const int64_t i = (int64_t)bid * 256 + threadIdx.x;
+  const int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   uint32_t* cw = a.adam_pre ? reinterpret_cast<uint32_t*>(const_cast<float*>(a.adam_pre)) : nullptr;
   // lazy (the fused T3 + T1 ring's flush): apply the Adam step T2 left pending, if any
   if (a.lazy && cw[CW_PENDING] == 0u) return;
@@ -3562,8 +3562,11 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
     a.stamps = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(workspace) + L.o_dbg) + 6144;
   }
 #endif
-
-  tower_update_kernel<<<dim3((unsigned)g3), dim3(256), 0, as_stream(stream)>>>(a);
+  int bs = 256;
+#if TT_EXPERIMENTS
+  if (const char* e = getenv("TT_T3_BLOCK")) bs = atoi(e) == 128 ? 128 : 256;  // EXPERIMENT
+#endif
+  tower_update_kernel<<<dim3((unsigned)ceil_div(a.P, (int64_t)bs)), dim3(bs), 0, as_stream(stream)>>>(a);
   return check_launch("tower_update");
 }
 
