@@ -10,9 +10,14 @@ labels Bernoulli(0.5), random-init weights. One "step" = the full training step:
 pooled forward, towers fwd (bf16 MFMA), dot + BCE, towers bwd, fused dedup + row-wise Adagrad on the
 tables, Adam on the towers.
 
-N = 1: the fused step replayed as one HIP graph. N > 1: DistributedModelParallel over RCCL (the
-tables row-wise sharded, towers data-parallel) — eager launches. Timing: W untimed steps, barrier +
-synchronize, K timed steps, synchronize + barrier, max over ranks; rank 0 prints ONE JSON line.
+N = 1: the fused ring step replayed as HIP graphs. N > 1: one process per GPU over RCCL running the
+pipelined sharded step (`sharded.FusedShardedTwoTowerStep`: table-wise at N = 2, row-wise from N = 4,
+data-parallel towers, two fixed-size all-to-alls per step captured into the HIP graphs with the
+kernels; config 5: `sharded_kjt.FusedShardedKJTStep`, three). `python bench.py --gpus N` without a
+launcher starts `torch.distributed.run --nproc-per-node N` itself as a child process (before any GPU
+call), relays its output and exits with its status; under a launcher the world size must equal
+--gpus. Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize + barrier, max over
+ranks; rank 0 prints ONE JSON line.
 Also reported: the embedding path's dominant kernel against the HBM roofline (HIP events on its
 own stream) and the CPU restatement's pairs/s on this host (rank 0, N = 1, bounded sample).
 """
@@ -967,11 +972,45 @@ def run_multi(args, world, rank, local_rank):
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: run the same command line as N ranks under
+    `torch.distributed.run` (one process per GPU, the reference's TorchDistributor(num_processes=N)
+    at 03_model_training.py:918) in a CHILD process, stdout / stderr inherited (rank 0's JSON line
+    passes straight through), and return its exit status. This process never touches the GPU:
+    torch.cuda.device_count() does not initialise HIP on this stack, and nothing else here does."""
+    import subprocess
+
+    rehearse = os.environ.get("TT_REHEARSE_GLOO") == "1"  # testing only: ranks share the visible GPUs
+    have = torch.cuda.device_count()
+    if not rehearse and have < n:
+        print(f"bench.py --gpus {n}: only {have} GPU(s) visible (one process per GPU)", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} under a launcher of world size {world}: they must agree")
     if args.ids is None:
         args.ids = SHARDED[args.workload]["ids"] if args.workload in SHARDED else "uniform"
     if args.workload in SHARDED:

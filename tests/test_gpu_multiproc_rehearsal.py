@@ -32,6 +32,24 @@ def test_bench_multiprocess_gloo_rehearsal(world):
 
 
 
+def test_bench_gpus2_self_launch_as_driver_runs_it():
+    """`python bench.py --gpus 2` with no launcher (the driver's form for the N-GPU line): the parent
+    starts torch.distributed.run with 2 ranks as a child, the ranks form a world of 2 (asserted in
+    bench.py against --gpus), rank 0's JSON line reaches the parent's stdout and the rc is 0."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TT_REHEARSE_GLOO="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "4", "--warmup", "2", "--batches", "8",
+           "--workload", "config2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 4 and d["value"] > 0
+    assert d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]
+    assert d["config"]["sharded"]["plan"].startswith("table-wise")
+
+
 @pytest.mark.parametrize("world", [2])
 def test_bench_config5_sharded_multiprocess_gloo_rehearsal(world):
     """bench.py's config-5 N > 1 path (the capturable multi-hot sharded step: users table-wise on the

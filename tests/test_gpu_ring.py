@@ -52,6 +52,27 @@ def test_ring_equals_classic_step(device, D, mode):
     assert torch.equal(a.logits, b.logits)
 
 
+def test_ring_large_batch_equals_classic_step(device):
+    """B = 32,768 (65,536 lookups, 4096 T1 segments: past the tail list role's 2048) — the tail's slot
+    role walks every claiming lookup instead of T1's list; bit for bit the classic step."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N, B = [3_000_000, 5_000_000], 32768
+    batches = _batches(N, B, 4, seed=32, device=device)
+    a = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=8)
+    b = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=8)
+    assert a.ring_supported()
+    a.capture_ring(batches, steps_per_graph=2)
+    a.run(4)
+    for cols, lab in batches:
+        b.load_batch(cols, lab)
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
+    assert torch.equal(a.params, b.params) and float(a.loss) == float(b.loss)
+    assert torch.equal(a.logits, b.logits)
+
+
 def test_ring_mixed_graph_sizes(device):
     """capture_ring(k = 4) also captures aligned 2-step graphs; run(3) + run(2) replays a 2-step
     graph, single steps and a 4-step one; align_ring() regroups the graphs from the cursor; the

@@ -82,9 +82,28 @@ def test_kjt_route_unpack_partials_vs_restatement(device, W, sharding, owners):
                                     ptr(send), ptr(flags), ptr(ws), ws.numel(), _lib.stream_handle(device)))
         torch.cuda.synchronize()
         assert int(flags[0]) == (cap < need) and int(flags[1]) == 0
-        if cap < need:
-            continue
         s = send.cpu().numpy().reshape(W, stride)
+        if cap < need:
+            # an overflowing block keeps the ids that fit and sends lengths that agree with them; the
+            # owner's unpack then stays inside its W * cap values (guard past them untouched)
+            for d in range(W):
+                kept = s[d, :F * B]
+                assert kept.sum() == min(cap, len(ids[d])) and (kept <= lens[d]).all()
+                np.testing.assert_array_equal(s[d, F * B:F * B + kept.sum()], ids[d][:kept.sum()])
+                recv = torch.from_numpy(np.tile(s[d], W)).to(device)
+                Fr = F
+                lo = torch.empty(W * Fr * B, dtype=torch.int32, device=device)
+                oo = torch.empty(W * Fr * B + 1, dtype=torch.int32, device=device)
+                vo = torch.full((W * cap + 4096,), -1, dtype=torch.int32, device=device)
+                uw = torch.empty(max(256, lib.tt_kjt_unpack_workspace_bytes(W, Fr, B)), dtype=torch.uint8,
+                                 device=device)
+                _lib.check(lib.tt_kjt_unpack(W, F, B, ptr(recv), stride, cap, (C.c_int32 * Fr)(*range(F)), Fr,
+                                             ptr(lo), ptr(oo), ptr(vo), ptr(uw), uw.numel(),
+                                             _lib.stream_handle(device)))
+                torch.cuda.synchronize()
+                assert int(oo[-1]) <= W * cap
+                assert (vo[W * cap:] == -1).all()
+            continue
         for d in range(W):
             np.testing.assert_array_equal(s[d, :F * B], lens[d])
             np.testing.assert_array_equal(s[d, F * B:F * B + len(ids[d])], ids[d])

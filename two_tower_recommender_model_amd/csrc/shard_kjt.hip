@@ -102,7 +102,18 @@ __global__ void __launch_bounds__(256) kjt_route_place_kernel(KjtRouteArgs a) {
   const int32_t o0 = a.offsets[i], o1 = a.offsets[i + 1];
   int c[KR_MAXW];
 #pragma unroll
-  for (int w = 0; w < KR_MAXW; ++w) c[w] = w < a.W ? a.base[(int64_t)w * n + i] - a.base[(int64_t)w * n] : 0;
+  for (int w = 0; w < KR_MAXW; ++w) {
+    c[w] = 0;
+    if (w < a.W) {
+      const int32_t lo = a.base[(int64_t)w * n + i], hi = a.base[(int64_t)w * n + i + 1];
+      c[w] = lo - a.base[(int64_t)w * n];
+      // a block over cap keeps the ids that fit (positions < cap) and the lengths it sends say so:
+      // the owner's offsets then never pass cap per source, whatever the flag says later
+      const int64_t room = a.cap - (int64_t)c[w];
+      const int32_t keep = (int32_t)(room <= 0 ? 0 : (room < hi - lo ? room : hi - lo));
+      if (keep != hi - lo) a.send[(int64_t)w * a.stride + i] = keep;
+    }
+  }
   kr_bag_ids(a, o0, o1, [&](int32_t, int64_t id) {
     if (id < 0 || id >= a.num_emb[f]) return;
     int64_t lr;

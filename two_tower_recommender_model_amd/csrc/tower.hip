@@ -4062,10 +4062,11 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
   if (getenv("TT_T1_CLASSIC")) list = false;  // EXPERIMENT: tower_l2_kernel T1 writes no list
   if (const char* e = getenv("TT_EXP_SKIP")) d.exp_skip = atoi(e);
 #endif
+  // the list role scans at most 2048 segments (B <= 16384); past that the slot role walks every
+  // claiming lookup (T1 still freed the single slots: their words read EMPTY there)
+  list = list && L.nwg * 4 <= std::min<int64_t>(d.ws.nseg, 2048);
   if (list) {
     d.multi_nseg = (int)(L.nwg * 4);
-    if (d.multi_nseg > d.ws.nseg || d.multi_nseg > 2048)
-      return fail(TT_EINVAL, "tower_tail: the T1 list needs a dedup workspace of its batch and B <= 16384");
     // a workgroup's share of the listed slots <= 256 (at most lookups / 2 slots are listed)
     int64_t nlb = std::max<int64_t>(8, ceil_div(2 * B, 512) * 4);
 #if TT_EXPERIMENTS

@@ -111,13 +111,19 @@ class TorchComm:
                     raise _lib.TTError("an eager collective did not complete before graph capture")
                 time.sleep(0.001)
         self._eager.clear()
-        # ProcessGroupNCCL's watchdog drops a completed work only on its next pass (every 100 ms) and
-        # queries its event until then; an event query racing the capture's first collective
-        # invalidated the capture on MI355X once in ~10 runs (hipErrorStreamCaptureInvalidated, then
-        # the watchdog aborting the process). Every eager work — these and the untracked synchronous
-        # ones (capacity / flag all-reduces) — is complete on the device now: let the watchdog
-        # retire them before the capture begins.
-        time.sleep(0.35)
+        # ProcessGroupNCCL's watchdog thread keeps a copy of every eager work (these and the untracked
+        # synchronous ones: capacity / flag all-reduces) until a pass of its loop finds it complete,
+        # queries its end event and erases it, destroying the event when it holds the last reference.
+        # That thread runs in HIP's default (global) capture mode, so a query or destroy it makes
+        # while this thread captures invalidates the capture (seen on MI355X once in ~10 runs:
+        # hipErrorStreamCaptureInvalidated, then the watchdog aborting the process). Every eager work
+        # is complete on the device now; ProcessGroupNCCL::waitForPendingWorks returns once the
+        # watchdog's list is empty (it checks under the lock the watchdog holds for its whole pass),
+        # after which the watchdog makes no HIP call until a new eager work exists, and captured
+        # collectives are never handed to it.
+        pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
+        if dist.get_backend(pg) == "nccl":
+            pg._wait_for_pending_works()
 
     def all_reduce_max_(self, t: torch.Tensor) -> None:
         if self.world > 1 or self.always:

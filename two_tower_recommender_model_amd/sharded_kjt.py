@@ -286,7 +286,9 @@ class FusedShardedKJTStep:
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                # thread_local: only this thread's calls are checked against the capture (the RCCL
+                # watchdog's pending works are retired above, TorchComm.retire)
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     self.step(v, o, l)
             torch.cuda.current_stream(self.device).wait_stream(s)
             _lib.graph_upload(g, self.device)
