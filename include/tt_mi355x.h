@@ -52,8 +52,11 @@
 extern "C" {
 #endif
 
-/* 2: tt_tower_shape_t._pad became `flags`; the 12 role-combination exports became tt_launch */
-#define TT_ABI_VERSION 2
+/* 2: tt_tower_shape_t._pad became `flags`; the 12 role-combination exports became tt_launch
+ * 3: the measured-and-rejected fused-T3 forms removed (tt_tower_fwd_bwd_gather_update_t3,
+ *    tt_tower_fwd_bwd_indexed2_bf16_t3, tt_tower_update_lazy, tt_tower_t3_fuse_supported,
+ *    tt_tower_counter_offset; the WGRAD | INSERT | ADAGRAD | UPDATE launch plan) */
+#define TT_ABI_VERSION 3
 
 /* status codes (besides hipError_t values, which are all < 1000) */
 #define TT_OK 0
@@ -380,45 +383,6 @@ int tt_tower_wgrad_pre(const tt_tower_shape_t* shape, int64_t B, float* loss, vo
 int tt_tower_update_pre(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
                         float eps, float beta1, float beta2, float weight_decay, float* grads_out, void* workspace,
                         size_t ws_bytes, void* stream);
-/* ---- the ring with T3 folded into the next step's T1 (two launches per step) -------------------
- * A WGRAD role (tt_launch, tt_tower_wgrad_pre) marks the step's Adam update pending in the tower
- * workspace; every T3 form that applies it clears the mark. tt_tower_fwd_bwd_gather_update_t3 is
- * tt_tower_fwd_bwd_gather_update (without the next-batch prefetch) whose launch first applies a
- * pending update exactly as tt_tower_update_pre would (same reduction order, same arithmetic, same
- * copies), every workgroup waiting in-launch for all of them before reading the weights: the
- * results are bit-identical to T3 followed by T1. It needs every workgroup resident at once
- * (tt_tower_t3_fuse_supported: the row-owned T1 shape, <= 32 slabs, one workgroup per 32 rows
- * within the device's residency) and fails with TT_EINVAL otherwise. After the last step of a run
- * the update is still pending: tt_tower_update_lazy (grads_in NULL: the slabs) applies it if (and only if) it is, so the
- * parameters / moments / copies are current before anything else reads them. Replaces the Adam
- * step of KeyedOptimizerWrapper(Adam) (03_model_training.py:826-829), deferred into the next step. */
-int tt_tower_t3_fuse_supported(const tt_tower_shape_t* shape, int64_t B);
-int tt_tower_fwd_bwd_gather_update_t3(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
-                                      const int64_t* num_embeddings, float* const* table_rows,
-                                      float* const* table_state, float* pooled_out, int64_t ldp, float* gpooled,
-                                      float* params, float* exp_avg, float* exp_avg_sq, float adam_eps,
-                                      float beta1, float beta2, float weight_decay, float* grads_out,
-                                      const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
-                                      float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
-                                      void* workspace, size_t ws_bytes, void* stream);
-int tt_tower_update_lazy(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
-                         float eps, float beta1, float beta2, float weight_decay, float* grads_out,
-                         const float* grads_in, int nsrc, int64_t src_stride, void* workspace, size_t ws_bytes,
-                         void* stream);
-/* The sharded step's T1 (tt_tower_fwd_bwd_indexed2_bf16) whose launch first applies the pending
- * update as tt_tower_adam_pre_grads_sum would: Adam on the fixed-order sum of the nsrc received
- * tower gradients (grads_in + q * src_stride, q < nsrc <= 32). tt_tower_update_lazy with the same
- * grads_in / nsrc / src_stride flushes the last step's. */
-int tt_tower_fwd_bwd_indexed2_bf16_t3(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
-                                      const int32_t* const* pos_out, const void* const* rows_in,
-                                      float* const* grad_rows_out, float* params, float* exp_avg, float* exp_avg_sq,
-                                      float adam_eps, float beta1, float beta2, float weight_decay,
-                                      const float* grads_in, int nsrc, int64_t src_stride, const void* labels,
-                                      int label_dtype, float grad_scale, float* logits, void* workspace,
-                                      size_t ws_bytes, void* stream);
-/* Byte offset of the tower workspace's counter words (uint32): [2] update pending, [6] in-launch
- * waits of tt_tower_fwd_bwd_gather_update_t3 that timed out (must stay 0); -1 for a bad shape. */
-int64_t tt_tower_counter_offset(const tt_tower_shape_t* shape, int64_t B);
 /* T3: fixed-order reduction of T2's partials, Adam (when do_adam; step_state as tt_adam_step),
  * and the bf16 weight copies for the next T1. grads_out (nullable) receives the gradient. */
 int tt_tower_update(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg,
@@ -595,9 +559,6 @@ int tt_pooled_grad_pack(int W, int F, int64_t B, int D, const float* grad, int64
  *   WGRAD | INSERT | ADAGRAD       single-GPU ring tail: T2 + the next batch's complete insert + the
  *                                  rows looked up more than once (ADAGRAD.multi_only = 1); T1 updated
  *                                  the others (03:455 backward + 03:791-795 RowWiseAdagrad)
- *   WGRAD | INSERT | ADAGRAD      the same + T3 in the same grid (its workgroups last, waiting for
- *     | UPDATE                     every T2 workgroup's write-through slab rows); row-owned T1
- *                                  shapes only; measured slower than the separate T3
  *   WGRAD | INSERT                 T2 + the next batch's insert, first CAS only (the rest deferred
  *                                  to the RESOLVE role of the following launch)
  *   UPDATE | ADAGRAD | RESOLVE     T3 + rows looked up more than once (multi_only = 1) + the

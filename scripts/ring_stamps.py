@@ -63,14 +63,6 @@ for it in range(6):
     torch.cuda.synchronize()
     if it < 2:
         continue
-    if st.ring_tail and st.t3_in_tail():  # T3 in the tail (TT_T3_IN_TAIL=1): its stamp 0 = the wait's end
-        n_ins, dd, g3 = 64, int(os.environ.get("K3_DD", "576")), (49536 + 255) // 256
-        t0 = n_ins + ntile + nbias + dd
-        show("tail+T3", base[4096:8192], [("insert", 0, n_ins), ("tiles", n_ins, n_ins + ntile),
-                                          ("bias", n_ins + ntile, n_ins + ntile + nbias),
-                                          ("hot", n_ins + ntile + nbias, n_ins + ntile + nbias + 64),
-                                          ("slots", n_ins + ntile + nbias + 64, t0), ("t3", t0, t0 + g3)])
-        continue
     if st.ring_tail:
         n_ins, dd = 64, int(os.environ.get("K3_DD", "576"))
         show("tail", base[4096:6144], [("insert", 0, n_ins), ("tiles", n_ins, n_ins + ntile),
@@ -86,7 +78,7 @@ for it in range(6):
          [("resolver", 0, 32)] + [(f"wg{a}", a, a + 64) for a in range(32, used, 64)])
 
 # T3 (tower_update_kernel) phases of the last step: 0 start, 1 gradient summed, 2 stores issued
-if st.ring_tail and not st.t3_in_tail():
+if st.ring_tail:
     base[6144:].zero_()
     st.run_eager(1)
     torch.cuda.synchronize()

@@ -38,7 +38,7 @@ def test_every_declared_symbol_exported(lib):
     assert not extra, f"exported but not declared in the header: {extra}"
     assert sorted(_lib.SIGNATURES) == declared
     assert lib.tt_num_entry_points() == len(_lib.COMPUTE_ENTRY_POINTS)
-    assert lib.tt_abi_version() == 2
+    assert lib.tt_abi_version() == 3
 
 
 def test_launch_plan_layout_matches_the_header(tmp_path):

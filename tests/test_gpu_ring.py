@@ -3,7 +3,6 @@ inside T1, the others by the tail launch from dX, then T3; or T2 + deferred inse
 update + T3): bit for bit the classic step (insert in T1, every row updated
 by K3), over resident batches with dropped ids, ids past N, repeated rows (2..30 lookups) and hot
 rows (> 30), through HIP graphs of several steps and eagerly."""
-import os
 
 import pytest
 import torch
@@ -154,75 +153,3 @@ def test_ring_one_row_batch_vs_formula(device):
     w1 = w0 - lr * G / (np.sqrt(s1) + 1e-10)
     np.testing.assert_allclose(float(st.tables.state_view(1)[row]), s1, rtol=1e-4)
     np.testing.assert_allclose(st.tables.table_view(1)[row].double().cpu().numpy(), w1.numpy(), rtol=1e-4, atol=1e-7)
-
-
-@pytest.mark.parametrize("B", [2048, 8192])
-def test_ring_t3_in_tail_equals_three_launches(device, B):
-    """T3 inside the tail launch (its workgroups last in the grid, waiting in-launch for every T2
-    workgroup's write-through slab rows) against the three-launch ring, bit for bit, through graphs
-    and eager steps; no wait may time out and the hand-off counters are reset after each launch."""
-    from two_tower_recommender_model_amd import _lib
-    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
-    import ctypes as C
-
-    N = [300_000, 500_000]
-    batches = _batches(N, B, 6, seed=B + 1, device=device)
-    a = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=7)
-    b = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=7)
-    a._t3t, b._t3t = True, False
-    for st in (a, b):
-        st.capture_ring(batches, steps_per_graph=2)
-        st.run(3)
-        st.run_eager(2)
-        st.run(1)
-    torch.cuda.synchronize()
-    off = _lib.load().tt_tower_counter_offset(C.byref(a.towers.shape), B)
-    words = a.towers.ws[off:off + 64].view(torch.int32).tolist()
-    assert words[10] == 0, words  # in-launch waits that timed out
-    assert words[2] == 0  # nothing pending
-    assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
-    for x, y in ((a.params, b.params), (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq), (a.grads, b.grads),
-                 (a.logits, b.logits)):
-        assert torch.equal(x, y)
-    assert float(a.loss) == float(b.loss)
-    assert int(a.adam_state[0]) == int(b.adam_state[0]) == 6
-
-
-@pytest.mark.parametrize("B", [2048, 8192])
-def test_ring_t3_folded_into_t1_equals_three_launches(device, B):
-    """The two-launch ring (T3 applied at the start of the next step's T1 launch, every workgroup
-    waiting in-launch for the update; flush() after the last step) against the three-launch ring,
-    bit for bit: tables, row state, tower parameters, both Adam moments, the tower gradient, loss
-    and logits, through graphs and eager steps. B = 2048: 64 workgroups of 774 parameters (4
-    rounds each); 8192: 256 workgroups of 194. No in-launch wait may time out, and nothing is left
-    pending after run()."""
-    from two_tower_recommender_model_amd import _lib
-    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
-    import ctypes as C
-
-    N = [300_000, 500_000]
-    batches = _batches(N, B, 6, seed=B, device=device)
-    a = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=6)
-    b = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=6)
-    b._t1f = False
-    a._t1f = None
-    os.environ["TT_T1_FUSE"] = "1"
-    try:
-        assert a.t1_fuse(), "the T3 + T1 launch should serve this shape on an MI355X"
-    finally:
-        del os.environ["TT_T1_FUSE"]
-    for st in (a, b):
-        st.capture_ring(batches, steps_per_graph=2)
-        st.run(3)
-        st.run_eager(2)
-        st.run(1)
-    torch.cuda.synchronize()
-    assert a.fuse_timeouts() == 0
-    off = _lib.load().tt_tower_counter_offset(C.byref(a.towers.shape), B)
-    assert int(a.towers.ws[off + 8:off + 12].view(torch.int32).item()) == 0  # nothing pending
-    assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
-    for x, y in ((a.params, b.params), (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq), (a.grads, b.grads),
-                 (a.logits, b.logits)):
-        assert torch.equal(x, y)
-    assert float(a.loss) == float(b.loss)
-    assert int(a.adam_state[0]) == int(b.adam_state[0]) == 6

@@ -5,7 +5,6 @@ in-process all-to-all (ThreadComm) against the oracle: the rows each rank's towe
 oracle tables bit for bit, every shard after each step equals the oracle's row-wise Adagrad over
 the union of the gradient rows the ranks produced (ascending (rank, bag) order), and the
 data-parallel towers stay identical on every rank."""
-import os
 import threading
 
 import numpy as np
@@ -466,60 +465,3 @@ def test_sharded_config3_w8_baseline_size(device):
 
     gc.collect()
     torch.cuda.empty_cache()
-
-
-@pytest.mark.parametrize("W", [1, 2])
-def test_sharded_adam_folded_into_t1_equals_separate_launch(device, W):
-    """The pipelined step with the tower Adam update applied at the start of the next step's T1
-    launch (tt_tower_fwd_bwd_indexed2_bf16_t3; flush() after the last step) equals the step with
-    Adam in its own launch bit for bit: tables, row state, parameters, moments, loss, logits."""
-    from two_tower_recommender_model_amd.sharded import FusedShardedTwoTowerStep, ThreadComm
-
-    B, D, N = 2048, 128, [40_000, 60_000]
-    gen = torch.Generator().manual_seed(70 + W)
-    full = [torch.empty(n, D).uniform_(-0.05, 0.05, generator=gen) for n in N]
-    pools = []
-    for r in range(W):
-        pool = []
-        for _ in range(4):
-            cols = [torch.randint(0, 2 * n, (B,), generator=gen).to(device) for n in N]
-            cols[1][:30] = 91  # a hot row
-            pool.append((cols, torch.randint(0, 2, (B,), generator=gen).to(torch.int32).to(device)))
-        pools.append(pool)
-    runs = {}
-    for fuse in (False, True):
-        comms = ThreadComm.group(W)
-        steps = [None] * W
-
-        def build(r):
-            torch.cuda.set_device(device)
-            steps[r] = FusedShardedTwoTowerStep(comms[r], N, D, [128, 64], B, device, full_tables=full, seed=9)
-            steps[r]._t1f = False
-
-        _run_ranks([lambda r=r: build(r) for r in range(W)])
-        if fuse:  # opt-in (TT_T1_FUSE=1), decided per step object before its first step
-            os.environ["TT_T1_FUSE"] = "1"
-            try:
-                for st in steps:
-                    st._t1f = None
-                    assert st.t1_fuse(), "the fused Adam + T1 launch should serve this shape on an MI355X"
-            finally:
-                del os.environ["TT_T1_FUSE"]
-
-        def go(r):
-            torch.cuda.set_device(device)
-            steps[r].run_eager(pools[r], 3)
-            steps[r].run_eager(pools[r], 4)
-            torch.cuda.synchronize()
-
-        _run_ranks([lambda r=r: go(r) for r in range(W)])
-        runs[fuse] = steps
-    for r in range(W):
-        a, b = runs[False][r], runs[True][r]
-        if W == 1:
-            b.check()
-        assert b.fuse_timeouts() == 0
-        assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
-        for x, y in ((a.params, b.params), (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq), (a.logits, b.logits)):
-            assert torch.equal(x, y)
-        assert float(a.loss) == float(b.loss)

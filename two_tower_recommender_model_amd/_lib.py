@@ -268,20 +268,6 @@ SIGNATURES = {
         _int,
         [_psh, _i64, _int, _vp, _vp, _vp, _vp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
     ),
-    "tt_tower_t3_fuse_supported": (_int, [_psh, _i64]),
-    "tt_tower_counter_offset": (_i64, [_psh, _i64]),
-    "tt_tower_fwd_bwd_gather_update_t3": (
-        _int,
-        [_psh, _i64, _pvp, _int, _pi64, _pvp, _pvp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp,
-         _int, _f32, _vp, _f32, _f32, _vp, _sz, _i64, _vp, _sz, _vp],
-    ),
-    "tt_tower_update_lazy": (_int, [_psh, _i64, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _int, _i64, _vp, _sz,
-                                    _vp]),
-    "tt_tower_fwd_bwd_indexed2_bf16_t3": (
-        _int,
-        [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _int, _i64, _vp, _int, _f32,
-         _vp, _vp, _sz, _vp],
-    ),
     "tt_bwd_rowwise_adagrad_part": (
         _int, [_ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _int, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _int, _vp],
     ),
@@ -337,9 +323,6 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_gather_update",
     "tt_tower_adam_pre_grads_sum",
     "tt_tower_fwd_bwd_indexed_multi_bf16",
-    "tt_tower_fwd_bwd_gather_update_t3",
-    "tt_tower_update_lazy",
-    "tt_tower_fwd_bwd_indexed2_bf16_t3",
     "tt_bwd_rowwise_adagrad_part",
     "tt_launch",
 ]

@@ -71,7 +71,6 @@ struct TowerArgs {
   __bf16* dzt;          // [2][MAXL][MAXW][B]
   float* dbpart;        // [2][MAXL][nwg][MAXW]
   float* loss_part;     // [nwg]
-  uint32_t* sync;       // row-owned T1: zeroes the tail's completion counters (tail_t3_block)
   int64_t in_max;
   int64_t Bp;           // strip rows per block (B rounded up to 32)
   int nwg;
@@ -1416,8 +1415,6 @@ struct UpdateArgs {
   int in_srcs;
   int64_t in_stride;
   char* wimg;  // nullable: the row-owned T1's weight image (rk_off), written beside the other copies
-  int lazy;    // apply Adam only if T2 left the step pending (CW_PENDING), then clear it
-  int fuse_per;  // the T3 + T1 launch: parameters per workgroup (rounds of 256, <= 4096)
 #if TT_EXPERIMENTS
   int64_t* stamps;  // EXPERIMENT (TT_RING_STAMPS): [workgroups][4] s_memrealtime per phase
 #endif
@@ -1457,7 +1454,7 @@ __device__ __forceinline__ T3Seg t3_seg(const UpdateArgs& a, int64_t i) {
 __device__ __forceinline__ void t3_apply(const UpdateArgs& a, int64_t i, const T3Seg& sg, float p, float m,
                                          float v0, float g, float step_size, float bc2_sqrt, bool adam) {
   // no fma contraction: the contraction choice would otherwise depend on the inlining context (T3,
-  // the fused T3 + T1 launch, the lazy flush), and every form must give the same bits
+  // the sharded step's launch G), and every form must give the same bits
 #pragma clang fp contract(off)
   const int64_t e = i - sg.soff;
   if (a.grads_out) {
@@ -1492,58 +1489,17 @@ __device__ __forceinline__ void t3_apply(const UpdateArgs& a, int64_t i, const T
   }
 }
 
-// the fused T3 share's gradient terms of parameter i, all loads issued at once (<= 32 terms: the
-// host checks S and in_srcs): the W received tower gradients (grads_in), or the weight's S slabs /
-// the bias's one reduced slab; t3_sum adds them in update_block's order
-__device__ __forceinline__ void t3_terms(const UpdateArgs& a, float (&v)[32], int64_t i, const T3Seg& sg) {
-  if (a.grads_in) {
-#pragma unroll
-    for (int k = 0; k < 32; ++k) v[k] = k < a.in_srcs ? a.grads_in[(int64_t)k * a.in_stride + i] : 0.f;
-  } else {
-#pragma unroll
-    for (int k = 0; k < 32; ++k) v[k] = k < a.S && (k == 0 || sg.sisw) ? a.slab[(int64_t)k * a.P + i] : 0.f;
-  }
-}
-__device__ __forceinline__ float t3_sum(const UpdateArgs& a, const float (&v)[32], const T3Seg& sg) {
-  if (a.grads_in) {
-    float g = v[0];
-#pragma unroll
-    for (int k = 1; k < 32; ++k)
-      if (k < a.in_srcs) g += v[k];
-    return g;
-  }
-  if (!sg.sisw) return v[0];
-  float g = 0.f;
-#pragma unroll
-  for (int k = 0; k < 32; ++k)
-    if (k < a.S) g += v[k];
-  return g;
-}
-
-// words of the tower workspace's counter region (adam_pre = its first two floats; tt_tower_counter_offset):
-// [2] Adam step pending (set by T2 with adam_pre, cleared by the T3 that applies it), [3] the lazy
-// T3's arrivals, [4] / [5] the fused T3 + T1 launch's arrivals / passes, [6] its poll timeouts
-constexpr int CW_PENDING = 2, CW_LAZY_ARRIVE = 3, CW_FUSE_ARRIVE = 4, CW_FUSE_PASSED = 5, CW_FUSE_TIMEOUT = 6;
-constexpr int SYNC_SPREAD = 8, SYNC_STRIDE = 32, CW_T3_TIMEOUT = 10;  // T3 in the tail (tail_t3_block)
-
 // IDX: the sharded step's form (tt_tower_fwd_bwd_indexed2_bf16): tower t's input row m is bf16 row
 // gpos[t][m] of gsrc[t] (-1: zeros; the rows an owner returned, dense), its dX goes to fp32 row
 // gpos_out[t][m] of gdst[t]; no in-place update, no insert
-// FUSE (the ring's T3 + T1 launch, tt_tower_fwd_bwd_gather_update_t3): the launch first applies the
-// Adam step the previous step's tail left pending (CW_PENDING): each workgroup takes u.fuse_per
-// parameters (one per thread: the slab sum, Adam, the bf16 copies T1 reads, the image), publishes
-// them (vmcnt(0), barrier, one agent-scope release, an arrival), and waits for every workgroup's
-// arrival before it reads the weight image and the biases. Every workgroup must be resident at
-// once (the host checks the occupancy); the wait is bounded (CW_FUSE_TIMEOUT records a miss).
-// The table rows are gathered while the update runs: they do not depend on it.
 // IN: the input width (128 or 64: config 2's D = 64; the first layer then has 2 k-steps and dX 4
 // M-tiles, the rows are 256 B)
 // POOL: the input rows are the pooled matrix's (tower t's row m at a.pooled + m ldp + in_col[t]:
 // the multi-hot path's T1 after tt_pooled_fwd), no ids, no dedup
-template <bool UPD, bool IDX, bool FUSE, int IN, bool POOL = false>
-__device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const UpdateArgs& u) {
+template <bool UPD, bool IDX, int IN, bool POOL = false>
+__device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   static_assert(IN == 128 || IN == 64, "row-owned T1: inputs of 128 or 64");
-  static_assert(!POOL || (!UPD && !IDX && !FUSE), "pooled input: the plain T1 only");
+  static_assert(!POOL || (!UPD && !IDX), "pooled input: the plain T1 only");
   constexpr int NI = IN / 32;   // layer-0 k-steps (B-operand pieces xb[s], s < NI)
   constexpr int MTI = IN / 16;  // dX M-tiles (row pieces xv[mt], mt < MTI)
   __shared__ __attribute__((aligned(16))) char wimg[RK_IMG];         // both towers' W0, W1 (rk_off)
@@ -1554,8 +1510,6 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
                                                                     // (fp32, 16-B chunk c of row n at c ^ n)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = wid >> 1, h = wid & 1, q = lane >> 4, n = lane & 15;
-  // the completion counters of the tail launch that follows (T3 in the tail): zero at its start
-  if (blockIdx.x == 0 && threadIdx.x < SYNC_SPREAD) a.sync[threadIdx.x * SYNC_STRIDE] = 0u;
   const int64_t B = a.B, m0 = (int64_t)blockIdx.x * TR, m = m0 + 16 * h + n;
   const bool live = m < B;
   RK_STAMP(0);
@@ -1590,34 +1544,9 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
     for (int k = 0; k < RK_IMG / 1024 / 4; ++k)
       wreg[k] = *reinterpret_cast<const bf16x8*>(a.wimg + (wid + 4 * k) * 1024 + lane * 16);
   };
-  // FUSE: this workgroup's share of the pending Adam step, loads issued now (beside the ids)
-  uint32_t* cw = FUSE ? reinterpret_cast<uint32_t*>(const_cast<float*>(u.adam_pre)) : nullptr;
-  bool pending = false;
-  int64_t ui = 0;
-  bool uon = false;
-  T3Seg useg;
-  float up = 0.f, um = 0.f, uv = 0.f, ug = 0.f;
-  float uslab[32];
-  if (FUSE) {
-    // the share's loads are issued before the pending word is known (it almost always is: a
-    // branch on it would put a whole memory round trip in front of them)
-    ui = (int64_t)blockIdx.x * u.fuse_per + threadIdx.x;
-    const bool mine = (int)threadIdx.x < u.fuse_per && ui < u.P;
-    const int64_t uc = mine ? ui : 0;
-    useg = t3_seg(u, uc);
-    up = u.params[uc];
-    um = u.exp_avg[uc];
-    uv = u.exp_avg_sq[uc];
-    t3_terms(u, uslab, uc, useg);
-    pending = __builtin_amdgcn_readfirstlane(
-                  __hip_atomic_load(cw + CW_PENDING, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
-    uon = pending && mine;
-    RK_STAMP2(4);
-  } else {
-    load_biases();
-    __builtin_amdgcn_sched_barrier(0);
-    load_image();
-  }
+  load_biases();
+  __builtin_amdgcn_sched_barrier(0);
+  load_image();
   __builtin_amdgcn_sched_barrier(0);
   int64_t r;  // the row's index in its source (table row / returned-rows buffer row), -1: zeros
   if (POOL) {
@@ -1674,57 +1603,6 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
     dd_insert_begin(a.dd, key, li, pend);
   }
   RK_STAMP(1);
-  if (FUSE) {
-    if (pending) {
-      // the gradient summed as update_block sums it, Adam, the copies; then publish
-      ug = t3_sum(u, uslab, useg);
-      if (uon) t3_apply(u, ui, useg, up, um, uv, ug, u.adam_pre[0], u.adam_pre[1], true);
-      // small batches (few workgroups): further rounds of 256 parameters, one after another
-      for (int k = 256; k < u.fuse_per; k += 256) {
-        const int64_t i2 = ui + k;
-        const bool on2 = (int)threadIdx.x + k < u.fuse_per && i2 < u.P;
-        const int64_t c2 = on2 ? i2 : 0;
-        const T3Seg sg2 = t3_seg(u, c2);
-        const float p2 = u.params[c2], m2 = u.exp_avg[c2], v2 = u.exp_avg_sq[c2];
-        t3_terms(u, uslab, c2, sg2);
-        const float g2 = t3_sum(u, uslab, sg2);
-        if (on2) t3_apply(u, i2, sg2, p2, m2, v2, g2, u.adam_pre[0], u.adam_pre[1], true);
-      }
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores (and the rows)
-      RK_STAMP2(5);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(cw + CW_FUSE_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        RK_STAMP2(8);
-        const unsigned nwg = gridDim.x;
-        int spin = 0;
-        while (__hip_atomic_load(cw + CW_FUSE_ARRIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg) {
-          if (++spin > (1 << 20)) {  // ~50 ms: a workgroup was not resident; recorded, not waited for
-            __hip_atomic_fetch_add(cw + CW_FUSE_TIMEOUT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prev = __hip_atomic_fetch_add(cw + CW_FUSE_PASSED, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == nwg - 1) {  // every workgroup is past the wait (and read CW_PENDING before it)
-          __hip_atomic_store(cw + CW_FUSE_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(cw + CW_FUSE_PASSED, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(cw + CW_PENDING, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      RK_STAMP2(6);
-      __syncthreads();
-      RK_STAMP2(7);
-    }
-    load_biases();
-    __builtin_amdgcn_sched_barrier(0);
-    load_image();
-    __builtin_amdgcn_sched_barrier(0);
-  }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the rows (LDS-DMA) and the image registers
   RK_STAMP(2);
 #pragma unroll
@@ -2002,12 +1880,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a, const Update
 }
 template <bool UPD, bool IDX = false, int IN = 128, bool POOL = false>
 __global__ void __launch_bounds__(256) tower_rows_kernel(TowerArgs a) {
-  const UpdateArgs u{};
-  tower_rows_body<UPD, IDX, false, IN, POOL>(a, u);
-}
-template <int IN = 128, bool IDX = false>
-__global__ void __launch_bounds__(256) tower_rows_t3_kernel(TowerArgs a, UpdateArgs u) {
-  tower_rows_body<!IDX, IDX, true, IN>(a, u);
+  tower_rows_body<UPD, IDX, IN, POOL>(a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2057,30 +1930,8 @@ struct WgradArgs {
 #endif
   DedupWs dd;           // tt_tower_wgrad_pre with a dedup workspace: the first n_res workgroups
   int n_res;            //   finish T1's deferred inserts (dd_resolve_block)
-  // T3 in the tail launch (tower_tail_t3_kernel): the slabs, bias sums and Adam scalars are stored
-  // write-through (sc1) and every T2 workgroup then adds one to a completion counter (MI355X_MICROARCH.md
-  // hand-off row 1: the T3 workgroups read them with sc1 loads once the count is complete)
-  int wt;
-  uint32_t* pub;          // completion counters (SYNC_SPREAD, SYNC_STRIDE apart; zeroed by T1)
-  uint32_t* pub_timeout;
 };
 
-// a write-through (sc1) 16-B store at byte offset off of the buffer that starts at base (< 4 GB)
-__device__ __forceinline__ void wt_store16(const void* base, uint32_t nbytes, uint32_t off, f32x4 v) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes,
-                                                                      0x00020000);
-  typedef __attribute__((ext_vector_type(4))) unsigned u4;
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, off, 0, 16 /* sc1 */);
-}
-// the T2 workgroup's hand-off to the T3 workgroups of the same launch: every wave's stores drained,
-// then one count (called by every thread of the workgroup)
-__device__ __forceinline__ void wgrad_publish(const WgradArgs& a) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(a.pub + (blockIdx.x % SYNC_SPREAD) * SYNC_STRIDE, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
 #if TT_EXPERIMENTS
 #define T2_STAMP(k) \
   do { if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); } while (0)
@@ -2295,43 +2146,17 @@ __device__ __forceinline__ void wgrad_lds_block_rm(const WgradArgs& a, int lb, c
   }
   T2_STAMP(2);
   float* dst = a.slab + (int64_t)s * a.P + a.woff[t][l];
-  if (a.wt) {
-    // 16-B write-through stores: a 4 x 4 transpose across the lanes r = 4 m .. 4 m + 3 of each
-    // 16-lane row gives lane 4 m + c row q * 4 + c, columns 4 m .. 4 m + 3 (contiguous in [n][K])
-    const int c = r & 3, m4 = r & ~3;
-    const uint32_t nbytes = (uint32_t)((int64_t)a.S * a.P * 4);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K) {
-          f32x4 o;
+    for (int j = 0; j < 4; ++j)
+      if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
 #pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int src = (c - d) & 3;  // the component this lane sends in round d
-            const float send = src == 0 ? acc[i][j][0] : src == 1 ? acc[i][j][1] : src == 2 ? acc[i][j][2] : acc[i][j][3];
-            const float got = __shfl(send, (lane & ~3) + ((c + d) & 3), 64);
-            const int dc = (c + d) & 3;
-            if (dc == 0) o[0] = got; else if (dc == 1) o[1] = got; else if (dc == 2) o[2] = got; else o[3] = got;
-          }
-          const int n = n0 + nh * 32 + i * 16 + q * 4 + c;
-          const int k = kh * 64 + j * 16 + m4;
-          wt_store16(a.slab, nbytes, (uint32_t)(((int64_t)s * a.P + a.woff[t][l] + (int64_t)n * K + k) * 4), o);
+        for (int rr = 0; rr < 4; ++rr) {
+          const int n = n0 + nh * 32 + i * 16 + q * 4 + rr;
+          const int k = kh * 64 + j * 16 + r;
+          dst[(int64_t)n * K + k] = acc[i][j][rr];
         }
-    wgrad_publish(a);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (nh * 32 + i * 16 < NT && kh * 64 + j * 16 < K)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int n = n0 + nh * 32 + i * 16 + q * 4 + rr;
-            const int k = kh * 64 + j * 16 + r;
-            dst[(int64_t)n * K + k] = acc[i][j][rr];
-          }
-  }
   T2_STAMP(3);
 }
 
@@ -2368,15 +2193,8 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
         a.step_state[0] = t_step;
         const double bc1 = 1.0 - pow((double)a.beta1, (double)t_step);
         const double bc2 = 1.0 - pow((double)a.beta2, (double)t_step);
-        if (a.wt) {  // read by the T3 workgroups of this launch (sc1 loads)
-          __hip_atomic_store(a.adam_pre, (float)((double)a.lr / bc1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(a.adam_pre + 1, (float)sqrt(bc2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          a.adam_pre[0] = (float)((double)a.lr / bc1);
-          a.adam_pre[1] = (float)sqrt(bc2);
-        }
-        // CW_PENDING: the step's Adam is due (coherent: a T3 of this launch may clear it)
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(a.adam_pre) + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.adam_pre[0] = (float)((double)a.lr / bc1);
+        a.adam_pre[1] = (float)sqrt(bc2);
       }
     }
     for (int t = 0; t < 2; ++t)
@@ -2396,16 +2214,10 @@ __device__ __forceinline__ void wgrad_block(const WgradArgs& a, const WgradTile*
             for (int k = 0; k < 8; ++k) s += v[k];
           }
           s = wave_sum(s);
-          if (lane == 0) {
-            if (a.wt)
-              __hip_atomic_store(a.slab + a.boff[t][l] + b, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-              a.slab[a.boff[t][l] + b] = s;
-          }
+          if (lane == 0) a.slab[a.boff[t][l] + b] = s;
         }
         if (b >= 0) b -= a.width[l];
       }
-    if (a.wt) wgrad_publish(a);
     T2_STAMP(3);
     return;
   }
@@ -2622,25 +2434,14 @@ __global__ void __launch_bounds__(256) tower_wgrad_route_rowwise_kernel(WgradArg
   }
 }
 
-// WT: T3 in the tail launch (tower_tail_t3_kernel): the slabs and the Adam scalars were stored
-// write-through by T2 workgroups of the same launch, so they are read with sc1 loads
-template <bool WT = false>
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
   T3_STAMP(0);
   const int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
-  uint32_t* cw = a.adam_pre ? reinterpret_cast<uint32_t*>(const_cast<float*>(a.adam_pre)) : nullptr;
-  // lazy (the fused T3 + T1 ring's flush): apply the Adam step T2 left pending, if any
-  if (a.lazy && cw[CW_PENDING] == 0u) return;
   int64_t t_step = 0;
   float step_size = 0.f, bc2_sqrt = 1.f;
   if (a.do_adam && a.adam_pre) {
-    if (WT) {
-      step_size = __hip_atomic_load(const_cast<float*>(a.adam_pre), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bc2_sqrt = __hip_atomic_load(const_cast<float*>(a.adam_pre) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      step_size = a.adam_pre[0];
-      bc2_sqrt = a.adam_pre[1];
-    }
+    step_size = a.adam_pre[0];
+    bc2_sqrt = a.adam_pre[1];
   } else if (a.do_adam) {
     t_step = a.step_state[0] + 1;
     const double bc1 = 1.0 - pow((double)a.beta1, (double)t_step);
@@ -2664,10 +2465,7 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
           float v[32];
 #pragma unroll
           for (int u = 0; u < 32; ++u) {
-            const float* sp = a.slab + (int64_t)(s0 + u) * a.P + i;
-            v[u] = s0 + u < a.S ? (WT ? __hip_atomic_load(const_cast<float*>(sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : *sp)
-                                : 0.f;
+            v[u] = s0 + u < a.S ? a.slab[(int64_t)(s0 + u) * a.P + i] : 0.f;
           }
 #pragma unroll
           for (int u = 0; u < 32; ++u)
@@ -2675,26 +2473,12 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
         }
       } else {
         // bias gradient, reduced over the T1 workgroups by T2's bias waves
-        g = WT ? __hip_atomic_load(const_cast<float*>(a.slab) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.slab[i];
+        g = a.slab[i];
       }
     }
     T3_STAMP(1);
     t3_apply(a, i, sg, p, m, v, g, step_size, bc2_sqrt, a.do_adam);
     T3_STAMP(2);
-  }
-  if (a.lazy) {  // the last workgroup to finish clears the pending step (every one read it first)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(cw + CW_LAZY_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == (unsigned)nblocks - 1) {
-        __hip_atomic_store(cw + CW_LAZY_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cw + CW_PENDING, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  } else if (a.do_adam && a.adam_pre && bid == 0 && threadIdx.x == 0) {
-    // applied (no workgroup of this launch reads the word; coherent: a WGRAD role of the same
-    // launch may have set it)
-    __hip_atomic_store(cw + CW_PENDING, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (a.do_adam && !a.adam_pre) {
     __syncthreads();
@@ -2711,38 +2495,6 @@ __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int n
 }
 
 __global__ void __launch_bounds__(256) tower_update_kernel(UpdateArgs a) { update_block(a, (int)blockIdx.x, (int)gridDim.x); }
-
-// T3 in the tail: the T2 workgroups of a launch count their completion on 8 counters 128 B apart
-// (workgroup id mod 8: single-address atomics from every workgroup serialise), zeroed by the
-// row-owned T1 that precedes every tail. The waits that timed out are counted in the counter
-// region's word 10 (must stay 0).
-__device__ __forceinline__ void tail_t3_block(const UpdateArgs& u, const uint32_t* pub, uint32_t* timeout,
-                                              int n_t2, int bid, int g3, int64_t* stamps) {
-  const int lane = threadIdx.x & 63;
-  if (threadIdx.x < 64) {
-    int spin = 0;
-    for (;;) {
-      uint32_t v = 0;
-      if (lane < SYNC_SPREAD)
-        v = __hip_atomic_load(const_cast<uint32_t*>(pub) + lane * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int o = 4; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (__builtin_amdgcn_readfirstlane(v) >= (uint32_t)n_t2) break;
-      if (++spin > (1 << 22)) {  // ~200 ms: recorded, not waited for
-        if (lane == 0) __hip_atomic_fetch_add(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-#if TT_EXPERIMENTS  // the wait's end (in place of the start) in the stamps of T3 in the tail
-  if (stamps && threadIdx.x == 0 && blockIdx.x < 2048) stamps[(int64_t)blockIdx.x * 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-#else
-  (void)stamps;
-#endif
-  update_block<true>(u, bid, g3);
-}
 
 // Pipelined sharded step, launch G (after launch U updated this rank's rows): the owner's gather of
 // batch i+1's rows (bf16, into exchange B's row blocks, filing batch i+1's dedup table), the tower
@@ -2889,24 +2641,6 @@ __device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, in
   }
 }
 
-__global__ void __launch_bounds__(256, 3) tower_tail_t3_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
-                                                            InsertArgs ins, DdUpdateArgs d, UpdateArgs u, int n_ins,
-                                                            int n_t2, int n_dd, int g3, int64_t* stamps) {
-  __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
-  RING_STAMP(stamps, 0);
-  // the T3 workgroups last (they wait for every T2 workgroup: dispatched before them)
-  int b = (int)blockIdx.x;
-  if (b < n_ins)
-    insert_next_full_block(ins, b, smem);
-  else if ((b -= n_ins) < n_t2)
-    wgrad_block(a2, tiles, b, smem);
-  else if ((b -= n_t2) < n_dd)
-    dd_update_block(d, b, smem);
-  else
-    tail_t3_block(u, a2.pub, a2.pub_timeout, n_t2, b - n_dd, g3, stamps);
-  RING_STAMP(stamps, 1);
-}
-
 __global__ void __launch_bounds__(256, 3) tower_tail_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
                                                          InsertArgs ins, DdUpdateArgs d, int n_ins, int n_t2,
                                                          int64_t* stamps) {
@@ -2950,8 +2684,7 @@ struct TowerLayout {
   int32_t t2_code[16];
   int rows;  // the row-owned T1 (tower_rows_kernel) serves this shape's single-hot gather launches
   // workspace carve (bytes)
-  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_wimg, o_tiles, o_dbg, o_sync,
-      total;
+  size_t o_xt, o_act, o_dzt, o_dbpart, o_slab, o_losspart, o_counter, o_wb, o_wtb, o_wbf, o_wtbf, o_wimg, o_tiles, o_dbg, total;
 };
 
 static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) {
@@ -3040,7 +2773,6 @@ static int tower_layout(const tt_tower_shape_t* s, int64_t B, TowerLayout* lay) 
   L.o_wimg = take(L.rows ? (size_t)RK_IMG : 0);
   L.o_tiles = take((size_t)nt * sizeof(WgradTile));
   L.o_dbg = take((size_t)(std::max<int64_t>(L.nwg * 2, 1024) * 8 + L.nwg * 16 * 9) * sizeof(int64_t));
-  L.o_sync = take(SYNC_SPREAD * SYNC_STRIDE * 4);
   L.total = off;
   *lay = L;
   return TT_OK;
@@ -3112,7 +2844,7 @@ namespace tt {
 // shared by tt_tower_fwd_bwd / tt_tower_fwd_bwd_gather: checks, T1 arguments, launch
 static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, const float* pooled, int64_t ldp,
                      float* gpooled, const float* params, const void* labels, int label_dtype, float grad_scale,
-                     float* logits, void* workspace, size_t ws_bytes, void* stream, const UpdateArgs* fuse = nullptr) {
+                     float* logits, void* workspace, size_t ws_bytes, void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
@@ -3153,7 +2885,6 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
   a.dzt = reinterpret_cast<__bf16*>(ws + L.o_dzt);
   a.dbpart = reinterpret_cast<float*>(ws + L.o_dbpart);
   a.loss_part = reinterpret_cast<float*>(ws + L.o_losspart);
-  a.sync = reinterpret_cast<uint32_t*>(ws + L.o_sync);
   a.in_max = L.in_max;
   a.Bp = L.Bp;
   a.nwg = L.nwg;
@@ -3193,19 +2924,8 @@ static int launch_t1(const tt_tower_shape_t* shape, int64_t B, TowerArgs& a, con
 #if TT_EXPERIMENTS
   if (getenv("TT_T1_CLASSIC")) rows_t1 = false;  // EXPERIMENT (A/B): tower_l2_kernel instead
 #endif
-  if (fuse && !(rows_t1 && ((a.uw[0] && !a.gpos[0]) || (a.gpos[0] && a.gsrc_bf16))))
-    return fail(TT_EINVAL, "tower: the T3 + T1 launch serves the row-owned gather + update and indexed bf16 forms only");
   if (rows_t1) {
     a.wimg = ws + L.o_wimg;
-    if (fuse) {
-      if (a.gpos[0])
-        i0 == 64 ? tower_rows_t3_kernel<64, true><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse)
-                 : tower_rows_t3_kernel<128, true><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse);
-      else
-        i0 == 64 ? tower_rows_t3_kernel<64, false><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse)
-                 : tower_rows_t3_kernel<128, false><<<g, dim3(256), 0, as_stream(stream)>>>(a, *fuse);
-      return check_launch("tower_rows_gather_update_t3");
-    }
     if (a.gpos[0])
       i0 == 64 ? tower_rows_kernel<false, true, 64><<<g, dim3(256), 0, as_stream(stream)>>>(a)
                : tower_rows_kernel<false, true, 128><<<g, dim3(256), 0, as_stream(stream)>>>(a);
@@ -3840,118 +3560,6 @@ int tt_tower_fwd_bwd_gather_update(const tt_tower_shape_t* shape, int64_t B, con
                    ws_bytes, stream);
 }
 
-// can every workgroup of the T3 + T1 launch (one per 32-row tile) be resident at once? (its
-// in-launch wait needs them all); cached per device
-static int t1f_capacity(int in, bool idx) {
-  static int cap[64][4];
-  static bool done[64][4];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  const int w = (in == 64 ? 1 : 0) + (idx ? 2 : 0);
-  if (!done[dev][w]) {
-    int per_cu = 0, cus = 0;
-    const void* ks[4] = {reinterpret_cast<const void*>(tower_rows_t3_kernel<128, false>),
-                         reinterpret_cast<const void*>(tower_rows_t3_kernel<64, false>),
-                         reinterpret_cast<const void*>(tower_rows_t3_kernel<128, true>),
-                         reinterpret_cast<const void*>(tower_rows_t3_kernel<64, true>)};
-    const void* k = ks[w];
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 0;
-    cap[dev][w] = per_cu * cus;
-    done[dev][w] = true;
-  }
-  return cap[dev][w];
-}
-
-static int t3_fuse_ok(const tt_tower_shape_t* shape, int64_t B, bool idx) {
-  TowerLayout L;
-  if (tower_layout(shape, B, &L) != TT_OK) return 0;
-  if (!L.rows || L.S > 32 || ceil_div(L.P, (int64_t)L.nwg) > 4096) return 0;
-  return L.nwg <= t1f_capacity(shape->in_dim[0], idx) ? 1 : 0;
-}
-
-int tt_tower_t3_fuse_supported(const tt_tower_shape_t* shape, int64_t B) {
-  return t3_fuse_ok(shape, B, false) && t3_fuse_ok(shape, B, true);
-}
-
-int64_t tt_tower_counter_offset(const tt_tower_shape_t* shape, int64_t B) {
-  TowerLayout L;
-  if (tower_layout(shape, B, &L) != TT_OK) return -1;
-  return (int64_t)L.o_counter;
-}
-
-int tt_tower_fwd_bwd_gather_update_t3(const tt_tower_shape_t* shape, int64_t B, const void* const* cols, int id_dtype,
-                                      const int64_t* num_embeddings, float* const* table_rows,
-                                      float* const* table_state, float* pooled_out, int64_t ldp, float* gpooled,
-                                      float* params, float* exp_avg, float* exp_avg_sq, float adam_eps,
-                                      float beta1, float beta2, float weight_decay, float* grads_out,
-                                      const void* labels, int label_dtype, float grad_scale, float* logits, float lr,
-                                      float eps, void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
-                                      void* workspace, size_t ws_bytes, void* stream) {
-  if (!cols || !num_embeddings || !table_rows || !table_state || !dedup_ws)
-    return fail(TT_EINVAL, "tower_gather_update_t3: null pointer");
-  if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_gather_update_t3: ids must be int32/int64");
-  if (dedup_max_lookups < 2 * B || dedup_max_lookups >= (int64_t)DD_CNT_MASK ||
-      dedup_ws_bytes < dedup_layout(nullptr, dedup_max_lookups, nullptr) || (reinterpret_cast<uintptr_t>(dedup_ws) & 63))
-    return fail(TT_ECAPACITY, "tower_gather_update_t3: dedup workspace too small / misaligned");
-  if (!t3_fuse_ok(shape, B, false))
-    return fail(TT_EINVAL, "tower_gather_update_t3: shape / batch not servable (row-owned T1, <= 32 slabs, <= 4096 "
-                           "parameters per workgroup, every workgroup resident)");
-  TowerArgs a{};
-  for (int t = 0; t < 2; ++t) {
-    if (!cols[t] || !table_rows[t] || !table_state[t] || num_embeddings[t] < 1)
-      return fail(TT_EINVAL, "tower_gather_update_t3: bad column");
-    if (reinterpret_cast<uintptr_t>(table_rows[t]) & 15)
-      return fail(TT_EINVAL, "tower_gather_update_t3: rows not 16-B aligned");
-    a.gcol[t] = cols[t];
-    a.gtab[t] = table_rows[t];
-    a.gmod[t] = num_embeddings[t];
-    a.uw[t] = table_rows[t];
-    a.us[t] = table_state[t];
-  }
-  a.gid_dtype = id_dtype;
-  a.pooled_out = pooled_out;
-  a.ulr = lr;
-  a.ueps = eps;
-  dedup_layout(dedup_ws, dedup_max_lookups, &a.dd);
-  TowerLayout L;
-  int rc = tower_layout(shape, B, &L);
-  if (rc) return rc;
-  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
-  UpdateArgs u;
-  int64_t g3 = 0;
-  rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, adam_eps, weight_decay, nullptr, 1, grads_out,
-               nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0, u, &g3);
-  if (rc) return rc;
-  u.fuse_per = (int)ceil_div(L.P, (int64_t)L.nwg);
-  return launch_t1(shape, B, a, nullptr, ldp, gpooled, params, labels, label_dtype, grad_scale, logits, workspace,
-                   ws_bytes, stream, &u);
-}
-
-int tt_tower_update_lazy(const tt_tower_shape_t* shape, int64_t B, float* params, float* exp_avg, float* exp_avg_sq,
-                         float eps, float beta1, float beta2, float weight_decay, float* grads_out,
-                         const float* grads_in, int nsrc, int64_t src_stride, void* workspace, size_t ws_bytes,
-                         void* stream) {
-  TowerLayout L;
-  int rc = tower_layout(shape, B, &L);
-  if (rc) return rc;
-  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if (grads_in && (nsrc < 1 || nsrc > 32 || (nsrc > 1 && src_stride < L.P)))
-    return fail(TT_EINVAL, "tower_update_lazy: bad gradient sources");
-  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
-  UpdateArgs u;
-  int64_t g3 = 0;
-  rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, grads_out,
-               grads_in, workspace, ws_bytes, pre, 1, nullptr, 1.f, grads_in ? nsrc : 1, grads_in ? src_stride : 0,
-               u, &g3);
-  if (rc) return rc;
-  u.lazy = 1;
-  tower_update_kernel<<<dim3((unsigned)g3), dim3(256), 0, as_stream(stream)>>>(u);
-  return check_launch("tower_update_lazy");
-}
-
 static int fused_wgrad_insert(const tt_tower_shape_t* shape, int64_t B, float* loss, void* workspace, size_t ws_bytes,
                               int64_t* adam_step_state, float adam_lr, float adam_beta1, float adam_beta2,
                               const void* const* next_cols, int id_dtype, const int64_t* num_embeddings,
@@ -4026,8 +3634,7 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
                                       const tt_table_meta_t* tables, int T, const tt_feature_meta_t* features,
                                       int F, const float* grad, int64_t ldg, float* weights, float* state,
                                       float lr, float emb_eps, void* dedup_ws, void* next_dedup_ws,
-                                      size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream,
-                                      const tt_update_role_t* t3 = nullptr) {
+                                      size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream) {
   if (!adam_step_state || !next_cols || !num_embeddings || !dedup_tables || !next_dedup_ws)
     return fail(TT_EINVAL, "tower_tail: null pointer");
   if (id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "tower_tail: ids must be int32/int64");
@@ -4076,25 +3683,6 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
     dd_grid = d.hot_wgs + nlb;
   }
   const int64_t n_ins = ceil_div(ceil_div(2 * B, 256 * INS_PT), 8) * 8;  // INS_PT lookups per thread; % 8 == 0
-  if (t3) {  // + T3 in the same launch, its workgroups after every other role's
-    if (!(L.lds && L.rows)) return fail(TT_EINVAL, "tower_tail: T3 in the tail needs the row-owned shape");
-    UpdateArgs u;
-    int64_t g3 = 0;
-    const float* pre = reinterpret_cast<const float*>(ws + L.o_counter);
-    rc = t3_args(shape, B, t3->params, t3->exp_avg, t3->exp_avg_sq, 0.f, t3->beta1, t3->beta2, t3->eps,
-                 t3->weight_decay, nullptr, 1, t3->grads_out, nullptr, workspace, ws_bytes, pre, 1, nullptr, 1.f, 1, 0,
-                 u, &g3);
-    if (rc) return rc;
-    a2.wt = 1;
-    a2.pub = reinterpret_cast<uint32_t*>(ws + L.o_sync);  // zeroed by the row-owned T1 before
-    a2.pub_timeout = reinterpret_cast<uint32_t*>(ws + L.o_counter) + CW_T3_TIMEOUT;
-    if (n_ins + wgs + dd_grid + g3 > INT32_MAX) return fail(TT_EINVAL, "tower_tail: grid too large");
-    int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
-    tower_tail_t3_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(
-        a2, reinterpret_cast<const WgradTile*>(ws + a2.tiles_off), ins, d, u, (int)n_ins, (int)wgs, (int)dd_grid,
-        (int)g3, stamps);
-    return check_launch("tower_wgrad_pre_insert_rowwise_adagrad_update");
-  }
   int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
   if (stamps && L.nwg > 256) stamps = nullptr;
   tower_tail_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
@@ -4134,7 +3722,7 @@ int tt_tower_fwd_bwd_indexed_multi_bf16(const tt_tower_shape_t* shape, int64_t B
 static int tower_indexed2(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
                           const int32_t* const* pos_out, const void* const* rows_in, float* const* grad_rows_out,
                           const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
-                          void* workspace, size_t ws_bytes, void* stream, const UpdateArgs* fuse) {
+                          void* workspace, size_t ws_bytes, void* stream) {
   if (!pos_in || !pos_out || !rows_in || !grad_rows_out) return fail(TT_EINVAL, "tower_indexed2: null pointer");
   TowerArgs a{};
   a.gsrc_bf16 = 1;
@@ -4149,7 +3737,7 @@ static int tower_indexed2(const tt_tower_shape_t* shape, int64_t B, const int32_
   }
   return launch_t1(shape, B, a, nullptr,
                    std::max(shape->in_col[0] + shape->in_dim[0], shape->in_col[1] + shape->in_dim[1]), nullptr, params,
-                   labels, label_dtype, grad_scale, logits, workspace, ws_bytes, stream, fuse);
+                   labels, label_dtype, grad_scale, logits, workspace, ws_bytes, stream);
 }
 
 int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
@@ -4158,34 +3746,7 @@ int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, con
                                    int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
                                    void* stream) {
   return tower_indexed2(shape, B, pos_in, pos_out, rows_in, grad_rows_out, params, labels, label_dtype, grad_scale,
-                        logits, workspace, ws_bytes, stream, nullptr);
-}
-
-int tt_tower_fwd_bwd_indexed2_bf16_t3(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
-                                      const int32_t* const* pos_out, const void* const* rows_in,
-                                      float* const* grad_rows_out, float* params, float* exp_avg, float* exp_avg_sq,
-                                      float adam_eps, float beta1, float beta2, float weight_decay,
-                                      const float* grads_in, int nsrc, int64_t src_stride, const void* labels,
-                                      int label_dtype, float grad_scale, float* logits, void* workspace,
-                                      size_t ws_bytes, void* stream) {
-  TowerLayout L;
-  int rc = tower_layout(shape, B, &L);
-  if (rc) return rc;
-  if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
-  if (!grads_in || nsrc < 1 || nsrc > 32 || (nsrc > 1 && src_stride < L.P))
-    return fail(TT_EINVAL, "tower_indexed2_t3: bad gradient sources");
-  if (!t3_fuse_ok(shape, B, true))
-    return fail(TT_EINVAL, "tower_indexed2_t3: shape / batch not servable (row-owned T1, <= 4096 parameters per "
-                           "workgroup, every workgroup resident)");
-  const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
-  UpdateArgs u;
-  int64_t g3 = 0;
-  rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, adam_eps, weight_decay, nullptr, 1, nullptr,
-               grads_in, workspace, ws_bytes, pre, 1, nullptr, 1.f, nsrc, src_stride, u, &g3);
-  if (rc) return rc;
-  u.fuse_per = (int)ceil_div(L.P, (int64_t)L.nwg);
-  return tower_indexed2(shape, B, pos_in, pos_out, rows_in, grad_rows_out, params, labels, label_dtype, grad_scale,
-                        logits, workspace, ws_bytes, stream, &u);
+                        logits, workspace, ws_bytes, stream);
 }
 
 // ---- launch plans (include/tt_mi355x.h): the multi-role fused launches behind one entry point ----
@@ -4222,17 +3783,6 @@ int tt_launch(const tt_launch_plan_t* p, void* stream) {
                                         in.dedup_tables, g.tables, g.T, g.features, g.F, g.grad, g.ldg, g.weights,
                                         g.state, g.lr, g.eps, g.dedup_ws, in.next_dedup_ws, g.dedup_ws_bytes,
                                         g.dedup_max_lookups, stream);
-    case TT_ROLE_WGRAD | TT_ROLE_INSERT | TT_ROLE_ADAGRAD | TT_ROLE_UPDATE:
-      if ((rc = need_multi(1)) || (rc = adam_mode())) return rc;
-      if (g.B && g.B != B) return fail(TT_EINVAL, "launch: this plan's ADAGRAD role uses the plan's B (adagrad.B = 0 or B)");
-      if ((in.dedup_ws_bytes && in.dedup_ws_bytes != g.dedup_ws_bytes) ||
-          (in.dedup_max_lookups && in.dedup_max_lookups != g.dedup_max_lookups))
-        return fail(TT_EINVAL, "launch: the ring's two dedup workspaces have one size (the ADAGRAD role's)");
-      return fused_wgrad_insert_adagrad(p->shape, B, w.loss, p->workspace, p->ws_bytes, w.adam_step_state, w.adam_lr,
-                                        w.adam_beta1, w.adam_beta2, in.next_cols, in.id_dtype, in.num_embeddings,
-                                        in.dedup_tables, g.tables, g.T, g.features, g.F, g.grad, g.ldg, g.weights,
-                                        g.state, g.lr, g.eps, g.dedup_ws, in.next_dedup_ws, g.dedup_ws_bytes,
-                                        g.dedup_max_lookups, stream, &u);
     case TT_ROLE_WGRAD | TT_ROLE_INSERT:
       return fused_wgrad_insert(p->shape, B, w.loss, p->workspace, p->ws_bytes, w.adam_step_state, w.adam_lr,
                                 w.adam_beta1, w.adam_beta2, in.next_cols, in.id_dtype, in.num_embeddings,

@@ -164,8 +164,7 @@ class FusedDropin:
                     return None, "Adam holds parameters besides the towers and the fused tables"
         if len(lrs) != 1:
             return None, "the towers' Adam parameters do not share one learning rate"
-        return cls(pipeline, task, ebc, ts, cfg, towers, adam, feats, dims,
-                   fresh_outputs=os.environ.get("TT_DROPIN_FRESH_OUTPUTS", "0") == "1"), "fused"
+        return cls(pipeline, task, ebc, ts, cfg, towers, adam, feats, dims), "fused"
 
     def _adam_group(self) -> dict:
         w = self.towers[0]._mlp[0]._linear.weight
@@ -206,12 +205,6 @@ class FusedDropin:
                                id_dtype=id_dtype, tables=ts)
         if not st.ring_supported():
             raise _lib.TTError("dropin: the fused ring does not support this shape")
-        # the tower Adam update stays in its own launch, so the model's parameters are current
-        # after every progress() (as the reference's optimizer.step() leaves them);
-        # TT_DROPIN_DEFER_ADAM=1 folds it into the next step's T1 (parameters one update behind
-        # until the chunk ends, a mode switch or a generic batch: FusedTwoTowerStep.flush)
-        if os.environ.get("TT_DROPIN_DEFER_ADAM", "0") != "1":
-            st._t1f = False
         # the towers' parameters -> views of the step's flat buffer (values copied first); Adam's
         # moments likewise (the flat layout is [W0, b0, W1, b1] of the query tower, then the
         # candidate tower's: FusedTwoTowerStep.qW / qb / cW / cb)
@@ -335,7 +328,6 @@ class FusedDropin:
         run at every chunk's end (StopIteration), so optimizer.state_dict() there is current."""
         if self.step is None:
             return
-        self.step.flush()
         n = torch.tensor(float(int(self.step.adam_state[0].item())))
         for q in self._params:
             self.adam.state[q]["step"] = n.clone()
@@ -351,7 +343,6 @@ class FusedDropin:
         items = [x for x in (self.cur, self.nxt) if x is not None]
         self.cur = self.nxt = None
         if self.step is not None:
-            self.step.flush()
             self.step.ring_reset()
         if items:
             pipeline._cur = _Staged(items[0].batch, None)
@@ -401,7 +392,6 @@ class FusedDropin:
         p = self.pipeline
         st = self.step
         if st is not None:
-            st.flush()
             n = int(st.adam_state[0].item())
             for q in self._params:
                 self.adam.state[q]["step"] = torch.tensor(float(n))

@@ -17,7 +17,6 @@ No host synchronisation inside ``step()``: buffers are sized for the worst case 
 """
 from __future__ import annotations
 
-import os
 
 from typing import List, Optional, Sequence
 
@@ -27,10 +26,6 @@ import torch
 
 from . import _lib, ops
 from ._lib import FeatureMeta, check, id_dtype_code, ptr, ptr_array, stream_handle
-
-# multi-hot pipelined step: the row update captured before the side branches (0: the previous
-# order, for same-box A/B measurements)
-_KJT_UPDATE_FIRST = os.environ.get("TT_KJT_UPDATE_FIRST", "1") != "0"
 
 
 class FusedTwoTowerStep:
@@ -164,14 +159,12 @@ class FusedTwoTowerStep:
         self.tables.ensure_bwd_workspace(self.max_lookups)
         self.side = torch.cuda.Stream(device=dev) if overlap_prepare else None
         # multi-hot step: the rows looked up more than once (tt_bwd_rowwise_adagrad_part 2) on their
-        # own stream beside the once-looked-up rows' update (part 1, the step's critical path);
-        # TT_KJT_SPLIT_UPDATE=0: one stream (A/B measurement)
-        self.side3 = (torch.cuda.Stream(device=dev)
-                      if overlap_prepare and os.environ.get("TT_KJT_SPLIT_UPDATE", "1") != "0" else None)
+        # own stream beside the once-looked-up rows' update (part 1, the step's critical path:
+        # 378-380 against 382-384 µs on one stream)
+        self.side3 = torch.cuda.Stream(device=dev) if overlap_prepare else None
         # multi-hot pipelined step: the next batch's grouping is joined by the NEXT step's update
-        # (it may run on beside that step's T1) instead of at this step's end;
-        # TT_KJT_CROSS_STEP=0: joined at the end (A/B measurement)
-        self.cross_step_grouping = os.environ.get("TT_KJT_CROSS_STEP", "1") != "0"
+        # (it may run on beside that step's T1) instead of at this step's end (383 against 388-391 µs)
+        self.cross_step_grouping = True
         self._prep_event = None
         # bf16 towers on the three fused kernels when the shape allows (else per-layer GEMMs)
         self.towers = None
@@ -189,14 +182,13 @@ class FusedTwoTowerStep:
             self.tables.ensure_dedup_workspace(F * B)
         self.materialize_pooled = bool(materialize_pooled)
         # ring: tower_l2_kernel's dedup wave touches the next batch's rows after its own gather (cache
-        # / TLB prefetch); the row-owned T1 (128-wide rows) touches nothing (there the touches'
-        # TLB misses stall the workgroup's later stores, and beside T3 they cost T3 more than they
-        # save T1: DESIGN.md section 3); TT_PREFETCH_NEXT=0 turns it off (A/B measurement)
-        self.prefetch_next = os.environ.get("TT_PREFETCH_NEXT", "1") != "0"
+        # / TLB prefetch); the row-owned T1 touches nothing (there the touches' TLB misses stall the
+        # workgroup's later stores, and beside T3 they cost T3 more than they save T1: DESIGN.md
+        # section 3)
+        self.prefetch_next = True
         # ring: T2 + complete next-batch insert + update of the rows looked up more than once in one
-        # launch, then T3 alone; TT_RING_TAIL=0: T2 + deferred insert, then resolver + update + T3
-        # (A/B measurement)
-        self.ring_tail = os.environ.get("TT_RING_TAIL", "1") != "0"
+        # launch, then T3 alone (False, tests: T2 + deferred insert, then resolver + update + T3)
+        self.ring_tail = True
         self.combined_bwd = bool(combined_bwd)
         # in-graph kernel timing (bench): while a list, step() records an event pair per launch
         self._timing: Optional[list] = None
@@ -205,8 +197,8 @@ class FusedTwoTowerStep:
                        and max(self.dims) <= 128)
         # multi-hot KJT input: the EBC forward (sum pool of every bag) runs inside T1
         # (tt_tower_fwd_bwd_kjt) for one key per tower, towers [128, 64] over 64- or 128-wide rows
-        # (TT_KJT_POOL_IN_T1=0: tt_pooled_fwd + T1 instead, A/B measurement)
-        self.gather_kjt = (fuse_gather and os.environ.get("TT_KJT_POOL_IN_T1", "1") != "0"
+        # (fuse_gather=False: tt_pooled_fwd + T1 on the pooled rows)
+        self.gather_kjt = (fuse_gather
                            and self.towers is not None and self.kjt_input and self.F == 2
                            and self.qf == [0] and self.cf == [1] and self.layer_sizes == [128, 64]
                            and self.dims[0] == self.dims[1] and self.dims[0] in (64, 128))
@@ -488,7 +480,7 @@ class FusedTwoTowerStep:
                 else:  # tt_pooled_fwd above, then T1 on the pooled rows
                     self.towers.fwd_bwd(self.pooled, self.gpooled, self.params, self.labels, self.logits)
                 self._mark("t1", 1)
-                if defer_prepare and self.side2 is not None and _KJT_UPDATE_FIRST:
+                if defer_prepare and self.side2 is not None:
                     # the row update (the step's critical path) enqueued right behind T1 on the
                     # capture stream, the two side branches forked from T1's end after it: in the
                     # graph the branches captured first started first, ~12 us apart, and the
@@ -587,7 +579,6 @@ class FusedTwoTowerStep:
         B = self.B
         if cols[0].numel() != B:
             raise _lib.TTError("eval_step: batch size differs from the step's")
-        self.flush()
         self.tables.pooled_fwd_cols(list(cols), self.num_embeddings, out=self.pooled)
         self._towers_fwd()
         L = len(self.layer_sizes)
@@ -600,45 +591,7 @@ class FusedTwoTowerStep:
         """Refresh the fused towers' bf16 weight copies after the fp32 parameters were changed
         outside step() (initialisation, loading a checkpoint)."""
         if self.towers is not None:
-            self.flush()
             self.towers.update(self.params, do_adam=False)
-
-    def t1_fuse(self) -> bool:
-        """Does the ring fold T3 into the next step's T1 (two launches per step)? Opt-in
-        (TT_T1_FUSE=1): measured slower than the three-launch ring (the in-launch
-        wait for every workgroup's share costs more than the kernel boundary it removes). The shape
-        must be the row-owned T1's with every T1 workgroup resident at once
-        (tt_tower_t3_fuse_supported)."""
-        if getattr(self, "_t1f", None) is None:
-            self._t1f = bool(self.towers is not None and os.environ.get("TT_T1_FUSE", "0") == "1"
-                             and self.ring_supported()
-                             and _lib.load().tt_tower_t3_fuse_supported(C.byref(self.towers.shape), self.B) == 1)
-        return self._t1f
-
-    def t3_in_tail(self) -> bool:
-        """Does the ring run T3 inside the tail launch (two launches per step, nothing pending after
-        a step)? Its workgroups come last in the tail's grid and wait in-launch for every T2
-        workgroup's write-through slab rows (TT_T3_IN_TAIL=1)."""
-        if getattr(self, "_t3t", None) is None:
-            self._t3t = os.environ.get("TT_T3_IN_TAIL", "0") == "1"
-        return self._t3t
-
-    def flush(self) -> None:
-        """Apply the tower Adam update the last fused ring step left pending (a no-op launch when
-        none is): parameters, moments and weight copies are current afterwards. run() / run_eager()
-        end with it; call it after driving ring_step() directly, before reading the parameters."""
-        if self.towers is None or not getattr(self, "_t1f", None):
-            return
-        tw = self.towers
-        check(_lib.load().tt_tower_update_lazy(C.byref(tw.shape), self.B, ptr(self.params), ptr(self.exp_avg),
-                                               ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads), None, 0,
-                                               0, ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
-              "tower_update_lazy")
-
-    def fuse_timeouts(self) -> int:
-        """In-launch waits of the fused T3 + T1 launch that gave up (must be 0; one sync)."""
-        off = _lib.load().tt_tower_counter_offset(C.byref(self.towers.shape), self.B)
-        return int(self.towers.ws[off + 24:off + 28].view(torch.int32).item())
 
     # ---- the pipelined ring (production): dedup one step ahead, single-lookup rows in T1 ---------
     def ring_supported(self) -> bool:
@@ -657,7 +610,6 @@ class FusedTwoTowerStep:
             check(lib.tt_dedup_workspace_init(ptr(ws1), ws1.numel(), ts._dd_cap, stream_handle(self.device)),
                   "dedup_workspace_init")
             self._ring = [ts._dd_ws, ws1]
-            self.t1_fuse()  # decided (a device query) before any capture
             self._ring_tab = (C.c_int32 * 2)(0, 1)
             self._ring_ne = (C.c_int64 * 2)(*self.num_embeddings)
         return self._ring
@@ -686,48 +638,30 @@ class FusedTwoTowerStep:
           tail  T2 (tower weight gradients, Adam scalars) + complete insert of the next batch +
                 update of the rows looked up more than once (from T1's dX)
           T3    slab reduction, Adam, bf16 weight copies
-        With t1_fuse() there are two: T3 runs at the start of the NEXT step's T1 launch (its
-        workgroups apply the pending update, wait for each other in-launch, then read the weights),
-        so after the last step the update is pending until flush() (run / run_eager call it).
         (ring_tail False: T2 + deferred insert of the next batch, then resolver + row update + T3)."""
         lib, tw, ts, B, dev = _lib.load(), self.towers, self.tables, self.B, self.device
         ring = self._ring_ws()
         ws, wsn = ring[parity], ring[parity ^ 1]
         st = stream_handle(dev)
-        fuse = self.ring_tail and self.t1_fuse()
         self._mark("t1", 0)
-        if fuse:  # T1 with the previous step's pending T3 folded in (bit-identical to T3 then T1)
-            check(lib.tt_tower_fwd_bwd_gather_update_t3(
-                C.byref(tw.shape), B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ring_ne,
-                ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
-                ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
-                ptr(self.params), ptr(self.exp_avg), ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads),
-                ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws), ws.numel(),
-                ts._dd_cap, ptr(tw.ws), tw.nbytes, st), "tower_fwd_bwd_gather_update_t3")
-        else:
-            check(lib.tt_tower_fwd_bwd_gather_update(
-                C.byref(tw.shape), B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ring_ne,
-                ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
-                ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
-                ptr(self.params), ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws),
-                ws.numel(), ts._dd_cap, ptr_array(list(next_cols)) if self.prefetch_next else None, ptr(tw.ws),
-                tw.nbytes, st), "tower_fwd_bwd_gather_update")
+        check(lib.tt_tower_fwd_bwd_gather_update(
+            C.byref(tw.shape), B, ptr_array(list(cols)), id_dtype_code(cols[0].dtype), self._ring_ne,
+            ptr_array([ts.table_view(0), ts.table_view(1)]), ptr_array([ts.state_view(0), ts.state_view(1)]),
+            ptr(self.pooled) if self.materialize_pooled else None, self.gpooled.stride(0), ptr(self.gpooled),
+            ptr(self.params), ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), self.lr_emb, self.eps, ptr(ws),
+            ws.numel(), ts._dd_cap, ptr_array(list(next_cols)) if self.prefetch_next else None, ptr(tw.ws),
+            tw.nbytes, st), "tower_fwd_bwd_gather_update")
         self._mark("t1", 1)
         if self.ring_tail:
             self._mark("tail", 0)
             # the tail: tower weight gradients (T2) + the next batch's complete insert + the rows
             # looked up more than once (tt_launch roles WGRAD | INSERT | ADAGRAD)
-            # (+ UPDATE: T3 in the same launch, TT_T3_IN_TAIL=1)
-            t3_tail = not fuse and self.t3_in_tail()
-            roles = _lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD | (_lib.ROLE_UPDATE if t3_tail else 0)
-            plan = self._plan(roles, ws, multi_only=1)
+            plan = self._plan(_lib.ROLE_WGRAD | _lib.ROLE_INSERT | _lib.ROLE_ADAGRAD, ws, multi_only=1)
             plan.insert = _lib.InsertRole(next_cols=ptr_array(list(next_cols)),
                                           id_dtype=id_dtype_code(next_cols[0].dtype), num_embeddings=self._ring_ne,
                                           dedup_tables=self._ring_tab, next_dedup_ws=ptr(wsn))
             _lib.launch(plan, st, "ring tail")
             self._mark("tail", 1)
-            if fuse or t3_tail:  # T3 runs in the next step's T1 (or flush()) / ran in the tail
-                return
             self._mark("t3", 0)
             check(lib.tt_tower_update_pre(C.byref(tw.shape), B, ptr(self.params), ptr(self.exp_avg),
                                           ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(self.grads), ptr(tw.ws),
@@ -843,7 +777,6 @@ class FusedTwoTowerStep:
                 (mid[sz][r // sz] if sz > 1 else self.ring_small[i]).replay()
             i, n = (i + sz) % nb, n - sz
         self.ring_cursor = i
-        self.flush()
 
     def timed_ring(self, n: int) -> dict:
         """n eager production steps (from the cursor) with a HIP event pair around every launch;
@@ -852,8 +785,7 @@ class FusedTwoTowerStep:
         try:
             for _ in range(n):
                 self._timing.append({})
-                self.run_eager(1, flush=False)
-            self.flush()
+                self.run_eager(1)
             torch.cuda.synchronize(self.device)
             acc = {}
             for m in self._timing:
@@ -863,7 +795,7 @@ class FusedTwoTowerStep:
             self._timing = None
         return {k: sum(v) / len(v) for k, v in acc.items()}
 
-    def run_eager(self, n: int, flush: bool = True) -> None:
+    def run_eager(self, n: int) -> None:
         """n production steps over the captured ring's batches without graphs (timing / tests)."""
         staged = self._ring_inputs
         nb = len(staged)
@@ -871,8 +803,6 @@ class FusedTwoTowerStep:
             i = self.ring_cursor
             self.ring_step(staged[i][0], staged[i][1], i % 2, staged[(i + 1) % nb][0])
             self.ring_cursor = (i + 1) % nb
-        if flush:
-            self.flush()
 
     # ------------------------------------------------------------------------------------------
     def capture(self, batches: Optional[Sequence] = None, keep_graph: bool = False,

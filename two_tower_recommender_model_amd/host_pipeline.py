@@ -220,8 +220,6 @@ class HostFedPipeline:
             steps += self.filled[slot]
             self._fill((g + 2) % D, it)  # the slot of group g - 2
             g += 1
-        if self.ring:
-            self.step.flush()  # the last step's tower update, when the ring folds T3 into T1
         return steps
 
 

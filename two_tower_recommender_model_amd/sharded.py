@@ -439,48 +439,9 @@ class FusedShardedTwoTowerStep:
         ``prime`` (its steps never ran), a ``load_state_dict`` in the middle of a run, a switch
         between the synchronous and the pipelined step. A dedup table filed twice with the same keys
         would join its own slots: those rows would never be updated."""
-        self.flush()
         torch.cuda.synchronize(self.device)
         self._init_dedup()
         self.cursor = None
-
-    # ---- the tower Adam update folded into the next step's T1 -----------------------------------
-    def t1_fuse(self) -> bool:
-        """Does the pipelined step apply the tower Adam update at the start of the NEXT step's T1
-        launch (tt_tower_fwd_bwd_indexed2_bf16_t3) instead of its own launch? Single feature per
-        tower (the row-owned T1), every T1 workgroup resident; opt-in (TT_T1_FUSE=1: measured slower,
-        as for the single-GPU ring)."""
-        if getattr(self, "_t1f", None) is None:
-            # ranks sharing this GPU (thread ranks; processes of a one-GPU rehearsal) run their T1
-            # launches concurrently: every one of their workgroups must be resident together, so
-            # the check is made for all of them at once (a larger batch: conservative)
-            if isinstance(self.comm, ThreadComm):
-                share = self.W
-            else:
-                local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-                share = max(1, -(-local // max(1, torch.cuda.device_count())))
-            self._t1f = bool(not self.multi and os.environ.get("TT_T1_FUSE", "0") == "1" and self.W <= 32
-                             and _lib.load().tt_tower_t3_fuse_supported(C.byref(self.towers.shape),
-                                                                        self.B * share) == 1)
-        return self._t1f
-
-    def fuse_timeouts(self) -> int:
-        """In-launch waits of the fused Adam + T1 launch that gave up (a workgroup was not resident:
-        the results are invalid; one sync)."""
-        off = _lib.load().tt_tower_counter_offset(C.byref(self.towers.shape), self.B)
-        return int(self.towers.ws[off + 24:off + 28].view(torch.int32).item())
-
-    def flush(self) -> None:
-        """Apply the tower update the last pipelined step left pending (a no-op launch when none is),
-        from the tower gradients exchange B delivered: parameters, moments and weight copies are
-        current afterwards. run() / run_eager() end with it."""
-        if not getattr(self, "_t1f", None):
-            return
-        tw = self.towers
-        check(_lib.load().tt_tower_update_lazy(
-            C.byref(tw.shape), self.B, ptr(self.params), ptr(self.exp_avg), ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999,
-            0.0, None, self.rows_in.data_ptr() + 4 * self._tw_in, self.W, self._tw_stride, ptr(tw.ws), tw.nbytes,
-            stream_handle(self.device)), "tower_update_lazy")
 
     def _layout(self) -> None:
         W, F, D, P = self.W, self.F, self.D, self.towers.num_params
@@ -574,17 +535,9 @@ class FusedShardedTwoTowerStep:
         self.comm.all_to_all(self.rows_in, self.rows_out, out_splits=[self.RSTR] * self.W,
                              in_splits=[self.RSTR] * self.W)
 
-    def _t1(self, parity: int, labels: torch.Tensor, fuse: bool = False) -> None:
+    def _t1(self, parity: int, labels: torch.Tensor) -> None:
         lib, tw, B = _lib.load(), self.towers, self.B
         pin, pout = self.pos_in[parity], self.pos_out[parity]
-        if fuse:  # the previous step's pending Adam update first, in the same launch
-            check(lib.tt_tower_fwd_bwd_indexed2_bf16_t3(
-                C.byref(tw.shape), B, ptr_array([pin[:B], pin[B:]]), ptr_array([pout[:B], pout[B:]]),
-                ptr_array([self.rows_in, self.rows_in]), ptr_array([self.sendA, self.sendA]), ptr(self.params),
-                ptr(self.exp_avg), ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0,
-                self.rows_in.data_ptr() + 4 * self._tw_in, self.W, self._tw_stride, ptr(labels), _lib.TT_I32, 1.0,
-                ptr(self.logits), ptr(tw.ws), tw.nbytes, stream_handle(self.device)), "tower_fwd_bwd_indexed2_t3")
-            return
         if self.multi:
             check(lib.tt_tower_fwd_bwd_indexed_multi_bf16(
                 C.byref(tw.shape), B, self.D, ptr(pin), ptr(pout), ptr(self.rows_in), ptr(self.sendA),
@@ -647,7 +600,6 @@ class FusedShardedTwoTowerStep:
         lib, tw = _lib.load(), self.towers
         if self.cursor is not None:  # a pipelined run left batches staged in the dedup tables
             self.reset_pipeline()
-        self.flush()
         self._route(self.cols, 0)
         self._exchange_a()
         self._gather(0)
@@ -680,8 +632,7 @@ class FusedShardedTwoTowerStep:
         """Step on the staged batch i (rows in place, parity ``parity``; batch i+1's keys placed),
         staging batch i+1's rows and routing ``next2_cols`` (batch i+2, same parity)."""
         lib, tw, ts, r, B, dev = _lib.load(), self.towers, self.tables, self.rank, self.B, self.device
-        fuse = self.t1_fuse()
-        self._t1(parity, labels, fuse=fuse)
+        self._t1(parity, labels)
         route = self._route_args(next2_cols, parity)
         ws = self.dd_ws[parity]
         main = torch.cuda.current_stream(dev)
@@ -715,8 +666,7 @@ class FusedShardedTwoTowerStep:
                                       dedup_ws=g[13], dedup_ws_bytes=g[14], dedup_max_lookups=g[15])
         _lib.launch(plan, stream_handle(dev), "tower_grads_replicated_route_place_gather")
         self._exchange_b()
-        if not fuse:  # otherwise the next step's T1 launch (or flush()) applies it
-            self._adam()
+        self._adam()
 
     # ---- checkpoint (03_model_training.py:474-502 / :1015-1054 format) -------------------------
     def spans(self, f: int) -> List[Tuple[int, int]]:
@@ -746,7 +696,6 @@ class FusedShardedTwoTowerStep:
         ``optim.*`` keys (the reference saves no optimizer state; this makes resume exact)."""
         from .lifecycle import _dense_items, _tower_views
 
-        self.flush()
         sd = {}
         for f, name in enumerate(self._names(feature_names)):
             full = self.comm.gather_rows(self.tables.table_view(f), self.spans(f), self.N[f])
@@ -770,8 +719,6 @@ class FusedShardedTwoTowerStep:
         """Every rank takes its blocks of the full tables and the towers from a gathered dict (and
         the optimizer state when the dict holds ``optim.*`` keys; otherwise it is reset)."""
         from .lifecycle import _dense_items, _tower_views
-
-        self.flush()  # a pending update belongs to the state being replaced
 
         with torch.no_grad():
             for f, name in enumerate(self._names(feature_names)):
@@ -813,9 +760,6 @@ class FusedShardedTwoTowerStep:
                                "results are invalid; raise `capacity`")
         if f[1]:
             raise _lib.TTError("sharded step: an owner received a key outside its shard")
-        if getattr(self, "_t1f", None) and self.fuse_timeouts():
-            raise _lib.TTError("sharded step: the fused Adam + T1 launch found workgroups not resident (another "
-                               "kernel held the GPU): results are invalid; run with TT_T1_FUSE=0")
 
     def release_graphs(self) -> None:
         """Drop the captured graphs (before tearing down the process group: a live graph holds
@@ -860,7 +804,6 @@ class FusedShardedTwoTowerStep:
         staged = self._staged(batches)
         self._pool_inputs = [staged]
         self.pool_k = k
-        self.t1_fuse()  # decided (a device query) before the capture
         # stage batch 0 (and place batch 1's keys) eagerly, then retire every eager collective
         self.prime(staged[0][0], 0, staged[1][0])
         self.cursor = 0
@@ -902,7 +845,6 @@ class FusedShardedTwoTowerStep:
                 i, n = i + 1, n - 1
             i %= nb
         self.cursor = i
-        self.flush()
 
     def run_eager(self, batches: Sequence, n: int) -> None:
         """n pipelined steps over a cyclic pool without graphs (continuing at the cursor)."""
@@ -916,7 +858,6 @@ class FusedShardedTwoTowerStep:
             i = self.cursor
             self.step_pipelined(batches[i][1].to(torch.int32), i % 2, list(batches[(i + 2) % nb][0]))
             self.cursor = (i + 1) % nb
-        self.flush()
 
 
 def capture_pool_or_eager(step: FusedShardedTwoTowerStep, batches: Sequence, steps_per_graph: int,
