@@ -769,14 +769,17 @@ def run_single(args):
     return value, ms, loss, roofline, cpu, steps_run
 
 
-def run_dropin(args):
+def run_dropin(args, world=1, rank=0, local_rank=0):
     """The reference's loop through the torchrec shim: main()'s wiring (EBC on meta, TwoTower,
     TwoTowerTrainTask, in-backward RowWiseAdagrad, DistributedModelParallel, KeyedOptimizerWrapper(Adam),
     TrainPipelineSparseDist; 03_model_training.py:770-829) and train()'s ``pipeline.progress`` loop
     (:612-625) over resident device KJT batches built by the device KJT builder (tt_kjt_build_mod_dropzero,
     the reference's transform_to_torchrec_batch semantics). progress() dispatches to the fused ring
     (dropin.py); K timed progress calls. Then the same model with the dispatch off (a fresh pipeline,
-    TT_DROPIN_FUSED=0: the generic per-op path on the same storage) for a few steps."""
+    TT_DROPIN_FUSED=0: the generic per-op path on the same storage) for a few steps.
+    At world > 1 (the process group already initialised by main): DMP shards the tables by the
+    default plan over the W ranks, progress() dispatches to the pipelined fused sharded step
+    (dropin.FusedShardedDropin), every rank times its loop between barriers and the max is taken."""
     import itertools
 
     import two_tower_recommender_model_amd as tt
@@ -796,7 +799,7 @@ def run_dropin(args):
     from two_tower_recommender_model_amd.task import TwoTower, TwoTowerTrainTask
 
     num_users, num_items, D, B, layers = WORKLOADS[args.workload]
-    dev = torch.device("cuda:0")
+    dev = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
     cat_cols = ["user_id", "product_id"]
@@ -809,7 +812,7 @@ def run_dropin(args):
     optimizer = KeyedOptimizerWrapper(dict(model.named_parameters()), lambda ps: torch.optim.Adam(ps, lr=0.01))
     nb = max(2, args.batches)
     batches = []
-    for cols, lab in synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1):
+    for cols, lab in synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1 + 1000 * rank):
         values, lengths, offsets, lpk = ops.kjt_build_mod_dropzero(cols, [num_users, num_items])
         n = int(lpk.sum())
         kjt = KeyedJaggedTensor(keys=cat_cols, values=values[:n], lengths=lengths, offsets=offsets,
@@ -822,16 +825,25 @@ def run_dropin(args):
         for _ in range(warmup):
             pipeline.progress(it)
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         t0 = time.perf_counter()
         for _ in range(steps):
             loss, _, _ = pipeline.progress(it)
         torch.cuda.synchronize()
-        return time.perf_counter() - t0, float(loss)
+        if world > 1:
+            dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t0], device=dev)
+        if world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt), float(loss)
 
     pipeline = TrainPipelineSparseDist(model, optimizer, dev)
     pipeline._model.train()
     dt, loss = timed(pipeline, args.warmup, args.steps)
     fd = pipeline._fused
+    if world > 1 and fd:
+        fd.check_errors()  # collective: a segment overflow or a multi-id bag would void the timing
     info = {"dispatch": pipeline._fused_reason, "fused_steps": fd.steps_fused if fd else 0,
             "generic_steps": fd.steps_generic if fd else args.warmup + args.steps,
             "loop": "DistributedModelParallel + TrainPipelineSparseDist.progress + KeyedOptimizerWrapper(Adam) + "
@@ -845,9 +857,13 @@ def run_dropin(args):
         gdt, _ = timed(gp, 3, gsteps)
     finally:
         os.environ.pop("TT_DROPIN_FUSED", None)
-    info["generic_path"] = {"ms_per_step": round(gdt / gsteps * 1e3, 4), "pairs/s": round(gsteps * B / gdt, 1),
+    info["generic_path"] = {"ms_per_step": round(gdt / gsteps * 1e3, 4), "pairs/s": round(world * gsteps * B / gdt, 1),
                             "steps": gsteps}
-    return args.steps * B / dt, dt / args.steps * 1e3, loss, args.steps, info
+    if world > 1 and fd:
+        info["sharded"] = {"sharding": fd.sharding, "owners": fd.owners,
+                           "capacity": list(fd.step.caps_f) if fd.step is not None else None,
+                           "mode": "hipgraph" if fd.graph_mode else "eager"}
+    return world * args.steps * B / dt, dt / args.steps * 1e3, loss, args.steps, info
 
 
 def run_host_fed(args):
@@ -1051,7 +1067,13 @@ def main():
         else:  # --sharded without a launcher (e.g. under rocprofv3): a one-rank group
             dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
                                     device_id=torch.device("cuda", local_rank))
-        if args.workload in MULTIHOT:
+        if args.path == "dropin":
+            value, ms, loss, steps_run, di = run_dropin(args, world, rank, local_rank)
+            config["dropin"] = di
+            config["parallelism"] = (f"the reference's DMP + TrainPipelineSparseDist loop x{world}, dispatched to the "
+                                     f"fused sharded step")
+            roofline, sharded_info = None, di.get("sharded")
+        elif args.workload in MULTIHOT:
             value, ms, loss, sharded_info, roofline = run_multi_kjt(args, world, rank, local_rank)
             config["parallelism"] = (f"{sharded_info['plan']} + data-parallel towers x{world}: 3 fixed-size RCCL "
                                      f"all-to-alls per step (ids, pooled rows, bag gradients), {sharded_info['mode']}")

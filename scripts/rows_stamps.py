@@ -8,7 +8,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["TT_T1_DEBUG"] = "8"
+os.environ["TT_T1_DEBUG"] = str(8 | int(os.environ.get("T1_ABLATE", "0")))  # + ablation bits (16: no image, 32: no rows)
 os.environ["TT_EXPERIMENT_LIB"] = "1"
 import torch  # noqa: E402
 
@@ -24,8 +24,12 @@ st.capture_ring(batches, steps_per_graph=8)
 nwg = B // 32
 dbg_bytes = (max(2 * nwg, 1024) * 8 + nwg * 16 * 9) * 8
 off = st.towers.nbytes - ((dbg_bytes + 255) // 256 * 256)
+graph = os.environ.get("GRAPH") == "1"  # the last step of an 8-step graph replay instead of an eager step
 for it in range(4):
-    st.run_eager(1)
+    if graph:
+        st.run(8)
+    else:
+        st.run_eager(1)
     torch.cuda.synchronize()
     if it < 3:
         continue
@@ -42,5 +46,9 @@ for it in range(4):
     ex = (extra - t0.unsqueeze(1)) / 100.0
     for k, what in enumerate(["G^2 sums", "step + LDS write-back", "row stores issued", "state / dX stores"]):
         print(f"  u{k} {what:24s}" + " ".join(f"{float(x):8.2f}" for x in ex[:, k, :].median(dim=0).values))
+    tmin = w[:, 0, :].min()
+    print("launch span (us from the first workgroup's start): last start %.2f, end p50 %.2f, last end %.2f" % (
+        float((w[:, 0, :].max() - tmin) / 100), float(((w[:, 15, :].max(dim=1).values - tmin) / 100).median()),
+        float((w[:, 15, :].max() - tmin) / 100)))
     print("workgroup start spread (us, p50 / max):",
           float(((t0 - t0.min()) / 100).median()), float(((t0 - t0.min()) / 100).max()))

@@ -50,6 +50,21 @@ def test_bench_gpus2_self_launch_as_driver_runs_it():
     assert d["config"]["sharded"]["plan"].startswith("table-wise")
 
 
+def test_bench_dropin_n2_rehearsal():
+    """`bench.py --gpus 2 --path dropin`: the reference's DMP + TrainPipelineSparseDist loop in two
+    processes (gloo, sharing the GPU) dispatched to the fused sharded step on every rank."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TT_REHEARSE_GLOO="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--path", "dropin", "--workload", "config2", "--steps", "6",
+           "--warmup", "2", "--batches", "8", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
+    di = d["config"]["dropin"]
+    assert di["dispatch"] == "fused sharded" and di["fused_steps"] == 8 and di["generic_steps"] == 0, di
+
+
 @pytest.mark.parametrize("world", [2])
 def test_bench_config5_sharded_multiprocess_gloo_rehearsal(world):
     """bench.py's config-5 N > 1 path (the capturable multi-hot sharded step: users table-wise on the

@@ -1542,7 +1542,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   auto load_image = [&]() {
 #pragma unroll
     for (int k = 0; k < RK_IMG / 1024 / 4; ++k)
-      wreg[k] = *reinterpret_cast<const bf16x8*>(a.wimg + (wid + 4 * k) * 1024 + lane * 16);
+      wreg[k] = TDBG(16) ? (bf16x8)(__bf16)0.f  // EXPERIMENT (timing only): no image fill
+                         : *reinterpret_cast<const bf16x8*>(a.wimg + (wid + 4 * k) * 1024 + lane * 16);
   };
   load_biases();
   __builtin_amdgcn_sched_barrier(0);
@@ -1588,7 +1589,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
       const int row = RPI * i + rr0;
       const int64_t rid = __shfl((long long)r, row, 64);
       const float* src = tab + (rid >= 0 ? rid : 0) * rstride + 4 * (pc ^ row);
-      __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(xw + i * 256), 16, 0, 0);
+      if (!TDBG(32))  // EXPERIMENT (timing only, garbage rows): no row gather
+        __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(xw + i * 256), 16, 0, 0);
     }
   }
   __builtin_amdgcn_sched_barrier(0);

@@ -36,7 +36,7 @@ from typing import Any, Iterator, List, Optional, Tuple
 import torch
 from torch import nn
 
-from . import _lib
+from . import _lib, ops
 
 
 def _named(obj, cls_name: str) -> bool:
@@ -89,11 +89,10 @@ class FusedDropin:
             return None, "not a GPU pipeline"
         import torch.distributed as dist
 
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            return None, "world size > 1 (FusedShardedTwoTowerStep is the fused sharded step)"
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         model = pipeline._model
         task = getattr(model, "module", model)
-        if getattr(model, "_ddp", None) is not None:
+        if world == 1 and getattr(model, "_ddp", None) is not None:
             return None, "DDP-wrapped dense modules"
         if not _named(task, "TwoTowerTrainTask") or not hasattr(task, "two_tower"):
             return None, "the model is not a TwoTowerTrainTask"
@@ -112,7 +111,24 @@ class FusedDropin:
         from .torchrec.modules.embedding_modules import EmbeddingBagCollection
 
         feats = [qf[0], cf[0]]
-        if isinstance(ebc, ShardedEmbeddingBagCollection):
+        sharded = None  # world > 1: (sharding, owner) per feature
+        if world > 1:
+            if not isinstance(ebc, ShardedEmbeddingBagCollection) or ebc._W != world:
+                return None, "world size > 1 without a ShardedEmbeddingBagCollection over every rank"
+            if ebc._be is not ops.HIP_BACKEND:
+                return None, "the sharded EBC does not run on the HIP lookup backend"
+            if ebc._pooling != _lib.TT_POOL_SUM or ebc._feature_names != feats or ebc._f_table != [0, 1]:
+                return None, "EBC features are not (query, candidate) with SUM pooling, one table each"
+            sharded = []
+            for f in range(2):
+                if f in ebc._rw_feats:
+                    sharded.append(("row_wise", 0))
+                else:
+                    sharded.append(("table_wise", next(o for o in range(world) if f in ebc._tw_by_owner[o])))
+            cfg = ebc._fused
+            dims = list(ebc._dims)
+            ts = ebc._ts
+        elif isinstance(ebc, ShardedEmbeddingBagCollection):
             if ebc._W != 1 or ebc._ts is None:
                 return None, "sharded over more than one rank"
             if ebc._pooling != _lib.TT_POOL_SUM or ebc._feature_names != feats:
@@ -131,7 +147,8 @@ class FusedDropin:
             return None, "the tower module's ebc is not an EmbeddingBagCollection"
         if cfg is None:
             return None, "tables without the fused in-backward RowWiseAdagrad"
-        dims = [ts.dims[0], ts.dims[1]]
+        if sharded is None:
+            dims = [ts.dims[0], ts.dims[1]]
         if dims[0] != dims[1] or dims[0] not in (64, 128):
             return None, "embedding dims must be equal, 64 or 128"
         towers = (tt.query_proj, tt.candidate_proj)
@@ -164,6 +181,9 @@ class FusedDropin:
                     return None, "Adam holds parameters besides the towers and the fused tables"
         if len(lrs) != 1:
             return None, "the towers' Adam parameters do not share one learning rate"
+        if sharded is not None:
+            return FusedShardedDropin(pipeline, task, ebc, ts, cfg, towers, adam, feats, dims, sharded), \
+                "fused sharded"
         return cls(pipeline, task, ebc, ts, cfg, towers, adam, feats, dims), "fused"
 
     def _adam_group(self) -> dict:
@@ -402,5 +422,338 @@ class FusedDropin:
         if st is not None:
             st.adam_state[0] = n + 1
             st.sync_weights()  # the towers' bf16 copies of the updated fp32 parameters
+        self.steps_generic += 1
+        return output
+
+
+class FusedShardedDropin:
+    """The reference's loop at world size W > 1 (DistributedModelParallel over W processes, one GPU
+    each, 03_model_training.py:812-815, :918) on the pipelined fused sharded step
+    (``sharded.FusedShardedTwoTowerStep``): TrainPipelineSparseDist.progress hands each single-hot
+    batch to the step, which trains the ShardedEmbeddingBagCollection's OWN shards (table-wise or
+    row-wise per the DMP plan; ``ops.TableSet.view_of``) and the towers' parameters and Adam moments
+    as views of its flat buffers (the DDP replicas: the step's fixed-order mean of the W tower
+    gradients is DDP's all-reduce mean). Per step two fixed-size all-to-alls instead of the eager
+    input_dist / output_dist / DDP collectives with their host-synchronised split sizes.
+
+    The step is pipelined two batches deep (batch i+1's rows are gathered during step i, batch
+    i+2's ids routed), so progress() looks two batches ahead; slot k's HIP graph (RCCL inside) is
+    the step on slot k routing slot k+2. Every rank must take the same path for the same batch (the
+    step is collective): the choice uses host metadata only (stride, value count, dtype), which the
+    reference's loaders give every rank alike. A batch the step does not take (another batch size,
+    multi-hot values) runs the generic DMP path between fused steps; the staged pipeline is dropped
+    first. Segment capacities come from the first batch's routes (max over ranks x 1.5, at least
+    1.5 B / W + 64); a later batch beyond them drops the excess lookups and sets a sticky flag
+    that is checked (collectively) at every StopIteration, as is a bag of several ids."""
+
+    def __init__(self, pipeline, task, ebc, ts, fused_cfg, towers, adam, feats, dims, sharded, depth: int = 8):
+        import torch.distributed as dist
+
+        self.pipeline = pipeline
+        self.task = task
+        self.ebc = ebc
+        self.ts = ts
+        self.fused_cfg = fused_cfg
+        self.towers = towers
+        self.adam = adam
+        self.feats = feats
+        self.dims = dims
+        self.sharding = [s for s, _ in sharded]
+        self.owners = [o for _, o in sharded]
+        self.depth = int(depth)  # even: parity = slot % 2
+        self.device = pipeline._device
+        self.W = dist.get_world_size(ebc._pg)
+        self.step = None
+        self.queue: List[_Item] = []  # fetched batches: cur, nxt, nxt2
+        self.k = 0
+        self.staged = False  # the step holds batch queue[0]'s rows and the next batch's route
+        self.dirty = False   # a fused step ran since the last reset (its dedup tables hold keys)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.steps_fused = 0
+        self.steps_generic = 0
+        self.graphs: List = []
+        self.graph_mode = None
+
+    # reuse of the single-GPU drop-in's helpers
+    _adam_group = FusedDropin._adam_group
+    _adam_lr = FusedDropin._adam_lr
+
+    def fusable(self, batch) -> bool:
+        kjt = getattr(batch, "sparse_features", None)
+        if kjt is None or list(kjt.keys()) != self.feats:
+            return False
+        B = kjt.stride()
+        if B < 8 or B % 8 or (self.step is not None and B != self.step.B):
+            return False
+        v = kjt.values()
+        if v.numel() > 2 * B or (v.numel() and v.dtype not in (torch.int32, torch.int64)):
+            return False
+        if self.step is not None and v.numel() and v.dtype != self.step.id_dtype:
+            return False
+        lab = batch.labels
+        return (lab.numel() == B and lab.dtype in (torch.int32, torch.int64) and lab.is_contiguous()
+                and lab.device == self.device and kjt.device() == self.device)
+
+    # ---- the step on the sharded EBC's storage ---------------------------------------------------
+    def _make_step(self, batch) -> None:
+        import ctypes as C
+
+        import torch.distributed as dist
+
+        from .sharded import FusedShardedTwoTowerStep, TorchComm, default_capacity
+
+        kjt = batch.sparse_features
+        B = kjt.stride()
+        v = kjt.values()
+        idt = v.dtype if v.numel() else torch.int64
+        dev, W, ebc = self.device, self.W, self.ebc
+        # every rank's first batch agrees on B and the id dtype (else: the generic path everywhere)
+        agree = torch.tensor([B, -B, 1 if idt == torch.int64 else 0, -(1 if idt == torch.int64 else 0)],
+                             dtype=torch.int64, device=dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=ebc._pg)
+        if int(agree[0]) != -int(agree[1]) or int(agree[2]) != -int(agree[3]):
+            raise _lib.TTError("dropin (sharded): the ranks' first batches differ in batch size or id dtype")
+        N = [c.num_embeddings for c in ebc._embedding_bag_configs]
+        D = self.dims[0]
+        cols = self._cols_of(kjt, B)
+        blocks = [-(-n // W) if s == "row_wise" else 0 for n, s in zip(N, self.sharding)]
+        seg_owner = [o if s == "table_wise" else 0 for o, s in zip(self.owners, self.sharding)]
+        from .sharded import segment_counts
+
+        need = segment_counts(cols, N, blocks, seg_owner, W).max().reshape(1).to(dev)
+        dist.all_reduce(need, op=dist.ReduceOp.MAX, group=ebc._pg)
+        cap = max(default_capacity(B, W, factor=1.5), -(-int(need) * 3 // 2))
+        cap = min(B, -(-cap // 8) * 8)
+        local = [ebc._local_index.get(ebc._f_table[f]) for f in range(2)]
+        tables = ops.TableSet.view_of(self.ts, local, [D, D], dev)
+        comm = TorchComm(group=ebc._pg, always_collective=True)
+        st = FusedShardedTwoTowerStep(comm, N, D, [128, 64], B, dev, sharding=self.sharding, tw_owners=self.owners,
+                                      lr_emb=self.fused_cfg["lr"], lr_dense=self._adam_lr(),
+                                      eps=self.fused_cfg["eps"], id_dtype=idt, capacity=cap, tables=tables)
+        # the towers' parameters -> views of the step's flat buffer; Adam's moments likewise
+        views = [x for layers in st.layer_views() for wb in layers for x in wb]
+        params = [p for m in self.towers for l in m._mlp for p in (l._linear.weight, l._linear.bias)]
+        steps, o = set(), 0
+        with torch.no_grad():
+            for p, vw in zip(params, views):
+                vw.copy_(p.detach())
+                n = vw.numel()
+                s = self.adam.state.get(p)
+                if s and "exp_avg" in s:
+                    st.exp_avg[o:o + n].view_as(vw).copy_(s["exp_avg"])
+                    st.exp_avg_sq[o:o + n].view_as(vw).copy_(s["exp_avg_sq"])
+                    steps.add(int(float(s["step"])))
+                o += n
+        if len(steps) > 1:
+            raise _lib.TTError("dropin: the towers' Adam step counts differ")
+        n_adam = steps.pop() if steps else 0
+        st.adam_state[0] = n_adam
+        o = 0
+        for p, vw in zip(params, views):
+            n = vw.numel()
+            p.data = vw
+            self.adam.state[p] = {"step": torch.tensor(float(n_adam)), "exp_avg": st.exp_avg[o:o + n].view_as(vw),
+                                  "exp_avg_sq": st.exp_avg_sq[o:o + n].view_as(vw)}
+            o += n
+        st.towers.update(st.params, do_adam=False)
+        self._params = params
+        self.step = st
+        Dp = self.depth
+        self.slot_cols = [[torch.zeros(B, dtype=idt, device=dev) for _ in range(2)] for _ in range(Dp)]
+        self.slot_labels = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in range(Dp)]
+        self.slot_logits = [torch.zeros(B, dtype=torch.float32, device=dev) for _ in range(Dp)]
+        self.slot_loss = [torch.zeros((), dtype=torch.float32, device=dev) for _ in range(Dp)]
+        self.zero_cols = [torch.zeros(B, dtype=idt, device=dev) for _ in range(2)]
+        self._lib = _lib.load()
+        self._ne = (C.c_int64 * 2)(*N)
+        self._slot_ptrs = [_lib.ptr_array(c) for c in self.slot_cols]
+        self._idt = _lib.id_dtype_code(idt)
+        self._group = self._adam_group()
+        # graphs with the collectives inside need RCCL (gloo collectives are not capturable)
+        self.graph_mode = dist.get_backend(ebc._pg) == "nccl"
+        if self.graph_mode:
+            try:
+                self._capture()
+            except Exception as e:  # noqa: BLE001 - the same collectives run eagerly
+                import sys
+
+                print(f"dropin (sharded): graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
+                torch.cuda.synchronize(dev)
+                self.graphs, self.graph_mode = [], False
+
+    def _cols_of(self, kjt, B):
+        """Host-side view of a batch's single-hot ids as id columns (the capacity probe only)."""
+        o = kjt.offsets().to(torch.int64)
+        v = kjt.values()
+        cols = []
+        for f in range(2):
+            ln = o[f * B + 1:(f + 1) * B + 1] - o[f * B:(f + 1) * B]
+            c = torch.zeros(B, dtype=torch.int64, device=v.device)
+            idx = o[f * B:(f + 1) * B][ln > 0]
+            c[ln > 0] = v[idx].to(torch.int64) % self.ebc._embedding_bag_configs[f].num_embeddings
+            c[(ln > 0) & (c == 0)] = self.ebc._embedding_bag_configs[f].num_embeddings  # row 0 kept
+            cols.append(c)
+        return cols
+
+    def _pipelined(self, slot: int, parity: int, next2) -> None:
+        st = self.step
+        keep = st.logits, st.loss
+        st.logits, st.loss = self.slot_logits[slot], self.slot_loss[slot]
+        try:
+            st.step_pipelined(self.slot_labels[slot], parity, next2)
+        finally:
+            st.logits, st.loss = keep
+
+    def _capture(self) -> None:
+        """Slot k's graph: the pipelined step on slot k (parity k % 2) routing slot k + 2."""
+        st, Dp, dev = self.step, self.depth, self.device
+        self.lr_captured = st.lr_dense
+        st.comm.retire()
+        self.graphs = []
+        torch.cuda.synchronize(dev)
+        for k in range(Dp):
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                    self._pipelined(k, k % 2, self.slot_cols[(k + 2) % Dp])
+            torch.cuda.current_stream(dev).wait_stream(s)
+            _lib.graph_upload(g, dev)
+            self.graphs.append(g)
+        torch.cuda.synchronize(dev)
+
+    # ---- staging -----------------------------------------------------------------------------
+    def _fetch(self, it: Iterator) -> Optional[_Item]:
+        try:
+            batch = next(it)
+        except StopIteration:
+            return None
+        batch = batch.to(self.device, non_blocking=True)
+        if not self.fusable(batch):
+            return _Item(batch)
+        kjt = batch.sparse_features
+        if self.step is None:
+            if int(kjt.lengths().max()) > 1 if kjt.lengths().numel() else False:
+                return _Item(batch)
+            self._make_step(batch)
+        v = kjt.values()
+        k = self.k
+        self.k += 1
+        slot = k % self.depth
+        offs = kjt.offsets()
+        if offs.dtype != torch.int32:
+            offs = offs.to(torch.int32)
+        lab = batch.labels
+        _lib.check(self._lib.tt_kjt_single_hot_cols(
+            2, self.step.B, v.data_ptr() if v.numel() else self.slot_cols[slot][0].data_ptr(), self._idt,
+            offs.data_ptr(), self._ne, self._slot_ptrs[slot], self.err.data_ptr(), lab.data_ptr(),
+            _lib.TT_I64 if lab.dtype == torch.int64 else _lib.TT_I32, self.slot_labels[slot].data_ptr(),
+            torch.cuda.current_stream(self.device).cuda_stream), "kjt_single_hot_cols")
+        return _Item(batch, slot, k % 2, lab)
+
+    def _fill(self, it: Iterator) -> None:
+        while len(self.queue) < 3:
+            x = self._fetch(it)
+            if x is None:
+                break
+            self.queue.append(x)
+
+    def _reset(self) -> None:
+        if self.step is not None and self.dirty:
+            self.step.reset_pipeline()
+        self.staged = self.dirty = False
+
+    def check_errors(self) -> None:
+        """Raise (on every rank) if a converted batch had a multi-id bag or an id out of range, or a
+        route overflowed a segment's capacity (collective)."""
+        import torch.distributed as dist
+
+        e = self.err.clone()
+        dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.ebc._pg)
+        if self.step is not None:
+            self.step.check()
+        if int(e.item()):
+            self.err.zero_()
+            raise _lib.TTError("dropin (sharded): a KJT batch had a bag of several ids or an id outside [0, N) "
+                               "(single-hot bags only on this path)")
+
+    def sync_optimizer_state(self) -> None:
+        if self.step is None:
+            return
+        n = torch.tensor(float(int(self.step.adam_state[0].item())))
+        for q in self._params:
+            self.adam.state[q]["step"] = n.clone()
+
+    def pending(self) -> bool:
+        return bool(self.queue)
+
+    def drain_to(self, pipeline) -> None:
+        """Mode switch with batches fetched: hand them back to the generic pipeline in order."""
+        from .torchrec.distributed.train_pipeline import _Staged
+
+        items, self.queue = self.queue, []
+        self._reset()
+        if items:
+            pipeline._cur = _Staged(items[0].batch, None)
+            pipeline._next = _Staged(items[1].batch, None) if len(items) > 1 else None
+            pipeline._pushback = [x.batch for x in items[2:]] + list(getattr(pipeline, "_pushback", []))
+
+    # ---- one progress() ----------------------------------------------------------------------
+    def progress(self, it: Iterator) -> Any:
+        self._fill(it)
+        if not self.queue:
+            self._reset()
+            self.check_errors()
+            self.sync_optimizer_state()
+            raise StopIteration
+        cur = self.queue[0]
+        if cur.slot is None:
+            self._reset()
+            out = self._generic(cur.batch)
+        else:
+            out = self._fused()
+        self.queue.pop(0)
+        return out
+
+    def _fused(self) -> Any:
+        st = self.step
+        q = self.queue
+        cur = q[0]
+        nxt = q[1] if len(q) > 1 and q[1].slot is not None else None
+        nxt2 = q[2] if nxt is not None and len(q) > 2 and q[2].slot is not None else None
+        lr = self._group["lr"]
+        if lr != st.lr_dense:  # the plans carry Adam's lr: re-capture after a change
+            st.lr_dense = float(lr)
+            if self.graph_mode:
+                self._capture()
+        if not self.staged:
+            st.prime(self.slot_cols[cur.slot], cur.parity,
+                     self.slot_cols[nxt.slot] if nxt is not None else self.zero_cols)
+        if self.graph_mode and nxt2 is not None and nxt2.slot == (cur.slot + 2) % self.depth:
+            self.graphs[cur.slot].replay()
+        else:
+            self._pipelined(cur.slot, cur.parity, self.slot_cols[nxt2.slot] if nxt2 is not None else self.zero_cols)
+        self.staged = nxt is not None
+        self.dirty = True
+        self.steps_fused += 1
+        return self.slot_loss[cur.slot], self.slot_logits[cur.slot], cur.labels
+
+    def _generic(self, batch) -> Any:
+        """A batch the fused step does not take: the DMP per-op path (collective on every rank),
+        the Adam step count carried across (the moments are shared views)."""
+        p = self.pipeline
+        st = self.step
+        if st is not None:
+            n = int(st.adam_state[0].item())
+            for q in self._params:
+                self.adam.state[q]["step"] = torch.tensor(float(n))
+        p._optimizer.zero_grad(set_to_none=True)
+        losses, output = p._model(batch)
+        torch.sum(losses, dim=0).backward()
+        p._optimizer.step()
+        if st is not None:
+            st.adam_state[0] = n + 1
+            st.towers.update(st.params, do_adam=False)
         self.steps_generic += 1
         return output

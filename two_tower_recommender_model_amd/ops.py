@@ -236,6 +236,28 @@ class TableSet:
         ts.state = self.state
         return ts
 
+    @classmethod
+    def view_of(cls, src: Optional["TableSet"], table_ids: Sequence[Optional[int]], dims: Sequence[int],
+                device: torch.device) -> "TableSet":
+        """Tables ``table_ids[t]`` of ``src`` as tables t of a new TableSet over the SAME weight and
+        state storage (feature t -> table t); ``None`` (or no ``src``): a table of 0 rows (a shard
+        this rank does not hold: every key of it is out of range, so no kernel touches storage for
+        it). What a step uses to train the shards a ShardedEmbeddingBagCollection already holds."""
+        n = len(table_ids)
+        if src is None:  # nothing held here: one zero element of storage behind every empty table
+            src = cls([0], [int(dims[0])], [0], device)
+        rows = [src.rows[i] if i is not None else 0 for i in table_ids]
+        ts = cls(rows, [int(d) for d in dims], list(range(n)), device, weights=src.weights)
+        ts.state = src.state
+        for t, i in enumerate(table_ids):
+            if i is not None and src.dims[i] != ts.dims[t]:
+                raise _lib.TTError("TableSet.view_of: table dims differ")
+            ts.weight_offsets[t] = src.weight_offsets[i] if i is not None else 0
+            ts.state_offsets[t] = src.state_offsets[i] if i is not None else 0
+            ts._tm[t].weight_offset = ts.weight_offsets[t]
+            ts._tm[t].state_offset = ts.state_offsets[t]
+        return ts
+
     def table_view(self, t: int) -> torch.Tensor:
         o = self.weight_offsets[t]
         return self.weights[o:o + self.rows[t] * self.dims[t]].view(self.rows[t], self.dims[t])

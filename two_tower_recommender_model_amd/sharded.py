@@ -263,7 +263,8 @@ class FusedShardedTwoTowerStep:
                  tw_owners: Optional[Sequence[int]] = None, lr_emb: float = 0.01, lr_dense: float = 0.01,
                  eps: float = 1e-10, id_dtype: torch.dtype = torch.int64, seed: int = 0,
                  capacity=None, full_tables: Optional[Sequence[torch.Tensor]] = None,
-                 num_query_features: Optional[int] = None, overlap: bool = False):
+                 num_query_features: Optional[int] = None, overlap: bool = False,
+                 tables: Optional[ops.TableSet] = None):
         """Single-hot features, one table each: features 0 .. Fq-1 feed the query tower (their rows
         concatenated in that order: torch.cat([kt[f] for f in query features]),
         03_model_training.py:420-425), features Fq .. F-1 the candidate tower; ``num_query_features``
@@ -278,7 +279,11 @@ class FusedShardedTwoTowerStep:
         general T1 over the concatenated rows (tt_tower_fwd_bwd_indexed_multi_bf16). ``overlap``: the
         pipelined step runs the towers' weight gradients (T2) on a parallel stream beside exchange A
         and the owner's update (else inside launch U, one stream; the default: the parallel branch
-        measured 94.1 against 70.5 us per world-1 step, profiles/r03_bench_sharded_w1*.log)."""
+        measured 94.1 against 70.5 us per world-1 step, profiles/r03_bench_sharded_w1*.log).
+        ``tables``: adopt this rank's shards instead of allocating them — table f of the TableSet is
+        feature f's local shard (rows [row_lo, row_lo + local rows) of a row-wise table, the whole
+        table-wise table on its owner, 0 rows elsewhere; ops.TableSet.view_of over a
+        ShardedEmbeddingBagCollection's storage, dropin.py): trained in place, not initialised."""
         self.comm = comm
         self.W, self.rank = comm.world, comm.rank
         self.device = torch.device(device)
@@ -324,9 +329,17 @@ class FusedShardedTwoTowerStep:
             else:
                 raise _lib.TTError(f"sharding must be row_wise / table_wise, got {sharding[f]}")
         self.local_rows = local_rows
-        self.tables = ops.TableSet([max(1, n) for n in local_rows], [D] * F, list(range(F)), dev)
-        self.tables.weights.zero_()  # a feature this rank holds no rows of keeps one zero dummy row
-        for f in range(F):
+        self._adopted = tables is not None
+        if self._adopted:
+            if tables.T != F or tables.dims != [D] * F or tables.device != dev or \
+                    any(tables.rows[f] != local_rows[f] for f in range(F)):
+                raise _lib.TTError(f"sharded step: adopted tables must be this rank's shards (rows {local_rows}, "
+                                   f"dim {D}), feature f -> table f; got rows {tables.rows}")
+            self.tables = tables
+        else:
+            self.tables = ops.TableSet([max(1, n) for n in local_rows], [D] * F, list(range(F)), dev)
+            self.tables.weights.zero_()  # a feature this rank holds no rows of keeps one zero dummy row
+        for f in range(F if not self._adopted else 0):
             view = self.tables.table_view(f)
             if local_rows[f] == 0:
                 continue

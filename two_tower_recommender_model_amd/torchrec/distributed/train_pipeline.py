@@ -15,9 +15,11 @@ Batch i's kernels are queued before batch i+1's input_dist starts, so the host-s
 input_dist (its split sizes) overlap batch i's device work. input_dist reads only ids, so running it
 before batch i's table update is exact. Without sharded modules the pipeline has two stages.
 
-Training ``progress`` on the reference's two-tower model (one rank, single-hot KJTs, bf16 towers)
-is dispatched to the fused production ring (``two_tower_recommender_model_amd.dropin``): the same
-step, in three fused launches per batch replayed as HIP graphs, on the model's own storage.
+Training ``progress`` on the reference's two-tower model (single-hot KJTs, bf16 towers) is
+dispatched to the fused steps (``two_tower_recommender_model_amd.dropin``) on the model's own
+storage: at world size 1 the production ring (three fused launches per batch replayed as HIP
+graphs), at world size W > 1 the pipelined sharded step on the DMP plan's shards (two fixed-size
+RCCL all-to-alls per batch inside the HIP graphs).
 ``_fused_reason`` says why a pipeline did not dispatch; ``TT_DROPIN_FUSED=0`` turns it off.
 """
 from __future__ import annotations
@@ -48,15 +50,19 @@ class TrainPipelineBase:
         self._connected = False
         self._fused = None          # dropin.FusedDropin once built (False: not applicable)
         self._fused_reason = "not tried"
+        self._pushback: List[Any] = []
 
     def _sharded(self) -> List[Any]:
         return []
 
     def _fetch(self, it: Iterator) -> Optional[_Staged]:
-        try:
-            batch = next(it)
-        except StopIteration:
-            return None
+        if self._pushback:  # batches a fused drop-in fetched ahead and handed back (dropin.drain_to)
+            batch = self._pushback.pop(0)
+        else:
+            try:
+                batch = next(it)
+            except StopIteration:
+                return None
         if not self._cuda:
             return _Staged(batch.to(self._device, non_blocking=True), None)
         with torch.cuda.stream(self._memcpy_stream):
