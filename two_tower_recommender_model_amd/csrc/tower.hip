@@ -1525,6 +1525,11 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   } else if (!POOL) {
     id_raw = rk_raw(t ? a.gcol[1] : a.gcol[0], wide, mc);
   }
+  // UPD: the claim of this row's lookup in the batch's completed dedup table (no dependency: issued
+  // beside the id, so the slot word's load can follow the row DMA instead of stalling the chain after
+  // layer 1 for a whole memory round trip)
+  int32_t cl = -1;
+  if (UPD) cl = a.dd.claim[live ? t * B + m : 0];
   const RkRaw lab_raw = rk_raw(a.labels, a.label_dtype == TT_I64, mc);
   f32x4 b0v[8], b1v[4];
   auto load_biases = [&]() {
@@ -1632,11 +1637,13 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
 #pragma unroll
     for (int s2 = 0; s2 < NI; ++s2) xb[s2] = rk_pack(xv[2 * s2], xv[2 * s2 + 1]);
   }
-  // UPD, past barrier 1 (nothing waits on these until the row update): is the row looked up once in
-  // this step (claim -> slot word in this batch's completed dedup table), its state
-  // (unconditional loads at clamped indices: a branch around a load pulls its first use, and the
-  // wait for it, into the branch)
-  int32_t cl = -1;
+  // UPD, past barrier 1 (nothing waits on these until the row update; the claim landed with the id,
+  // so neither waits for a round trip here): the slot word (its low half holds the lookup count:
+  // DD_CNT_BITS < 32, little-endian) and the row's state — unconditional loads at clamped indices
+  // (a branch around a load pulls its first use, and the wait for it, into the branch); the state
+  // is used only for a single-lookup row. Issued before the row DMA, the two random loads held the
+  // DMA's issue back 1.4 us (profiles/r05_t1_claim_ab.log)
+  uint32_t word = 0u;
   float s_old = 0.f;
   if (UPD) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the table's hot-row count for the tail (dd_update_block)
@@ -1644,8 +1651,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
       a.dd.ctr[2] = nh;
       a.dd.ctr[0] = 0;
     }
-    cl = a.dd.claim[live ? t * B + m : 0];
-    s_old = (t ? a.us[1] : a.us[0])[r >= 0 ? r : 0];  // speculative: used only for a single-lookup row
+    word = reinterpret_cast<const uint32_t*>(&a.dd.slots[cl >= 0 ? cl : 0].word)[0];
+    s_old = (t ? a.us[1] : a.us[0])[r >= 0 ? r : 0];
   }
   __builtin_amdgcn_sched_barrier(0);
   const char* img0 = wimg + t * RK_IMG_T;
@@ -1678,8 +1685,6 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
     *reinterpret_cast<f32x4*>(&xo[t][h][n * 64 + ((c ^ n) << 2)]) = uo[mt];
   }
   RK_STAMP(5);
-  // the slot word's low half holds the lookup count (little-endian; DD_CNT_BITS < 32)
-  const uint32_t word = UPD ? reinterpret_cast<const uint32_t*>(&a.dd.slots[cl >= 0 ? cl : 0].word)[0] : 0u;
   // the T1 -> T2 strips of X and h (row-major): fire-and-forget stores
   rk_strip<NI>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);
   rk_strip<4>(hb, a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
@@ -1892,7 +1897,6 @@ struct WgradTile {
   int32_t t, l, n0, k0;
 };
 
-constexpr int MAX_WTILES = 2 * MAXL * (MAXW / 32) * (1024 / 32);
 
 struct WgradArgs {
   const __bf16* xt;
