@@ -139,3 +139,28 @@ def test_tower_shape_flags_validated(lib):
     fake = 1 << 20  # never dereferenced: the call must return before any launch
     rc = lib.tt_tower_fwd_bwd(C.byref(sh), B, fake, 256, fake, fake, fake, _lib.TT_I32, 1.0, fake, fake, ws, None)
     assert rc == 1001 and b"GENERAL_T1" in lib.tt_last_error_string()
+
+
+def test_tableset_view_of_maps_shards_onto_shared_storage():
+    """ops.TableSet.view_of (the fused sharded step adopting a ShardedEmbeddingBagCollection's
+    shards, dropin.FusedShardedDropin): table t of the view is table table_ids[t] of the source —
+    same offsets in the same weight / state storage — and a missing shard is a 0-row table."""
+    import torch
+
+    from two_tower_recommender_model_amd import ops
+
+    src = ops.TableSet([5, 7, 3], [8, 8, 8], [0, 1, 2], torch.device("cpu"))
+    src.weights.copy_(torch.arange(src.weights.numel(), dtype=torch.float32))
+    src.state.copy_(torch.arange(src.state.numel(), dtype=torch.float32))
+    v = ops.TableSet.view_of(src, [2, None, 0], [8, 8, 8], torch.device("cpu"))
+    assert v.rows == [3, 0, 5] and v.weights.data_ptr() == src.weights.data_ptr() and v.state is src.state
+    assert torch.equal(v.table_view(0), src.table_view(2)) and torch.equal(v.table_view(2), src.table_view(0))
+    assert v.table_view(1).shape == (0, 8) and v.state_view(1).numel() == 0
+    assert torch.equal(v.state_view(0), src.state_view(2))
+    for t, i in enumerate([2, None, 0]):
+        assert v._tm[t].num_rows == (src.rows[i] if i is not None else 0)
+        if i is not None:
+            assert v._tm[t].weight_offset == src.weight_offsets[i] and v._tm[t].state_offset == src.state_offsets[i]
+    # a rank holding no shard at all: empty tables over a one-element storage
+    e = ops.TableSet.view_of(None, [None, None], [8, 8], torch.device("cpu"))
+    assert e.rows == [0, 0] and e.weights.numel() >= 1

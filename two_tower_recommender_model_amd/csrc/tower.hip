@@ -1686,8 +1686,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   }
   RK_STAMP(5);
   // the T1 -> T2 strips of X and h (row-major): fire-and-forget stores
-  rk_strip<NI>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);
-  rk_strip<4>(hb, a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
+  if (!TDBG(512)) rk_strip<NI>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);  // (TDBG: timing only)
+  if (!TDBG(256)) rk_strip<4>(hb, a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
   RK_STAMP(6);
   __syncthreads();
   RK_STAMP(7);
@@ -1757,6 +1757,10 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
     for (int j = 0; j < 8; ++j) v[j] = (__bf16)z0[8 * s + j];
     z0b[s] = v;
   }
+  // the dZ strips (T1 -> T2), issued here so they drain beside dX and the row update instead of at
+  // the kernel's end
+  if (!TDBG(512)) rk_strip<2>(z1b, a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + m * MAXW, q);
+  if (!TDBG(128)) rk_strip<4>(z0b, a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
   // ---- 6. dX^T = W0^T dZ0^T: 8 M-tiles x 4 k-steps; acc[mt] = dX features of xv[mt]
   RK_STAMP(9);
   rk_gemm<MTI, 4, true>(acc, img0, z0b, lane);
@@ -1851,10 +1855,8 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
     for (int mt = 0; mt < MTI; ++mt) *reinterpret_cast<f32x4*>(prow + 32 * (mt >> 1) + 8 * q + 4 * (mt & 1)) = xv[mt];
   }
   RK_STAMP(11);
-  // ---- 8. the dZ strips; bias partials (fp32 column sums over the wave's rows, then row half 0 +
+  // ---- 8. bias partials (fp32 column sums over the wave's rows, then row half 0 +
   // row half 1); the loss partial (the tile's 32 row losses in order)
-  rk_strip<2>(z1b, a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + m * MAXW, q);
-  rk_strip<4>(z0b, a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
   RK_STAMP(12);
   rk_colsum<32>(z0, n);  // lane n: k = 2 n + i, i < 2 (k = 4 mt + j)
   rk_colsum<16>(z1, n);  // lane n: k = n

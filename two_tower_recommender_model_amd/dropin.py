@@ -341,7 +341,11 @@ class FusedDropin:
             self.err.zero_()
             raise _lib.TTError(f"dropin: a KJT batch had {'a bag of several ids' if e & 1 else ''}"
                                f"{' and ' if e == 3 else ''}{'an id outside [0, N)' if e & 2 else ''} "
-                               "(TorchRec's EBC takes ids in range; single-hot bags only on this path)")
+                               "(TorchRec's EBC takes ids in range; single-hot bags only on this path). The "
+                               "fused ring trained on the converted batch (such a bag as an empty one) and on "
+                               "every batch after it in this chunk: the tables, towers and optimizer state are "
+                               "not what the reference's loop would hold — restore a checkpoint, or run such "
+                               "data with TT_DROPIN_FUSED=0")
 
     def sync_optimizer_state(self) -> None:
         """torch Adam's per-parameter step count <- the fused step's (the moments are shared views);
@@ -676,7 +680,10 @@ class FusedShardedDropin:
         if int(e.item()):
             self.err.zero_()
             raise _lib.TTError("dropin (sharded): a KJT batch had a bag of several ids or an id outside [0, N) "
-                               "(single-hot bags only on this path)")
+                               "(single-hot bags only on this path). The fused step trained on the converted "
+                               "batch and the ones after it in this chunk: the model state is not what the "
+                               "reference's loop would hold — restore a checkpoint, or run such data with "
+                               "TT_DROPIN_FUSED=0")
 
     def sync_optimizer_state(self) -> None:
         if self.step is None:
