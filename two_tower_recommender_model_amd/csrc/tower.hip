@@ -1659,6 +1659,9 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   const char* img1 = img0 + RK_W0 * 256;
   // ---- 1. layer 0: h^T = relu(W0 X^T + b0), 8 M-tiles x 4 k-steps
   f32x4 acc[8];
+  // the T1 -> T2 strip of X (row-major), fire-and-forget: issued before the layer's MFMAs so the
+  // stores drain under them (likewise h's after layer 0, the dZ strips before dX)
+  if (!TDBG(512)) rk_strip<NI>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);  // (TDBG: timing only)
   rk_gemm<8, NI, false>(acc, img0, xb, lane);
   RK_STAMP(4);
   bf16x8 hb[4];
@@ -1672,6 +1675,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
     }
     hb[s] = rk_pack(u0, u1);
   }
+  if (!TDBG(256)) rk_strip<4>(hb, a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
   // ---- 2. layer 1: out^T = relu(W1 h^T + b1) (fp32), 4 M-tiles x 4 k-steps; exchanged in LDS
   f32x4 uo[4];
   rk_gemm<4, 4, false>(acc, img1, hb, lane);
@@ -1685,9 +1689,6 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
     *reinterpret_cast<f32x4*>(&xo[t][h][n * 64 + ((c ^ n) << 2)]) = uo[mt];
   }
   RK_STAMP(5);
-  // the T1 -> T2 strips of X and h (row-major): fire-and-forget stores
-  if (!TDBG(512)) rk_strip<NI>(xb, a.xt + (int64_t)t * a.in_max * a.Bp + m * a.in_max, q);  // (TDBG: timing only)
-  if (!TDBG(256)) rk_strip<4>(hb, a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + m * MAXW, q);
   RK_STAMP(6);
   __syncthreads();
   RK_STAMP(7);
