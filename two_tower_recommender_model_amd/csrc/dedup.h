@@ -267,9 +267,10 @@ constexpr int DD_HOT_TEAM = 8;              // at most this many workgroups shar
 #if DD_HOT_STAMPS && !TT_EXPERIMENTS
 #error "DD_HOT_STAMPS needs the experiment build (DD_STAMP records nothing without TT_EXPERIMENTS): build --experiments"
 #endif
-// LDS of the hot role (list + wave totals + group partials), provided by the launching kernel so a
-// combined launch can overlay it on its other roles' LDS
-constexpr int DD_SMEM_HOT = DD_HOT_CH * 4 + 16 + 8 * 32 * 16;
+// LDS of the hot role (list + per (pass slice, wave) match counts and their prefix + group
+// partials), provided by the launching kernel so a combined launch can overlay it on its other
+// roles' LDS
+constexpr int DD_SMEM_HOT = DD_HOT_CH * 4 + 2 * DD_HOT_PT * 4 * 4 + 16 + 8 * 32 * 16;
 constexpr int DD_SMEM = DD_SMEM_HOT + (int)sizeof(DdMeta);  // + the per-workgroup meta copy
 
 // members per hot row: as many as the hot workgroups allow in one round (at least 1), at most one
@@ -303,10 +304,11 @@ __device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs) {
 __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
                                             float* __restrict__ weights, float* __restrict__ state, float lr,
                                             float eps, const DedupWs& ws, int hot_wgs, int bid, char* smem, int nh,
-                                            bool ticket) {
+                                            bool ticket, int32_t hc) {
   f32x4v (*part)[32] = reinterpret_cast<f32x4v (*)[32]>(smem);       // [8][32], 16-B aligned
   int* list = reinterpret_cast<int*>(smem + 8 * 32 * 16);             // [DD_HOT_CH]
-  int* wtot = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4);  // [4]
+  int* qc = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4);  // [PT][4] matches per (q, wave)
+  int* qoff = qc + DD_HOT_PT * 4;                                          // [PT][4] their prefix, + total
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = tid >> 5, hl = tid & 31;
   const int nn = (int)n;  // lookups < 2^18 (DD_CNT_BITS): 32-bit indices
@@ -314,65 +316,79 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
   const int K = dd_hot_team(nh, n, hot_wgs);
   for (int w = bid; w < nh * K; w += hot_wgs) {
     const int j = w / K, k = w - j * K;
-    const int32_t h = ws.hot[j];
+    // hc: lane l holds hot[bid / (l + 1)], loaded beside the count (the first item for team size K)
+    const int32_t h = w == bid ? __shfl(hc, K - 1, 64) : ws.hot[j];
     const uint64_t key = ws.slots[h].word >> DD_CNT_BITS;
     const int t = (int)(key >> DD_TABLE_SHIFT);
     const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
     const int D = gm.lm->dim[t];
     const bool col_ok = hl * 4 < D;
+    // the row and its state, loaded now for whichever member applies the update (nothing else in
+    // the launch writes a hot row): off the chain's end
+    float* wrow = weights + gm.lm->woff[t] + r * D;
+    float* srow = state + gm.lm->soff[t] + r;
+    const f32x4v wpre = col_ok && wid == 0 && lane < 32 ? *reinterpret_cast<const f32x4v*>(wrow + hl * 4) : (f32x4v)(0.f);
+    const float spre = wid == 0 ? *srow : 0.f;
     f32x4v acc = (f32x4v)(0.f);
     uint64_t kc[DD_HOT_PT], kn[DD_HOT_PT];
+    // thread tid holds lookups pass * CH + 256 q + tid (q < PT): every key load instruction reads
+    // 512 contiguous bytes (16 consecutive keys per thread made each instruction touch 64 lines)
 #pragma unroll
     for (int q = 0; q < DD_HOT_PT; ++q) {
-      const int i = k * DD_HOT_CH + DD_HOT_PT * tid + q;
+      const int i = k * DD_HOT_CH + 256 * q + tid;
       kc[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
     }
+    const uint64_t lt = (1ull << lane) - 1;
     for (int p = k; p < npass; p += K) {
-      // thread tid covers lookups [i0, i0 + PT): PT-bit match mask
-      const int i0 = p * DD_HOT_CH + DD_HOT_PT * tid;
+      const int pb = p * DD_HOT_CH;
 #pragma unroll
       for (int q = 0; q < DD_HOT_PT; ++q) {
-        const int i = i0 + K * DD_HOT_CH + q;
+        const int i = pb + K * DD_HOT_CH + 256 * q + tid;
         kn[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
       }
-      uint32_t mask = 0;
+      // matches per (q, wave) by ballot; their exclusive prefix in (q, wave) order is the
+      // ascending lookup order (lookup pb + 256 q + 64 wave + lane): the list is the same as before
+      uint64_t bq[DD_HOT_PT];
 #pragma unroll
-      for (int q = 0; q < DD_HOT_PT; ++q)
-        if (kc[q] == key) mask |= 1u << q;
-      const int mc = __popc(mask);
-      int inc = mc;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += y;
+      for (int q = 0; q < DD_HOT_PT; ++q) {
+        bq[q] = __ballot(kc[q] == key);
+        if (lane == 0) qc[q * 4 + wid] = __popcll(bq[q]);
       }
-      if (lane == 63) wtot[wid] = inc;
+      __syncthreads();
+      if (wid == 0) {  // 64 counts, one per lane: inclusive scan
+        const int v = qc[lane];
+        int inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(inc, o, 64);
+          if (lane >= o) inc += y;
+        }
+        qoff[lane] = inc - v;
+        if (lane == 63) qoff[DD_HOT_PT * 4] = inc;
+      }
       __syncthreads();
 #if DD_HOT_STAMPS
       if (p == k) DD_STAMP(4);  // first pass: keys matched, scanned
 #endif
-      int base = 0, total = 0;
+      const int total = qoff[DD_HOT_PT * 4];
 #pragma unroll
-      for (int w4 = 0; w4 < 4; ++w4) {
-        if (w4 < wid) base += wtot[w4];
-        total += wtot[w4];
-      }
-      int pos = base + inc - mc;
       for (int q = 0; q < DD_HOT_PT; ++q)
-        if (mask & (1u << q)) list[pos++] = i0 + q;
+        if ((bq[q] >> lane) & 1) list[qoff[q * 4 + wid] + __popcll(bq[q] & lt)] = pb + 256 * q + tid;
       __syncthreads();
-      int pp = grp;
-      for (; pp + 56 < total; pp += 64) {
+      // 8 matched rows in flight per group, the pass's last partial round included (a one-row-per-
+      // iteration remainder was up to 7 dependent round trips per pass); added in position order
+      for (int pp = grp; pp < total; pp += 64) {
         f32x4v x[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          x[u] = col_ok ? *reinterpret_cast<const f32x4v*>(gm.row(list[pp + 8 * u]) + hl * 4) : (f32x4v)(0.f);
+        for (int u = 0; u < 8; ++u) {
+          const bool on = col_ok && pp + 8 * u < total;
+          x[u] = on ? *reinterpret_cast<const f32x4v*>(gm.row(list[pp + 8 * u]) + hl * 4) : (f32x4v)(0.f);
+        }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc += x[u];
+        for (int u = 0; u < 8; ++u)
+          if (pp + 8 * u < total) acc += x[u];
       }
-      for (; pp < total; pp += 8)
-        if (col_ok) acc += *reinterpret_cast<const f32x4v*>(gm.row(list[pp]) + hl * 4);
-      __syncthreads();  // the list and wtot are rewritten by the next pass
+      __syncthreads();  // the list and the counts are rewritten by the next pass
 #pragma unroll
       for (int q = 0; q < DD_HOT_PT; ++q) kc[q] = kn[q];
     }
@@ -421,13 +437,9 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
 #pragma unroll
         for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
         if (lane < 32) {
-          float* wrow = weights + gm.lm->woff[t] + r * D;
-          float* srow = state + gm.lm->soff[t] + r;
-          const float snew = rw_state(*srow, sq, D);
+          const float snew = rw_state(spre, sq, D);
           const float step = rw_step(snew, lr, eps);
-          if (col_ok)
-            *reinterpret_cast<f32x4v*>(wrow + hl * 4) =
-                rw_apply(*reinterpret_cast<const f32x4v*>(wrow + hl * 4), g, step);
+          if (col_ok) *reinterpret_cast<f32x4v*>(wrow + hl * 4) = rw_apply(wpre, g, step);
           __builtin_amdgcn_wave_barrier();
           if (lane == 0) {
             *srow = snew;
@@ -624,6 +636,7 @@ __device__ __forceinline__ void dd_multi_block(const DdUpdateArgs& a, const Grad
 
 // One workgroup (256 threads) of the update launch: bid < hot_wgs -> hot role, else 8 slots.
 // smem: DD_SMEM bytes of 16-B aligned LDS.
+template <bool LIST_ONLY = false>
 __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, char* smem) {
   const EmbMeta& m = a.m;
   const DedupWs& ws = a.ws;
@@ -643,6 +656,9 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     // T1 moved the count to ctr[2] and zeroed ctr[0] (no ticket: 64 returning atomics on one word
     // serialise, the last check-in ended the ring's tail ~3 us after its other roles)
     const bool ticket = !a.skip_single;
+    // beside the count: the hot-list entry this workgroup takes first for each team size it can get
+    // (lane l: team size l + 1), so the slot word is the next hop, not the list entry
+    const int32_t hc = ws.hot[min(bid / (min((int)(threadIdx.x & 63), DD_HOT_TEAM - 1) + 1), ws.hot_cap - 1)];
     const int nh = min(ticket ? __hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ws.ctr[2],
                        ws.hot_cap);
     if (bid >= nh * dd_hot_team(nh, a.n, a.hot_wgs)) {
@@ -651,10 +667,10 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     }
     dd_meta_fill(m, lm);
     __syncthreads();
-    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem, nh, ticket);
+    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem, nh, ticket, hc);
     return;
   }
-  if (a.multi_nseg > 0) {
+  if (LIST_ONLY || a.multi_nseg > 0) {
     dd_multi_block(a, gm, lm, bid - a.hot_wgs, (int)(a.slot_hw / 8), smem, bid);
     return;
   }

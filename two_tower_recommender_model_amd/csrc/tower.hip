@@ -2650,6 +2650,7 @@ __device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, in
   }
 }
 
+template <bool LIST>
 __global__ void __launch_bounds__(256, 3) tower_tail_kernel(WgradArgs a2, const WgradTile* __restrict__ tiles,
                                                          InsertArgs ins, DdUpdateArgs d, int n_ins, int n_t2,
                                                          int64_t* stamps) {
@@ -2661,7 +2662,7 @@ __global__ void __launch_bounds__(256, 3) tower_tail_kernel(WgradArgs a2, const 
   else if ((b -= n_ins) < n_t2)
     wgrad_block(a2, tiles, b, smem);  // n_ins % 8 == 0: b keeps the XCD placement of wgrad_block
   else
-    dd_update_block(d, b - n_t2, smem);
+    dd_update_block<LIST>(d, b - n_t2, smem);
   RING_STAMP(stamps, 1);
 }
 
@@ -3694,7 +3695,9 @@ static int fused_wgrad_insert_adagrad(const tt_tower_shape_t* shape, int64_t B, 
   const int64_t n_ins = ceil_div(ceil_div(2 * B, 256 * INS_PT), 8) * 8;  // INS_PT lookups per thread; % 8 == 0
   int64_t* stamps = TT_EXPERIMENTS && getenv("TT_RING_STAMPS") ? reinterpret_cast<int64_t*>(ws + L.o_dbg) + 4096 : nullptr;
   if (stamps && L.nwg > 256) stamps = nullptr;
-  tower_tail_kernel<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
+  // the list role (the ring) in a kernel of its own code: no slot-role instructions in its footprint
+  auto kern = list ? tower_tail_kernel<true> : tower_tail_kernel<false>;
+  kern<<<dim3((unsigned)(n_ins + wgs + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
       a2, reinterpret_cast<const WgradTile*>(ws + a2.tiles_off), ins, d, (int)n_ins, (int)wgs, stamps);
   return check_launch("tower_wgrad_pre_insert_rowwise_adagrad");
 }
