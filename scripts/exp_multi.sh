@@ -1,5 +1,6 @@
 # EXPERIMENT: several libraries round-robin on one box (interleaved 100-step bench runs, R rounds):
-# VARS names libraries — "prev" (lib_prev/), "new" (the tree's lib/), anything else lib_var/<name>/
+# VARS names libraries — "prev" (lib_prev/), "new" (the tree's lib/), "exp" (lib_exp/), anything else
+# lib_var/<name>/; "<lib>+VAR=value" adds an environment setting to that run (e.g. exp+TT_DD_HOT_WGS=128)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -8,13 +9,18 @@ mkdir -p $O
 P=$PWD/two_tower_recommender_model_amd
 for i in $(seq 1 ${R:-3}); do
   for v in ${VARS:-prev new}; do
-    case $v in
+    lib=${v%%+*}
+    extra=""
+    [ "$lib" != "$v" ] && extra=${v#*+}
+    case $lib in
       prev) L="TT_EXPERIMENT_LIB=$P/lib_prev/libtt_mi355x.so" ;;
       new) L="" ;;
-      *) L="TT_EXPERIMENT_LIB=$P/lib_var/$v/libtt_mi355x.so" ;;
+      exp) L="TT_EXPERIMENT_LIB=1" ;;
+      *) L="TT_EXPERIMENT_LIB=$P/lib_var/$lib/libtt_mi355x.so" ;;
     esac
-    env $L timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 --warmup 20 ${BENCH_ARGS:-} > $O/${v}_$i.log 2>&1 || exit $?
-    python - $O/${v}_$i.log $v <<'PY' || exit $?
+    L="$L $extra"
+    env $L timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 --warmup 20 ${BENCH_ARGS:-} > "$O/${v//[+=]/_}_$i.log" 2>&1 || exit $?
+    python - "$O/${v//[+=]/_}_$i.log" $v <<'PY' || exit $?
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 k = d["roofline"]["kernels"] if d.get("roofline") else {}

@@ -5,7 +5,8 @@ csrc/shard_kjt.hip; BASELINE config 5's shape: users table-wise, items row-wise,
   input_dist (block_bucketize by row block, table-wise owner) and output_dist (reduce-scatter =
   sum of the owners' partial pools), bit-exact for the integer work;
 * W = 1 against the single-GPU multi-hot fused step (FusedTwoTowerStep(max_lookups=...));
-* W = 2, 3, 4 ranks as threads over an in-process all-to-all (ThreadComm) against the oracle: each
+* W = 2, 3, 4 ranks as threads over an in-process all-to-all (ThreadComm) against the oracle (and
+  W = 2 at BASELINE config 5's table sizes and batch): each
   rank's pooled tower input against the oracle's sum pools of the tables before the step (fp32
   summation-order bound), its towers element-wise against the fp64 emulation of the bf16 kernels
   on ITS OWN batch, every touched row against the oracle's row-wise Adagrad over the union of the
@@ -219,16 +220,28 @@ def _run_ranks(fns):
                                                (4, ("table_wise", "row_wise"), (3, 0)),
                                                (3, ("row_wise", "row_wise"), (0, 0))])
 def test_sharded_kjt_threads_vs_oracle(device, W, sharding, owners):
+    _threads_vs_oracle(device, W, sharding, owners, [3000, 5000], 256, 9, 2, full_init=True)
+
+
+def test_sharded_kjt_threads_baseline_sizes_vs_oracle(device):
+    """BASELINE config 5 at full size as W = 2 thread ranks: 50M users table-wise on rank 1, 100M
+    items row-wise, B = 16,384 bags of 1..39 ids per tower and rank (~0.65M lookups a feature a
+    step), both ranks' shards on the one GPU (77 GB); tables drawn on the device, the oracle fed
+    the touched rows read back before each step."""
+    _threads_vs_oracle(device, 2, ("table_wise", "row_wise"), (1, 0), [50_000_000, 100_000_000], 16384, 39, 2,
+                       full_init=False)
+
+
+def _threads_vs_oracle(device, W, sharding, owners, N, B, maxlen, nsteps, full_init):
     from tower_emul import acc_err, check_adagrad, check_towers, check_within, emulate_bounds, split_params
 
     from two_tower_recommender_model_amd.sharded import ThreadComm
     from two_tower_recommender_model_amd.sharded_kjt import FusedShardedKJTStep, route_counts
 
-    N, B, D, lr, layers, F = [3000, 5000], 256, 128, 0.02, [128, 64], 2
+    D, lr, layers, F = 128, 0.02, [128, 64], 2
     gen = torch.Generator().manual_seed(50 + W)
-    full = [torch.empty(n, D).uniform_(-0.05, 0.05, generator=gen) for n in N]
-    nsteps = 2
-    data = [[_kjt(N, B, 9, gen) + (torch.randint(0, 2, (B,), generator=gen).to(torch.int32),) for _ in range(W)]
+    full = [torch.empty(n, D).uniform_(-0.05, 0.05, generator=gen) for n in N] if full_init else None
+    data = [[_kjt(N, B, maxlen, gen) + (torch.randint(0, 2, (B,), generator=gen).to(torch.int32),) for _ in range(W)]
             for _ in range(nsteps)]
     for step_batches in data:  # a hot item in every rank's batch (rows summed across ranks)
         for v, o, _, _ in step_batches:
