@@ -435,18 +435,22 @@ def run_multihot(args):
     maxlen = MULTIHOT[args.workload]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    batches = synth_kjt_batches(num_users, num_items, B, maxlen, 4, dev, args.ids, seed=4)
+    ahead = not args.no_kjt_ahead
+    k = (args.steps_per_graph or 8) if ahead else 1  # several steps per graph: no gap between them
+    batches = synth_kjt_batches(num_users, num_items, B, maxlen, max(4, k), dev, args.ids, seed=4)
     cap = max(v.numel() for v, _, _ in batches)
     step = FusedTwoTowerStep([num_users, num_items], [D, D], [0], [1], layers, B, dev, lr_emb=0.01, lr_dense=0.01,
                              id_dtype=torch.int64, seed=0, max_lookups=cap)
     # pipelined grouping: batch i+1's tt_bwd_prepare runs on the side stream during step i
-    ahead = not args.no_kjt_ahead
-    k = min(args.steps_per_graph or 8, len(batches)) if ahead else 1  # several steps per graph: no gap between them
     step.capture_pool_kjt(batches, ahead=ahead, steps_per_graph=k)
 
     def run(n):
         step.replay_pool(n)
 
+    # the timed steps grouped into k-step graphs (the remainder first, in aligned smaller graphs):
+    # a graph ends by joining its last step's side branches, so each graph launch costs the stream
+    # an idle gap; regrouped BEFORE the warm-up, which runs right up to the timed region
+    step.align_pool(args.steps, after=args.warmup)
     run(args.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()

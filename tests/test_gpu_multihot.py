@@ -137,7 +137,7 @@ def test_config3_shape_step_vs_oracle(device, precision):
             np.testing.assert_allclose(st.tables.table_view(f).cpu().numpy(), s0.tables[f].numpy(), rtol=0, atol=1e-5)
 
 
-@pytest.mark.parametrize("k", [1, 2], ids=["graph1", "graph2"])
+@pytest.mark.parametrize("k", [1, 2, 4], ids=["graph1", "graph2", "graph4-aligned"])
 @pytest.mark.parametrize("hot", [False, True], ids=["uniform", "zipf"])
 def test_multihot_pipelined_grouping_bitwise(device, hot, k):
     """The pipelined pool (capture_pool_kjt(ahead=True): batch i+1's backward grouping built on the
@@ -145,7 +145,9 @@ def test_multihot_pipelined_grouping_bitwise(device, hot, k):
     pool: 4 batches x 2 cycles of graph replays, tables / row-wise state / tower parameters / loss
     bitwise equal; then 3 eager pipelined steps (pool_step_eager) continue bitwise like 3 more
     unpipelined graph replays. Zipf ids exercise the hot-row kernels; k = 2 replays graphs of two
-    pipelined steps where the cursor allows (replay_pool)."""
+    pipelined steps where the cursor allows (replay_pool); k = 4 regroups the graphs for a run of 6
+    steps after 1 (align_pool: graphs grouped from pool position 3, the run's 2 remainder steps
+    first as a 2-step graph, then one 4-step graph), around single-step graphs."""
     from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
 
     rng = np.random.default_rng(23 if hot else 24)
@@ -165,7 +167,14 @@ def test_multihot_pipelined_grouping_bitwise(device, hot, k):
     pipe.capture_pool_kjt(batches, ahead=True, steps_per_graph=k)  # k > 1: graphs of k steps too
     for i in range(8):
         ref_st.pool_graphs[i % 4].replay()
-    pipe.replay_pool(8)
+    if k == 4:
+        pipe.align_pool(6, after=1)
+        assert pipe.pool_offset == 3 and set(pipe.pool_mid) == {2}
+        pipe.replay_pool(1)  # position 0 alone
+        pipe.replay_pool(6)  # 1-2 as a 2-step graph, 3, 0, 1, 2 as a 4-step graph
+        pipe.replay_pool(1)
+    else:
+        pipe.replay_pool(8)
     torch.cuda.synchronize()
     for a, b in ((ref_st.tables.weights, pipe.tables.weights), (ref_st.tables.state, pipe.tables.state),
                  (ref_st.params, pipe.params), (ref_st.loss, pipe.loss)):

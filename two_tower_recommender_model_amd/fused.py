@@ -264,31 +264,67 @@ class FusedTwoTowerStep:
         keep = self.values, self.offsets, self.labels
         self.pool_graphs = []
         self.pool_graphs_k = []
+        self.pool_mid = {}
+        self.pool_offset = 0
         self.pool_ahead = bool(ahead)
         self._kjt_pool = staged
+        self._kjt_keep_graph = keep_graph
         if ahead:
             self.kjt_ring_prime(staged[0][0], staged[0][1], 0)
-
-        def item(i):
-            v, o, lab = staged[i]
-            return v, o, lab, ((staged[(i + 1) % n][0], staged[(i + 1) % n][1]) if ahead else None), i % 2
-
+        self.steps_per_graph = k
         try:
             for i in range(n):
-                self.pool_graphs.append(self._capture_kjt_steps([item(i)], keep_graph))
-            if k > 1:
-                self.pool_graphs_k = [self._capture_kjt_steps([item(i) for i in range(j, j + k)], keep_graph)
-                                      for j in range(0, n, k)]
+                self.pool_graphs.append(self._capture_kjt_steps([self._kjt_item(i)], keep_graph))
         finally:
             self.values, self.offsets, self.labels = keep
+        self._kjt_groups(0)
         self.graph = self.pool_graphs[-1]
-        self.steps_per_graph = k
         self.pool_cursor = 0
 
-    def _capture_kjt_steps(self, items, keep_graph: bool):
+    def _kjt_item(self, i):
+        """(values, offsets, labels, next batch's KJT or None, parity) of pool position i."""
+        staged, n = self._kjt_pool, len(self._kjt_pool)
+        v, o, lab = staged[i]
+        nxt = (staged[(i + 1) % n][0], staged[(i + 1) % n][1]) if self.pool_ahead else None
+        return v, o, lab, nxt, i % 2
+
+    def _kjt_groups(self, offset: int) -> None:
+        """The multi-step pool graphs grouped from pool position ``offset``: k-step graphs and (k a
+        power of two) k/2, ..., 2-step ones at the same alignment, so a run replays few graph
+        launches (a graph ends by joining its last step's side branches and the next one launches:
+        the stream idles ~20-40 us between two graphs, which single-step graphs pay every step)."""
+        n, k = len(self._kjt_pool), self.steps_per_graph
+        self.pool_offset = offset % n
+        self.pool_graphs_k, self.pool_mid = [], {}
+        if k < 2:
+            return
+        keep = self.values, self.offsets, self.labels
+        span = lambda j, sz: [self._kjt_item((offset + j + t) % n) for t in range(sz)]  # noqa: E731
+        try:
+            kg = self._kjt_keep_graph
+            self.pool_graphs_k = [self._capture_kjt_steps(span(j, k), kg, sync=False) for j in range(0, n, k)]
+            sz = k // 2 if k & (k - 1) == 0 else 0
+            while sz >= 2:
+                self.pool_mid[sz] = [self._capture_kjt_steps(span(j, sz), kg, sync=False) for j in range(0, n, sz)]
+                sz //= 2
+        finally:
+            self.values, self.offsets, self.labels = keep
+
+    def align_pool(self, n_next: int = 0, after: int = 0) -> None:
+        """Regroup the multi-step pool graphs for a run of ``n_next`` steps that starts ``after``
+        steps from the cursor (the training state is untouched: only how the steps are grouped into
+        graph launches changes): the run replays its n_next % k remainder first, in aligned smaller
+        graphs, then n_next // k full graphs. Call it before the warm-up that precedes the run."""
+        k, n = self.steps_per_graph, len(self.pool_graphs)
+        off = (self.pool_cursor + after + (n_next % k)) % n
+        if k > 1 and off != self.pool_offset:
+            self._kjt_groups(off)
+
+    def _capture_kjt_steps(self, items, keep_graph: bool, sync: bool = True):
         """One HIP graph of consecutive multi-hot steps; items: (values, offsets, labels, next_kjt,
-        parity) per step."""
-        self.sync_weights()
+        parity) per step. sync: refresh the bf16 weight copies first (not when regrouping mid-run)."""
+        if sync:
+            self.sync_weights()
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph(keep_graph=keep_graph)
         s = torch.cuda.Stream(device=self.device)
@@ -327,13 +363,17 @@ class FusedTwoTowerStep:
         the order: graph i expects batch i's grouping from graph i-1)."""
         i, nb = self.pool_cursor, len(self.pool_graphs)
         k = getattr(self, "steps_per_graph", 1)
+        mid = getattr(self, "pool_mid", {})
+        off = getattr(self, "pool_offset", 0)
         while n > 0:
-            if k > 1 and self.pool_graphs_k and i % k == 0 and n >= k:
-                self.pool_graphs_k[i // k].replay()
-                i, n = (i + k) % nb, n - k
+            r = (i - off) % nb  # position relative to the multi-step graphs' grouping
+            if k > 1 and self.pool_graphs_k and r % k == 0 and n >= k:
+                self.pool_graphs_k[r // k].replay()
+                sz = k
             else:
-                self.pool_graphs[i].replay()
-                i, n = (i + 1) % nb, n - 1
+                sz = next((m for m in sorted(mid, reverse=True) if r % m == 0 and n >= m), 1)
+                (mid[sz][r // sz] if sz > 1 else self.pool_graphs[i]).replay()
+            i, n = (i + sz) % nb, n - sz
         self.pool_cursor = i
 
     def pool_step_eager(self) -> None:
