@@ -16,6 +16,7 @@ OUT=gpurun_out/pmc bash scripts/pmc_traffic.sh > $F/pmc.log 2>&1 || exit $?
 cp gpurun_out/pmc/summary.json profiles/${T}_pmc_traffic.json
 timeout -k 10 600 python bench.py > $F/bench.log 2>&1 || exit $?
 tail -c 300 $F/bench.log
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $F/bench_driverlike.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --ids zipf --no-cpu-baseline > $F/bench_idszipf.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --workload config2 --no-cpu-baseline > $F/bench_workloadconfig2.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --sharded --no-cpu-baseline > $F/bench_sharded.log 2>&1 || exit $?
