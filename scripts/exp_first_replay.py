@@ -32,6 +32,16 @@ elif pre == "touch":  # one read per 64 KB of the tables and their state (page-w
     float(step.tables.weights.view(-1)[::16384].sum()) + float(step.tables.state.view(-1)[::16384].sum())
 elif pre == "touch2m":  # one read per 2 MB
     float(step.tables.weights.view(-1)[::524288].sum()) + float(step.tables.state.view(-1)[::524288].sum())
+elif pre.startswith("steps"):  # N ring steps (the bench's warm-up) right before
+    step.run(int(pre[5:]))
+    torch.cuda.synchronize()
+elif pre.startswith("wsread"):  # read the step's workspaces (towers ws, both dedup tables) N times
+    bufs = [step.towers.ws] + list(step._ring_ws()) + [step.params, step.exp_avg, step.exp_avg_sq]
+    for _ in range(int(pre[6:] or 10)):
+        for b_ in bufs:
+            b_.view(torch.uint8).sum(dtype=torch.int64)
+    torch.cuda.synchronize()
+    print("ws MB", sum(b_.numel() * b_.element_size() for b_ in bufs) / 1e6, flush=True)
 elif pre == "sleep":
     torch.cuda._sleep(int(2.0e9 * 0.02))
     torch.cuda.synchronize()
