@@ -575,18 +575,29 @@ __device__ __forceinline__ void dd_slots_finish(const DdUpdateArgs& a, const Gra
 // the list role (DdUpdateArgs::multi_nseg): every workgroup scans the segment counts (thread t owns
 // segments t, t + 256, ...), takes the equal share [lb per, (lb + 1) per) of the listed slots in
 // that order (per <= 256: the host sizes nlb >= lookups / 512), gathers their slot indices into LDS
-// and updates those slots, DD_SPH per half-wave per round
+// and updates those slots, DD_SPH per half-wave per round. Sparse steps (at most one listed slot per
+// workgroup on average: uniform ids list one or two a step) skip that gather's round trip: workgroup
+// lb takes the slots of its own 8 segments, whose counts and entries it loaded beside the scan's
+// counts (skewed steps cluster their slots in few segments: they keep the equal share). Each slot's
+// update is the same whichever half-wave takes it.
 __device__ __forceinline__ void dd_multi_block(const DdUpdateArgs& a, const GradMap& gm, DdMeta* lm, int lb, int nlb,
                                                char* smem, int bid) {
   const DedupWs& ws = a.ws;
   int* lst = reinterpret_cast<int*>(smem);  // [256]
-  int* wsum = lst + 256;                    // [4] wave totals
+  int* wsum = lst + 256;                    // [4] wave totals, then [8] own segment counts
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nseg = a.multi_nseg;
   constexpr int SPT = 8;  // segments per thread (nseg <= 2048)
   int c[SPT];
 #pragma unroll
   for (int k = 0; k < SPT; ++k) c[k] = tid + 256 * k < nseg ? ws.mcnt[tid + 256 * k] : 0;
+  // the sparse form's own segments, beside the counts: thread tid < 128 holds entry tid & 15 of
+  // segment lb * 8 + (tid >> 4) and that segment's count
+  const bool own_form = nlb * 8 >= nseg;  // every segment belongs to some workgroup's 8
+  const int oseg = lb * 8 + (tid >> 4);
+  const bool own_ok = own_form && tid < 128 && oseg < nseg;
+  const int own_ent = own_ok ? ws.multi[(int64_t)oseg * 16 + (tid & 15)] : -1;
+  const int own_cnt = own_ok ? ws.mcnt[oseg] : 0;
   dd_meta_fill(a.m, lm);
   int mine = 0;
 #pragma unroll
@@ -605,16 +616,32 @@ __device__ __forceinline__ void dd_multi_block(const DdUpdateArgs& a, const Grad
     base += w < wid ? wsum[w] : 0;
     total += wsum[w];
   }
-  const int per = (total + nlb - 1) / nlb;
-  const int r0 = lb * per, r1 = min(total, r0 + per);
-  int p = base;
+  int len;
+  if (own_form && total <= nlb) {  // sparse (workgroup-uniform)
+    int* oc = wsum + 4;  // [8] own segment counts
+    if (tid < 128 && (tid & 15) == 0) oc[tid >> 4] = own_cnt;
+    __syncthreads();
+    int ob = 0, ot = 0;
 #pragma unroll
-  for (int k = 0; k < SPT; ++k) {
-    for (int e = 0; e < c[k]; ++e, ++p)
-      if (p >= r0 && p < r1) lst[p - r0] = ws.multi[(int64_t)(tid + 256 * k) * 16 + e];
+    for (int j = 0; j < 8; ++j) {
+      const int cj = oc[j];
+      ob += j < (tid >> 4) ? cj : 0;
+      ot += cj;
+    }
+    if (tid < 128 && (tid & 15) < own_cnt) lst[ob + (tid & 15)] = own_ent;
+    len = ot;
+  } else {
+    const int per = (total + nlb - 1) / nlb;
+    const int r0 = lb * per, r1 = min(total, r0 + per);
+    int p = base;
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      for (int e = 0; e < c[k]; ++e, ++p)
+        if (p >= r0 && p < r1) lst[p - r0] = ws.multi[(int64_t)(tid + 256 * k) * 16 + e];
+    }
+    len = max(0, r1 - r0);
   }
   __syncthreads();
-  const int len = max(0, r1 - r0);
   const int hl = lane & 31;
   const int hw = wid * 2 + ((lane & 32) >> 5);  // half-wave of the workgroup (8)
   for (int j0 = 0; j0 < len; j0 += 8 * DD_SPH) {
