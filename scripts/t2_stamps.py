@@ -22,7 +22,7 @@ st.capture_ring(batches, steps_per_graph=8)
 nwg = B // 32
 dbg_bytes = (max(2 * nwg, 1024) * 8 + nwg * 16 * 9) * 8
 off = st.towers.nbytes - ((dbg_bytes + 255) // 256 * 256)
-INS_PT = 2
+INS_PT = 1
 n_ins = -(-(-(-2 * B // (256 * INS_PT))) // 8) * 8
 ntile = 6 * 32
 nbias = (2 * (128 + 64) + 1 + 3) // 4
