@@ -30,6 +30,8 @@ if pre == "mm":
         torch.cuda.synchronize()
 elif pre == "touch":  # one read per 64 KB of the tables and their state (page-walk caches warm)
     float(step.tables.weights.view(-1)[::16384].sum()) + float(step.tables.state.view(-1)[::16384].sum())
+elif pre == "touch4k":  # one read per 4 KB of the tables and their state
+    float(step.tables.weights.view(-1)[::1024].sum()) + float(step.tables.state.view(-1)[::1024].sum())
 elif pre == "touch2m":  # one read per 2 MB
     float(step.tables.weights.view(-1)[::524288].sum()) + float(step.tables.state.view(-1)[::524288].sum())
 elif pre.startswith("steps"):  # N ring steps (the bench's warm-up) right before
