@@ -1,7 +1,6 @@
 """EXPERIMENT: per-workgroup start / end (wave 0, s_memrealtime, 100 MHz) of the ring's tail launch
-(tower_tail_kernel: next-batch insert, tiles, bias/loss, row update) or, with TT_RING_TAIL=0,
-of T2 (tower_wgrad_insert_kernel) and K3 (tower_update_dedup_resolve_kernel), at the north-star
-shape. Times in us from each launch's first workgroup start; per role: start p50 / max, end p50 /
+(tower_tail_kernel: next-batch insert, tiles, bias/loss, hot and list roles), and T3's phases, at
+the north-star shape (IDS=zipf: Zipf-skewed ids; GRAPH=1: the last tail of an 8-step graph replay). Times in us from each launch's first workgroup start; per role: start p50 / max, end p50 /
 max."""
 import os
 import sys
