@@ -89,6 +89,9 @@ def parse():
                     help="multi-hot workloads: group each batch inside its own step instead of one step ahead")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
+    ap.add_argument("--exchange", default="rccl", choices=["rccl", "peer"],
+                    help="sharded single-hot step: the two all-to-alls over RCCL (default) or device-initiated "
+                         "into IPC-mapped peer buffers (sharded.PeerComm)")
     ap.add_argument("--overlap", action="store_true",
                     help="sharded step: T2 on a parallel graph branch beside exchange A (default: inside launch U, "
                          "one stream; the branch measured slower at world 1, DESIGN.md section 6)")
@@ -917,7 +920,12 @@ def run_multi(args, world, rank, local_rank):
     N, Fq, D, B, layers, sharding, owners, ids, seed, plan = sharded_spec(args, world)
     F = len(N)
     dev = torch.device("cuda", local_rank % torch.cuda.device_count())  # (rehearsal: ranks may share one GPU)
-    comm = TorchComm(always_collective=True)
+    if args.exchange == "peer":
+        from two_tower_recommender_model_amd.sharded import PeerComm
+
+        comm = PeerComm(device=dev)
+    else:
+        comm = TorchComm(always_collective=True)
     k = args.steps_per_graph or 8
     nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k
     batches = synth_cols(N, B, nb, dev, ids, seed=seed * 1000 + 1 + rank)
@@ -935,7 +943,9 @@ def run_multi(args, world, rank, local_rank):
     step.load_batch(*batches[0])
     step.step()  # creates the RCCL communicators before any capture
     # gloo collectives (TT_REHEARSE_GLOO, testing only) are not capturable: eager steps
-    mode = capture_pool_or_eager(step, batches, k, allow_capture=os.environ.get("TT_REHEARSE_GLOO") != "1")
+    # (the device-initiated exchange is capturable whatever the backend: gloo only carries its setup)
+    mode = capture_pool_or_eager(step, batches, k, allow_capture=os.environ.get("TT_REHEARSE_GLOO") != "1" or
+                                 args.exchange == "peer")
 
     def run(n):
         if mode == "eager":
@@ -958,6 +968,9 @@ def run_multi(args, world, rank, local_rank):
     loss = float(step.loss)
     step.release_graphs()  # before the process group is destroyed
     r = step.rank
+    if args.exchange == "peer":
+        dist.barrier()  # no rank unmaps a peer's buffer while that peer may still store into it
+        comm.close()
     # SURVEY 8(d) embedding-path bytes per rank and step over the whole step's time (no per-launch
     # timing in this mode): every rank routes B x F lookups and owns ~B x F of the W x B x F lookups
     # for the update; U counted on this rank's resident batches (distinct (table, row) per batch)
@@ -975,6 +988,8 @@ def run_multi(args, world, rank, local_rank):
             "exchange_A_bytes_sent": 4 * step.A_total,
             "exchange_B_bytes_sent": 2 * D * world * step.S[r],
             "collectives_per_step": 2, "mode": mode,
+            "exchange": ("device-initiated puts into IPC-mapped peer buffers (" + comm.memory + " memory)"
+                         if args.exchange == "peer" else "RCCL all_to_all_single"),
             "overlap": "T2 (tower weight gradients) on a parallel graph branch beside exchange A + the owner's "
                        "update" if step.overlap else "none (one stream)"}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
@@ -1084,7 +1099,8 @@ def main():
         else:
             value, ms, loss, sharded_info, roofline = run_multi(args, world, rank, local_rank)
             config["parallelism"] = (f"{sharded_info['plan']} sharded tables + data-parallel towers x{world}: pipelined, "
-                                     f"2 RCCL all-to-alls per step ([grad rows | tower grad | next ids], next rows), "
+                                     f"2 {'device-initiated' if args.exchange == 'peer' else 'RCCL'} all-to-alls per "
+                                     f"step ([grad rows | tower grad | next ids], next rows), "
                                      f"{sharded_info['mode']}")
         cpu, steps_run = None, args.steps
         config["sharded"] = sharded_info

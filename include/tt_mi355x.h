@@ -693,6 +693,40 @@ int tt_adam_step(float* params, const float* grads, float* exp_avg, float* exp_a
                  float lr, float beta1, float beta2, float eps, float weight_decay,
                  int64_t* step_state, void* stream);
 
+/* ---- device-initiated fixed-block exchange (opt-in, sharded.PeerComm) ---------------------------
+ * Replaces dist.all_to_all_single on the sharded step's data path: the all-to-alls TorchRec's
+ * ShardedEmbeddingBagCollection input_dist / output_dist issue under DistributedModelParallel
+ * (03_model_training.py:812-815) and DDP's gradient all-reduce of the towers (:812), both reached
+ * through TrainPipelineSparseDist.progress (:648). Each rank stores its blocks straight into every
+ * peer's receive buffer (mapped with hipIpcOpenMemHandle) and signals one flag word per (peer,
+ * source); the receiver waits on its W flag words. Setup calls (alloc / export / import) are the
+ * only entry points of this library that allocate or synchronise. */
+#define TT_PEER_MAXW 16
+#define TT_PEER_HANDLE_BYTES 64
+
+typedef struct {
+  int32_t W, rank;
+  const void* src;                 /* this rank's send buffer */
+  int64_t src_off[TT_PEER_MAXW];   /* bytes: where destination d's block starts in src */
+  int64_t len[TT_PEER_MAXW];       /* bytes sent to d (multiple of 16; 16-B aligned blocks) */
+  void* dst[TT_PEER_MAXW];         /* d's receive buffer at this rank's slot (mapped address) */
+  int32_t* flag[TT_PEER_MAXW];     /* d's flag word for this source (mapped address) */
+  int32_t* state;                  /* this rank's int32[1 + W] for the exchange: epoch, counts */
+} tt_peer_put_t;
+
+/* fine-grained device memory, zeroed (hipExtMallocWithFlags(hipDeviceMallocFinegrained)) */
+int tt_peer_alloc(size_t bytes, void** out);
+int tt_peer_free(void* p);
+/* IPC handle (TT_PEER_HANDLE_BYTES) of the allocation holding p, and p's offset in it */
+int tt_peer_export(const void* p, void* handle, int64_t* offset);
+int tt_peer_import(const void* handle, void** base);
+int tt_peer_unimport(void* base);
+/* block d of src -> dst[d], then flag[d] = epoch + 1 (release, system scope) */
+int tt_peer_put(const tt_peer_put_t* p, void* stream);
+/* wait until flags[0..W) >= epoch + 1 (acquire, system scope), then epoch += 1; a wait longer than
+ * timeout_s gives up and sets *err = 1 (sticky; the exchange's data is then invalid) */
+int tt_peer_wait(const int32_t* flags, int W, int32_t* state, int32_t* err, double timeout_s, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,91 @@
+"""Host logic of the device-initiated exchange (sharded.PeerComm.all_to_all, no GPU): where each block of
+the send buffer goes — peer d's receive buffer at this rank's slot, its flag word for this source — and
+the argument checks, with the library's put / wait replaced by recorders."""
+import ctypes as C
+import types
+
+import pytest
+import torch
+
+from two_tower_recommender_model_amd import _lib, sharded
+
+
+class _Rec:
+    def __init__(self):
+        self.puts, self.waits = [], []
+
+    def tt_peer_put(self, p, stream):
+        self.puts.append(C.cast(p, C.POINTER(_lib.PeerPut)).contents)
+        return 0
+
+    def tt_peer_wait(self, flags, W, state, err, timeout, stream):
+        self.waits.append((flags, W, state, err, timeout))
+        return 0
+
+
+def _comm(monkeypatch, W, rank, peers, out):
+    rec = _Rec()
+    monkeypatch.setattr(_lib, "load", lambda path=None: rec)
+    monkeypatch.setattr(sharded, "stream_handle", lambda device=None: 0)
+    pc = object.__new__(sharded.PeerComm)
+    pc.world, pc.rank, pc.timeout_s = W, rank, 5.0
+    pc.err = torch.zeros(1, dtype=torch.int32)
+    pc._puts = {}
+    pc._bufs = {out.data_ptr(): {"peers": peers, "flags": torch.zeros(W, dtype=torch.int32),
+                                 "state": torch.zeros(1 + W, dtype=torch.int32)}}
+    return pc, rec
+
+
+def test_blocks_land_at_this_ranks_slot_of_every_peer(monkeypatch):
+    W, r = 3, 1
+    sizes = [8, 4, 12]  # rows sent to each destination (1-D fp32: a row is 4 B)
+    inp = torch.zeros(sum(sizes) + 4)
+    out = torch.zeros(W * sizes[r])
+    peers = [(1 << 20, 4096), (2 << 20, 8192), (3 << 20, 1024)]
+    pc, rec = _comm(monkeypatch, W, r, peers, out)
+    pc.all_to_all(out, inp, out_splits=[sizes[r]] * W, in_splits=sizes)
+    (p,) = rec.puts
+    assert (p.W, p.rank, p.src) == (W, r, inp.data_ptr())
+    off = 0
+    for d in range(W):
+        assert p.src_off[d] == off * 4 and p.len[d] == sizes[d] * 4
+        assert p.dst[d] == peers[d][0] + r * sizes[d] * 4  # peer d receives equal blocks of sizes[d] rows
+        assert p.flag[d] == peers[d][0] + peers[d][1] + 4 * r
+        off += sizes[d]
+    assert rec.waits[0][1] == W and rec.waits[0][4] == 5.0
+    pc.all_to_all(out, inp, out_splits=[sizes[r]] * W, in_splits=sizes)
+    assert len(pc._puts) == 1 and len(rec.puts) == 2  # the put arguments are built once per exchange
+
+
+def test_equal_blocks_of_rows(monkeypatch):
+    W, r, rows, D = 2, 0, 6, 8
+    inp = torch.zeros(W * rows, D, dtype=torch.bfloat16)
+    out = torch.zeros(W * rows, D, dtype=torch.bfloat16)
+    peers = [(1 << 20, 256), (5 << 20, 512)]
+    pc, rec = _comm(monkeypatch, W, r, peers, out)
+    pc.all_to_all(out, inp)
+    (p,) = rec.puts
+    rowb = D * 2
+    assert [p.src_off[d] for d in range(W)] == [0, rows * rowb]
+    assert [p.len[d] for d in range(W)] == [rows * rowb] * W
+    assert [p.dst[d] for d in range(W)] == [peers[d][0] for d in range(W)]  # rank 0's slot is block 0
+
+
+def test_rejects_foreign_and_mismatched_buffers(monkeypatch):
+    W, r = 2, 0
+    out = torch.zeros(8)
+    pc, _ = _comm(monkeypatch, W, r, [(1 << 20, 64), (2 << 20, 64)], out)
+    with pytest.raises(_lib.TTError, match="recv_buffer"):
+        pc.all_to_all(torch.zeros(8), torch.zeros(8))
+    with pytest.raises(_lib.TTError, match="do not match"):
+        pc.all_to_all(out, torch.zeros(16), out_splits=[4, 4], in_splits=[6, 2])  # 6 sent to self, 4 expected
+    with pytest.raises(_lib.TTError, match="equal receive blocks"):
+        pc.all_to_all(out, torch.zeros(8), out_splits=[3, 5], in_splits=[4, 4])
+
+
+def test_torch_and_thread_comms_give_plain_receive_buffers():
+    t = types.SimpleNamespace()
+    b = sharded.TorchComm.recv_buffer(t, (4, 2), torch.float32, "cpu")
+    assert b.shape == (4, 2) and not b.any()
+    th = sharded.ThreadComm.group(1)[0]
+    assert th.recv_buffer((3,), torch.bfloat16, "cpu").dtype == torch.bfloat16

@@ -113,6 +113,16 @@ class LaunchPlan(C.Structure):
                 ("gather", GatherRole)]
 
 
+TT_PEER_MAXW = 16
+TT_PEER_HANDLE_BYTES = 64
+
+
+class PeerPut(C.Structure):
+    _fields_ = [("W", C.c_int32), ("rank", C.c_int32), ("src", C.c_void_p),
+                ("src_off", C.c_int64 * TT_PEER_MAXW), ("len", C.c_int64 * TT_PEER_MAXW),
+                ("dst", C.c_void_p * TT_PEER_MAXW), ("flag", C.c_void_p * TT_PEER_MAXW), ("state", C.c_void_p)]
+
+
 def launch(plan: LaunchPlan, stream: int, what: str = "launch") -> None:
     """tt_launch(plan) on ``stream``; raises on a non-zero status. Keep every array the plan points
     to alive until the call returns (the launch copies what it needs into kernel arguments)."""
@@ -272,6 +282,13 @@ SIGNATURES = {
         _int, [_ptm, _int, _pfm, _int, _i64, _vp, _i64, _vp, _int, _vp, _vp, _f32, _f32, _vp, _sz, _i64, _int, _vp],
     ),
     "tt_launch": (_int, [C.c_void_p, _vp]),
+    "tt_peer_alloc": (_int, [_sz, _pvp]),
+    "tt_peer_free": (_int, [_vp]),
+    "tt_peer_export": (_int, [_vp, _vp, _pi64]),
+    "tt_peer_import": (_int, [_vp, _pvp]),
+    "tt_peer_unimport": (_int, [_vp]),
+    "tt_peer_put": (_int, [C.c_void_p, _vp]),
+    "tt_peer_wait": (_int, [_vp, _int, _vp, _vp, C.c_double, _vp]),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -325,6 +342,8 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_indexed_multi_bf16",
     "tt_bwd_rowwise_adagrad_part",
     "tt_launch",
+    "tt_peer_put",
+    "tt_peer_wait",
 ]
 
 _lib = None

@@ -28,7 +28,7 @@ LIB_EXP = PKG / "lib_exp" / "libtt_mi355x.so"
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["api.cpp", "kjt.hip", "embedding.hip", "gemm.hip", "loss_adam.hip", "tower.hip", "dedup.hip", "shard.hip", "shard_kjt.hip"]
+SOURCES = ["api.cpp", "kjt.hip", "embedding.hip", "gemm.hip", "loss_adam.hip", "tower.hip", "dedup.hip", "shard.hip", "shard_kjt.hip", "peer.hip"]
 HEADERS = [CSRC / "tt_common.h", CSRC / "dedup.h", CSRC / "shard.h", INCLUDE / "tt_mi355x.h"]
 
 CFLAGS = [

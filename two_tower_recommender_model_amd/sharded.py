@@ -154,6 +154,153 @@ class TorchComm:
         if self.world > 1:
             dist.broadcast(t, src=src, group=self.group)
 
+    def recv_buffer(self, shape, dtype: torch.dtype, device) -> torch.Tensor:
+        """A receive buffer of an all-to-all (zeroed)."""
+        return torch.zeros(shape, dtype=dtype, device=device)
+
+
+class _DeviceArray:
+    """A device allocation as __cuda_array_interface__ (bytes), for torch.as_tensor."""
+
+    def __init__(self, p: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (p, False), "version": 2}
+
+
+class PeerComm(TorchComm):
+    """TorchComm whose all-to-alls on the step's data path are device-initiated (opt-in):
+    every rank stores its blocks straight into the peers' receive buffers — allocated here
+    (``recv_buffer``, fine-grained device memory) and mapped into every other rank's process with
+    hipIpcOpenMemHandle — and signals a flag word per (peer, source); the receiver's wait kernel spins
+    on its W words (csrc/peer.hip). No RCCL kernel runs on the step path, and the exchange is
+    capturable whatever the process group's backend (gloo included: it only carries the setup).
+    The other collectives (capacities, flags, checkpoints) stay torch.distributed. A wait past
+    ``timeout_s`` gives up and sets a sticky error word that ``check()`` of the step raises on.
+    Replaces the all_to_all_single calls TorchComm issues (TorchRec's input_dist / output_dist
+    all-to-alls and DDP's tower all-reduce under DistributedModelParallel, 03_model_training.py:812-815)."""
+
+    def __init__(self, group=None, timeout_s: float = 5.0, device=None, memory: Optional[str] = None):
+        """memory: "fine-grained" (default; hipDeviceMallocFinegrained, coherent across devices) or
+        "device" (torch's allocator: coarse-grained, coherent only within one device)."""
+        super().__init__(group, always_collective=True)
+        if self.world > _lib.TT_PEER_MAXW:
+            raise _lib.TTError(f"PeerComm: at most {_lib.TT_PEER_MAXW} ranks")
+        self.timeout_s = float(timeout_s)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.memory = memory or os.environ.get("TT_PEER_MEMORY") or None
+        if self.memory not in (None, "fine-grained", "device"):
+            raise _lib.TTError('PeerComm: memory is "fine-grained" or "device"')
+        self._bufs: Dict[int, dict] = {}
+        self._own: List[int] = []
+        self._imports: Dict[bytes, int] = {}
+        self._puts: Dict[tuple, _lib.PeerPut] = {}
+
+    def _alloc(self, nbytes: int) -> torch.Tensor:
+        lib = _lib.load()
+        if self.memory in (None, "fine-grained"):
+            p = C.c_void_p()
+            rc = lib.tt_peer_alloc(nbytes, C.byref(p))
+            if rc == 0:
+                try:
+                    raw = torch.as_tensor(_DeviceArray(p.value, nbytes), device=self.device)
+                    self._own.append(p.value)
+                    self.memory = "fine-grained"
+                    return raw
+                except Exception:  # noqa: BLE001 - torch cannot wrap the allocation: use its own
+                    check(lib.tt_peer_free(p), "peer_free")
+            if self.memory == "fine-grained":
+                check(rc, "peer_alloc")
+        self.memory = "device"
+        return torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+
+    def recv_buffer(self, shape, dtype: torch.dtype, device) -> torch.Tensor:
+        """Collective (every rank, same order): a zeroed receive buffer followed by this exchange's W
+        flag words, exported to every other rank; the peers' buffers are mapped in return."""
+        lib = _lib.load()
+        shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+        n = 1
+        for s in shape:
+            n *= s
+        item = torch.empty((), dtype=dtype).element_size()
+        body = -(-max(1, n * item) // 256) * 256
+        raw = self._alloc(body + 256)
+        buf = raw[:n * item].view(dtype).view(shape)
+        h = (C.c_char * _lib.TT_PEER_HANDLE_BYTES)()
+        off = C.c_int64()
+        base = raw.data_ptr()
+        if self.world > 1:
+            check(lib.tt_peer_export(C.c_void_p(base), h, C.byref(off)), "peer_export")
+        mine = (bytes(h), int(off.value), body)
+        allv = [None] * self.world
+        if self.world > 1:
+            dist.all_gather_object(allv, mine, group=self.group)
+        else:
+            allv[0] = mine
+        peers = []
+        for s, (hs, o, b) in enumerate(allv):
+            if s == self.rank:
+                peers.append((base, b))
+                continue
+            if hs not in self._imports:
+                p = C.c_void_p()
+                check(lib.tt_peer_import(hs, C.byref(p)), "peer_import")
+                self._imports[hs] = p.value
+            peers.append((self._imports[hs] + o, b))
+        self._bufs[buf.data_ptr()] = {"peers": peers, "flags": raw[body:body + 4 * self.world].view(torch.int32),
+                                      "state": torch.zeros(1 + self.world, dtype=torch.int32, device=self.device),
+                                      "raw": raw}
+        return buf
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Optional[List[int]] = None,
+                   in_splits: Optional[List[int]] = None):
+        """All-to-all along dim 0 into a buffer from ``recv_buffer``: block d of ``inp`` (``in_splits[d]``
+        rows, or equal blocks) lands in rank d's buffer at block ``rank``; every rank's blocks are
+        equal-sized at the receiver (what the sharded step's fixed layout guarantees)."""
+        e = self._bufs.get(out.data_ptr())
+        if e is None:
+            raise _lib.TTError("PeerComm.all_to_all: the receive buffer was not allocated by recv_buffer()")
+        W, r = self.world, self.rank
+        key = (out.data_ptr(), inp.data_ptr(), tuple(in_splits or ()), inp.shape[0])
+        put = self._puts.get(key)
+        if put is None:
+            rowb = inp.element_size() * (inp.numel() // max(1, inp.shape[0]))
+            sizes = list(in_splits) if in_splits is not None else [inp.shape[0] // W] * W
+            if len(sizes) != W or sum(sizes) > inp.shape[0]:
+                raise _lib.TTError("PeerComm.all_to_all: one block per rank within the input")
+            mine = (out_splits[0] if out_splits is not None else out.shape[0] // W) * rowb
+            if out_splits is not None and any(s != out_splits[0] for s in out_splits):
+                raise _lib.TTError("PeerComm.all_to_all: equal receive blocks only")
+            if mine * W > out.numel() * out.element_size() or sizes[r] * rowb != mine:
+                raise _lib.TTError("PeerComm.all_to_all: receive blocks do not match the senders' blocks")
+            put = _lib.PeerPut()
+            put.W, put.rank, put.src, put.state = W, r, inp.data_ptr(), e["state"].data_ptr()
+            o = 0
+            for d in range(W):
+                base, body = e["peers"][d]
+                put.src_off[d] = o * rowb
+                put.len[d] = sizes[d] * rowb
+                put.dst[d] = base + r * sizes[d] * rowb
+                put.flag[d] = base + body + 4 * r
+                o += sizes[d]
+            self._puts[key] = put
+        st = stream_handle(out.device)
+        check(_lib.load().tt_peer_put(C.byref(put), st), "peer_put")
+        check(_lib.load().tt_peer_wait(e["flags"].data_ptr(), W, e["state"].data_ptr(), self.err.data_ptr(),
+                                       self.timeout_s, st), "peer_wait")
+
+    def close(self) -> None:
+        """Unmap the peers' buffers and free this rank's (the buffers from recv_buffer are invalid after)."""
+        torch.cuda.synchronize(self.device)
+        lib = _lib.load()
+        for p in self._imports.values():
+            check(lib.tt_peer_unimport(C.c_void_p(p)), "peer_unimport")
+        self._imports.clear()
+        self._bufs.clear()
+        self._puts.clear()
+        for p in self._own:
+            check(lib.tt_peer_free(C.c_void_p(p)), "peer_free")
+        self._own.clear()
+
 
 class ThreadComm:
     """W ranks as W threads of ONE process on one device (tests): each collective is a rendezvous
@@ -230,6 +377,9 @@ class ThreadComm:
         torch.cuda.current_stream().synchronize()
         self.shared.barrier.wait()
         t.copy_(v)
+
+    def recv_buffer(self, shape, dtype: torch.dtype, device) -> torch.Tensor:
+        return torch.zeros(shape, dtype=dtype, device=device)
 
 
 # ---- the step -----------------------------------------------------------------------------------
@@ -388,9 +538,10 @@ class FusedShardedTwoTowerStep:
         self._layout()
         # ---- buffers
         self.sendA = torch.zeros(self.A_total, dtype=torch.float32, device=dev)
-        self.recvA = torch.zeros(W * self.Asz[r], dtype=torch.float32, device=dev)
+        # receive buffers from the comm (PeerComm: mapped into every peer for its device-initiated puts)
+        self.recvA = comm.recv_buffer((W * self.Asz[r],), torch.float32, dev)
         self.rows_out = torch.zeros(W * self.RSTR, D, dtype=torch.bfloat16, device=dev)
-        self.rows_in = torch.zeros(W * self.RSTR, D, dtype=torch.bfloat16, device=dev)
+        self.rows_in = comm.recv_buffer((W * self.RSTR, D), torch.bfloat16, dev)
         self.pos_in = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
         self.pos_out = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(2, dtype=torch.int32, device=dev)  # {overflow, bad key}
@@ -765,9 +916,15 @@ class FusedShardedTwoTowerStep:
         ``collective`` (default) the flags are first max-reduced over the ranks, so every rank
         raises together (call it on every rank, outside any graph capture)."""
         f = self.flags.clone()
+        perr = getattr(self.comm, "err", None)  # PeerComm: a wait that timed out
+        if perr is not None:
+            f = torch.cat([f, perr])
         if collective:
             self.comm.all_reduce_max_(f)
         f = f.cpu().tolist()
+        if len(f) > 2 and f[2]:
+            raise _lib.TTError("sharded step: a device-initiated exchange timed out waiting for a peer: results are "
+                               "invalid")
         if f[0]:
             raise _lib.TTError(f"sharded step: a segment exceeded its capacity {self.caps_f} (skewed ids): "
                                "results are invalid; raise `capacity`")
