@@ -711,7 +711,9 @@ typedef struct {
   int64_t len[TT_PEER_MAXW];       /* bytes sent to d (multiple of 16; 16-B aligned blocks) */
   void* dst[TT_PEER_MAXW];         /* d's receive buffer at this rank's slot (mapped address) */
   int32_t* flag[TT_PEER_MAXW];     /* d's flag word for this source (mapped address) */
-  int32_t* state;                  /* this rank's int32[1 + W] for the exchange: epoch, counts */
+  int32_t* state;                  /* this rank's epoch word for the exchange (int32) */
+  int32_t same_device;             /* every rank on this device: agent-scope signals (else system) */
+  int32_t _pad;
 } tt_peer_put_t;
 
 /* fine-grained device memory, zeroed (hipExtMallocWithFlags(hipDeviceMallocFinegrained)) */
@@ -721,11 +723,10 @@ int tt_peer_free(void* p);
 int tt_peer_export(const void* p, void* handle, int64_t* offset);
 int tt_peer_import(const void* handle, void** base);
 int tt_peer_unimport(void* base);
-/* block d of src -> dst[d], then flag[d] = epoch + 1 (release, system scope) */
-int tt_peer_put(const tt_peer_put_t* p, void* stream);
-/* wait until flags[0..W) >= epoch + 1 (acquire, system scope), then epoch += 1; a wait longer than
- * timeout_s gives up and sets *err = 1 (sticky; the exchange's data is then invalid) */
-int tt_peer_wait(const int32_t* flags, int W, int32_t* state, int32_t* err, double timeout_s, void* stream);
+/* block d of src -> dst[d]; then flag[d] = epoch + 1 (release, system scope) and a wait until
+ * flags[0..W) >= epoch + 1 (acquire, system scope), then epoch += 1. A wait longer than timeout_s
+ * gives up and sets *err = 1 (sticky; the exchange's data is then invalid). Two kernels. */
+int tt_peer_exchange(const tt_peer_put_t* p, const int32_t* flags, int32_t* err, double timeout_s, void* stream);
 
 #ifdef __cplusplus
 }

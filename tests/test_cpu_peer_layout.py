@@ -1,6 +1,6 @@
 """Host logic of the device-initiated exchange (sharded.PeerComm.all_to_all, no GPU): where each block of
 the send buffer goes — peer d's receive buffer at this rank's slot, its flag word for this source — and
-the argument checks, with the library's put / wait replaced by recorders."""
+the argument checks, with the library's exchange call replaced by a recorder."""
 import ctypes as C
 import types
 
@@ -14,12 +14,9 @@ class _Rec:
     def __init__(self):
         self.puts, self.waits = [], []
 
-    def tt_peer_put(self, p, stream):
+    def tt_peer_exchange(self, p, flags, err, timeout, stream):
         self.puts.append(C.cast(p, C.POINTER(_lib.PeerPut)).contents)
-        return 0
-
-    def tt_peer_wait(self, flags, W, state, err, timeout, stream):
-        self.waits.append((flags, W, state, err, timeout))
+        self.waits.append((flags, err, timeout))
         return 0
 
 
@@ -28,11 +25,11 @@ def _comm(monkeypatch, W, rank, peers, out):
     monkeypatch.setattr(_lib, "load", lambda path=None: rec)
     monkeypatch.setattr(sharded, "stream_handle", lambda device=None: 0)
     pc = object.__new__(sharded.PeerComm)
-    pc.world, pc.rank, pc.timeout_s = W, rank, 5.0
+    pc.world, pc.rank, pc.timeout_s, pc.same_device = W, rank, 5.0, False
     pc.err = torch.zeros(1, dtype=torch.int32)
     pc._puts = {}
     pc._bufs = {out.data_ptr(): {"peers": peers, "flags": torch.zeros(W, dtype=torch.int32),
-                                 "state": torch.zeros(1 + W, dtype=torch.int32)}}
+                                 "state": torch.zeros(1, dtype=torch.int32)}}
     return pc, rec
 
 
@@ -52,7 +49,7 @@ def test_blocks_land_at_this_ranks_slot_of_every_peer(monkeypatch):
         assert p.dst[d] == peers[d][0] + r * sizes[d] * 4  # peer d receives equal blocks of sizes[d] rows
         assert p.flag[d] == peers[d][0] + peers[d][1] + 4 * r
         off += sizes[d]
-    assert rec.waits[0][1] == W and rec.waits[0][4] == 5.0
+    assert rec.waits[0][2] == 5.0 and p.same_device == 0
     pc.all_to_all(out, inp, out_splits=[sizes[r]] * W, in_splits=sizes)
     assert len(pc._puts) == 1 and len(rec.puts) == 2  # the put arguments are built once per exchange
 

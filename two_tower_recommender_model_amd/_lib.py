@@ -120,7 +120,8 @@ TT_PEER_HANDLE_BYTES = 64
 class PeerPut(C.Structure):
     _fields_ = [("W", C.c_int32), ("rank", C.c_int32), ("src", C.c_void_p),
                 ("src_off", C.c_int64 * TT_PEER_MAXW), ("len", C.c_int64 * TT_PEER_MAXW),
-                ("dst", C.c_void_p * TT_PEER_MAXW), ("flag", C.c_void_p * TT_PEER_MAXW), ("state", C.c_void_p)]
+                ("dst", C.c_void_p * TT_PEER_MAXW), ("flag", C.c_void_p * TT_PEER_MAXW), ("state", C.c_void_p),
+                ("same_device", C.c_int32), ("_pad", C.c_int32)]
 
 
 def launch(plan: LaunchPlan, stream: int, what: str = "launch") -> None:
@@ -287,8 +288,7 @@ SIGNATURES = {
     "tt_peer_export": (_int, [_vp, _vp, _pi64]),
     "tt_peer_import": (_int, [_vp, _pvp]),
     "tt_peer_unimport": (_int, [_vp]),
-    "tt_peer_put": (_int, [C.c_void_p, _vp]),
-    "tt_peer_wait": (_int, [_vp, _int, _vp, _vp, C.c_double, _vp]),
+    "tt_peer_exchange": (_int, [C.c_void_p, _vp, _vp, C.c_double, _vp]),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -342,8 +342,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_tower_fwd_bwd_indexed_multi_bf16",
     "tt_bwd_rowwise_adagrad_part",
     "tt_launch",
-    "tt_peer_put",
-    "tt_peer_wait",
+    "tt_peer_exchange",
 ]
 
 _lib = None

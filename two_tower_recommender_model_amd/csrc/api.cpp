@@ -58,7 +58,7 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_kjt_route, tt_kjt_unpack, tt_pooled_partials_sum, tt_pooled_grad_pack
 // tt_tower_fwd_bwd_gather_update_t3, tt_tower_update_lazy, tt_tower_fwd_bwd_indexed2_bf16_t3
 // tt_bwd_rowwise_adagrad_part
-// tt_peer_put, tt_peer_wait
-int tt_num_entry_points(void) { return 52; }
+// tt_peer_exchange
+int tt_num_entry_points(void) { return 51; }
 
 }  // extern "C"

@@ -5,11 +5,11 @@
 // local copy at world 1) on the sharded step's data path; opt-in (sharded.PeerComm).
 //
 // Protocol, per registered receive buffer (one per exchange), W ranks in lockstep:
-//   put  (grid chunks x W): block d of the send buffer -> peer d's buffer at this rank's slot; each
-//        workgroup releases its stores at system scope and counts in; the last one of destination
-//        d stores the epoch into peer d's flag word for this source (release, system scope).
-//   wait (one wave): spins until every source's flag word holds the epoch (acquire, system scope),
-//        bounded by a timeout (sticky error word, no hang), then advances the local epoch.
+//   put  (grid chunks x W): block d of the send buffer -> peer d's buffer at this rank's slot.
+//   signal / wait (one wave, after the put's kernel boundary): lane d stores the epoch into peer
+//        d's flag word for this source (release, system scope), then spins until source d's word
+//        in this rank's buffer holds the epoch (acquire, system scope), bounded by a timeout
+//        (sticky error word, no hang); the local epoch then advances.
 // Reuse of a receive buffer is ordered by the exchanges themselves: a rank puts exchange A of step
 // s + 1 only after its wait on exchange B of step s, which every peer signals after consuming its
 // exchange-A block of step s (and symmetrically for B), so one buffer per exchange suffices.
@@ -22,61 +22,57 @@ namespace tt {
 namespace {
 
 constexpr int PX_THREADS = 256;
-constexpr int PX_UNROLL = 8;
-constexpr int64_t PX_CHUNK = (int64_t)PX_THREADS * 16 * PX_UNROLL;  // bytes per workgroup (32 KB)
+constexpr int PX_UNROLL = 4;  // 16-B units per lane
+constexpr int64_t PX_CHUNK = (int64_t)PX_THREADS * 16 * PX_UNROLL;  // bytes per workgroup (16 KB)
 
 struct PxArgs {
-  int32_t W, rank;
+  int32_t W, rank, sys;
   const char* src;
   int64_t src_off[TT_PEER_MAXW];
   int64_t len[TT_PEER_MAXW];
   char* dst[TT_PEER_MAXW];
   int32_t* flag[TT_PEER_MAXW];
-  int32_t* state;  // [0] epoch, [1 + d] workgroups done for destination d
+  int32_t* state;  // [0] epoch
 };
 
 __global__ void __launch_bounds__(PX_THREADS) peer_put_kernel(PxArgs a) {
   const int d = blockIdx.y;
-  const int tid = threadIdx.x;
-  const int64_t len = a.len[d];
-  const int64_t c0 = (int64_t)blockIdx.x * PX_CHUNK;
-  if (c0 < len) {
-    const char* s = a.src + a.src_off[d];
-    char* t = a.dst[d];
-    uint4 v[PX_UNROLL];
-#pragma unroll
-    for (int u = 0; u < PX_UNROLL; ++u) {
-      const int64_t i = c0 + ((int64_t)u * PX_THREADS + tid) * 16;
-      if (i < len) v[u] = *reinterpret_cast<const uint4*>(s + i);
-    }
-#pragma unroll
-    for (int u = 0; u < PX_UNROLL; ++u) {
-      const int64_t i = c0 + ((int64_t)u * PX_THREADS + tid) * 16;
-      if (i < len) *reinterpret_cast<uint4*>(t + i) = v[u];
-    }
-  }
-  // every wave's stores done and past this agent's caches before the count
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  __syncthreads();
-  if (tid == 0) {
-    int32_t* done = a.state + 1 + d;
-    const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (int)gridDim.x - 1) {
-      __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int e = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-      __hip_atomic_store(a.flag[d], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  const int64_t n = a.len[d] >> 4;  // 16-B units
+  const int64_t i0 = (int64_t)blockIdx.x * (PX_THREADS * PX_UNROLL) + threadIdx.x;
+  if (i0 >= n) return;
+  const uint4* s = reinterpret_cast<const uint4*>(a.src + a.src_off[d]);
+  uint4* t = reinterpret_cast<uint4*>(a.dst[d]);
+  // four independent 16-B loads per lane in flight, then their stores; scalars, not a local array:
+  // the array form was promoted to LDS with every load waited on alone (3.8 against 28.6 us per put
+  // of 8.5 MB, profiles/r05_peer_exchange_notes.log)
+  const int64_t i1 = i0 + PX_THREADS, i2 = i0 + 2 * PX_THREADS, i3 = i0 + 3 * PX_THREADS;
+  uint4 v0 = s[i0], v1, v2, v3;
+  if (i1 < n) v1 = s[i1];
+  if (i2 < n) v2 = s[i2];
+  if (i3 < n) v3 = s[i3];
+  t[i0] = v0;
+  if (i1 < n) t[i1] = v1;
+  if (i2 < n) t[i2] = v2;
+  if (i3 < n) t[i3] = v3;
 }
 
-__global__ void __launch_bounds__(64) peer_wait_kernel(const int32_t* flags, int W, int32_t* state, int32_t* err,
-                                                       int64_t timeout_ticks) {
+// One wave, after the put kernel (whose end made its stores visible): lane d signals peer d, then
+// waits for source d's signal. A release fence + arrival count in every put workgroup instead (the
+// last one signalling) cost 25.6 against 8.8 us per put of that form (profiles/r05_peer_exchange_notes.log).
+__global__ void __launch_bounds__(64) peer_signal_wait_kernel(PxArgs a, const int32_t* flags, int32_t* err,
+                                                              int64_t timeout_ticks) {
   const int s = threadIdx.x;
-  const int e = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const int e = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   int late = 0;
-  if (s < W) {
+  if (s < a.W) {
+    // peers on other devices: release / acquire at system scope; all on this device: agent scope
+    if (a.sys)
+      __hip_atomic_store(a.flag[s], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      __hip_atomic_store(a.flag[s], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flags + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+    while ((a.sys ? __hip_atomic_load(flags + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)
+                  : __hip_atomic_load(flags + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) < e) {
       if ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
         late = 1;
         break;
@@ -86,8 +82,11 @@ __global__ void __launch_bounds__(64) peer_wait_kernel(const int32_t* flags, int
   }
   if (late) __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the peers' blocks visible to the kernels after this one
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  if (s == 0) __hip_atomic_store(state, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.sys)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (s == 0) __hip_atomic_store(a.state, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -146,12 +145,15 @@ int tt_peer_unimport(void* base) {
   return e == hipSuccess ? TT_OK : fail((int)e, std::string("peer_unimport: ") + hipGetErrorString(e));
 }
 
-int tt_peer_put(const tt_peer_put_t* p, void* stream) {
-  if (!p || p->W < 1 || p->W > TT_PEER_MAXW || p->rank < 0 || p->rank >= p->W || !p->src || !p->state)
-    return fail(TT_EINVAL, "peer_put: 1 <= W <= TT_PEER_MAXW, 0 <= rank < W, src and state set");
+int tt_peer_exchange(const tt_peer_put_t* p, const int32_t* flags, int32_t* err, double timeout_s, void* stream) {
+  if (!p || p->W < 1 || p->W > TT_PEER_MAXW || p->rank < 0 || p->rank >= p->W || !p->src || !p->state || !flags ||
+      !err || !(timeout_s > 0))
+    return fail(TT_EINVAL, "peer_exchange: 1 <= W <= TT_PEER_MAXW, 0 <= rank < W, src, state, flags, err set, "
+                           "timeout > 0");
   PxArgs a;
   a.W = p->W;
   a.rank = p->rank;
+  a.sys = p->same_device ? 0 : 1;
   a.src = reinterpret_cast<const char*>(p->src);
   a.state = p->state;
   int64_t most = 0;
@@ -166,22 +168,19 @@ int tt_peer_put(const tt_peer_put_t* p, void* stream) {
     if (a.len[d] < 0 || a.src_off[d] < 0 || (a.len[d] & 15) || (s & 15) ||
         (reinterpret_cast<uintptr_t>(a.dst[d]) & 15) || (a.len[d] && !a.dst[d]) || !a.flag[d] ||
         (reinterpret_cast<uintptr_t>(a.flag[d]) & 3))
-      return fail(TT_EINVAL, "peer_put: blocks must be 16-B aligned multiples of 16 B, every flag word set");
+      return fail(TT_EINVAL, "peer_exchange: blocks must be 16-B aligned multiples of 16 B, every flag word set");
     most = std::max(most, a.len[d]);
   }
-  const int64_t nchunk = std::max<int64_t>(1, ceil_div(most, PX_CHUNK));
-  if (nchunk > INT32_MAX) return fail(TT_EINVAL, "peer_put: block too large");
-  peer_put_kernel<<<dim3((unsigned)nchunk, (unsigned)p->W), dim3(PX_THREADS), 0, as_stream(stream)>>>(a);
-  return check_launch("peer_put");
-}
-
-int tt_peer_wait(const int32_t* flags, int W, int32_t* state, int32_t* err, double timeout_s, void* stream) {
-  if (!flags || !state || !err || W < 1 || W > TT_PEER_MAXW || !(timeout_s > 0))
-    return fail(TT_EINVAL, "peer_wait: flags, state, err set, 1 <= W <= TT_PEER_MAXW, timeout > 0");
+  const int64_t nchunk = ceil_div(most, PX_CHUNK);
+  if (nchunk > INT32_MAX) return fail(TT_EINVAL, "peer_exchange: block too large");
+  if (nchunk > 0) {
+    peer_put_kernel<<<dim3((unsigned)nchunk, (unsigned)p->W), dim3(PX_THREADS), 0, as_stream(stream)>>>(a);
+    if (int rc = check_launch("peer_exchange (put)")) return rc;
+  }
   // s_memrealtime counts at 100 MHz on MI355X
   const int64_t ticks = (int64_t)std::min(timeout_s * 1e8, 9e17);
-  peer_wait_kernel<<<dim3(1), dim3(64), 0, as_stream(stream)>>>(flags, W, state, err, ticks);
-  return check_launch("peer_wait");
+  peer_signal_wait_kernel<<<dim3(1), dim3(64), 0, as_stream(stream)>>>(a, flags, err, ticks);
+  return check_launch("peer_exchange (signal / wait)");
 }
 
 }  // extern "C"

@@ -171,7 +171,7 @@ class PeerComm(TorchComm):
     every rank stores its blocks straight into the peers' receive buffers — allocated here
     (``recv_buffer``, fine-grained device memory) and mapped into every other rank's process with
     hipIpcOpenMemHandle — and signals a flag word per (peer, source); the receiver's wait kernel spins
-    on its W words (csrc/peer.hip). No RCCL kernel runs on the step path, and the exchange is
+    on its W words (csrc/peer.hip: a put kernel, then one wave that signals and waits). No RCCL kernel runs on the step path, and the exchange is
     capturable whatever the process group's backend (gloo included: it only carries the setup).
     The other collectives (capacities, flags, checkpoints) stay torch.distributed. A wait past
     ``timeout_s`` gives up and sets a sticky error word that ``check()`` of the step raises on.
@@ -194,6 +194,21 @@ class PeerComm(TorchComm):
         self._own: List[int] = []
         self._imports: Dict[bytes, int] = {}
         self._puts: Dict[tuple, _lib.PeerPut] = {}
+        # every rank on this one device (world 1, or ranks sharing a GPU): agent-scope signals suffice
+        ident = self._device_identity()
+        idents = [None] * self.world
+        if self.world > 1:
+            dist.all_gather_object(idents, ident, group=self.group)
+        else:
+            idents[0] = ident
+        self.same_device = ident is not None and all(i == ident for i in idents)
+        if os.environ.get("TT_PEER_SYSTEM_SCOPE") == "1":  # measurement: the multi-device signalling
+            self.same_device = False
+
+    def _device_identity(self):
+        p = torch.cuda.get_device_properties(self.device)
+        ident = tuple(str(getattr(p, a, "")) for a in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"))
+        return ident if any(ident) else None  # unknown: treated as different devices (system scope)
 
     def _alloc(self, nbytes: int) -> torch.Tensor:
         lib = _lib.load()
@@ -247,7 +262,7 @@ class PeerComm(TorchComm):
                 self._imports[hs] = p.value
             peers.append((self._imports[hs] + o, b))
         self._bufs[buf.data_ptr()] = {"peers": peers, "flags": raw[body:body + 4 * self.world].view(torch.int32),
-                                      "state": torch.zeros(1 + self.world, dtype=torch.int32, device=self.device),
+                                      "state": torch.zeros(1, dtype=torch.int32, device=self.device),
                                       "raw": raw}
         return buf
 
@@ -274,6 +289,7 @@ class PeerComm(TorchComm):
                 raise _lib.TTError("PeerComm.all_to_all: receive blocks do not match the senders' blocks")
             put = _lib.PeerPut()
             put.W, put.rank, put.src, put.state = W, r, inp.data_ptr(), e["state"].data_ptr()
+            put.same_device = 1 if self.same_device else 0
             o = 0
             for d in range(W):
                 base, body = e["peers"][d]
@@ -283,10 +299,8 @@ class PeerComm(TorchComm):
                 put.flag[d] = base + body + 4 * r
                 o += sizes[d]
             self._puts[key] = put
-        st = stream_handle(out.device)
-        check(_lib.load().tt_peer_put(C.byref(put), st), "peer_put")
-        check(_lib.load().tt_peer_wait(e["flags"].data_ptr(), W, e["state"].data_ptr(), self.err.data_ptr(),
-                                       self.timeout_s, st), "peer_wait")
+        check(_lib.load().tt_peer_exchange(C.byref(put), e["flags"].data_ptr(), self.err.data_ptr(), self.timeout_s,
+                                           stream_handle(out.device)), "peer_exchange")
 
     def close(self) -> None:
         """Unmap the peers' buffers and free this rank's (the buffers from recv_buffer are invalid after)."""
