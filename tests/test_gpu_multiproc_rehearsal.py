@@ -80,3 +80,19 @@ def test_bench_config5_sharded_multiprocess_gloo_rehearsal(world):
     assert d["n_gpus"] == world and d["steps"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
     sh = d["config"]["sharded"]
     assert sh["mode"] == "eager" and sh["collectives_per_step"] == 3
+
+
+def test_bench_gpus2_peer_exchange_rehearsal():
+    """`bench.py --gpus 2 --exchange peer` (the driver's form, gloo rehearsal: ranks sharing the GPU):
+    the sharded step's two exchanges as device-initiated puts into the other process's IPC-mapped
+    buffers, captured into HIP graphs (gloo only carries the setup), flags checked on every rank."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TT_REHEARSE_GLOO="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--exchange", "peer", "--steps", "8", "--warmup", "2",
+           "--batches", "8", "--steps-per-graph", "2", "--workload", "config2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    sh = d["config"]["sharded"]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
+    assert sh["mode"] == "hipgraph" and sh["exchange"].startswith("device-initiated"), sh
