@@ -20,6 +20,7 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $F/bench_driv
 timeout -k 10 300 python bench.py --ids zipf --no-cpu-baseline > $F/bench_idszipf.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --workload config2 --no-cpu-baseline > $F/bench_workloadconfig2.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --sharded --no-cpu-baseline > $F/bench_sharded.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --sharded --exchange peer --no-cpu-baseline > $F/bench_sharded_peer.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --path dropin --no-cpu-baseline > $F/bench_pathdropin.log 2>&1 || exit $?
 timeout -k 10 500 python bench.py --workload config5 --steps 30 --warmup 5 --no-cpu-baseline > $F/bench_workloadconfig5.log 2>&1 || exit $?
 mkdir -p gpurun_out/prof
