@@ -552,10 +552,13 @@ class FusedShardedTwoTowerStep:
         self._layout()
         # ---- buffers
         self.sendA = torch.zeros(self.A_total, dtype=torch.float32, device=dev)
-        # receive buffers from the comm (PeerComm: mapped into every peer for its device-initiated puts)
-        self.recvA = comm.recv_buffer((W * self.Asz[r],), torch.float32, dev)
+        # receive buffers from the comm when it provides them (PeerComm: mapped into every peer for
+        # its device-initiated puts); plain device tensors for any other comm
+        recv = getattr(comm, "recv_buffer", None) or (lambda shape, dtype, device: torch.zeros(shape, dtype=dtype,
+                                                                                              device=device))
+        self.recvA = recv((W * self.Asz[r],), torch.float32, dev)
         self.rows_out = torch.zeros(W * self.RSTR, D, dtype=torch.bfloat16, device=dev)
-        self.rows_in = comm.recv_buffer((W * self.RSTR, D), torch.bfloat16, dev)
+        self.rows_in = recv((W * self.RSTR, D), torch.bfloat16, dev)
         self.pos_in = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
         self.pos_out = torch.full((2, F * B), -1, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(2, dtype=torch.int32, device=dev)  # {overflow, bad key}
