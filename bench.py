@@ -90,8 +90,8 @@ def parse():
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "peer"],
-                    help="sharded single-hot step: the two all-to-alls over RCCL (default) or device-initiated "
-                         "into IPC-mapped peer buffers (sharded.PeerComm)")
+                    help="sharded steps (single-hot and config 5): the all-to-alls over RCCL (default) or "
+                         "device-initiated into IPC-mapped peer buffers (sharded.PeerComm)")
     ap.add_argument("--overlap", action="store_true",
                     help="sharded step: T2 on a parallel graph branch beside exchange A (default: inside launch U, "
                          "one stream; the branch measured slower at world 1, DESIGN.md section 6)")
@@ -556,7 +556,12 @@ def run_multi_kjt(args, world, rank, local_rank):
     N = [num_users, num_items]
     sharding, owners = ["table_wise", "row_wise"], [world - 1, 0]
     dev = torch.device("cuda", local_rank % torch.cuda.device_count())
-    comm = TorchComm(always_collective=True)
+    if args.exchange == "peer":
+        from two_tower_recommender_model_amd.sharded import PeerComm
+
+        comm = PeerComm(device=dev)
+    else:
+        comm = TorchComm(always_collective=True)
     batches = synth_kjt_batches(num_users, num_items, B, maxlen, 4, dev, args.ids, seed=4 * 1000 + 1 + rank)
     need = torch.zeros(1, dtype=torch.int64)
     for v, o, _ in batches:
@@ -566,7 +571,7 @@ def run_multi_kjt(args, world, rank, local_rank):
     cap = -(-int(need) // 8) * 8
     step = FusedShardedKJTStep(comm, N, D, layers, B, dev, cap=cap, sharding=sharding, tw_owners=owners,
                                lr_emb=0.01, lr_dense=0.01, seed=0)
-    graphs = os.environ.get("TT_REHEARSE_GLOO") != "1"
+    graphs = os.environ.get("TT_REHEARSE_GLOO") != "1" or args.exchange == "peer"
     if graphs:
         step.capture_pool(batches)
         run = step.run
@@ -592,6 +597,9 @@ def run_multi_kjt(args, world, rank, local_rank):
     step.check()
     loss = float(step.loss)
     step.release_graphs()
+    if args.exchange == "peer":
+        dist.barrier()  # no rank unmaps a peer's buffer while that peer may still store into it
+        comm.close()
     # SURVEY 8(d) embedding-path bytes per rank and step over the whole step (lookups of this rank's
     # batch, unique rows counted on it): nnz (8 id fwd + 8 id bwd + 4D row) + F B (4 + 8D) + U (8D + 8)
     nnz = sum(v.numel() for v, _, _ in batches) // len(batches)
@@ -609,7 +617,9 @@ def run_multi_kjt(args, world, rank, local_rank):
     info = {"plan": f"users table-wise (rank {world - 1}) + items row-wise", "ids": args.ids, "capacity": cap,
             "exchange_bytes_per_rank": {"A_ids": 4 * step.sendA.numel(), "B_pooled": 4 * step.sendB.numel(),
                                         "C_grads": 4 * step.sendC.numel()},
-            "collectives_per_step": 3, "mode": "hipgraph" if graphs else "eager"}
+            "collectives_per_step": 3, "mode": "hipgraph" if graphs else "eager",
+            "exchange": ("device-initiated puts into IPC-mapped peer buffers (" + comm.memory + " memory)"
+                         if args.exchange == "peer" else "RCCL all_to_all_single")}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
 
 
@@ -1094,7 +1104,7 @@ def main():
             roofline, sharded_info = None, di.get("sharded")
         elif args.workload in MULTIHOT:
             value, ms, loss, sharded_info, roofline = run_multi_kjt(args, world, rank, local_rank)
-            config["parallelism"] = (f"{sharded_info['plan']} + data-parallel towers x{world}: 3 fixed-size RCCL "
+            config["parallelism"] = (f"{sharded_info['plan']} + data-parallel towers x{world}: 3 fixed-size {'device-initiated' if args.exchange == 'peer' else 'RCCL'} "
                                      f"all-to-alls per step (ids, pooled rows, bag gradients), {sharded_info['mode']}")
         else:
             value, ms, loss, sharded_info, roofline = run_multi(args, world, rank, local_rank)

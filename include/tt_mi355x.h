@@ -708,7 +708,7 @@ typedef struct {
   int32_t W, rank;
   const void* src;                 /* this rank's send buffer */
   int64_t src_off[TT_PEER_MAXW];   /* bytes: where destination d's block starts in src */
-  int64_t len[TT_PEER_MAXW];       /* bytes sent to d (multiple of 16; 16-B aligned blocks) */
+  int64_t len[TT_PEER_MAXW];       /* bytes sent to d (multiple of 4, 4-B aligned; 16 B: wide copy) */
   void* dst[TT_PEER_MAXW];         /* d's receive buffer at this rank's slot (mapped address) */
   int32_t* flag[TT_PEER_MAXW];     /* d's flag word for this source (mapped address) */
   int32_t* state;                  /* this rank's epoch word for the exchange (int32) */

@@ -1,7 +1,8 @@
 """Child of tests/test_gpu_sharded_kjt.py::test_sharded_kjt_rccl_world1_graph_equals_eager: the multi-hot
 sharded step with its three all-to-alls on RCCL (a one-rank "nccl" group, collectives forced on),
 captured into HIP graphs over resident batches, equals the same steps run eagerly, bit for bit.
-Prints RCCL-KJT-GRAPH-OK."""
+With TT_KJT_COMM=peer the graphs run on sharded.PeerComm (device-initiated puts) against the eager
+RCCL steps. Prints RCCL-KJT-GRAPH-OK."""
 import os
 import sys
 
@@ -45,7 +46,12 @@ def main():
         a.step(v, o, l)
     torch.cuda.synchronize()
     stage("graphs")
-    b = mk(TorchComm(always_collective=True))
+    peer = os.environ.get("TT_KJT_COMM") == "peer"  # the graphs over the device-initiated exchange
+    if peer:
+        from two_tower_recommender_model_amd.sharded import PeerComm
+
+        pc = PeerComm(device=device)
+    b = mk(pc if peer else TorchComm(always_collective=True))
     b.capture_pool(batches)
     b.run(6)
     torch.cuda.synchronize()
@@ -59,6 +65,8 @@ def main():
     b.release_graphs()
     del a, b
     torch.cuda.synchronize()
+    if peer:
+        pc.close()
     dist.destroy_process_group()
     print("RCCL-KJT-GRAPH-OK", flush=True)
     return 0

@@ -96,3 +96,18 @@ def test_bench_gpus2_peer_exchange_rehearsal():
     sh = d["config"]["sharded"]
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
     assert sh["mode"] == "hipgraph" and sh["exchange"].startswith("device-initiated"), sh
+
+
+def test_bench_config5_peer_exchange_rehearsal():
+    """`bench.py --gpus 2 --workload config5 --exchange peer` (gloo rehearsal, ranks sharing the GPU): the
+    multi-hot sharded step's three exchanges as device-initiated puts, captured into HIP graphs."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TT_REHEARSE_GLOO="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--workload", "config5", "--exchange", "peer", "--steps", "4",
+           "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    sh = d["config"]["sharded"]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
+    assert sh["mode"] == "hipgraph" and sh["exchange"].startswith("device-initiated"), sh

@@ -340,3 +340,14 @@ def test_sharded_kjt_rccl_world1_graph_equals_eager(device):
     from child_util import run_child
 
     run_child(["tests/rccl_kjt_graph_check.py"], "RCCL-KJT-GRAPH-OK", timeout=300)
+
+
+def test_sharded_kjt_peer_world1_graph_equals_rccl_eager(device):
+    """The three exchanges on the device-initiated PeerComm, captured, against the eager RCCL steps, bit
+    for bit (the same child with TT_KJT_COMM=peer)."""
+    import os
+
+    from child_util import run_child
+
+    run_child(["tests/rccl_kjt_graph_check.py"], "RCCL-KJT-GRAPH-OK", timeout=300,
+              env=dict(os.environ, TT_KJT_COMM="peer"))

@@ -23,7 +23,7 @@ namespace {
 
 constexpr int PX_THREADS = 256;
 constexpr int PX_UNROLL = 4;  // 16-B units per lane
-constexpr int64_t PX_CHUNK = (int64_t)PX_THREADS * 16 * PX_UNROLL;  // bytes per workgroup (16 KB)
+constexpr int64_t PX_CHUNK = (int64_t)PX_THREADS * 16 * PX_UNROLL;  // bytes per workgroup (16 KB; 4 KB narrow)
 
 struct PxArgs {
   int32_t W, rank, sys;
@@ -35,18 +35,20 @@ struct PxArgs {
   int32_t* state;  // [0] epoch
 };
 
+// V = uint4 (every block 16-B aligned, the sharded steps' usual layout) or uint32_t (4-B blocks)
+template <typename V>
 __global__ void __launch_bounds__(PX_THREADS) peer_put_kernel(PxArgs a) {
   const int d = blockIdx.y;
-  const int64_t n = a.len[d] >> 4;  // 16-B units
+  const int64_t n = a.len[d] / (int64_t)sizeof(V);
   const int64_t i0 = (int64_t)blockIdx.x * (PX_THREADS * PX_UNROLL) + threadIdx.x;
   if (i0 >= n) return;
-  const uint4* s = reinterpret_cast<const uint4*>(a.src + a.src_off[d]);
-  uint4* t = reinterpret_cast<uint4*>(a.dst[d]);
-  // four independent 16-B loads per lane in flight, then their stores; scalars, not a local array:
+  const V* s = reinterpret_cast<const V*>(a.src + a.src_off[d]);
+  V* t = reinterpret_cast<V*>(a.dst[d]);
+  // four independent loads per lane in flight, then their stores; scalars, not a local array:
   // the array form was promoted to LDS with every load waited on alone (3.8 against 28.6 us per put
   // of 8.5 MB, profiles/r05_peer_exchange_notes.log)
   const int64_t i1 = i0 + PX_THREADS, i2 = i0 + 2 * PX_THREADS, i3 = i0 + 3 * PX_THREADS;
-  uint4 v0 = s[i0], v1, v2, v3;
+  V v0 = s[i0], v1, v2, v3;
   if (i1 < n) v1 = s[i1];
   if (i2 < n) v2 = s[i2];
   if (i3 < n) v3 = s[i3];
@@ -159,6 +161,7 @@ int tt_peer_exchange(const tt_peer_put_t* p, const int32_t* flags, int32_t* err,
   a.src = reinterpret_cast<const char*>(p->src);
   a.state = p->state;
   int64_t most = 0;
+  bool wide = true;
   for (int d = 0; d < TT_PEER_MAXW; ++d) {
     const bool live = d < p->W;
     a.src_off[d] = live ? p->src_off[d] : 0;
@@ -167,16 +170,21 @@ int tt_peer_exchange(const tt_peer_put_t* p, const int32_t* flags, int32_t* err,
     a.flag[d] = live ? p->flag[d] : nullptr;
     if (!live) continue;
     const uintptr_t s = reinterpret_cast<uintptr_t>(a.src) + (uintptr_t)a.src_off[d];
-    if (a.len[d] < 0 || a.src_off[d] < 0 || (a.len[d] & 15) || (s & 15) ||
-        (reinterpret_cast<uintptr_t>(a.dst[d]) & 15) || (a.len[d] && !a.dst[d]) || !a.flag[d] ||
-        (reinterpret_cast<uintptr_t>(a.flag[d]) & 3))
-      return fail(TT_EINVAL, "peer_exchange: blocks must be 16-B aligned multiples of 16 B, every flag word set");
+    const uintptr_t t = reinterpret_cast<uintptr_t>(a.dst[d]);
+    if (a.len[d] < 0 || a.src_off[d] < 0 || (a.len[d] & 3) || (s & 3) || (t & 3) || (a.len[d] && !a.dst[d]) ||
+        !a.flag[d] || (reinterpret_cast<uintptr_t>(a.flag[d]) & 3))
+      return fail(TT_EINVAL, "peer_exchange: blocks must be 4-B aligned multiples of 4 B, every flag word set");
+    if ((a.len[d] & 15) || (s & 15) || (t & 15)) wide = false;
     most = std::max(most, a.len[d]);
   }
-  const int64_t nchunk = ceil_div(most, PX_CHUNK);
+  const int64_t nchunk = ceil_div(most, wide ? PX_CHUNK : PX_CHUNK / 4);
   if (nchunk > INT32_MAX) return fail(TT_EINVAL, "peer_exchange: block too large");
   if (nchunk > 0) {
-    peer_put_kernel<<<dim3((unsigned)nchunk, (unsigned)p->W), dim3(PX_THREADS), 0, as_stream(stream)>>>(a);
+    const dim3 grid((unsigned)nchunk, (unsigned)p->W);
+    if (wide)
+      peer_put_kernel<uint4><<<grid, dim3(PX_THREADS), 0, as_stream(stream)>>>(a);
+    else
+      peer_put_kernel<uint32_t><<<grid, dim3(PX_THREADS), 0, as_stream(stream)>>>(a);
     if (int rc = check_launch("peer_exchange (put)")) return rc;
   }
   // s_memrealtime counts at 100 MHz on MI355X

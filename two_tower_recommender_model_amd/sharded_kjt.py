@@ -164,11 +164,14 @@ class FusedShardedKJTStep:
         self.prows = -(-P // FD)
         self.strideC = (B + self.prows) * FD
         self.sendA = torch.zeros(W * self.strideA, dtype=torch.int32, device=dev)
-        self.recvA = torch.zeros_like(self.sendA)
+        # receive buffers from the comm when it provides them (sharded.PeerComm: IPC-mapped for its puts)
+        recv = getattr(comm, "recv_buffer", None) or (lambda shape, dtype, device: torch.zeros(shape, dtype=dtype,
+                                                                                              device=device))
+        self.recvA = recv((W * self.strideA,), torch.int32, dev)
         self.sendB = torch.zeros(W * self.strideB, dtype=torch.float32, device=dev)
-        self.recvB = torch.zeros_like(self.sendB)
+        self.recvB = recv((W * self.strideB,), torch.float32, dev)
         self.sendC = torch.zeros(W * self.strideC, dtype=torch.float32, device=dev)
-        self.recvC = torch.zeros_like(self.sendC)
+        self.recvC = recv((W * self.strideC,), torch.float32, dev)
         self.flags = torch.zeros(2, dtype=torch.int32, device=dev)  # {over capacity, id out of range}
         lib = _lib.load()
         self.route_ws = torch.empty(max(256, lib.tt_kjt_route_workspace_bytes(F, B, W)), dtype=torch.uint8, device=dev)
@@ -323,9 +326,15 @@ class FusedShardedKJTStep:
     def check(self, collective: bool = True) -> None:
         """Raise (on every rank) if a destination block overflowed or an id was out of range."""
         f = self.flags.clone()
+        perr = getattr(self.comm, "err", None)  # PeerComm: a wait that timed out
+        if perr is not None:
+            f = torch.cat([f, perr])
         if collective:
             self.comm.all_reduce_max_(f)
         f = f.cpu().tolist()
+        if len(f) > 2 and f[2]:
+            raise _lib.TTError("sharded KJT step: a device-initiated exchange timed out waiting for a peer: results "
+                               "are invalid")
         if f[0]:
             raise _lib.TTError(f"sharded KJT step: a destination block exceeded its capacity {self.cap}: results are "
                                "invalid; raise `cap`")
