@@ -89,9 +89,10 @@ def parse():
                     help="multi-hot workloads: group each batch inside its own step instead of one step ahead")
     ap.add_argument("--sharded", action="store_true",
                     help="run the sharded (multi-GPU) step even at N = 1 (under torch.distributed.run)")
-    ap.add_argument("--exchange", default="rccl", choices=["rccl", "peer"],
-                    help="sharded steps (single-hot and config 5): the all-to-alls over RCCL (default) or "
-                         "device-initiated into IPC-mapped peer buffers (sharded.PeerComm)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "rccl", "peer"],
+                    help="sharded steps (single-hot and config 5): auto (default) = device-initiated into "
+                         "IPC-mapped peer buffers (sharded.PeerComm) when its startup self-test passes on every "
+                         "rank, else RCCL; rccl = all_to_all_single; peer = PeerComm or fail")
     ap.add_argument("--overlap", action="store_true",
                     help="sharded step: T2 on a parallel graph branch beside exchange A (default: inside launch U, "
                          "one stream; the branch measured slower at world 1, DESIGN.md section 6)")
@@ -548,7 +549,7 @@ def run_multi_kjt(args, world, rank, local_rank):
     RCCL), one HIP graph per resident batch (eager under TT_REHEARSE_GLOO). B = 16,384 bags per
     feature and rank, bags of Uniform{1..39} ids. Capacity: the most ids any rank's resident batch
     sends to one destination (all-reduced)."""
-    from two_tower_recommender_model_amd.sharded import TorchComm
+    from two_tower_recommender_model_amd.sharded import PeerComm, exchange_comm
     from two_tower_recommender_model_amd.sharded_kjt import FusedShardedKJTStep, route_counts
 
     num_users, num_items, D, B, layers = WORKLOADS[args.workload]
@@ -556,12 +557,8 @@ def run_multi_kjt(args, world, rank, local_rank):
     N = [num_users, num_items]
     sharding, owners = ["table_wise", "row_wise"], [world - 1, 0]
     dev = torch.device("cuda", local_rank % torch.cuda.device_count())
-    if args.exchange == "peer":
-        from two_tower_recommender_model_amd.sharded import PeerComm
-
-        comm = PeerComm(device=dev)
-    else:
-        comm = TorchComm(always_collective=True)
+    comm, xdesc = exchange_comm(args.exchange, device=dev)
+    peer = isinstance(comm, PeerComm)
     batches = synth_kjt_batches(num_users, num_items, B, maxlen, 4, dev, args.ids, seed=4 * 1000 + 1 + rank)
     need = torch.zeros(1, dtype=torch.int64)
     for v, o, _ in batches:
@@ -571,7 +568,7 @@ def run_multi_kjt(args, world, rank, local_rank):
     cap = -(-int(need) // 8) * 8
     step = FusedShardedKJTStep(comm, N, D, layers, B, dev, cap=cap, sharding=sharding, tw_owners=owners,
                                lr_emb=0.01, lr_dense=0.01, seed=0)
-    graphs = os.environ.get("TT_REHEARSE_GLOO") != "1" or args.exchange == "peer"
+    graphs = os.environ.get("TT_REHEARSE_GLOO") != "1" or peer
     if graphs:
         step.capture_pool(batches)
         run = step.run
@@ -597,7 +594,7 @@ def run_multi_kjt(args, world, rank, local_rank):
     step.check()
     loss = float(step.loss)
     step.release_graphs()
-    if args.exchange == "peer":
+    if peer:
         dist.barrier()  # no rank unmaps a peer's buffer while that peer may still store into it
         comm.close()
     # SURVEY 8(d) embedding-path bytes per rank and step over the whole step (lookups of this rank's
@@ -617,9 +614,7 @@ def run_multi_kjt(args, world, rank, local_rank):
     info = {"plan": f"users table-wise (rank {world - 1}) + items row-wise", "ids": args.ids, "capacity": cap,
             "exchange_bytes_per_rank": {"A_ids": 4 * step.sendA.numel(), "B_pooled": 4 * step.sendB.numel(),
                                         "C_grads": 4 * step.sendC.numel()},
-            "collectives_per_step": 3, "mode": "hipgraph" if graphs else "eager",
-            "exchange": ("device-initiated puts into IPC-mapped peer buffers (" + comm.memory + " memory)"
-                         if args.exchange == "peer" else "RCCL all_to_all_single")}
+            "collectives_per_step": 3, "mode": "hipgraph" if graphs else "eager", "exchange": xdesc}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
 
 
@@ -924,18 +919,14 @@ def run_multi(args, world, rank, local_rank):
     collectives inside (eager launches if capture is refused). Segment capacities are sized from the
     resident batches (max over batches and ranks), so no timed step can overflow; the sticky
     overflow / bad-key flags are all-reduced and checked before and after the timed region."""
-    from two_tower_recommender_model_amd.sharded import (FusedShardedTwoTowerStep, TorchComm,
-                                                         capture_pool_or_eager, default_capacity, segment_counts)
+    from two_tower_recommender_model_amd.sharded import (FusedShardedTwoTowerStep, PeerComm, capture_pool_or_eager,
+                                                         default_capacity, exchange_comm, segment_counts)
 
     N, Fq, D, B, layers, sharding, owners, ids, seed, plan = sharded_spec(args, world)
     F = len(N)
     dev = torch.device("cuda", local_rank % torch.cuda.device_count())  # (rehearsal: ranks may share one GPU)
-    if args.exchange == "peer":
-        from two_tower_recommender_model_amd.sharded import PeerComm
-
-        comm = PeerComm(device=dev)
-    else:
-        comm = TorchComm(always_collective=True)
+    comm, xdesc = exchange_comm(args.exchange, device=dev)
+    peer = isinstance(comm, PeerComm)
     k = args.steps_per_graph or 8
     nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k
     batches = synth_cols(N, B, nb, dev, ids, seed=seed * 1000 + 1 + rank)
@@ -954,8 +945,7 @@ def run_multi(args, world, rank, local_rank):
     step.step()  # creates the RCCL communicators before any capture
     # gloo collectives (TT_REHEARSE_GLOO, testing only) are not capturable: eager steps
     # (the device-initiated exchange is capturable whatever the backend: gloo only carries its setup)
-    mode = capture_pool_or_eager(step, batches, k, allow_capture=os.environ.get("TT_REHEARSE_GLOO") != "1" or
-                                 args.exchange == "peer")
+    mode = capture_pool_or_eager(step, batches, k, allow_capture=os.environ.get("TT_REHEARSE_GLOO") != "1" or peer)
 
     def run(n):
         if mode == "eager":
@@ -978,7 +968,7 @@ def run_multi(args, world, rank, local_rank):
     loss = float(step.loss)
     step.release_graphs()  # before the process group is destroyed
     r = step.rank
-    if args.exchange == "peer":
+    if peer:
         dist.barrier()  # no rank unmaps a peer's buffer while that peer may still store into it
         comm.close()
     # SURVEY 8(d) embedding-path bytes per rank and step over the whole step's time (no per-launch
@@ -998,8 +988,7 @@ def run_multi(args, world, rank, local_rank):
             "exchange_A_bytes_sent": 4 * step.A_total,
             "exchange_B_bytes_sent": 2 * D * world * step.S[r],
             "collectives_per_step": 2, "mode": mode,
-            "exchange": ("device-initiated puts into IPC-mapped peer buffers (" + comm.memory + " memory)"
-                         if args.exchange == "peer" else "RCCL all_to_all_single"),
+            "exchange": xdesc,
             "overlap": "T2 (tower weight gradients) on a parallel graph branch beside exchange A + the owner's "
                        "update" if step.overlap else "none (one stream)"}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
@@ -1104,12 +1093,14 @@ def main():
             roofline, sharded_info = None, di.get("sharded")
         elif args.workload in MULTIHOT:
             value, ms, loss, sharded_info, roofline = run_multi_kjt(args, world, rank, local_rank)
-            config["parallelism"] = (f"{sharded_info['plan']} + data-parallel towers x{world}: 3 fixed-size {'device-initiated' if args.exchange == 'peer' else 'RCCL'} "
+            xk = "RCCL" if sharded_info["exchange"].startswith("RCCL") else "device-initiated"
+            config["parallelism"] = (f"{sharded_info['plan']} + data-parallel towers x{world}: 3 fixed-size {xk} "
                                      f"all-to-alls per step (ids, pooled rows, bag gradients), {sharded_info['mode']}")
         else:
             value, ms, loss, sharded_info, roofline = run_multi(args, world, rank, local_rank)
+            xk = "RCCL" if sharded_info["exchange"].startswith("RCCL") else "device-initiated"
             config["parallelism"] = (f"{sharded_info['plan']} sharded tables + data-parallel towers x{world}: pipelined, "
-                                     f"2 {'device-initiated' if args.exchange == 'peer' else 'RCCL'} all-to-alls per "
+                                     f"2 {xk} all-to-alls per "
                                      f"step ([grad rows | tower grad | next ids], next rows), "
                                      f"{sharded_info['mode']}")
         cpu, steps_run = None, args.steps

@@ -3,7 +3,9 @@
  * the two-tower training step of alexmillerdb/two_tower_recommender_model.
  *
  * Every entry point takes raw device pointers, sizes and a hipStream_t (passed as void*), is
- * asynchronous on that stream, never allocates, frees or synchronises, and returns 0 on success
+ * asynchronous on that stream, never allocates, frees or synchronises (the one exception: the
+ * device-initiated exchange's SETUP calls tt_peer_alloc / _free / _export / _import / _unimport,
+ * which allocate, map and synchronise; called once per buffer at setup, never per step), and returns 0 on success
  * or a non-zero status (a hipError_t value, or one of the TT_E* codes below). The message of the
  * last failure on the calling thread is returned by tt_last_error_string(). No C++ exception
  * crosses this boundary. The caller owns every buffer, including workspaces (size queries first).
@@ -55,8 +57,29 @@ extern "C" {
 /* 2: tt_tower_shape_t._pad became `flags`; the 12 role-combination exports became tt_launch
  * 3: the measured-and-rejected fused-T3 forms removed (tt_tower_fwd_bwd_gather_update_t3,
  *    tt_tower_fwd_bwd_indexed2_bf16_t3, tt_tower_update_lazy, tt_tower_t3_fuse_supported,
- *    tt_tower_counter_offset; the WGRAD | INSERT | ADAGRAD | UPDATE launch plan) */
-#define TT_ABI_VERSION 3
+ *    tt_tower_counter_offset; the WGRAD | INSERT | ADAGRAD | UPDATE launch plan)
+ * 4: direct stores into the peers' receive buffers (tt_peer_direct_t): tt_tower_fwd_bwd_indexed2_bf16
+ *    gained its `direct` argument, tt_gather_role_t its `direct` field (last) */
+#define TT_ABI_VERSION 4
+
+/* ---- device-initiated exchange: the producer stores straight into the peers' buffers ------------
+ * A producer of an all-to-all's send buffer (the sharded step's T1 for exchange A, the owner's
+ * gather for exchange B) given a tt_peer_direct_t writes each unit (row) of destination block d at
+ * row0[d] + (row - first_row[d]) * row_bytes — destination d's receive buffer as mapped into this
+ * process (tt_peer_import) — instead of into the send buffer; block d holds rows [first_row[d],
+ * first_row[d + 1]). The copy fields name further bytes (the exchange's non-row region) that the
+ * producer copies to each destination beside its rows. Only the exchange's signal / wait then runs
+ * (tt_peer_exchange with every len 0). NULL: the send buffer is written as before. */
+#define TT_PEER_MAXW 16
+typedef struct {
+  int32_t W;                             /* destination blocks, 1..TT_PEER_MAXW */
+  int32_t _pad;
+  int64_t first_row[TT_PEER_MAXW];       /* ascending; first_row[0] = 0 */
+  void* row0[TT_PEER_MAXW];              /* mapped address of row first_row[d] at destination d */
+  const void* copy_src[TT_PEER_MAXW];    /* 16-B aligned; NULL / copy_len 0: nothing to copy */
+  void* copy_dst[TT_PEER_MAXW];          /* 16-B aligned mapped address at destination d */
+  int64_t copy_len[TT_PEER_MAXW];        /* bytes, a multiple of 16 */
+} tt_peer_direct_t;
 
 /* status codes (besides hipError_t values, which are all < 1000) */
 #define TT_OK 0
@@ -484,12 +507,15 @@ int tt_shard_gather_segs_bf16(const float* weights, const tt_table_meta_t* table
                               size_t dedup_ws_bytes, int64_t dedup_max_lookups, void* stream);
 /* T1 of the pipelined sharded step: tt_tower_fwd_bwd_indexed_bf16 with the dX row of (tower t,
  * bag m) written at row pos_out[t][m] (units of in_dim floats) of grad_rows_out[t] — the gradient
- * region of exchange A's send buffer — instead of at its input row. */
+ * region of exchange A's send buffer — instead of at its input row. direct (nullable, ABI 4): that
+ * row goes to its destination's receive buffer instead (row units of in_dim floats, rows counted
+ * from grad_rows_out[0] == grad_rows_out[1]), and the copy fields' bytes (exchange A's key region)
+ * travel beside them. */
 int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
                                    const int32_t* const* pos_out, const void* const* rows_in,
                                    float* const* grad_rows_out, const float* params, const void* labels,
                                    int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
-                                   void* stream);
+                                   const tt_peer_direct_t* direct, void* stream);
 /* T1 of the pipelined sharded step with SEVERAL single-hot features per tower (BASELINE configs 3
  * and 4: 8 table-wise features per tower, 1024-wide tower inputs; TorchRec KeyedTensor slices
  * concatenated per tower, 03_model_training.py:420-436, generalised as in
@@ -600,7 +626,8 @@ typedef struct {
   int32_t replicated;      /* 1: no Adam; gradient x scale to base + offsets[q], q < copies <= 16 */
   int32_t copies;
   float* base;
-  const int64_t* offsets;  /* host array, floats */
+  const int64_t* offsets;  /* host array, floats (any flat address: a direct exchange points copy q
+                              into destination q's mapped receive buffer) */
   float scale;
 } tt_update_role_t;
 
@@ -666,6 +693,8 @@ typedef struct {
   void* dedup_ws;
   size_t dedup_ws_bytes;
   int64_t dedup_max_lookups;
+  const tt_peer_direct_t* direct; /* nullable (ABI 4): source s's rows to row0[s] + j rows (first_row[s] =
+                                     s * out_stride); the copy fields are not used */
 } tt_gather_role_t;
 
 typedef struct {
@@ -693,15 +722,17 @@ int tt_adam_step(float* params, const float* grads, float* exp_avg, float* exp_a
                  float lr, float beta1, float beta2, float eps, float weight_decay,
                  int64_t* step_state, void* stream);
 
-/* ---- device-initiated fixed-block exchange (opt-in, sharded.PeerComm) ---------------------------
+/* ---- device-initiated fixed-block exchange (sharded.PeerComm; the sharded steps' N > 1 default) -----
  * Replaces dist.all_to_all_single on the sharded step's data path: the all-to-alls TorchRec's
  * ShardedEmbeddingBagCollection input_dist / output_dist issue under DistributedModelParallel
  * (03_model_training.py:812-815) and DDP's gradient all-reduce of the towers (:812), both reached
  * through TrainPipelineSparseDist.progress (:648). Each rank stores its blocks straight into every
  * peer's receive buffer (mapped with hipIpcOpenMemHandle) and signals one flag word per (peer,
- * source); the receiver waits on its W flag words. Setup calls (alloc / export / import) are the
- * only entry points of this library that allocate or synchronise. */
-#define TT_PEER_MAXW 16
+ * source); the receiver waits on its W flag words.
+ * SETUP ONLY: tt_peer_alloc / tt_peer_free / tt_peer_export / tt_peer_import / tt_peer_unimport
+ * allocate (hipExtMallocWithFlags), map (hipIpcOpenMemHandle) and synchronise — the only entry
+ * points of this library that do; the caller runs them once per receive buffer, before any step,
+ * never inside a graph capture. tt_peer_exchange is asynchronous like every compute entry point. */
 #define TT_PEER_HANDLE_BYTES 64
 
 typedef struct {
@@ -716,7 +747,8 @@ typedef struct {
   int32_t _pad;
 } tt_peer_put_t;
 
-/* fine-grained device memory, zeroed (hipExtMallocWithFlags(hipDeviceMallocFinegrained)) */
+/* SETUP: fine-grained device memory, zeroed (hipExtMallocWithFlags(hipDeviceMallocFinegrained),
+ * hipMemset, hipDeviceSynchronize) */
 int tt_peer_alloc(size_t bytes, void** out);
 int tt_peer_free(void* p);
 /* IPC handle (TT_PEER_HANDLE_BYTES) of the allocation holding p, and p's offset in it */
@@ -725,7 +757,8 @@ int tt_peer_import(const void* handle, void** base);
 int tt_peer_unimport(void* base);
 /* block d of src -> dst[d]; then flag[d] = epoch + 1 (release, system scope) and a wait until
  * flags[0..W) >= epoch + 1 (acquire, system scope), then epoch += 1. A wait longer than timeout_s
- * gives up and sets *err = 1 (sticky; the exchange's data is then invalid). Two kernels. */
+ * gives up and sets *err = 1 (sticky; the exchange's data is then invalid). Two kernels; one (the
+ * signal / wait) when every len is 0 — the producers stored the data (tt_peer_direct_t). */
 int tt_peer_exchange(const tt_peer_put_t* p, const int32_t* flags, int32_t* err, double timeout_s, void* stream);
 
 #ifdef __cplusplus

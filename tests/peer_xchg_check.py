@@ -42,6 +42,9 @@ def main():
     cap = 2048  # per (owner, feature) segment: >= the ~B / W + noise any batch sends one owner
     stage("peer comm")
     pc = PeerComm(timeout_s=5.0, device=device)
+    ok, why = pc.self_test()  # the startup check exchange_comm runs before trusting the protocol
+    print(f"rank {r}: self-test ok {ok} ({why}), same_device {pc.same_device}", flush=True)
+    assert ok, why
     a = FusedShardedTwoTowerStep(pc, N, D, [128, 64], B, device, full_tables=full, capacity=cap)
     ref_comm = TorchComm() if launched else ThreadComm.group(1)[0]
     b = FusedShardedTwoTowerStep(ref_comm, N, D, [128, 64], B, device, full_tables=full, capacity=cap)

@@ -38,7 +38,7 @@ def test_every_declared_symbol_exported(lib):
     assert not extra, f"exported but not declared in the header: {extra}"
     assert sorted(_lib.SIGNATURES) == declared
     assert lib.tt_num_entry_points() == len(_lib.COMPUTE_ENTRY_POINTS)
-    assert lib.tt_abi_version() == 3
+    assert lib.tt_abi_version() == 4
 
 
 def test_launch_plan_layout_matches_the_header(tmp_path):
@@ -51,7 +51,8 @@ def test_launch_plan_layout_matches_the_header(tmp_path):
     structs = {"tt_launch_plan_t": _lib.LaunchPlan, "tt_wgrad_role_t": _lib.WgradRole,
                "tt_update_role_t": _lib.UpdateRole, "tt_insert_role_t": _lib.InsertRole,
                "tt_resolve_role_t": _lib.ResolveRole, "tt_adagrad_role_t": _lib.AdagradRole,
-               "tt_route_role_t": _lib.RouteRole, "tt_gather_role_t": _lib.GatherRole, "tt_peer_put_t": _lib.PeerPut}
+               "tt_route_role_t": _lib.RouteRole, "tt_gather_role_t": _lib.GatherRole, "tt_peer_put_t": _lib.PeerPut,
+               "tt_peer_direct_t": _lib.PeerDirect}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "tt_mi355x.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} sizeof %zu\\n", sizeof({cname}));')

@@ -86,3 +86,83 @@ def test_torch_and_thread_comms_give_plain_receive_buffers():
     assert b.shape == (4, 2) and not b.any()
     th = sharded.ThreadComm.group(1)[0]
     assert th.recv_buffer((3,), torch.bfloat16, "cpu").dtype == torch.bfloat16
+
+
+def test_stored_exchange_signals_only(monkeypatch):
+    """stored=True (the producers wrote the blocks themselves): a descriptor of the same flags and
+    destinations with every length 0 — tt_peer_exchange then runs only its signal / wait kernel."""
+    W, r = 2, 1
+    sizes = [8, 4]
+    inp = torch.zeros(sum(sizes))
+    out = torch.zeros(W * sizes[r])
+    peers = [(1 << 20, 4096), (2 << 20, 8192)]
+    pc, rec = _comm(monkeypatch, W, r, peers, out)
+    pc.all_to_all(out, inp, out_splits=[sizes[r]] * W, in_splits=sizes, stored=True)
+    (p,) = rec.puts
+    assert [p.len[d] for d in range(W)] == [0, 0]
+    assert [p.flag[d] for d in range(W)] == [peers[d][0] + peers[d][1] + 4 * r for d in range(W)]
+    pc.all_to_all(out, inp, out_splits=[sizes[r]] * W, in_splits=sizes)
+    assert rec.puts[1].len[0] == sizes[0] * 4 and len(pc._puts) == 2  # put and signal-only cached apart
+
+
+def test_direct_descriptor_addresses_rows_and_copies(monkeypatch):
+    """PeerComm.direct: block d of the send buffer starts at unit first_row[d] and lands at peer d's
+    buffer at this rank's slot (row0[d]); the copy range of block d goes to the same place + lo."""
+    W, r, D = 3, 2, 4
+    rows = [16, 8, 24]  # units (rows of D floats) per destination block
+    inp = torch.zeros(sum(rows), D)
+    out = torch.zeros(W * rows[r], D)
+    peers = [(1 << 24, 65536), (2 << 24, 65536), (3 << 24, 65536)]
+    pc, _ = _comm(monkeypatch, W, r, peers, out)
+    rowb = 4 * D
+    x = pc.direct(out, inp, rowb, out_splits=[rows[r]] * W, in_splits=rows,
+                  copy=[(rowb * (n - 2), rowb * n) for n in rows])  # the last two rows of each block
+    assert x.W == W
+    o = 0
+    for d in range(W):
+        assert x.first_row[d] == o
+        assert x.row0[d] == peers[d][0] + r * rows[d] * rowb
+        assert x.copy_src[d] == inp.data_ptr() + (o + rows[d] - 2) * rowb
+        assert x.copy_dst[d] == x.row0[d] + (rows[d] - 2) * rowb and x.copy_len[d] == 2 * rowb
+        o += rows[d]
+    with pytest.raises(_lib.TTError, match="16-B aligned"):
+        pc.direct(out, inp, rowb, out_splits=[rows[r]] * W, in_splits=rows, copy=[(4, 16)] * W)
+    with pytest.raises(_lib.TTError, match="do not match"):
+        pc.block_dst(out, inp, out_splits=[rows[r] + 1] * W, in_splits=rows)
+
+
+def test_exchange_comm_falls_back_to_rccl_when_the_self_test_fails(monkeypatch):
+    """exchange_comm("auto"): a failed PeerComm self-test (on any rank: the result is agreed on)
+    gives TorchComm on every rank; "peer" raises instead; "rccl" never builds a PeerComm."""
+    made = []
+
+    class FakePeer:
+        def __init__(self, group=None, device=None):
+            made.append(self)
+            self.closed = False
+            self.memory = "fine-grained"
+
+        def self_test(self):
+            return False, "rank 1: round 0: 3 of 64 received words differ"
+
+        def close(self):
+            self.closed = True
+
+    class FakeTorch:
+        def __init__(self, group=None, always_collective=False):
+            self.always = always_collective
+
+    monkeypatch.setattr(sharded, "PeerComm", FakePeer)
+    monkeypatch.setattr(sharded, "TorchComm", FakeTorch)
+    monkeypatch.setattr(sharded.dist, "get_rank", lambda group=None: 0)
+    comm, desc = sharded.exchange_comm("auto")
+    assert isinstance(comm, FakeTorch) and comm.always and made[-1].closed
+    assert desc.startswith("RCCL") and "differ" in desc
+    with pytest.raises(_lib.TTError, match="self-test failed"):
+        sharded.exchange_comm("peer")
+    n = len(made)
+    comm, desc = sharded.exchange_comm("rccl")
+    assert isinstance(comm, FakeTorch) and len(made) == n
+    FakePeer.self_test = lambda self: (True, "")
+    comm, desc = sharded.exchange_comm("auto")
+    assert isinstance(comm, FakePeer) and desc.startswith("device-initiated")

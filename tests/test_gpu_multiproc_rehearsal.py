@@ -20,7 +20,8 @@ def test_bench_multiprocess_gloo_rehearsal(world):
     env = dict(os.environ, TT_REHEARSE_GLOO="1", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(29517 + world), "bench.py", "--gpus", str(world),
-           "--workload", "config2", "--steps", "4", "--warmup", "2", "--batches", "8", "--no-cpu-baseline"]
+           "--workload", "config2", "--steps", "4", "--warmup", "2", "--batches", "8", "--no-cpu-baseline",
+           "--exchange", "rccl"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
@@ -48,6 +49,32 @@ def test_bench_gpus2_self_launch_as_driver_runs_it():
     assert d["n_gpus"] == 2 and d["steps"] == 4 and d["value"] > 0
     assert d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]
     assert d["config"]["sharded"]["plan"].startswith("table-wise")
+    # the default exchange: the device-initiated one after its self-test, captured into graphs
+    assert d["config"]["sharded"]["exchange"].startswith("device-initiated"), d["config"]["sharded"]
+    assert d["config"]["sharded"]["mode"] == "hipgraph"
+
+
+def test_bench_gpus2_northstar_table_wise_as_driver_runs_it():
+    """The driver's N = 2 line on the north star itself (`bench.py --gpus 2`, defaults: 100M x 50M
+    tables, D 128, B 8192 per rank): table-wise plan (users on rank 0, items on rank 1, 76.8 GB on the
+    shared GPU), the default exchange (device-initiated after its self-test), HIP graphs, flags
+    checked on both ranks, one JSON line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TT_REHEARSE_GLOO="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "16", "--warmup", "4", "--batches", "16",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    print(lines[0][:600], flush=True)
+    sh = d["config"]["sharded"]
+    assert d["n_gpus"] == 2 and d["config"]["per_gpu_batch"] == 8192 and d["config"]["emb_dim"] == 128
+    assert d["config"]["workload"].startswith("northstar")
+    assert sh["plan"].startswith("table-wise") and sh["mode"] == "hipgraph", sh
+    assert sh["exchange"].startswith("device-initiated"), sh
+    assert d["value"] > 0 and d["loss"] == d["loss"]
 
 
 def test_bench_dropin_n2_rehearsal():
@@ -73,7 +100,7 @@ def test_bench_config5_sharded_multiprocess_gloo_rehearsal(world):
     env = dict(os.environ, TT_REHEARSE_GLOO="1", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(29537 + world), "bench.py", "--gpus", str(world),
-           "--workload", "config5", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+           "--workload", "config5", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--exchange", "rccl"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])

@@ -18,6 +18,25 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / "libtt_mi355x.so"
 # measurement scripts only: an experiment build (TT_EXPERIMENTS=1, built with
 # `python -m two_tower_recommender_model_amd.build --experiments`) sits beside the release library
 EXP_LIB_PATH = Path(__file__).resolve().parent / "lib_exp" / "libtt_mi355x.so"
+# same-box A/B libraries of the measurement scripts (scripts/exp_ab.sh): only these two places
+_AB_DIRS = ("lib_prev", "lib_var")
+
+
+def _experiment_lib():
+    """TT_EXPERIMENT_LIB (measurement scripts only): "1" = the experiment build above, or a
+    ``libtt_mi355x.so`` under this package's ``lib_prev/`` or ``lib_var/<name>/`` (an A/B of an
+    earlier build of this tree). Anything else is refused: the product loads no other library."""
+    exp = os.environ.get("TT_EXPERIMENT_LIB", "")
+    if not exp:
+        return None
+    if exp == "1":
+        return EXP_LIB_PATH
+    p = Path(exp).resolve()
+    pkg = Path(__file__).resolve().parent
+    if p.name == "libtt_mi355x.so" and any(pkg / d in p.parents for d in _AB_DIRS):
+        return p
+    raise TTError(f"TT_EXPERIMENT_LIB={exp!r}: only '1' (lib_exp/) or a libtt_mi355x.so under "
+                  f"{', '.join(d + '/' for d in _AB_DIRS)} of the package")
 
 TT_OK = 0
 TT_I32, TT_I64, TT_F32, TT_BF16 = 0, 1, 2, 3
@@ -99,11 +118,23 @@ class RouteRole(C.Structure):
                 ("route_ws_bytes", C.c_size_t)]
 
 
+TT_PEER_MAXW = 16
+TT_PEER_HANDLE_BYTES = 64
+
+
+class PeerDirect(C.Structure):
+    """tt_peer_direct_t (ABI 4): a producer's stores straight into the destinations' receive buffers."""
+    _fields_ = [("W", C.c_int32), ("_pad", C.c_int32), ("first_row", C.c_int64 * TT_PEER_MAXW),
+                ("row0", C.c_void_p * TT_PEER_MAXW), ("copy_src", C.c_void_p * TT_PEER_MAXW),
+                ("copy_dst", C.c_void_p * TT_PEER_MAXW), ("copy_len", C.c_int64 * TT_PEER_MAXW)]
+
+
 class GatherRole(C.Structure):
     _fields_ = [("weights", C.c_void_p), ("tables", C.POINTER(TableMeta)), ("T", C.c_int32), ("recv", C.c_void_p),
                 ("block_i64", C.c_int64), ("counts_i64", C.c_int64), ("seg_off", C.POINTER(C.c_int64)),
                 ("slots", C.c_int64), ("rows_out", C.c_void_p), ("out_stride", C.c_int64), ("bad", C.c_void_p),
-                ("dedup_ws", C.c_void_p), ("dedup_ws_bytes", C.c_size_t), ("dedup_max_lookups", C.c_int64)]
+                ("dedup_ws", C.c_void_p), ("dedup_ws_bytes", C.c_size_t), ("dedup_max_lookups", C.c_int64),
+                ("direct", C.POINTER(PeerDirect))]
 
 
 class LaunchPlan(C.Structure):
@@ -111,10 +142,6 @@ class LaunchPlan(C.Structure):
                 ("workspace", C.c_void_p), ("ws_bytes", C.c_size_t), ("wgrad", WgradRole), ("update", UpdateRole),
                 ("insert", InsertRole), ("resolve", ResolveRole), ("adagrad", AdagradRole), ("route", RouteRole),
                 ("gather", GatherRole)]
-
-
-TT_PEER_MAXW = 16
-TT_PEER_HANDLE_BYTES = 64
 
 
 class PeerPut(C.Structure):
@@ -264,7 +291,7 @@ SIGNATURES = {
     ),
     "tt_tower_fwd_bwd_indexed2_bf16": (
         _int,
-        [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, _vp],
+        [_psh, _i64, _pvp, _pvp, _pvp, _pvp, _vp, _vp, _int, _f32, _vp, _vp, _sz, C.POINTER(PeerDirect), _vp],
     ),
     "tt_tower_grads_replicated": (_int, [_psh, _i64, _vp, _vp, _int, _pi64, _f32, _vp, _sz, _vp]),
     "tt_tower_fwd_bwd_gather_update": (
@@ -359,9 +386,7 @@ def load(path: os.PathLike | None = None):
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        exp = os.environ.get("TT_EXPERIMENT_LIB", "")
-        # measurement scripts: "1" = the experiment build, or a path to another experiment .so (A/B)
-        p = Path(path) if path else (EXP_LIB_PATH if exp == "1" else Path(exp) if exp.endswith(".so") else LIB_PATH)
+        p = Path(path) if path else _experiment_lib() or LIB_PATH
         if not p.exists():
             raise TTError(
                 f"libtt_mi355x.so not found at {p}: build it with "

@@ -152,6 +152,9 @@ struct GatherSegArgs {
   DedupWs dd;
   int dd_on;
   int32_t* bad;
+  // direct exchange (dW > 0): source s's slot j -> dblk[s] + j * D (s's mapped receive buffer)
+  int dW;
+  __bf16* dblk[TT_PEER_MAXW];
 };
 
 __device__ __forceinline__ void shard_gather_block(const GatherSegArgs& a, int blk) {
@@ -202,6 +205,13 @@ __device__ __forceinline__ void shard_gather_block(const GatherSegArgs& a, int b
     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
     typedef __attribute__((ext_vector_type(4))) float f32x4g;
     __bf16* dst = a.rows_out + (s * a.out_stride + j) * a.D;
+    if (a.dW) {  // uniform loop, scalar kernarg loads (s differs per half-wave)
+      __bf16* b0 = a.dblk[0];
+#pragma unroll
+      for (int q = 1; q < TT_PEER_MAXW; ++q)
+        if (q < a.dW && s == q) b0 = a.dblk[q];
+      dst = b0 + j * a.D;
+    }
     for (int c = hl * 4; c < a.D; c += 128) {
       const f32x4g v = *reinterpret_cast<const f32x4g*>(src + c);
       bf16x4v o;

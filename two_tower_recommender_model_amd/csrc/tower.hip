@@ -122,6 +122,9 @@ struct TowerArgs {
   int iD;
   // the row-owned T1 (tower_rows_kernel): both towers' bf16 weight image, the LDS layout (rk_off)
   const char* wimg;
+  // indexed2 with a direct exchange (W > 0): dX rows go to the destinations' mapped receive buffers
+  // (px_row) and the copy fields' bytes travel beside them (px_copy_*); W = 0: gdst as above
+  tt_peer_direct_t xd;
 #if TT_EXPERIMENTS
   int dbg;  // EXPERIMENT: 1 skip T2 operand stores, 2 skip dX stores, 4 gather row 0 only, 8 stamps
   int64_t* stamps;  // EXPERIMENT: [nwg][16] s_memrealtime per phase (thread 0)
@@ -1339,6 +1342,44 @@ __device__ __forceinline__ void rk_strip(const bf16x8 (&v)[4], __bf16* row, int 
   for (int s = 0; s < NS; ++s) *reinterpret_cast<bf16x8*>(row + 32 * s + 8 * q) = v[s];
 }
 
+// direct exchange (tt_peer_direct_t): where send-buffer row `row` lands (the destination block's
+// mapped receive buffer); a uniform loop with scalar kernarg loads selects the block
+__device__ __forceinline__ char* px_row(const tt_peer_direct_t& x, int64_t row, int64_t row_bytes) {
+  char* base = reinterpret_cast<char*>(x.row0[0]);
+  int64_t f0 = 0;
+#pragma unroll
+  for (int q = 1; q < TT_PEER_MAXW; ++q) {
+    if (q < x.W && row >= x.first_row[q]) {
+      base = reinterpret_cast<char*>(x.row0[q]);
+      f0 = x.first_row[q];
+    }
+  }
+  return base + (row - f0) * row_bytes;
+}
+// the copy fields split over the grid: workgroup b takes 16-B units [b per, (b + 1) per) of their
+// concatenation (d ascending); unit u of this thread -> (src, dst), or false past the end
+__device__ __forceinline__ bool px_copy_unit(const tt_peer_direct_t& x, int64_t u, const uint4*& src, uint4*& dst) {
+  int64_t pre = 0;
+  bool hit = false;
+#pragma unroll
+  for (int q = 0; q < TT_PEER_MAXW; ++q) {
+    const int64_t n = q < x.W ? x.copy_len[q] >> 4 : 0;
+    if (!hit && u >= pre && u < pre + n) {
+      src = reinterpret_cast<const uint4*>(x.copy_src[q]) + (u - pre);
+      dst = reinterpret_cast<uint4*>(x.copy_dst[q]) + (u - pre);
+      hit = true;
+    }
+    pre += n;
+  }
+  return hit;
+}
+__device__ __forceinline__ int64_t px_copy_units(const tt_peer_direct_t& x) {
+  int64_t n = 0;
+#pragma unroll
+  for (int q = 0; q < TT_PEER_MAXW; ++q) n += q < x.W ? x.copy_len[q] >> 4 : 0;
+  return n;
+}
+
 // raw 4- or 8-byte element i of an id / label column: the conversion is left to the caller, so a
 // dtype branch does not put a wait for the load right behind it (the loads of a prologue all issue
 // before the first wait)
@@ -1554,6 +1595,22 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   __builtin_amdgcn_sched_barrier(0);
   load_image();
   __builtin_amdgcn_sched_barrier(0);
+  // direct exchange: this workgroup's first share of the copy region (exchange A's keys), loaded
+  // now beside the prologue's loads, stored at the end (the rest of a large share there too)
+  uint4 cpv = make_uint4(0u, 0u, 0u, 0u);
+  uint4* cpd = nullptr;
+  int64_t cp_per = 0, cp_end = 0;
+  if constexpr (IDX) {
+    if (a.xd.W) {
+      const int64_t tot = px_copy_units(a.xd);
+      cp_per = (tot + gridDim.x - 1) / gridDim.x;
+      cp_end = min(tot, ((int64_t)blockIdx.x + 1) * cp_per);
+      const int64_t u = (int64_t)blockIdx.x * cp_per + threadIdx.x;
+      const uint4* cps;
+      if (u < cp_end && px_copy_unit(a.xd, u, cps, cpd)) cpv = *cps;
+      else cpd = nullptr;
+    }
+  }
   int64_t r;  // the row's index in its source (table row / returned-rows buffer row), -1: zeros
   if (POOL) {
     r = live ? m : -1;
@@ -1775,6 +1832,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
     const int32_t po = (int32_t)pout_raw.lo;
     store_dx = r >= 0 && po >= 0;
     grow = (t ? a.gdst[1] : a.gdst[0]) + (int64_t)(store_dx ? po : 0) * IN;
+    if (a.xd.W) grow = reinterpret_cast<float*>(px_row(a.xd, store_dx ? po : 0, IN * 4));
   } else {
     grow = live ? a.gpooled + m * a.ldp + a.s.in_col[t] : nullptr;
     store_dx = live;
@@ -1886,6 +1944,16 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   // every row's overflow entry is written (EMPTY for a dropped id or a dead row of a ragged tile):
   // the resolver reads all 64 entries of the group
   if (!UPD && a.dd_on && q == 0) dd_insert_defer_finish_at(a.dd, pend, li, (int)blockIdx.x, 16 * wid + n);
+  if constexpr (IDX) {
+    if (cpd) *cpd = cpv;
+    if (a.xd.W) {  // a share past 256 units (not at the sharded steps' sizes)
+      for (int64_t u = (int64_t)blockIdx.x * cp_per + threadIdx.x + 256; u < cp_end; u += 256) {
+        const uint4* s2;
+        uint4* d2;
+        if (px_copy_unit(a.xd, u, s2, d2)) *d2 = *s2;
+      }
+    }
+  }
   RK_STAMP(15);
 }
 template <bool UPD, bool IDX = false, int IN = 128, bool POOL = false>
@@ -3509,7 +3577,7 @@ static int fused_grads_route_place_gather(const tt_tower_shape_t* shape, int64_t
                                           int64_t block_i64, int64_t counts_i64, const int64_t* seg_off,
                                           int64_t slots, void* rows_out, int64_t out_stride, int32_t* bad,
                                           void* dedup_ws, size_t dedup_ws_bytes, int64_t dedup_max_lookups,
-                                          void* stream) {
+                                          const tt_peer_direct_t* direct, void* stream) {
   if (!params || !base || !offsets || copies < 1 || copies > 16) return fail(TT_EINVAL, "tower_grads_replicated: bad output");
   RouteArgs r{};
   int rc = route_segs_args(F, B, cols, id_dtype, num_embeddings, block_sizes, owners, W, segs, send, pos_in, pos_out,
@@ -3519,6 +3587,16 @@ static int fused_grads_route_place_gather(const tt_tower_shape_t* shape, int64_t
   rc = gather_segs_args(weights, tables, T, F, W, recv, block_i64, counts_i64, seg_off, slots, rows_out, out_stride,
                         bad, dedup_ws, dedup_ws_bytes, dedup_max_lookups, g);
   if (rc) return rc;
+  if (direct) {
+    if ((rc = peer_direct_check(*direct, "tower_grads_place_gather"))) return rc;
+    if (direct->W != W) return fail(TT_EINVAL, "tower_grads_place_gather: direct.W must be the route's W");
+    for (int s = 0; s < W; ++s) {
+      if (direct->first_row[s] != (int64_t)s * out_stride)
+        return fail(TT_EINVAL, "tower_grads_place_gather: direct.first_row[s] must be s * out_stride");
+      g.dblk[s] = reinterpret_cast<__bf16*>(direct->row0[s]);
+    }
+    g.dW = W;
+  }
   int64_t off[16];
   for (int q = 0; q < copies; ++q) off[q] = offsets[q];
   if (copies == 1) off[1] = off[0];  // one copy takes the multi-copy path too (scale applied)
@@ -3734,9 +3812,15 @@ int tt_tower_fwd_bwd_indexed_multi_bf16(const tt_tower_shape_t* shape, int64_t B
 static int tower_indexed2(const tt_tower_shape_t* shape, int64_t B, const int32_t* const* pos_in,
                           const int32_t* const* pos_out, const void* const* rows_in, float* const* grad_rows_out,
                           const float* params, const void* labels, int label_dtype, float grad_scale, float* logits,
-                          void* workspace, size_t ws_bytes, void* stream) {
+                          void* workspace, size_t ws_bytes, const tt_peer_direct_t* direct, void* stream) {
   if (!pos_in || !pos_out || !rows_in || !grad_rows_out) return fail(TT_EINVAL, "tower_indexed2: null pointer");
   TowerArgs a{};
+  if (direct) {
+    if (int rc = peer_direct_check(*direct, "tower_indexed2")) return rc;
+    if (grad_rows_out[0] != grad_rows_out[1])
+      return fail(TT_EINVAL, "tower_indexed2: a direct exchange takes one send buffer (grad_rows_out[0] == [1])");
+    a.xd = *direct;
+  }
   a.gsrc_bf16 = 1;
   for (int t = 0; t < 2; ++t) {
     if (!pos_in[t] || !pos_out[t] || !rows_in[t] || !grad_rows_out[t]) return fail(TT_EINVAL, "tower_indexed2: null pointer");
@@ -3756,9 +3840,9 @@ int tt_tower_fwd_bwd_indexed2_bf16(const tt_tower_shape_t* shape, int64_t B, con
                                    const int32_t* const* pos_out, const void* const* rows_in,
                                    float* const* grad_rows_out, const float* params, const void* labels,
                                    int label_dtype, float grad_scale, float* logits, void* workspace, size_t ws_bytes,
-                                   void* stream) {
+                                   const tt_peer_direct_t* direct, void* stream) {
   return tower_indexed2(shape, B, pos_in, pos_out, rows_in, grad_rows_out, params, labels, label_dtype, grad_scale,
-                        logits, workspace, ws_bytes, stream);
+                        logits, workspace, ws_bytes, direct, stream);
 }
 
 // ---- launch plans (include/tt_mi355x.h): the multi-role fused launches behind one entry point ----
@@ -3840,7 +3924,7 @@ int tt_launch(const tt_launch_plan_t* p, void* stream) {
                                             r.owners, r.W, r.segs, r.send, r.pos_in, r.pos_out, r.overflow, r.route_ws,
                                             r.route_ws_bytes, ga.weights, ga.tables, ga.T, ga.recv, ga.block_i64,
                                             ga.counts_i64, ga.seg_off, ga.slots, ga.rows_out, ga.out_stride, ga.bad,
-                                            ga.dedup_ws, ga.dedup_ws_bytes, ga.dedup_max_lookups, stream);
+                                            ga.dedup_ws, ga.dedup_ws_bytes, ga.dedup_max_lookups, ga.direct, stream);
     default:
       return fail(TT_EINVAL, "launch: no fused launch runs this set of roles (see tt_launch_plan_t)");
   }

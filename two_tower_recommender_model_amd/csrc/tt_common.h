@@ -44,6 +44,22 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// host: a direct-exchange descriptor (tt_peer_direct_t) the kernels can follow blindly
+inline int peer_direct_check(const tt_peer_direct_t& x, const char* who) {
+  const std::string w(who);
+  if (x.W < 1 || x.W > TT_PEER_MAXW) return fail(TT_EINVAL, w + ": direct.W must be 1..TT_PEER_MAXW");
+  if (x.first_row[0] != 0) return fail(TT_EINVAL, w + ": direct.first_row[0] must be 0");
+  for (int d = 0; d < x.W; ++d) {
+    if (!x.row0[d]) return fail(TT_EINVAL, w + ": direct.row0[d] is null");
+    if (d && x.first_row[d] < x.first_row[d - 1]) return fail(TT_EINVAL, w + ": direct.first_row not ascending");
+    if (x.copy_len[d] < 0 || (x.copy_len[d] & 15) ||
+        (x.copy_len[d] && (!x.copy_src[d] || !x.copy_dst[d] || (reinterpret_cast<uintptr_t>(x.copy_src[d]) & 15) ||
+                           (reinterpret_cast<uintptr_t>(x.copy_dst[d]) & 15))))
+      return fail(TT_EINVAL, w + ": direct copies must be 16-B aligned multiples of 16 B");
+  }
+  return TT_OK;
+}
+
 // Kernel-argument bundle of the table / feature metadata (passed by value: graph-capturable, no
 // host->device copy per call). 64 tables x 32 B + 64 features x 8 B + 16 = 2.6 KB < 4 KB limit.
 struct EmbMeta {

@@ -70,6 +70,19 @@ def graph_safe_nccl_env() -> None:
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
+def _wait_for_watchdog(pg) -> None:
+    """ProcessGroupNCCL::waitForPendingWorks through torch's private binding
+    (``ProcessGroup._wait_for_pending_works``, present in torch 2.1 .. 2.10). Without it a capture
+    after eager collectives can race the watchdog thread (``TorchComm.retire``), so its absence is an
+    error, not a silent skip: graph capture is refused and ``capture_pool_or_eager`` / the drop-in
+    fall back to eager steps."""
+    fn = getattr(pg, "_wait_for_pending_works", None)
+    if fn is None:
+        raise _lib.TTError(f"torch {torch.__version__}: ProcessGroup._wait_for_pending_works is missing; RCCL "
+                           "collectives cannot be captured safely (eager steps instead)")
+    fn()
+
+
 class TorchComm:
     """torch.distributed collectives on the current stream (backend "nccl" = RCCL over xGMI)."""
 
@@ -123,7 +136,7 @@ class TorchComm:
         # collectives are never handed to it.
         pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
         if dist.get_backend(pg) == "nccl":
-            pg._wait_for_pending_works()
+            _wait_for_watchdog(pg)
 
     def all_reduce_max_(self, t: torch.Tensor) -> None:
         if self.world > 1 or self.always:
@@ -167,20 +180,32 @@ class _DeviceArray:
 
 
 class PeerComm(TorchComm):
-    """TorchComm whose all-to-alls on the step's data path are device-initiated (opt-in):
-    every rank stores its blocks straight into the peers' receive buffers — allocated here
-    (``recv_buffer``, fine-grained device memory) and mapped into every other rank's process with
-    hipIpcOpenMemHandle — and signals a flag word per (peer, source); the receiver's wait kernel spins
-    on its W words (csrc/peer.hip: a put kernel, then one wave that signals and waits). No RCCL kernel runs on the step path, and the exchange is
-    capturable whatever the process group's backend (gloo included: it only carries the setup).
-    The other collectives (capacities, flags, checkpoints) stay torch.distributed. A wait past
-    ``timeout_s`` gives up and sets a sticky error word that ``check()`` of the step raises on.
-    Replaces the all_to_all_single calls TorchComm issues (TorchRec's input_dist / output_dist
-    all-to-alls and DDP's tower all-reduce under DistributedModelParallel, 03_model_training.py:812-815)."""
+    """TorchComm whose all-to-alls on the step's data path are device-initiated (the
+    sharded steps' default at N > 1 through ``exchange_comm``, which runs ``self_test`` first and falls
+    back to RCCL on every rank when it fails): every rank stores its blocks straight into the peers'
+    receive buffers — allocated here (``recv_buffer``, fine-grained device memory) and mapped into
+    every other rank's process with hipIpcOpenMemHandle — and signals a flag word per (peer, source);
+    the receiver's wait kernel spins on its W words (csrc/peer.hip: a put kernel, then one wave that
+    signals and waits). No RCCL kernel runs on the step path, and the exchange is capturable whatever
+    the process group's backend (gloo included: it only carries the setup). The other collectives
+    (capacities, flags, checkpoints) stay torch.distributed. A wait past ``timeout_s`` gives up and
+    sets a sticky error word that ``check()`` of the step raises on: the results of every step from
+    then on are invalid and the run must be restarted (nothing clears the word). Replaces the
+    all_to_all_single calls TorchComm issues (TorchRec's input_dist / output_dist all-to-alls and DDP's
+    tower all-reduce under DistributedModelParallel, 03_model_training.py:812-815).
 
-    def __init__(self, group=None, timeout_s: float = 5.0, device=None, memory: Optional[str] = None):
-        """memory: "fine-grained" (default; hipDeviceMallocFinegrained, coherent across devices) or
-        "device" (torch's allocator: coarse-grained, coherent only within one device)."""
+    Verified here: ranks sharing one GPU (world 1, and W processes on the test box's one MI355X),
+    with both signalling scopes (``TT_PEER_SYSTEM_SCOPE=1`` forces the cross-device one). Ranks on
+    different GPUs (xGMI) run the same protocol at system scope; only the startup self-test checks it
+    on that hardware."""
+
+    def __init__(self, group=None, timeout_s: float = 60.0, device=None, memory: Optional[str] = None):
+        """memory: None (fine-grained, or torch's allocator when every rank is on one device and the
+        fine-grained allocation is refused), "fine-grained" (hipDeviceMallocFinegrained, coherent
+        across devices; required for ranks on different devices) or "device" (torch's allocator:
+        coarse-grained, coherent only within one device: refused for ranks on different devices).
+        timeout_s: how long a wait kernel spins for a peer's signal before it gives up (the
+        process-group timeout's order: a rank may lag by a graph capture or a slow first batch)."""
         super().__init__(group, always_collective=True)
         if self.world > _lib.TT_PEER_MAXW:
             raise _lib.TTError(f"PeerComm: at most {_lib.TT_PEER_MAXW} ranks")
@@ -202,8 +227,11 @@ class PeerComm(TorchComm):
         else:
             idents[0] = ident
         self.same_device = ident is not None and all(i == ident for i in idents)
-        if os.environ.get("TT_PEER_SYSTEM_SCOPE") == "1":  # measurement: the multi-device signalling
+        if os.environ.get("TT_PEER_SYSTEM_SCOPE") == "1":  # tests / measurement: the multi-device signalling
             self.same_device = False
+        if self.memory == "device" and not self.same_device:
+            raise _lib.TTError('PeerComm: memory="device" (coarse-grained) is coherent within one device only; '
+                               "ranks on different devices need fine-grained memory")
 
     def _device_identity(self):
         p = torch.cuda.get_device_properties(self.device)
@@ -211,6 +239,9 @@ class PeerComm(TorchComm):
         return ident if any(ident) else None  # unknown: treated as different devices (system scope)
 
     def _alloc(self, nbytes: int) -> torch.Tensor:
+        """Fine-grained device memory (setup only: tt_peer_alloc allocates and synchronises). Torch's
+        coarse-grained allocator only when asked for, or when every rank is on this one device and
+        the fine-grained allocation was refused (coherent there: the kernel boundaries publish it)."""
         lib = _lib.load()
         if self.memory in (None, "fine-grained"):
             p = C.c_void_p()
@@ -218,19 +249,31 @@ class PeerComm(TorchComm):
             if rc == 0:
                 try:
                     raw = torch.as_tensor(_DeviceArray(p.value, nbytes), device=self.device)
+                except Exception as e:  # noqa: BLE001
+                    check(lib.tt_peer_free(p), "peer_free")
+                    if self.memory == "fine-grained" or not self.same_device:
+                        raise _lib.TTError(f"PeerComm: torch cannot wrap the fine-grained allocation ({e})") from e
+                else:
                     self._own.append(p.value)
                     self.memory = "fine-grained"
                     return raw
-                except Exception:  # noqa: BLE001 - torch cannot wrap the allocation: use its own
-                    check(lib.tt_peer_free(p), "peer_free")
-            if self.memory == "fine-grained":
+            elif self.memory == "fine-grained" or not self.same_device:
                 check(rc, "peer_alloc")
         self.memory = "device"
         return torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
 
+    def _agree(self, ok: bool) -> bool:
+        """Collective: True iff ``ok`` on every rank."""
+        t = torch.tensor([0 if ok else 1], dtype=torch.int32, device=self.device)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item()) == 0
+
     def recv_buffer(self, shape, dtype: torch.dtype, device) -> torch.Tensor:
         """Collective (every rank, same order): a zeroed receive buffer followed by this exchange's W
-        flag words, exported to every other rank; the peers' buffers are mapped in return."""
+        flag words, exported to every other rank; the peers' buffers are mapped in return. Setup
+        only (allocates, synchronises). A local failure (allocation, export, import) is agreed on
+        before anyone raises, so every rank raises the same error and none waits in a collective."""
         lib = _lib.load()
         shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
         n = 1
@@ -238,44 +281,97 @@ class PeerComm(TorchComm):
             n *= s
         item = torch.empty((), dtype=dtype).element_size()
         body = -(-max(1, n * item) // 256) * 256
-        raw = self._alloc(body + 256)
-        buf = raw[:n * item].view(dtype).view(shape)
-        h = (C.c_char * _lib.TT_PEER_HANDLE_BYTES)()
-        off = C.c_int64()
-        base = raw.data_ptr()
-        if self.world > 1:
-            check(lib.tt_peer_export(C.c_void_p(base), h, C.byref(off)), "peer_export")
-        mine = (bytes(h), int(off.value), body)
+        why = ""
+        raw, mine = None, None
+        try:
+            raw = self._alloc(body + 256)
+            h = (C.c_char * _lib.TT_PEER_HANDLE_BYTES)()
+            off = C.c_int64()
+            if self.world > 1:
+                check(lib.tt_peer_export(C.c_void_p(raw.data_ptr()), h, C.byref(off)), "peer_export")
+            mine = (bytes(h), int(off.value), body)
+        except Exception as e:  # noqa: BLE001 - agreed on below
+            why = f"rank {self.rank}: {e}"
         allv = [None] * self.world
         if self.world > 1:
             dist.all_gather_object(allv, mine, group=self.group)
         else:
             allv[0] = mine
         peers = []
-        for s, (hs, o, b) in enumerate(allv):
-            if s == self.rank:
-                peers.append((base, b))
-                continue
-            if hs not in self._imports:
-                p = C.c_void_p()
-                check(lib.tt_peer_import(hs, C.byref(p)), "peer_import")
-                self._imports[hs] = p.value
-            peers.append((self._imports[hs] + o, b))
+        if all(v is not None for v in allv):
+            try:
+                for s, (hs, o, b) in enumerate(allv):
+                    if s == self.rank:
+                        peers.append((raw.data_ptr(), b))
+                        continue
+                    if hs not in self._imports:
+                        p = C.c_void_p()
+                        check(lib.tt_peer_import(hs, C.byref(p)), "peer_import")
+                        self._imports[hs] = p.value
+                    peers.append((self._imports[hs] + o, b))
+            except Exception as e:  # noqa: BLE001
+                why = why or f"rank {self.rank}: {e}"
+        elif not why:
+            why = "a peer could not allocate or export its buffer"
+        if not self._agree(not why):
+            raise _lib.TTError(f"PeerComm.recv_buffer failed on some rank{': ' + why if why else ''}")
+        buf = raw[:n * item].view(dtype).view(shape)
         self._bufs[buf.data_ptr()] = {"peers": peers, "flags": raw[body:body + 4 * self.world].view(torch.int32),
                                       "state": torch.zeros(1, dtype=torch.int32, device=self.device),
-                                      "raw": raw}
+                                      "raw": raw, "body": body}
         return buf
 
+    def self_test(self, nbytes: int = 1 << 16, rounds: int = 3, timeout_s: float = 10.0) -> Tuple[bool, str]:
+        """Collective startup check of the protocol on this node: ``rounds`` all-to-alls of a
+        (source, destination, round)-tagged pattern through one receive buffer, at the signalling
+        scope the steps will use, each checked on the host; the wait kernels give up after
+        ``timeout_s``. Returns (ok on every rank, the first reason a rank gave)."""
+        why = ""
+        W, r = self.world, self.rank
+        n = max(64, nbytes // 4 // 64 * 64)  # int32 per block
+        keep, self.timeout_s = self.timeout_s, min(self.timeout_s, float(timeout_s))
+        try:
+            out = self.recv_buffer((W * n,), torch.int32, self.device)
+            idx = torch.arange(n, dtype=torch.int64, device=self.device)
+            for k in range(rounds):
+                inp = torch.cat([((r * 1_000_003 + d * 7_919 + k * 104_729 + idx * 31) % 2_000_000_011).to(torch.int32)
+                                 for d in range(W)])
+                self.all_to_all(out, inp)
+                torch.cuda.synchronize(self.device)
+                if int(self.err.item()):
+                    why = f"rank {r}: a wait timed out ({timeout_s} s) in round {k}"
+                else:
+                    want = torch.cat([((s * 1_000_003 + r * 7_919 + k * 104_729 + idx * 31) % 2_000_000_011)
+                                      .to(torch.int32) for s in range(W)])
+                    if not torch.equal(out, want):
+                        why = f"rank {r}: round {k}: {int((out != want).sum())} of {W * n} received words differ"
+                # every rank checks before anyone overwrites the buffer; all stop together
+                if not self._agree(not why):
+                    break
+        except Exception as e:  # noqa: BLE001 - a local error (setup is agreed on inside recv_buffer)
+            why = why or f"rank {r}: {e}"
+            self._agree(False)
+        finally:
+            self.timeout_s = keep
+        ok = self._agree(not why)  # every path above ran the same collectives on every rank
+        if not ok and not why:
+            why = "a peer failed its check"
+        return ok, why
+
+    supports_direct = True
+
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Optional[List[int]] = None,
-                   in_splits: Optional[List[int]] = None):
+                   in_splits: Optional[List[int]] = None, stored: bool = False):
         """All-to-all along dim 0 into a buffer from ``recv_buffer``: block d of ``inp`` (``in_splits[d]``
         rows, or equal blocks) lands in rank d's buffer at block ``rank``; every rank's blocks are
-        equal-sized at the receiver (what the sharded step's fixed layout guarantees)."""
+        equal-sized at the receiver (what the sharded step's fixed layout guarantees). ``stored``:
+        the producers already stored every block at its destination (``direct``): only the signal /
+        wait runs."""
         e = self._bufs.get(out.data_ptr())
         if e is None:
             raise _lib.TTError("PeerComm.all_to_all: the receive buffer was not allocated by recv_buffer()")
         W, r = self.world, self.rank
-        key = (out.data_ptr(), inp.data_ptr(), tuple(in_splits or ()), inp.shape[0])
+        key = (out.data_ptr(), inp.data_ptr(), tuple(in_splits or ()), inp.shape[0], bool(stored))
         put = self._puts.get(key)
         if put is None:
             rowb = inp.element_size() * (inp.numel() // max(1, inp.shape[0]))
@@ -294,13 +390,55 @@ class PeerComm(TorchComm):
             for d in range(W):
                 base, body = e["peers"][d]
                 put.src_off[d] = o * rowb
-                put.len[d] = sizes[d] * rowb
+                put.len[d] = 0 if stored else sizes[d] * rowb
                 put.dst[d] = base + r * sizes[d] * rowb
                 put.flag[d] = base + body + 4 * r
                 o += sizes[d]
             self._puts[key] = put
         check(_lib.load().tt_peer_exchange(C.byref(put), e["flags"].data_ptr(), self.err.data_ptr(), self.timeout_s,
                                            stream_handle(out.device)), "peer_exchange")
+
+    def block_dst(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Optional[List[int]] = None,
+                  in_splits: Optional[List[int]] = None) -> List[Tuple[int, int, int]]:
+        """Per destination d of ``all_to_all(out, inp, ...)``: (byte offset of block d in ``inp``,
+        its bytes, the mapped address where it lands at d)."""
+        e = self._bufs.get(out.data_ptr())
+        if e is None:
+            raise _lib.TTError("PeerComm.block_dst: the receive buffer was not allocated by recv_buffer()")
+        W, r = self.world, self.rank
+        rowb = inp.element_size() * (inp.numel() // max(1, inp.shape[0]))
+        sizes = list(in_splits) if in_splits is not None else [inp.shape[0] // W] * W
+        out_rows = out_splits[0] if out_splits is not None else out.shape[0] // W
+        if len(sizes) != W or sizes[r] != out_rows:
+            raise _lib.TTError("PeerComm.block_dst: receive blocks do not match the senders' blocks")
+        res, o = [], 0
+        for d in range(W):
+            res.append((o * rowb, sizes[d] * rowb, e["peers"][d][0] + r * sizes[d] * rowb))
+            o += sizes[d]
+        return res
+
+    def direct(self, out: torch.Tensor, inp: torch.Tensor, unit_bytes: int, out_splits: Optional[List[int]] = None,
+               in_splits: Optional[List[int]] = None, copy: Optional[Sequence[Tuple[int, int]]] = None):
+        """tt_peer_direct_t for a producer of ``inp`` (units of ``unit_bytes``, counted from ``inp``'s
+        start) whose all-to-all into ``out`` then runs with ``stored=True``: block d's units go to
+        their place in rank d's receive buffer. ``copy[d] = (lo, hi)``: bytes [lo, hi) of block d
+        (relative to its start) that the producer copies to rank d beside its units."""
+        blocks = self.block_dst(out, inp, out_splits, in_splits)
+        x = _lib.PeerDirect()
+        x.W = self.world
+        for d, (off, n, dst) in enumerate(blocks):
+            if off % unit_bytes:
+                raise _lib.TTError("PeerComm.direct: a block does not start on a unit")
+            x.first_row[d] = off // unit_bytes
+            x.row0[d] = dst
+            if copy is not None:
+                lo, hi = copy[d]
+                if not 0 <= lo <= hi <= n or (lo | hi | off | dst | inp.data_ptr()) % 16:
+                    raise _lib.TTError("PeerComm.direct: copy ranges must be 16-B aligned inside the block")
+                x.copy_src[d] = inp.data_ptr() + off + lo
+                x.copy_dst[d] = dst + lo
+                x.copy_len[d] = hi - lo
+        return x
 
     def close(self) -> None:
         """Unmap the peers' buffers and free this rank's (the buffers from recv_buffer are invalid after)."""
@@ -314,6 +452,35 @@ class PeerComm(TorchComm):
         for p in self._own:
             check(lib.tt_peer_free(C.c_void_p(p)), "peer_free")
         self._own.clear()
+
+
+def exchange_comm(kind: str = "auto", group=None, device=None, verbose: bool = True):
+    """The sharded steps' comm (collective: every rank calls it with the same ``kind``).
+    "rccl": TorchComm (all_to_all_single, RCCL over xGMI with backend "nccl"); "peer": PeerComm, the
+    device-initiated exchange, after its startup ``self_test`` — raises if the test fails; "auto"
+    (the default): PeerComm when its self-test passes on every rank, else TorchComm on every rank
+    (the reason printed on rank 0). Returns (comm, description)."""
+    if kind not in ("auto", "peer", "rccl"):
+        raise _lib.TTError(f"exchange_comm: kind is auto, peer or rccl, got {kind!r}")
+    if kind == "rccl":
+        return TorchComm(group, always_collective=True), "RCCL all_to_all_single"
+    why = ""
+    try:
+        pc = PeerComm(group, device=device)
+    except _lib.TTError as e:  # raised on every rank alike (argument / memory-kind checks)
+        pc, why = None, str(e)
+    if pc is not None:
+        ok, why = pc.self_test()
+        if ok:
+            return pc, f"device-initiated puts into IPC-mapped peer buffers ({pc.memory} memory, self-test passed)"
+        pc.close()
+    if kind == "peer":
+        raise _lib.TTError(f"PeerComm self-test failed: {why}")
+    if verbose and dist.get_rank(group) == 0:
+        import sys
+
+        print(f"exchange_comm: device-initiated exchange unavailable ({why}); RCCL all-to-alls", file=sys.stderr)
+    return TorchComm(group, always_collective=True), f"RCCL all_to_all_single (peer self-test failed: {why})"
 
 
 class ThreadComm:
@@ -600,6 +767,26 @@ class FusedShardedTwoTowerStep:
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
         self.logits = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
+        # direct exchange (PeerComm, two features): T1 stores its gradient rows and copies the key
+        # region straight into the owners' exchange-A buffers, launch G its gathered rows and the
+        # tower gradient into the requesters' exchange-B buffers; the exchanges are then only their
+        # signal / wait (TT_PEER_DIRECT=0: the put kernels instead)
+        self.direct = (getattr(comm, "supports_direct", False) and not self.multi
+                       and os.environ.get("TT_PEER_DIRECT", "1") != "0")
+        if self.direct:
+            self._dA = comm.direct(self.recvA, self.sendA, 4 * D, out_splits=[self.Asz[r]] * W,
+                                   in_splits=list(self.Asz),
+                                   copy=[(4 * self.S[d] * D, 4 * self.Asz[d]) for d in range(W)])
+            self._dB = comm.direct(self.rows_in, self.rows_out, 2 * D, out_splits=[self.RSTR] * W,
+                                   in_splits=[self.RSTR] * W)
+            base = self.rows_out.data_ptr()
+            offs = []
+            for d in range(W):
+                addr = self._dB.row0[d] + 2 * D * self.Smax  # the tower block of my block at rank d
+                if (addr - base) % 4:
+                    raise _lib.TTError("sharded step: exchange B's tower block is not 4-B aligned")
+                offs.append((addr - base) // 4)
+            self._tw_off_direct = (C.c_int64 * W)(*offs)
         self.overlap = bool(overlap)
         self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         self.pool_graphs: list = []
@@ -698,9 +885,10 @@ class FusedShardedTwoTowerStep:
                                       ptr(self.route_ws), self.route_ws.numel(), stream_handle(self.device)),
               "shard_route_segs")
 
-    def _exchange_a(self) -> None:
+    def _exchange_a(self, stored: bool = False) -> None:
         r = self.rank
-        self.comm.all_to_all(self.recvA, self.sendA, out_splits=[self.Asz[r]] * self.W, in_splits=list(self.Asz))
+        kw = {"stored": True} if stored else {}
+        self.comm.all_to_all(self.recvA, self.sendA, out_splits=[self.Asz[r]] * self.W, in_splits=list(self.Asz), **kw)
 
     def _gather(self, parity: int) -> None:
         check(_lib.load().tt_shard_gather_segs_bf16(*self._gather_args(parity)), "shard_gather_segs")
@@ -712,11 +900,12 @@ class FusedShardedTwoTowerStep:
                 self.S[r] * self.D // 2, self._segoff_me, self.S[r], ptr(self.rows_out), self.RSTR,
                 ptr(self.flags[1:]), ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device))
 
-    def _exchange_b(self) -> None:
+    def _exchange_b(self, stored: bool = False) -> None:
+        kw = {"stored": True} if stored else {}
         self.comm.all_to_all(self.rows_in, self.rows_out, out_splits=[self.RSTR] * self.W,
-                             in_splits=[self.RSTR] * self.W)
+                             in_splits=[self.RSTR] * self.W, **kw)
 
-    def _t1(self, parity: int, labels: torch.Tensor) -> None:
+    def _t1(self, parity: int, labels: torch.Tensor, direct: bool = False) -> None:
         lib, tw, B = _lib.load(), self.towers, self.B
         pin, pout = self.pos_in[parity], self.pos_out[parity]
         if self.multi:
@@ -728,7 +917,8 @@ class FusedShardedTwoTowerStep:
         check(lib.tt_tower_fwd_bwd_indexed2_bf16(
             C.byref(tw.shape), B, ptr_array([pin[:B], pin[B:]]), ptr_array([pout[:B], pout[B:]]),
             ptr_array([self.rows_in, self.rows_in]), ptr_array([self.sendA, self.sendA]), ptr(self.params),
-            ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
+            ptr(labels), _lib.TT_I32, 1.0, ptr(self.logits), ptr(tw.ws), tw.nbytes,
+            C.byref(self._dA) if direct else None, stream_handle(self.device)),
             "tower_fwd_bwd_indexed2")
 
     def _rows_update(self, parity: int) -> None:
@@ -813,7 +1003,8 @@ class FusedShardedTwoTowerStep:
         """Step on the staged batch i (rows in place, parity ``parity``; batch i+1's keys placed),
         staging batch i+1's rows and routing ``next2_cols`` (batch i+2, same parity)."""
         lib, tw, ts, r, B, dev = _lib.load(), self.towers, self.tables, self.rank, self.B, self.device
-        self._t1(parity, labels)
+        direct = self.direct
+        self._t1(parity, labels, direct=direct)
         route = self._route_args(next2_cols, parity)
         ws = self.dd_ws[parity]
         main = torch.cuda.current_stream(dev)
@@ -826,13 +1017,13 @@ class FusedShardedTwoTowerStep:
                 check(lib.tt_tower_wgrad_pre(C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes,
                                              ptr(self.adam_state), self.lr_dense, 0.9, 0.999, None, 0, 0,
                                              stream_handle(dev)), "tower_wgrad_pre")
-            self._exchange_a()
+            self._exchange_a(stored=direct)
             # launch U without T2: the owner's row-wise Adagrad + the count pass of batch i+2's route
             _lib.launch(self._plan(_lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws), stream_handle(dev),
                         "shard_route_count_rowwise_adagrad")
             main.wait_stream(self.side)
         else:
-            self._exchange_a()
+            self._exchange_a(stored=direct)
             # launch U: T2 + the count pass of batch i+2's route + the owner's row-wise Adagrad
             _lib.launch(self._plan(_lib.ROLE_WGRAD | _lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws),
                         stream_handle(dev), "tower_wgrad_route_count_rowwise_adagrad")
@@ -840,13 +1031,15 @@ class FusedShardedTwoTowerStep:
         # the owner's gather of batch i+1's rows
         plan = self._plan(_lib.ROLE_UPDATE | _lib.ROLE_ROUTE_PLACE | _lib.ROLE_GATHER, route, ws)
         plan.update = _lib.UpdateRole(params=ptr(self.params), replicated=1, copies=self.W,
-                                      base=self.rows_out.data_ptr(), offsets=self._tw_off, scale=1.0 / self.W)
+                                      base=self.rows_out.data_ptr(),
+                                      offsets=self._tw_off_direct if direct else self._tw_off, scale=1.0 / self.W)
         g = self._gather_args(parity ^ 1)
         plan.gather = _lib.GatherRole(weights=g[0], tables=g[1], T=g[2], recv=g[5], block_i64=g[6], counts_i64=g[7],
                                       seg_off=g[8], slots=g[9], rows_out=g[10], out_stride=g[11], bad=g[12],
-                                      dedup_ws=g[13], dedup_ws_bytes=g[14], dedup_max_lookups=g[15])
+                                      dedup_ws=g[13], dedup_ws_bytes=g[14], dedup_max_lookups=g[15],
+                                      direct=C.pointer(self._dB) if direct else None)
         _lib.launch(plan, stream_handle(dev), "tower_grads_replicated_route_place_gather")
-        self._exchange_b()
+        self._exchange_b(stored=direct)
         self._adam()
 
     # ---- checkpoint (03_model_training.py:474-502 / :1015-1054 format) -------------------------
