@@ -824,12 +824,20 @@ def run_dropin(args, world=1, rank=0, local_rank=0):
     optimizer = KeyedOptimizerWrapper(dict(model.named_parameters()), lambda ps: torch.optim.Adam(ps, lr=0.01))
     nb = max(2, args.batches)
     batches = []
-    for cols, lab in synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1 + 1000 * rank):
-        values, lengths, offsets, lpk = ops.kjt_build_mod_dropzero(cols, [num_users, num_items])
-        n = int(lpk.sum())
-        kjt = KeyedJaggedTensor(keys=cat_cols, values=values[:n], lengths=lengths, offsets=offsets,
-                                length_per_key=lpk.tolist())
-        batches.append(Batch(dense_features=torch.zeros(1, device=dev), sparse_features=kjt, labels=lab))
+    if args.workload in MULTIHOT:  # config 5: multi-hot bags (the KJT the reference's loader would give)
+        for v, o, lab in synth_kjt_batches(num_users, num_items, B, MULTIHOT[args.workload], min(nb, 8), dev,
+                                           args.ids, seed=4 * 1000 + 1 + rank):
+            lengths = (o[1:] - o[:-1]).to(torch.int32)
+            lpk = [int(o[B]), int(o[2 * B]) - int(o[B])]
+            kjt = KeyedJaggedTensor(keys=cat_cols, values=v, lengths=lengths, offsets=o, length_per_key=lpk)
+            batches.append(Batch(dense_features=torch.zeros(1, device=dev), sparse_features=kjt, labels=lab))
+    else:
+        for cols, lab in synth_batches(num_users, num_items, B, nb, dev, args.ids, seed=1 + 1000 * rank):
+            values, lengths, offsets, lpk = ops.kjt_build_mod_dropzero(cols, [num_users, num_items])
+            n = int(lpk.sum())
+            kjt = KeyedJaggedTensor(keys=cat_cols, values=values[:n], lengths=lengths, offsets=offsets,
+                                    length_per_key=lpk.tolist())
+            batches.append(Batch(dense_features=torch.zeros(1, device=dev), sparse_features=kjt, labels=lab))
     torch.cuda.synchronize()
 
     def timed(pipeline, warmup, steps):
@@ -872,9 +880,11 @@ def run_dropin(args, world=1, rank=0, local_rank=0):
     info["generic_path"] = {"ms_per_step": round(gdt / gsteps * 1e3, 4), "pairs/s": round(world * gsteps * B / gdt, 1),
                             "steps": gsteps}
     if world > 1 and fd:
-        info["sharded"] = {"sharding": fd.sharding, "owners": fd.owners,
-                           "capacity": list(fd.step.caps_f) if fd.step is not None else None,
-                           "mode": "hipgraph" if fd.graph_mode else "eager"}
+        st = fd.step
+        info["sharded"] = {"sharding": fd.sharding, "owners": fd.owners, "step": fd.mode,
+                           "capacity": (list(st.caps_f) if fd.mode == "pipelined" else st.cap) if st is not None else None,
+                           "mode": "hipgraph" if fd.graph_mode else "eager", "exchange": fd.exchange,
+                           "rejected": dict(fd.rejected)}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, args.steps, info
 
 

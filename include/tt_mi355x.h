@@ -546,6 +546,17 @@ int tt_tower_adam_grads(const tt_tower_shape_t* shape, int64_t B, float* params,
                         float* exp_avg, float* exp_avg_sq, float lr, float beta1, float beta2, float eps,
                         float weight_decay, int64_t* step_state, void* workspace, size_t ws_bytes, void* stream);
 
+/* Admission counts of one KJT batch for the N > 1 drop-in (dropin.FusedShardedDropin; what TorchRec's
+ * input_dist learns from its host-read split sizes, torchrec/distributed/embeddingbag.py, reached
+ * from 03_model_training.py:648, :812-815): out[0] = 1 if a bag holds more than one id, out[1] = 2
+ * if a value lies outside [0, num_embeddings[f]), out[2 + d * F + f] = the ids of feature f that
+ * owner d would receive (row-wise: id / block_sizes[f]; table-wise: owners[f]). out (int32
+ * [2 + W * F]) is zeroed by the call (memset + one kernel, asynchronous). offsets: int32
+ * [F * B + 1] of the key-major KJT, nnz = offsets[F * B]. W <= 16. */
+int tt_kjt_admit(int F, int64_t B, const void* values, int id_dtype, int64_t nnz, const int32_t* offsets,
+                 const int64_t* num_embeddings, const int64_t* block_sizes, const int32_t* owners, int W, int32_t* out,
+                 void* stream);
+
 /* ---- multi-hot sharded step (config 5, sharded_kjt.py): fixed-size exchanges ------------------------
  * TorchRec's KJTAllToAll / PooledEmbeddingsAllToAll / reduce-scatter (torchrec/distributed/embeddingbag.py,
  * reached from 03_model_training.py:812-815) exchange variable split sizes the host reads every batch;

@@ -9,7 +9,11 @@ all-to-alls are captured into the slot graphs.
   state, tower parameters and Adam moments), for the default plan (both tables row-wise), both
   tables table-wise and the mixed plan;
 * mixed: a smaller batch in the middle runs the generic DMP path on every rank and the fused
-  steps re-prime after it; eval runs forward-only."""
+  steps re-prime after it; eval runs forward-only; the run matches the generic-only run;
+* skew: a later batch past the first batch's capacities and a two-id bag on one rank go down the
+  generic path on EVERY rank by the agreed admission; nothing raises; matches the generic-only run;
+* kjt: multi-hot bags (config 5's shape, scaled down) dispatch to the KJT mode, bit for bit against
+  FusedShardedKJTStep built directly."""
 import os
 import socket
 import sys
@@ -46,3 +50,12 @@ def test_dropin_sharded_bitwise_equals_direct_step(world, plan):
 
 def test_dropin_sharded_generic_batch_and_eval():
     _run(2, "--mode", "mixed", "--plan", "mixed", "--dim", "64")
+
+
+def test_dropin_sharded_skewed_and_multi_id_batches_go_generic_on_every_rank():
+    _run(2, "--mode", "skew", "--plan", "default", "--steps", "6")
+
+
+@pytest.mark.parametrize("world,plan", [(2, "mixed"), (2, "default")])
+def test_dropin_sharded_multihot_kjt_mode_bitwise(world, plan):
+    _run(world, "--mode", "kjt", "--plan", plan)

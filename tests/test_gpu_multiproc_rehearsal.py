@@ -92,6 +92,25 @@ def test_bench_dropin_n2_rehearsal():
     assert di["dispatch"] == "fused sharded" and di["fused_steps"] == 8 and di["generic_steps"] == 0, di
 
 
+def test_bench_dropin_config5_n2_dispatches_kjt_step():
+    """`bench.py --gpus 2 --path dropin --workload config5`: the reference's loop on multi-hot bags
+    (BASELINE config 5: B = 16,384, bags of 1..39 ids, 100M x 50M tables) in two processes sharing
+    the GPU, dispatched to the fused sharded KJT step on every rank: no generic step, no rejection."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TT_REHEARSE_GLOO="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--path", "dropin", "--workload", "config5", "--steps", "6",
+           "--warmup", "2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=230)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    print(line[:1500], flush=True)
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
+    di = d["config"]["dropin"]
+    assert di["dispatch"] == "fused sharded" and di["fused_steps"] == 8 and di["generic_steps"] == 0, di
+    assert di["sharded"]["step"] == "kjt" and not di["sharded"]["rejected"], di
+
+
 @pytest.mark.parametrize("world", [2])
 def test_bench_config5_sharded_multiprocess_gloo_rehearsal(world):
     """bench.py's config-5 N > 1 path (the capturable multi-hot sharded step: users table-wise on the

@@ -316,6 +316,7 @@ SIGNATURES = {
     "tt_peer_import": (_int, [_vp, _pvp]),
     "tt_peer_unimport": (_int, [_vp]),
     "tt_peer_exchange": (_int, [C.c_void_p, _vp, _vp, C.c_double, _vp]),
+    "tt_kjt_admit": (_int, [_int, _i64, _vp, _int, _i64, _vp, _pi64, _pi64, _pi32, _int, _vp, _vp]),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -370,6 +371,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_bwd_rowwise_adagrad_part",
     "tt_launch",
     "tt_peer_exchange",
+    "tt_kjt_admit",
 ]
 
 _lib = None

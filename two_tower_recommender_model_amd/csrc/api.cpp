@@ -56,9 +56,9 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_launch (every multi-role fused launch, by plan)
 // tt_kjt_single_hot_cols
 // tt_kjt_route, tt_kjt_unpack, tt_pooled_partials_sum, tt_pooled_grad_pack
-// tt_tower_fwd_bwd_gather_update_t3, tt_tower_update_lazy, tt_tower_fwd_bwd_indexed2_bf16_t3
 // tt_bwd_rowwise_adagrad_part
 // tt_peer_exchange
-int tt_num_entry_points(void) { return 51; }
+// tt_kjt_admit
+int tt_num_entry_points(void) { return 52; }
 
 }  // extern "C"

@@ -156,6 +156,73 @@ int gather_segs_args(const float* weights, const tt_table_meta_t* tables, int T,
   return TT_OK;
 }
 
+// Admission counts of one KJT batch (tt_kjt_admit, the N > 1 drop-in): the bags longer than one id,
+// the values outside [0, N), and the ids each (owner, feature) segment would receive. Workgroups
+// [0, nbw) check 2048 bags each (lengths from the offsets), the rest 2048 values each; every
+// workgroup reduces in LDS and adds to the zeroed output with one atomic per word.
+constexpr int ADM_PT = 8;  // bags / values per thread
+struct AdmArgs {
+  int F, W, id_dtype, nbw;
+  int64_t B, nnz;
+  const void* values;
+  const int32_t* offsets;
+  int32_t* out;
+  int64_t ne[TT_MAX_FEATURES], blk[TT_MAX_FEATURES];
+  int32_t own[TT_MAX_FEATURES];
+};
+__global__ void __launch_bounds__(256) kjt_admit_kernel(AdmArgs a) {
+  const int F = a.F, W = a.W, id_dtype = a.id_dtype, nbw = a.nbw;
+  const int64_t B = a.B, nnz = a.nnz;
+  const void* values = a.values;
+  const int32_t* offsets = a.offsets;
+  int32_t* out = a.out;
+  __shared__ int cnt[TT_PEER_MAXW * TT_MAX_FEATURES];
+  __shared__ int flags[2];
+  const int tid = threadIdx.x;
+  for (int u = tid; u < W * F; u += 256) cnt[u] = 0;
+  if (tid < 2) flags[tid] = 0;
+  __syncthreads();
+  int multi = 0, bad = 0;
+  if ((int)blockIdx.x < nbw) {
+    const int64_t nb = (int64_t)F * B;
+#pragma unroll
+    for (int k = 0; k < ADM_PT; ++k) {
+      const int64_t b = ((int64_t)blockIdx.x * ADM_PT + k) * 256 + tid;
+      if (b < nb && offsets[b + 1] - offsets[b] > 1) multi = 1;
+    }
+  } else {
+    // feature boundaries: a uniform loop over the F segment starts (scalar loads)
+#pragma unroll
+    for (int k = 0; k < ADM_PT; ++k) {
+      const int64_t i = ((int64_t)(blockIdx.x - nbw) * ADM_PT + k) * 256 + tid;
+      if (i >= nnz) break;
+      int f = 0;
+      int64_t nef = a.ne[0], bf = a.blk[0];
+      int of = a.own[0];
+      for (int q = 1; q < F; ++q)
+        if (i >= (int64_t)offsets[(int64_t)q * B]) {
+          f = q;
+          nef = a.ne[q];
+          bf = a.blk[q];
+          of = a.own[q];
+        }
+      const int64_t id = load_id(values, id_dtype, i);
+      if (id < 0 || id >= nef) {
+        bad = 1;
+        continue;
+      }
+      const int d = bf > 0 ? (int)udiv64(id, bf) : of;
+      if (d >= 0 && d < W) atomicAdd(&cnt[d * F + f], 1);
+    }
+  }
+  if (multi) flags[0] = 1;
+  if (bad) flags[1] = 2;
+  __syncthreads();
+  if (tid < 2 && flags[tid]) atomicOr(&out[tid], flags[tid]);
+  for (int u = tid; u < W * F; u += 256)
+    if (cnt[u]) atomicAdd(&out[2 + u], cnt[u]);
+}
+
 }  // namespace tt
 
 using namespace tt;
@@ -326,6 +393,40 @@ int tt_shard_gather_segs_bf16(const float* weights, const tt_table_meta_t* table
   if (n == 0) return TT_OK;
   shard_gather_segs_kernel<<<dim3((unsigned)ceil_div(n, 8)), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("shard_gather_segs");
+}
+
+int tt_kjt_admit(int F, int64_t B, const void* values, int id_dtype, int64_t nnz, const int32_t* offsets,
+                 const int64_t* num_embeddings, const int64_t* block_sizes, const int32_t* owners, int W, int32_t* out,
+                 void* stream) {
+  if (F < 1 || F > TT_MAX_FEATURES || B < 1 || W < 1 || W > TT_PEER_MAXW || nnz < 0)
+    return fail(TT_EINVAL, "kjt_admit: 1 <= F <= 64, B >= 1, 1 <= W <= 16, nnz >= 0");
+  if (!offsets || !num_embeddings || !block_sizes || !owners || !out || (nnz && !values))
+    return fail(TT_EINVAL, "kjt_admit: null pointer");
+  if (nnz && id_dtype != TT_I32 && id_dtype != TT_I64) return fail(TT_EINVAL, "kjt_admit: ids must be int32/int64");
+  AdmArgs a{};
+  a.F = F;
+  a.W = W;
+  a.id_dtype = id_dtype;
+  a.B = B;
+  a.nnz = nnz;
+  a.values = values;
+  a.offsets = offsets;
+  a.out = out;
+  for (int f = 0; f < F; ++f) {
+    if (num_embeddings[f] < 1 || block_sizes[f] < 0 || (block_sizes[f] == 0 && (owners[f] < 0 || owners[f] >= W)))
+      return fail(TT_EINVAL, "kjt_admit: bad table size or sharding of a feature");
+    a.ne[f] = num_embeddings[f];
+    a.blk[f] = block_sizes[f];
+    a.own[f] = owners[f];
+  }
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(int32_t) * (size_t)(2 + W * F), as_stream(stream));
+  if (e != hipSuccess) return fail((int)e, std::string("kjt_admit: ") + hipGetErrorString(e));
+  const int64_t per = 256 * ADM_PT;
+  const int64_t nbw = ceil_div((int64_t)F * B, per), nvw = ceil_div(nnz, per);
+  if (nbw + nvw > INT32_MAX) return fail(TT_EINVAL, "kjt_admit: grid too large");
+  a.nbw = (int)nbw;
+  kjt_admit_kernel<<<dim3((unsigned)(nbw + nvw)), dim3(256), 0, as_stream(stream)>>>(a);
+  return check_launch("kjt_admit");
 }
 
 }  // extern "C"

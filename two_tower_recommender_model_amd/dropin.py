@@ -44,7 +44,7 @@ def _named(obj, cls_name: str) -> bool:
 
 
 class _Item:
-    __slots__ = ("batch", "slot", "parity", "labels", "primed")
+    __slots__ = ("batch", "slot", "parity", "labels", "primed", "seq", "adm", "event", "work", "agreed")
 
     def __init__(self, batch, slot=None, parity=0, labels=None):
         self.batch = batch
@@ -52,6 +52,11 @@ class _Item:
         self.parity = parity
         self.labels = labels
         self.primed = False
+        self.seq = -1
+        self.adm = None      # N > 1: this rank's admission vector (pinned int64) / the agreed one
+        self.event = None    # N > 1: the admission counts have reached the host
+        self.work = None     # N > 1: the async all-reduce of the admission vector
+        self.agreed = None   # N > 1: the MAX over the ranks (numpy), once known
 
 
 class FusedDropin:
@@ -430,27 +435,49 @@ class FusedDropin:
         return output
 
 
+
+
+# The N > 1 drop-in's admission vector of one batch (int64), MAX-reduced over the ranks before the
+# batch trains on a fused sharded step: every rank then takes the same path for it, whatever its own
+# data looked like (a mismatch would run different collectives on different ranks).
+A_REJECT, A_B, A_NEGB, A_DT, A_NEGDT, A_MULTI, A_OVER, A_ERR, A_SEG, A_DEST, A_NNZ = range(11)
+A_LEN = 12
+_RING = 16  # admission count buffers in flight (fetched, not yet on the host)
+
+
 class FusedShardedDropin:
     """The reference's loop at world size W > 1 (DistributedModelParallel over W processes, one GPU
-    each, 03_model_training.py:812-815, :918) on the pipelined fused sharded step
-    (``sharded.FusedShardedTwoTowerStep``): TrainPipelineSparseDist.progress hands each single-hot
-    batch to the step, which trains the ShardedEmbeddingBagCollection's OWN shards (table-wise or
-    row-wise per the DMP plan; ``ops.TableSet.view_of``) and the towers' parameters and Adam moments
-    as views of its flat buffers (the DDP replicas: the step's fixed-order mean of the W tower
-    gradients is DDP's all-reduce mean). Per step two fixed-size all-to-alls instead of the eager
-    input_dist / output_dist / DDP collectives with their host-synchronised split sizes.
+    each, 03_model_training.py:812-815, :918) on the fused sharded steps: TrainPipelineSparseDist.progress
+    hands each batch to a step that trains the ShardedEmbeddingBagCollection's OWN shards (table-wise or
+    row-wise per the DMP plan; ``ops.TableSet.view_of``) and the towers' parameters and Adam moments as
+    views of its flat buffers (the DDP replicas: the step's fixed-order mean of the W tower gradients is
+    DDP's all-reduce mean). Fixed-size exchanges (device-initiated into the peers' buffers after
+    ``sharded.exchange_comm``'s self-test, else RCCL) instead of the eager input_dist / output_dist /
+    DDP collectives with their host-synchronised split sizes (torchrec/distributed/embeddingbag.py).
 
-    The step is pipelined two batches deep (batch i+1's rows are gathered during step i, batch
-    i+2's ids routed), so progress() looks two batches ahead; slot k's HIP graph (RCCL inside) is
-    the step on slot k routing slot k+2. Every rank must take the same path for the same batch (the
-    step is collective): the choice uses host metadata only (stride, value count, dtype), which the
-    reference's loaders give every rank alike. A batch the step does not take (another batch size,
-    multi-hot values) runs the generic DMP path between fused steps; the staged pipeline is dropped
-    first. Segment capacities come from the first batch's routes (max over ranks x 1.5, at least
-    1.5 B / W + 64); a later batch beyond them drops the excess lookups and sets a sticky flag
-    that is checked (collectively) at every StopIteration, as is a bag of several ids."""
+    Two modes, fixed by the first batch every rank admits:
+      "pipelined"  single-hot bags: ``sharded.FusedShardedTwoTowerStep``, two batches of lookahead
+                   (batch i+1's rows gathered during step i, batch i+2's ids routed), one HIP graph per
+                   slot; a multi-hot batch later runs the generic DMP path;
+      "kjt"        multi-hot bags (BASELINE config 5): ``sharded_kjt.FusedShardedKJTStep``, three
+                   exchanges per batch (ids in, one pooled row per (bag, owner) out, bag gradients
+                   back), one HIP graph per slot; any bag lengths.
+
+    Admission. Every fetched batch gets an admission vector (``tt_kjt_admit`` on a side stream: bags
+    longer than one id, values outside [0, N), ids per (owner, feature) segment; plus batch size, id
+    dtype, value count and this rank's own shape checks), MAX-reduced over the ranks by an async
+    all-reduce on a gloo group of the same ranks (issued in fetch order, typically two progress calls
+    before it is needed). A batch trains fused only if EVERY rank admits it: same batch size and id
+    dtype, no value out of range, no segment over its capacity (the capacities come from the first
+    batch: its largest segment x 1.5), single-hot in the pipelined mode. Anything else — a smaller
+    last batch, a skewed batch beyond a capacity, a multi-id bag in the pipelined mode — runs the
+    generic DMP path on every rank between fused steps (the staged pipeline dropped first; a route
+    that overflowed only ever belonged to such a batch, so no fused step trains on dropped lookups).
+    ``TT_DROPIN_EXCHANGE`` = auto (default) / peer / rccl picks the exchange."""
 
     def __init__(self, pipeline, task, ebc, ts, fused_cfg, towers, adam, feats, dims, sharded, depth: int = 8):
+        import ctypes as C
+
         import torch.distributed as dist
 
         self.pipeline = pipeline
@@ -466,23 +493,45 @@ class FusedShardedDropin:
         self.owners = [o for _, o in sharded]
         self.depth = int(depth)  # even: parity = slot % 2
         self.device = pipeline._device
-        self.W = dist.get_world_size(ebc._pg)
+        self.W = W = dist.get_world_size(ebc._pg)
+        self.N = [c.num_embeddings for c in ebc._embedding_bag_configs]
+        self.blocks = [-(-n // W) if s == "row_wise" else 0 for n, s in zip(self.N, self.sharding)]
+        self.seg_owner = [o if s == "table_wise" else 0 for o, s in zip(self.owners, self.sharding)]
+        self.mode = None  # "pipelined" | "kjt", fixed by the first admitted batch
         self.step = None
+        self.comm = None
+        self.exchange = ""
         self.queue: List[_Item] = []  # fetched batches: cur, nxt, nxt2
-        self.k = 0
-        self.staged = False  # the step holds batch queue[0]'s rows and the next batch's route
-        self.dirty = False   # a fused step ran since the last reset (its dedup tables hold keys)
-        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.staged = False  # pipelined: the step holds batch queue[0]'s rows and the next batch's route
+        self.dirty = False   # pipelined: a fused step ran since the last reset (its dedup tables hold keys)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)  # the conversion's word (unused:
+        # the admission vector carries the same facts per batch)
         self.steps_fused = 0
         self.steps_generic = 0
+        self.rejected = {}  # reason -> batches sent down the generic path by the agreed admission
         self.graphs: List = []
         self.graph_mode = None
+        self.lr_captured = None
+        # admission: counts on a side stream, agreement over a gloo group of the same ranks
+        self._apg = dist.new_group(ranks=dist.get_process_group_ranks(ebc._pg), backend="gloo")
+        self._astream = torch.cuda.Stream(device=self.device)
+        self._aout = [torch.zeros(2 + W * 2, dtype=torch.int32, device=self.device) for _ in range(_RING)]
+        self._ahost = [torch.zeros(2 + W * 2, dtype=torch.int32).pin_memory() for _ in range(_RING)]
+        self._pending: List[_Item] = []  # admission vectors not yet reduced, in fetch order
+        self._works: List[_Item] = []    # reductions issued, not yet waited on
+        self._seq = 0
+        self._lib = _lib.load()
+        self._ne = (C.c_int64 * 2)(*self.N)
+        self._bs = (C.c_int64 * 2)(*self.blocks)
+        self._ow = (C.c_int32 * 2)(*self.seg_owner)
 
     # reuse of the single-GPU drop-in's helpers
     _adam_group = FusedDropin._adam_group
     _adam_lr = FusedDropin._adam_lr
 
-    def fusable(self, batch) -> bool:
+    # ---- admission ---------------------------------------------------------------------------
+    def _local_ok(self, batch) -> bool:
+        """This rank's own shape checks (the agreed admission adds everything that needs all ranks)."""
         kjt = getattr(batch, "sparse_features", None)
         if kjt is None or list(kjt.keys()) != self.feats:
             return False
@@ -490,51 +539,129 @@ class FusedShardedDropin:
         if B < 8 or B % 8 or (self.step is not None and B != self.step.B):
             return False
         v = kjt.values()
-        if v.numel() > 2 * B or (v.numel() and v.dtype not in (torch.int32, torch.int64)):
+        if v.numel() and v.dtype not in (torch.int32, torch.int64):
             return False
-        if self.step is not None and v.numel() and v.dtype != self.step.id_dtype:
+        if self.step is not None and v.numel() and v.dtype != self.id_dtype:
+            return False
+        if self.mode == "kjt" and v.numel() > self.vcap:
             return False
         lab = batch.labels
         return (lab.numel() == B and lab.dtype in (torch.int32, torch.int64) and lab.is_contiguous()
                 and lab.device == self.device and kjt.device() == self.device)
 
-    # ---- the step on the sharded EBC's storage ---------------------------------------------------
-    def _make_step(self, batch) -> None:
-        import ctypes as C
+    @staticmethod
+    def _offsets32(kjt) -> torch.Tensor:
+        o = kjt.offsets()
+        return o if o.dtype == torch.int32 else o.to(torch.int32)
 
+    def _counts(self, batch, offs, out, stream) -> None:
+        kjt = batch.sparse_features
+        v = kjt.values()
+        idt = _lib.id_dtype_code(v.dtype) if v.numel() else _lib.TT_I64
+        _lib.check(self._lib.tt_kjt_admit(2, kjt.stride(), v.data_ptr() if v.numel() else None, idt, v.numel(),
+                                          offs.data_ptr(), self._ne, self._bs, self._ow, self.W, out.data_ptr(),
+                                          stream.cuda_stream), "kjt_admit")
+
+    def _vector(self, ok: bool, batch, counts: Optional[torch.Tensor]) -> torch.Tensor:
+        """This rank's admission vector (host int64) from its shape checks and the batch's counts."""
+        import numpy as np
+
+        a = np.zeros(A_LEN, dtype=np.int64)
+        kjt = getattr(batch, "sparse_features", None)
+        B = kjt.stride() if kjt is not None else 0
+        a[A_B], a[A_NEGB] = B, -B
+        a[A_REJECT] = 0 if ok else 1
+        if ok:
+            v = kjt.values()
+            dt = 1 if (v.dtype == torch.int64 if v.numel() else (self.id_dtype == torch.int64 if self.step else True)) \
+                else 0
+            a[A_DT], a[A_NEGDT] = dt, -dt
+            c = counts.numpy().astype(np.int64)
+            cnt = c[2:].reshape(self.W, 2)
+            a[A_MULTI] = 1 if c[0] else 0
+            a[A_ERR] = c[1]
+            rw = [f for f in range(2) if self.sharding[f] == "row_wise"]
+            a[A_SEG] = int(cnt[:, rw].max()) if rw else 0
+            a[A_DEST] = int(cnt.sum(axis=1).max())
+            a[A_NNZ] = v.numel()
+            if self.step is not None:
+                if self.mode == "pipelined":
+                    a[A_OVER] = int(any(cnt[d, f] > self.step.caps_f[f] for d in range(self.W) for f in rw))
+                else:
+                    a[A_OVER] = int(a[A_DEST] > self.step.cap)
+        return torch.from_numpy(a)
+
+    def _reason(self, ag, first: bool = False) -> str:
+        """'' if every rank admits the batch (agreed vector ``ag``), else why not."""
+        if ag[A_REJECT]:
+            return "a rank's batch is not the step's shape (keys, batch size, dtypes, value capacity)"
+        if ag[A_B] != -ag[A_NEGB]:
+            return "the ranks' batch sizes differ"
+        if ag[A_DT] != -ag[A_NEGDT]:
+            return "the ranks' id dtypes differ"
+        if ag[A_ERR]:
+            return "an id outside [0, N)"
+        if not first and ag[A_OVER]:
+            return "a segment over its capacity (skewed ids)"
+        if not first and self.mode == "pipelined" and ag[A_MULTI]:
+            return "a bag of several ids (the single-hot pipelined step)"
+        return ""
+
+    def _poll(self, upto: int = -1) -> None:
+        """Issue the agreement of every fetched batch whose counts reached the host, in fetch order
+        (forcing those up to sequence number ``upto``)."""
         import torch.distributed as dist
 
-        from .sharded import FusedShardedTwoTowerStep, TorchComm, default_capacity
+        while self._pending:
+            x = self._pending[0]
+            if x.event is not None:
+                if not x.event.query():
+                    if x.seq > upto:
+                        break
+                    x.event.synchronize()
+                x.adm = self._vector(True, x.batch, x.adm)
+                x.event = None
+            x.work = dist.all_reduce(x.adm, op=dist.ReduceOp.MAX, group=self._apg, async_op=True)
+            self._works.append(x)
+            self._pending.pop(0)
 
-        kjt = batch.sparse_features
-        B = kjt.stride()
-        v = kjt.values()
-        idt = v.dtype if v.numel() else torch.int64
-        dev, W, ebc = self.device, self.W, self.ebc
-        # every rank's first batch agrees on B and the id dtype (else: the generic path everywhere)
-        agree = torch.tensor([B, -B, 1 if idt == torch.int64 else 0, -(1 if idt == torch.int64 else 0)],
-                             dtype=torch.int64, device=dev)
-        dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=ebc._pg)
-        if int(agree[0]) != -int(agree[1]) or int(agree[2]) != -int(agree[3]):
-            raise _lib.TTError("dropin (sharded): the ranks' first batches differ in batch size or id dtype")
-        N = [c.num_embeddings for c in ebc._embedding_bag_configs]
-        D = self.dims[0]
-        cols = self._cols_of(kjt, B)
-        blocks = [-(-n // W) if s == "row_wise" else 0 for n, s in zip(N, self.sharding)]
-        seg_owner = [o if s == "table_wise" else 0 for o, s in zip(self.owners, self.sharding)]
-        from .sharded import segment_counts
+    def _agreed(self, x: _Item):
+        if x.agreed is None:
+            self._poll(upto=x.seq)
+            x.work.wait()
+            x.agreed = x.adm.numpy().copy()
+            self._works = [w for w in self._works if w is not x]
+        return x.agreed
 
-        need = segment_counts(cols, N, blocks, seg_owner, W).max().reshape(1).to(dev)
-        dist.all_reduce(need, op=dist.ReduceOp.MAX, group=ebc._pg)
-        cap = max(default_capacity(B, W, factor=1.5), -(-int(need) * 3 // 2))
-        cap = min(B, -(-cap // 8) * 8)
-        local = [ebc._local_index.get(ebc._f_table[f]) for f in range(2)]
-        tables = ops.TableSet.view_of(self.ts, local, [D, D], dev)
-        comm = TorchComm(group=ebc._pg, always_collective=True)
-        st = FusedShardedTwoTowerStep(comm, N, D, [128, 64], B, dev, sharding=self.sharding, tw_owners=self.owners,
-                                      lr_emb=self.fused_cfg["lr"], lr_dense=self._adam_lr(),
-                                      eps=self.fused_cfg["eps"], id_dtype=idt, capacity=cap, tables=tables)
-        # the towers' parameters -> views of the step's flat buffer; Adam's moments likewise
+    def _settle(self) -> None:
+        """Every fetched batch's agreement issued and completed (before the pipeline hands batches back
+        or ends: every rank reduces every batch it fetched)."""
+        self._poll(upto=self._seq)
+        for x in self._works:
+            x.work.wait()
+            if x.agreed is None:
+                x.agreed = x.adm.numpy().copy()
+        self._works = []
+
+    def _admit_first(self, batch, ok: bool, offs) -> Tuple[bool, Any]:
+        """The first batch(es), before any step exists: counted and agreed synchronously (every rank
+        reaches this with the same batch index)."""
+        import torch.distributed as dist
+
+        counts = None
+        if ok:
+            out = self._aout[0]
+            self._counts(batch, offs, out, torch.cuda.current_stream(self.device))
+            counts = out.cpu()
+        a = self._vector(ok, batch, counts)
+        dist.all_reduce(a, op=dist.ReduceOp.MAX, group=self._apg)
+        ag = a.numpy().copy()
+        why = self._reason(ag, first=True)
+        return not why, ag
+
+    # ---- the steps on the sharded EBC's storage -------------------------------------------------
+    def _adopt_towers(self, st) -> None:
+        """The towers' parameters -> views of the step's flat buffer; Adam's moments likewise."""
         views = [x for layers in st.layer_views() for wb in layers for x in wb]
         params = [p for m in self.towers for l in m._mlp for p in (l._linear.weight, l._linear.bias)]
         steps, o = set(), 0
@@ -561,43 +688,79 @@ class FusedShardedDropin:
             o += n
         st.towers.update(st.params, do_adam=False)
         self._params = params
+
+    def _make_step(self, batch, ag) -> None:
+        import ctypes as C
+
+        import torch.distributed as dist
+
+        from .sharded import PeerComm, default_capacity, exchange_comm
+        from .sharded_kjt import FusedShardedKJTStep
+
+        kjt = batch.sparse_features
+        B = kjt.stride()
+        self.id_dtype = idt = torch.int64 if ag[A_DT] else torch.int32
+        dev, W, ebc, D = self.device, self.W, self.ebc, self.dims[0]
+        self.mode = "kjt" if ag[A_MULTI] else "pipelined"
+        local = [ebc._local_index.get(ebc._f_table[f]) for f in range(2)]
+        tables = ops.TableSet.view_of(self.ts, local, [D, D], dev)
+        self.comm, self.exchange = exchange_comm(os.environ.get("TT_DROPIN_EXCHANGE", "auto"), group=ebc._pg,
+                                                 device=dev)
+        kw = dict(lr_emb=self.fused_cfg["lr"], lr_dense=self._adam_lr(), eps=self.fused_cfg["eps"], tables=tables)
+        if self.mode == "pipelined":
+            from .sharded import FusedShardedTwoTowerStep
+
+            cap = max(default_capacity(B, W, factor=1.5), -(-int(ag[A_SEG]) * 3 // 2))
+            cap = min(B, -(-cap // 8) * 8)
+            st = FusedShardedTwoTowerStep(self.comm, self.N, D, [128, 64], B, dev, sharding=self.sharding,
+                                          tw_owners=self.owners, id_dtype=idt, capacity=cap, **kw)
+        else:
+            cap = max(64, -(-int(ag[A_DEST]) * 3 // 2))
+            cap = -(-cap // 8) * 8
+            st = FusedShardedKJTStep(self.comm, self.N, D, [128, 64], B, dev, cap, sharding=self.sharding,
+                                     tw_owners=self.owners, **kw)
+        self._adopt_towers(st)
         self.step = st
         Dp = self.depth
-        self.slot_cols = [[torch.zeros(B, dtype=idt, device=dev) for _ in range(2)] for _ in range(Dp)]
         self.slot_labels = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in range(Dp)]
         self.slot_logits = [torch.zeros(B, dtype=torch.float32, device=dev) for _ in range(Dp)]
         self.slot_loss = [torch.zeros((), dtype=torch.float32, device=dev) for _ in range(Dp)]
-        self.zero_cols = [torch.zeros(B, dtype=idt, device=dev) for _ in range(2)]
-        self._lib = _lib.load()
-        self._ne = (C.c_int64 * 2)(*N)
-        self._slot_ptrs = [_lib.ptr_array(c) for c in self.slot_cols]
+        if self.mode == "pipelined":
+            self.slot_cols = [[torch.zeros(B, dtype=idt, device=dev) for _ in range(2)] for _ in range(Dp)]
+            self.zero_cols = [torch.zeros(B, dtype=idt, device=dev) for _ in range(2)]
+            self._slot_ptrs = [_lib.ptr_array(c) for c in self.slot_cols]
+        else:
+            # values capacity per slot: twice the largest first batch (a larger batch: generic path)
+            self.vcap = max(2 * int(ag[A_NNZ]), 2 * B)
+            self.slot_values = [torch.zeros(self.vcap, dtype=idt, device=dev) for _ in range(Dp)]
+            self.slot_offsets = [torch.zeros(2 * B + 1, dtype=torch.int32, device=dev) for _ in range(Dp)]
+        self._ne2 = (C.c_int64 * 2)(*self.N)
         self._idt = _lib.id_dtype_code(idt)
         self._group = self._adam_group()
-        # graphs with the collectives inside need RCCL (gloo collectives are not capturable)
-        self.graph_mode = dist.get_backend(ebc._pg) == "nccl"
+        # graphs with the collectives inside: the device-initiated exchange (any backend) or RCCL
+        self.graph_mode = isinstance(self.comm, PeerComm) or dist.get_backend(ebc._pg) == "nccl"
         if self.graph_mode:
             try:
                 self._capture()
             except Exception as e:  # noqa: BLE001 - the same collectives run eagerly
                 import sys
 
-                print(f"dropin (sharded): graph capture with collectives refused ({e}); eager steps", file=sys.stderr)
+                print(f"dropin (sharded): graph capture refused ({e}); eager steps", file=sys.stderr)
                 torch.cuda.synchronize(dev)
                 self.graphs, self.graph_mode = [], False
+                if self.mode == "pipelined":
+                    st.reset_pipeline()
+        if self.mode == "kjt":
+            st.cursor = 0
 
-    def _cols_of(self, kjt, B):
-        """Host-side view of a batch's single-hot ids as id columns (the capacity probe only)."""
-        o = kjt.offsets().to(torch.int64)
-        v = kjt.values()
-        cols = []
-        for f in range(2):
-            ln = o[f * B + 1:(f + 1) * B + 1] - o[f * B:(f + 1) * B]
-            c = torch.zeros(B, dtype=torch.int64, device=v.device)
-            idx = o[f * B:(f + 1) * B][ln > 0]
-            c[ln > 0] = v[idx].to(torch.int64) % self.ebc._embedding_bag_configs[f].num_embeddings
-            c[(ln > 0) & (c == 0)] = self.ebc._embedding_bag_configs[f].num_embeddings  # row 0 kept
-            cols.append(c)
-        return cols
+    def _kjt_step(self, slot: int) -> None:
+        st = self.step
+        keep = st.logits, st.loss
+        st.logits, st.loss = self.slot_logits[slot], self.slot_loss[slot]
+        try:
+            st.step(self.slot_values[slot], self.slot_offsets[slot], self.slot_labels[slot])
+        finally:
+            st.logits, st.loss = keep
 
     def _pipelined(self, slot: int, parity: int, next2) -> None:
         st = self.step
@@ -609,9 +772,12 @@ class FusedShardedDropin:
             st.logits, st.loss = keep
 
     def _capture(self) -> None:
-        """Slot k's graph: the pipelined step on slot k (parity k % 2) routing slot k + 2."""
+        """Slot k's graph: pipelined, the step on slot k (parity k % 2) routing slot k + 2; kjt, the
+        step on slot k's batch."""
         st, Dp, dev = self.step, self.depth, self.device
         self.lr_captured = st.lr_dense
+        if self.mode == "kjt" and not self.graphs:
+            st.warmup()  # communicators, workspaces (the training state is left as it was)
         st.comm.retire()
         self.graphs = []
         torch.cuda.synchronize(dev)
@@ -621,40 +787,76 @@ class FusedShardedDropin:
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                    self._pipelined(k, k % 2, self.slot_cols[(k + 2) % Dp])
+                    if self.mode == "kjt":
+                        self._kjt_step(k)
+                    else:
+                        self._pipelined(k, k % 2, self.slot_cols[(k + 2) % Dp])
             torch.cuda.current_stream(dev).wait_stream(s)
             _lib.graph_upload(g, dev)
             self.graphs.append(g)
         torch.cuda.synchronize(dev)
 
     # ---- staging -----------------------------------------------------------------------------
+    def _stage(self, x: _Item, batch, offs) -> None:
+        """The batch into slot seq % depth (main stream): pipelined, its single-hot ids as id columns
+        (tt_kjt_single_hot_cols); kjt, its values / offsets copied; labels as int32."""
+        kjt = batch.sparse_features
+        v = kjt.values()
+        slot = x.seq % self.depth
+        lab = batch.labels
+        stream = torch.cuda.current_stream(self.device)
+        if self.mode == "pipelined":
+            _lib.check(self._lib.tt_kjt_single_hot_cols(
+                2, self.step.B, v.data_ptr() if v.numel() else self.slot_cols[slot][0].data_ptr(), self._idt,
+                offs.data_ptr(), self._ne2, self._slot_ptrs[slot], self.err.data_ptr(), lab.data_ptr(),
+                _lib.TT_I64 if lab.dtype == torch.int64 else _lib.TT_I32, self.slot_labels[slot].data_ptr(),
+                stream.cuda_stream), "kjt_single_hot_cols")
+        else:
+            if v.numel():
+                self.slot_values[slot][:v.numel()].copy_(v, non_blocking=True)
+            self.slot_offsets[slot].copy_(offs, non_blocking=True)
+            self.slot_labels[slot].copy_(lab, non_blocking=True)
+        x.slot, x.parity, x.labels = slot, x.seq % 2, lab
+
     def _fetch(self, it: Iterator) -> Optional[_Item]:
         try:
             batch = next(it)
         except StopIteration:
             return None
         batch = batch.to(self.device, non_blocking=True)
-        if not self.fusable(batch):
-            return _Item(batch)
-        kjt = batch.sparse_features
+        x = _Item(batch)
+        x.seq = self._seq
+        self._seq += 1
+        ok = self._local_ok(batch)
+        offs = self._offsets32(batch.sparse_features) if ok else None
         if self.step is None:
-            if int(kjt.lengths().max()) > 1 if kjt.lengths().numel() else False:
-                return _Item(batch)
-            self._make_step(batch)
-        v = kjt.values()
-        k = self.k
-        self.k += 1
-        slot = k % self.depth
-        offs = kjt.offsets()
-        if offs.dtype != torch.int32:
-            offs = offs.to(torch.int32)
-        lab = batch.labels
-        _lib.check(self._lib.tt_kjt_single_hot_cols(
-            2, self.step.B, v.data_ptr() if v.numel() else self.slot_cols[slot][0].data_ptr(), self._idt,
-            offs.data_ptr(), self._ne, self._slot_ptrs[slot], self.err.data_ptr(), lab.data_ptr(),
-            _lib.TT_I64 if lab.dtype == torch.int64 else _lib.TT_I32, self.slot_labels[slot].data_ptr(),
-            torch.cuda.current_stream(self.device).cuda_stream), "kjt_single_hot_cols")
-        return _Item(batch, slot, k % 2, lab)
+            adm, ag = self._admit_first(batch, ok, offs)
+            x.agreed = ag
+            if not adm:
+                self._note(self._reason(ag, first=True))
+                return x
+            self._make_step(batch, ag)
+            self._stage(x, batch, offs)
+            return x
+        if ok:
+            j = x.seq % _RING
+            main = torch.cuda.current_stream(self.device)
+            ev0 = torch.cuda.Event()
+            ev0.record(main)
+            with torch.cuda.stream(self._astream):
+                self._astream.wait_event(ev0)
+                self._counts(batch, offs, self._aout[j], self._astream)
+                self._ahost[j].copy_(self._aout[j], non_blocking=True)
+                x.event = torch.cuda.Event()
+                x.event.record(self._astream)
+            offs.record_stream(self._astream)
+            batch.sparse_features.values().record_stream(self._astream)
+            x.adm = self._ahost[j]  # the counts until _poll turns them into the vector
+            self._stage(x, batch, offs)
+        else:
+            x.adm = self._vector(False, batch, None)
+        self._pending.append(x)
+        return x
 
     def _fill(self, it: Iterator) -> None:
         while len(self.queue) < 3:
@@ -663,27 +865,21 @@ class FusedShardedDropin:
                 break
             self.queue.append(x)
 
+    def _note(self, why: str) -> None:
+        if why:
+            self.rejected[why] = self.rejected.get(why, 0) + 1
+
     def _reset(self) -> None:
-        if self.step is not None and self.dirty:
+        if self.mode == "pipelined" and self.step is not None and self.dirty:
             self.step.reset_pipeline()
         self.staged = self.dirty = False
 
     def check_errors(self) -> None:
-        """Raise (on every rank) if a converted batch had a multi-id bag or an id out of range, or a
-        route overflowed a segment's capacity (collective)."""
-        import torch.distributed as dist
-
-        e = self.err.clone()
-        dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.ebc._pg)
+        """Raise (on every rank) if a step received a key outside its shard or a device-initiated
+        exchange timed out (collective). Multi-id bags, ids out of range and segment overflows never
+        reach a fused step (the agreed admission sends such batches down the generic path)."""
         if self.step is not None:
             self.step.check()
-        if int(e.item()):
-            self.err.zero_()
-            raise _lib.TTError("dropin (sharded): a KJT batch had a bag of several ids or an id outside [0, N) "
-                               "(single-hot bags only on this path). The fused step trained on the converted "
-                               "batch and the ones after it in this chunk: the model state is not what the "
-                               "reference's loop would hold — restore a checkpoint, or run such data with "
-                               "TT_DROPIN_FUSED=0")
 
     def sync_optimizer_state(self) -> None:
         if self.step is None:
@@ -696,9 +892,11 @@ class FusedShardedDropin:
         return bool(self.queue)
 
     def drain_to(self, pipeline) -> None:
-        """Mode switch with batches fetched: hand them back to the generic pipeline in order."""
+        """Mode switch with batches fetched: hand them back to the generic pipeline in order (their
+        agreements completed first: every rank reduced every batch it fetched)."""
         from .torchrec.distributed.train_pipeline import _Staged
 
+        self._settle()
         items, self.queue = self.queue, []
         self._reset()
         if items:
@@ -709,19 +907,49 @@ class FusedShardedDropin:
     # ---- one progress() ----------------------------------------------------------------------
     def progress(self, it: Iterator) -> Any:
         self._fill(it)
+        self._poll()
         if not self.queue:
+            self._settle()
             self._reset()
             self.check_errors()
             self.sync_optimizer_state()
             raise StopIteration
         cur = self.queue[0]
+        if cur.slot is not None and self.step is not None:
+            why = self._reason(self._agreed(cur))
+            if why:  # some rank cannot run it fused: every rank runs it through the generic path
+                self._note(why)
+                cur.slot = None
+                if self.mode == "pipelined":
+                    self.step.flags[0:1].zero_()  # an overflow of THIS batch's route (dropped lookups, untrained)
         if cur.slot is None:
             self._reset()
             out = self._generic(cur.batch)
+        elif self.mode == "kjt":
+            out = self._fused_kjt(cur)
         else:
             out = self._fused()
         self.queue.pop(0)
         return out
+
+    def _relr(self) -> None:
+        lr = self._group["lr"]
+        if lr != self.step.lr_dense:  # the plans carry Adam's lr: re-capture after a change
+            self.step.lr_dense = float(lr)
+            if self.graph_mode:
+                if self.mode == "pipelined" and self.dirty:
+                    self.step.reset_pipeline()
+                    self.staged = self.dirty = False
+                self._capture()
+
+    def _fused_kjt(self, cur: _Item) -> Any:
+        self._relr()
+        if self.graph_mode:
+            self.graphs[cur.slot].replay()
+        else:
+            self._kjt_step(cur.slot)
+        self.steps_fused += 1
+        return self.slot_loss[cur.slot], self.slot_logits[cur.slot], cur.labels
 
     def _fused(self) -> Any:
         st = self.step
@@ -729,11 +957,7 @@ class FusedShardedDropin:
         cur = q[0]
         nxt = q[1] if len(q) > 1 and q[1].slot is not None else None
         nxt2 = q[2] if nxt is not None and len(q) > 2 and q[2].slot is not None else None
-        lr = self._group["lr"]
-        if lr != st.lr_dense:  # the plans carry Adam's lr: re-capture after a change
-            st.lr_dense = float(lr)
-            if self.graph_mode:
-                self._capture()
+        self._relr()
         if not self.staged:
             st.prime(self.slot_cols[cur.slot], cur.parity,
                      self.slot_cols[nxt.slot] if nxt is not None else self.zero_cols)

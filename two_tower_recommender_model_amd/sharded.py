@@ -662,8 +662,11 @@ class FusedShardedTwoTowerStep:
         self.local_rows = local_rows
         self._adopted = tables is not None
         if self._adopted:
+            # a shard of no rows may be a one-row placeholder (ShardedEmbeddingBagCollection allocates
+            # max(1, n) rows, torchrec/distributed/embeddingbag.py): no key ever reaches it
             if tables.T != F or tables.dims != [D] * F or tables.device != dev or \
-                    any(tables.rows[f] != local_rows[f] for f in range(F)):
+                    any(tables.rows[f] != local_rows[f] and not (local_rows[f] == 0 and tables.rows[f] <= 1)
+                        for f in range(F)):
                 raise _lib.TTError(f"sharded step: adopted tables must be this rank's shards (rows {local_rows}, "
                                    f"dim {D}), feature f -> table f; got rows {tables.rows}")
             self.tables = tables

@@ -72,12 +72,15 @@ class FusedShardedKJTStep:
                  batch_size: int, device: torch.device, cap: int, sharding: Optional[Sequence[str]] = None,
                  tw_owners: Optional[Sequence[int]] = None, num_query_features: int = 1, lr_emb: float = 0.01,
                  lr_dense: float = 0.01, eps: float = 1e-10, seed: int = 0,
-                 full_tables: Optional[Sequence[torch.Tensor]] = None):
+                 full_tables: Optional[Sequence[torch.Tensor]] = None, tables: Optional[ops.TableSet] = None):
         """Features 0 .. Fq-1 feed the query tower (concatenated), Fq .. F-1 the candidate tower; one
         table per feature, ``sharding[f]`` "row_wise" (block ceil(N/W)) or "table_wise" (owner
         ``tw_owners[f]``). ``cap``: ids per destination block of exchange A. ``full_tables`` (CPU,
         optional) give the initial weights, else each rank draws its shard from U(-sqrt(1/N),
-        sqrt(1/N)); tower parameters from ``seed``, identical on every rank (DDP's broadcast)."""
+        sqrt(1/N)); tower parameters from ``seed``, identical on every rank (DDP's broadcast).
+        ``tables``: adopt this rank's shards (table f = feature f's local shard; a shard of no rows
+        may be a placeholder of one row, as ShardedEmbeddingBagCollection allocates) instead of
+        allocating them — trained in place, not initialised (the N > 1 drop-in, dropin.py)."""
         self.comm = comm
         self.W, self.rank = comm.world, comm.rank
         W, r = self.W, self.rank
@@ -114,9 +117,17 @@ class FusedShardedKJTStep:
                 self.local_rows.append(self.N[f] if owners[f] == r else 0)
             else:
                 raise _lib.TTError(f"sharding must be row_wise / table_wise, got {self.sharding[f]}")
-        self.tables = ops.TableSet([max(1, n) for n in self.local_rows], [D] * F, list(range(F)), dev)
-        self.tables.weights.zero_()
-        for f in range(F):
+        if tables is not None:
+            if tables.T != F or tables.dims != [D] * F or tables.device != dev or any(
+                    tables.rows[f] != self.local_rows[f] and not (self.local_rows[f] == 0 and tables.rows[f] <= 1)
+                    for f in range(F)):
+                raise _lib.TTError(f"sharded KJT step: adopted tables must be this rank's shards (rows "
+                                   f"{self.local_rows}, dim {D}), feature f -> table f; got rows {tables.rows}")
+            self.tables = tables
+        else:
+            self.tables = ops.TableSet([max(1, n) for n in self.local_rows], [D] * F, list(range(F)), dev)
+            self.tables.weights.zero_()
+        for f in range(F if tables is None else 0):
             n = self.local_rows[f]
             if not n:
                 continue
@@ -202,6 +213,21 @@ class FusedShardedKJTStep:
         self.graphs: list = []
         self._pool_inputs: list = []
         torch.cuda.synchronize(dev)
+
+    def layer_views(self):
+        """[(W, b)] per tower (query, candidate) as views of the flat parameter buffer."""
+        out, o = [], 0
+        for t in range(2):
+            layers, i = [], self.in_dims[t]
+            for n in self.layer_sizes:
+                w = self.params[o:o + n * i].view(n, i)
+                o += n * i
+                b = self.params[o:o + n]
+                o += n
+                layers.append((w, b))
+                i = n
+            out.append(layers)
+        return out
 
     # ---- the step ------------------------------------------------------------------------------
     def _route(self, values: torch.Tensor, offsets: torch.Tensor) -> None:
