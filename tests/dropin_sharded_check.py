@@ -159,18 +159,38 @@ def compare_with_generic(args, world, rank, device, lr, batches, a, outs_a):
         wa, wb = sebc_a._ts.weights, sebc_b._ts.weights
         w0 = init["weights"]
         da, db = wa - w0, wb - w0  # the updates (rows untouched by both: exactly 0)
-        err = (da - db).abs().max().item()
-        scale = db.abs().max().item()
-        worst["rows"] = err / max(scale, 1e-30)
-        assert err <= 5e-2 * scale + 1e-7, f"rank {rank}: shard updates differ by {err} (largest {scale})"
         D = args.dim
-        assert torch.equal((da.view(-1, D) != 0).any(dim=-1), (db.view(-1, D) != 0).any(dim=-1)), \
-            f"rank {rank}: touched rows differ"
-    for p, q in zip(tparams_a, tparams_b):
-        err = (p.detach() - q.detach()).abs().max().item()
-        scale = q.detach().abs().max().item()
-        worst["towers"] = max(worst["towers"], err / max(scale, 1e-30))
-        assert err <= 2e-2 * scale + 1e-6, f"rank {rank}: tower parameter differs by {err} (largest {scale})"
+        # every lookup reached its row in both runs: the same rows moved (a dropped lookup would
+        # leave its row untouched in one of them)
+        ta, tb = (da.view(-1, D) != 0).any(dim=-1), (db.view(-1, D) != 0).any(dim=-1)
+        assert torch.equal(ta, tb), f"rank {rank}: touched rows differ ({int((ta != tb).sum())} rows)"
+        e = (da - db).abs().view(-1, D)[tb]
+        scale = db.abs().max().item()
+        q = torch.quantile(e.flatten().float()[:1 << 24], torch.tensor([0.5, 0.99, 0.999], device=e.device)).tolist()
+        err = e.max().item()
+        worst["rows"] = err / max(scale, 1e-30)
+        print(f"rank {rank}: row updates |fused - generic| p50 {q[0]:.3g} p99 {q[1]:.3g} p99.9 {q[2]:.3g} max {err:.3g} "
+              f"(largest update {scale:.3g}, {int(tb.sum())} rows)", flush=True)
+        # the towers round at different points (fused bf16 MFMA chain vs per-op bf16 GEMMs), and the
+        # row-wise Adagrad normalises each row's gradient: a row whose gradient nearly cancels (a
+        # hot row summed over many lookups) moves by a noisy direction in both. Bulk bound + a
+        # loose bound on the worst element
+        assert q[1] <= 2e-2 * scale and q[2] <= 5e-2 * scale and err <= 0.25 * scale, \
+            f"rank {rank}: shard updates differ (p99 {q[1]}, p99.9 {q[2]}, max {err}; largest {scale})"
+    # towers: Adam normalises every element's step (m / sqrt(v): about +-lr at the first steps), so an
+    # element whose gradient is near zero may step either way in the two runs (at most 2 lr per
+    # step apart); the bulk must agree: compare the parameters' updates by quantiles
+    ua = torch.cat([(p.detach() - v).flatten() for p, v in zip(tparams_a, init["towers"])])
+    ub = torch.cat([(q.detach() - v).flatten() for q, v in zip(tparams_b, init["towers"])])
+    e = (ua - ub).abs()
+    q = torch.quantile(e.float(), torch.tensor([0.5, 0.9, 0.99], device=e.device)).tolist()
+    scale = ub.abs().max().item()
+    worst["towers"] = q[2] / max(scale, 1e-30)
+    print(f"rank {rank}: tower updates |fused - generic| p50 {q[0]:.3g} p90 {q[1]:.3g} p99 {q[2]:.3g} max "
+          f"{e.max().item():.3g} (largest update {scale:.3g})", flush=True)
+    steps = len(outs_a)
+    assert q[0] <= 2e-2 * scale and q[1] <= 1e-1 * scale and e.max().item() <= 2 * lr * steps + 1e-6, \
+        f"rank {rank}: tower updates differ (p50 {q[0]}, p90 {q[1]}, max {e.max().item()}; largest {scale})"
     print(f"rank {rank}: fused dispatch vs generic-only run, worst relative: {worst}", flush=True)
     del model_b, opt_b, pipe_b
 

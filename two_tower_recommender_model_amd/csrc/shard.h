@@ -157,72 +157,103 @@ struct GatherSegArgs {
   __bf16* dblk[TT_PEER_MAXW];
 };
 
+// SL slots per half-wave (slot hw + u * nhw, u < SL, nhw = ceil(W S / SL)), their loads, claiming
+// CASes and row gathers interleaved: the launch's grid then fits one round of residency (one slot per
+// half-wave was 2048 workgroups at 16k lookups, past the 8 per CU the combined launch G holds)
+constexpr int GS_SL = 2;
 __device__ __forceinline__ void shard_gather_block(const GatherSegArgs& a, int blk) {
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
+  typedef __attribute__((ext_vector_type(4))) float f32x4g;
   const int lane = threadIdx.x & 63, hl = lane & 31;
   const int64_t n = (int64_t)a.W * a.S;
-  const int64_t i = ((int64_t)blk * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
-  if (i >= n) return;
-  const int64_t s = (int64_t)((uint32_t)i / (uint32_t)a.S), j = i - s * a.S;  // W * S < 2^31 (host-checked)
-  // feature of slot j and its segment start: a loop over the (uniform) feature list with scalar
-  // kernarg loads (a per-lane index into the kernarg arrays is a dependent vector load)
-  int f = 0;
-  int64_t so = a.seg_off[0];
-  for (int q = 1; q < a.F; ++q)
-    if (j >= a.seg_off[q]) {
-      f = q;
-      so = a.seg_off[q];
-    }
-  const int64_t k = j - so;
-  const int64_t* blkp = a.recv + s * a.blk64 + a.cnt64;
-  const int64_t cnt = blkp[f];
-  // the slot's key is loaded beside its segment's count (slot j lies inside the block: a stale
-  // value past the count is never used), not after it: one dependent round trip fewer
-  const uint64_t kraw = (uint64_t)blkp[a.F + j];
-  uint64_t key = DD_EMPTY;
-  const float* src = nullptr;
-  if (k < cnt) {
-    key = kraw;
-    const int t = (int)(key >> DD_TABLE_SHIFT);
-    const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
-    int64_t woff = 0, nrows = 0;
-    int dim = 0;
-    for (int u = 0; u < a.T; ++u)
-      if (u == t) {
-        woff = a.tables[u].weight_offset;
-        nrows = a.tables[u].num_rows;
-        dim = a.tables[u].dim;
+  const int64_t hw = ((int64_t)blk * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const int64_t nhw = (n + GS_SL - 1) / GS_SL;
+  if (hw >= nhw) return;
+  int64_t iu[GS_SL], s[GS_SL], j[GS_SL], kk[GS_SL], cnt[GS_SL];
+  uint64_t kraw[GS_SL];
+  int fu[GS_SL];
+#pragma unroll
+  for (int u = 0; u < GS_SL; ++u) {
+    const int64_t i = hw + u * nhw;
+    iu[u] = i;
+    const int64_t ic = i < n ? i : 0;
+    s[u] = (int64_t)((uint32_t)ic / (uint32_t)a.S);  // W * S < 2^31 (host-checked)
+    j[u] = ic - s[u] * a.S;
+    // feature of slot j and its segment start: a loop over the (uniform) feature list with scalar
+    // kernarg loads (a per-lane index into the kernarg arrays is a dependent vector load)
+    int f = 0;
+    int64_t so = a.seg_off[0];
+    for (int q = 1; q < a.F; ++q)
+      if (j[u] >= a.seg_off[q]) {
+        f = q;
+        so = a.seg_off[q];
       }
-    if (t == f && t < a.T && r < nrows && dim == a.D) {
-      src = a.weights + woff + r * a.D;
-    } else {
-      key = DD_EMPTY;
-      if (hl == 0) atomicOr(a.bad, 1);
+    fu[u] = f;
+    kk[u] = j[u] - so;
+    const int64_t* blkp = a.recv + s[u] * a.blk64 + a.cnt64;
+    // the slot's key is loaded beside its segment's count (slot j lies inside the block: a stale
+    // value past the count is never used), not after it: one dependent round trip fewer
+    cnt[u] = blkp[f];
+    kraw[u] = (uint64_t)blkp[a.F + j[u]];
+  }
+  uint64_t key[GS_SL];
+  const float* src[GS_SL];
+#pragma unroll
+  for (int u = 0; u < GS_SL; ++u) {
+    key[u] = DD_EMPTY;
+    src[u] = nullptr;
+    if (iu[u] < n && kk[u] < cnt[u]) {
+      key[u] = kraw[u];
+      const int t = (int)(key[u] >> DD_TABLE_SHIFT);
+      const int64_t r = (int64_t)(key[u] & ((1ull << DD_TABLE_SHIFT) - 1));
+      int64_t woff = 0, nrows = 0;
+      int dim = 0;
+      for (int q = 0; q < a.T; ++q)
+        if (q == t) {
+          woff = a.tables[q].weight_offset;
+          nrows = a.tables[q].num_rows;
+          dim = a.tables[q].dim;
+        }
+      if (t == fu[u] && t < a.T && r < nrows && dim == a.D) {
+        src[u] = a.weights + woff + r * a.D;
+      } else {
+        key[u] = DD_EMPTY;
+        if (hl == 0) atomicOr(a.bad, 1);
+      }
     }
   }
-  DdPend pend;
-  if (a.dd_on && hl == 0) dd_insert_begin(a.dd, key, (int32_t)i, pend);
-  if (src) {
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
-    typedef __attribute__((ext_vector_type(4))) float f32x4g;
-    __bf16* dst = a.rows_out + (s * a.out_stride + j) * a.D;
+  DdPend pend[GS_SL];
+#pragma unroll
+  for (int u = 0; u < GS_SL; ++u)
+    if (a.dd_on && hl == 0 && iu[u] < n) dd_insert_begin(a.dd, key[u], (int32_t)iu[u], pend[u]);
+  f32x4g v[GS_SL][1];
+#pragma unroll
+  for (int u = 0; u < GS_SL; ++u)
+    v[u][0] = src[u] && hl * 4 < a.D ? *reinterpret_cast<const f32x4g*>(src[u] + hl * 4) : (f32x4g)(0.f);
+#pragma unroll
+  for (int u = 0; u < GS_SL; ++u) {
+    if (!src[u]) continue;
+    __bf16* dst = a.rows_out + (s[u] * a.out_stride + j[u]) * a.D;
     if (a.dW) {  // uniform loop, scalar kernarg loads (s differs per half-wave)
       __bf16* b0 = a.dblk[0];
 #pragma unroll
       for (int q = 1; q < TT_PEER_MAXW; ++q)
-        if (q < a.dW && s == q) b0 = a.dblk[q];
-      dst = b0 + j * a.D;
+        if (q < a.dW && s[u] == q) b0 = a.dblk[q];
+      dst = b0 + j[u] * a.D;
     }
     for (int c = hl * 4; c < a.D; c += 128) {
-      const f32x4g v = *reinterpret_cast<const f32x4g*>(src + c);
+      const f32x4g x = c == hl * 4 ? v[u][0] : *reinterpret_cast<const f32x4g*>(src[u] + c);
       bf16x4v o;
-      o[0] = (__bf16)v[0];
-      o[1] = (__bf16)v[1];
-      o[2] = (__bf16)v[2];
-      o[3] = (__bf16)v[3];
+      o[0] = (__bf16)x[0];
+      o[1] = (__bf16)x[1];
+      o[2] = (__bf16)x[2];
+      o[3] = (__bf16)x[3];
       *reinterpret_cast<bf16x4v*>(dst + c) = o;
     }
   }
-  if (a.dd_on && hl == 0) dd_insert_finish(a.dd, pend, (int32_t)i);
+#pragma unroll
+  for (int u = 0; u < GS_SL; ++u)
+    if (a.dd_on && hl == 0 && iu[u] < n) dd_insert_finish(a.dd, pend[u], (int32_t)iu[u]);
 }
 
 int gather_segs_args(const float* weights, const tt_table_meta_t* tables, int T, int F, int W, const int64_t* recv,

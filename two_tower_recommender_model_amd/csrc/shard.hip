@@ -391,7 +391,7 @@ int tt_shard_gather_segs_bf16(const float* weights, const tt_table_meta_t* table
   if (rc) return rc;
   const int64_t n = (int64_t)W * slots;
   if (n == 0) return TT_OK;
-  shard_gather_segs_kernel<<<dim3((unsigned)ceil_div(n, 8)), dim3(256), 0, as_stream(stream)>>>(a);
+  shard_gather_segs_kernel<<<dim3((unsigned)ceil_div(ceil_div(n, GS_SL), 8)), dim3(256), 0, as_stream(stream)>>>(a);
   return check_launch("shard_gather_segs");
 }
 

@@ -2488,7 +2488,7 @@ __global__ void __launch_bounds__(256) tower_wgrad_insert_kernel(WgradArgs a, co
 // n_dd > 0: the owner's update workgroups come FIRST in the grid (they carry the launch's longest
 // chain, claim -> slot -> rows -> stores; dispatched behind the T2 tiles, the last of them started
 // ~4.5 us late), then the T2 tiles, then the route count
-__global__ void __launch_bounds__(256) tower_wgrad_route_rowwise_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
+__global__ void __launch_bounds__(256, 3) tower_wgrad_route_rowwise_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
                                                                         RouteArgs r, DdUpdateArgs d, int n_t2,
                                                                         int n_cnt, int n_dd) {
   __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
@@ -3605,7 +3605,7 @@ static int fused_grads_route_place_gather(const tt_tower_shape_t* shape, int64_t
   rc = t3_args(shape, B, params, nullptr, nullptr, 0.f, 0.9f, 0.999f, 1e-8f, 0.f, nullptr, 0, base, nullptr, workspace,
                ws_bytes, nullptr, copies == 1 ? 2 : copies, off, scale, 1, 0, a, &g3);
   if (rc) return rc;
-  const int64_t n_place = (int64_t)r.nblk * F, n_gather = ceil_div((int64_t)W * slots, 8);
+  const int64_t n_place = (int64_t)r.nblk * F, n_gather = ceil_div(ceil_div((int64_t)W * slots, GS_SL), 8);
   if (g3 + n_place + n_gather > INT32_MAX) return fail(TT_EINVAL, "tower_grads_place_gather: grid too large");
   tower_grads_place_gather_kernel<<<dim3((unsigned)(g3 + n_place + n_gather)), dim3(256), 0, as_stream(stream)>>>(
       a, r, g, (int)g3, (int)n_place);
