@@ -19,8 +19,11 @@ the pipeline hands the batches to ``FusedTwoTowerStep`` instead:
   dedup table (the ring needs the next batch, which the pipeline has already fetched);
 * progress() returns ``(loss, logits, labels)`` device tensors, as the reference's task does.
 
-Conditions (else the generic per-op path runs, unchanged): world size 1 (the fused sharded step is a
-separate API), ``TwoTowerTrainTask(TwoTower)`` with one feature per tower, equal embedding dims of
+At world size W > 1 (DistributedModelParallel over W processes) ``FusedShardedDropin`` below takes the
+loop instead: the pipelined sharded step for single-hot bags, the sharded KJT step for multi-hot
+bags, each batch admitted by every rank (an agreed per-batch check) or run through the generic DMP
+path on every rank. Conditions at world size 1 (else the generic per-op path runs, unchanged):
+``TwoTowerTrainTask(TwoTower)`` with one feature per tower, equal embedding dims of
 64 or 128, towers [128, 64] in bf16 (the production precision; the fp32 parity mode stays generic),
 fused RowWiseAdagrad on the tables, Adam with default betas / eps and no weight decay, SUM pooling,
 a KJT whose keys are (query feature, candidate feature) with bags of at most one id and a batch size
