@@ -334,7 +334,11 @@ def check_adam(p_before, m_before, v_before, step: int, g, e_g, p_got, m_got, v_
     for name, got, want, e in (("exp_avg", m_got, m, e_m), ("exp_avg_sq", v_got, v, e_v), ("param", p_got, p, e_p)):
         lim = e + 1e-5 * want.abs() + (1e-6 * lr if name == "param" else 1e-30)
         bad = ~((got.double() - want).abs() <= lim)
-        assert not bool(bad.any()), f"{what} Adam {name}: {int(bad.sum())} of {want.numel()} outside the bound"
+        if bool(bad.any()):
+            idx = torch.nonzero(bad).flatten()[:6].tolist()
+            detail = "; ".join(f"[{i}] got {float(got[i]):.9g} want {float(want[i]):.9g} lim {float(lim[i]):.3g} "
+                               f"g {float(g[i]):.4g} e_g {float(e_g[i]):.3g}" for i in idx)
+            raise AssertionError(f"{what} Adam {name}: {int(bad.sum())} of {want.numel()} outside the bound: {detail}")
 
 
 def rel_err(got: torch.Tensor, want: torch.Tensor) -> float:
