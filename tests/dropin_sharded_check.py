@@ -313,6 +313,10 @@ def main():
         assert torch.equal(st.exp_avg_sq, ref.exp_avg_sq)
         assert tparams[0].data_ptr() == st.params.data_ptr()
         del ref
+        # and the whole run against the generic DMP path on the same batches
+        stage("generic-only run (kjt)")
+        compare_with_generic(args, world, rank, device, lr, [kjt_multihot_batch(v, ln, lab, device) for v, ln, lab in mh],
+                             (model, sebc, tparams, init), outs)
     else:
         if args.mode == "mixed":
             half = make_cols(N, B // 2, rank, 99)

@@ -2442,7 +2442,22 @@ struct InsertArgs {
   int id_dtype;
   int64_t B;
   DedupWs dd;
+  int xcd_wpt;  // > 0: insert_next_full_block files by T1 tile class (ins_lookup), this many workgroups
+                // per (XCD class, tower); 0: 256 consecutive lookups per workgroup
 };
+// lookup of thread tid in insert workgroup blk (blk < 2B / 256). xcd_wpt > 0 (B % 2048 == 0): the
+// workgroup takes only rows of T1 tiles b (32 rows each) with b = blk (mod 8) — T1's workgroup for
+// tile b runs on XCD b % 8, as this workgroup runs on XCD blk % 8 — so the next batch's ids and the
+// claims T1 reads first are in that XCD's L2 when its T1 tile starts (plain loads and stores keep
+// their lines there). Lookup order is irrelevant to the results: every row's lookups are summed in
+// ascending lookup order whatever their slot positions.
+__device__ __forceinline__ int64_t ins_lookup(const InsertArgs& ins, int blk, int tid) {
+  if (ins.xcd_wpt <= 0) return (int64_t)blk * 256 + tid;
+  const int c = blk & 7, j = blk >> 3;
+  const int t = j / ins.xcd_wpt, qi = j - t * ins.xcd_wpt;
+  const int64_t b = c + 8 * (8 * qi + (tid >> 5));
+  return (int64_t)t * ins.B + 32 * b + (tid & 31);
+}
 
 __device__ __forceinline__ void insert_next_block(const InsertArgs& ins, int blk) {
   const int lane = threadIdx.x & 63;
@@ -2641,7 +2656,8 @@ __device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, in
   uint64_t key[INS_PT];
 #pragma unroll
   for (int u = 0; u < INS_PT; ++u) {
-    const int64_t i = ((int64_t)blk * INS_PT + u) * 256 + threadIdx.x;
+    const int64_t i = INS_PT == 1 ? ins_lookup(ins, blk, (int)threadIdx.x)
+                                  : ((int64_t)blk * INS_PT + u) * 256 + threadIdx.x;
     iv[u] = i;
     key[u] = DD_EMPTY;
     if (i < 2 * ins.B) {
@@ -2912,6 +2928,8 @@ static int insert_args(int64_t B, const void* const* next_cols, int id_dtype, co
   }
   ins.id_dtype = id_dtype;
   ins.B = B;
+  // tile-class filing (ins_lookup): 2B / 256 workgroups, B / 2048 of them per (class, tower)
+  ins.xcd_wpt = (INS_PT == 1 && B % 2048 == 0) ? (int)(B / 2048) : 0;
   dedup_layout(next_dedup_ws, dedup_max_lookups, &ins.dd);
   return TT_OK;
 }
