@@ -11,9 +11,11 @@ These check the GENERIC DMP path (TT_DROPIN_FUSED=0): since round 6 the pipeline
 config 5's multi-hot batches at W > 1 to the fused sharded KJT step (dropin.py, "kjt" mode), which
 tests/test_gpu_dropin_sharded.py checks bit for bit against FusedShardedKJTStep and against this
 generic path's results, and tests/test_gpu_sharded_kjt.py against the oracle at BASELINE sizes.
-(The fused step's Adam also passes an oracle check fed its own tower gradient; against the
-emulated gradient here, a few tower parameters of units dead in both runs land 4e-8 outside the
-1e-5-relative bound, a margin this check was not built for.)"""
+(Run on the dispatched KJT step instead, step 1 of config 5 at W = 2 put 27-31 of the 49,536 tower
+parameters ~4.4e-8 outside this check's Adam bound: parameters whose EMULATED gradient is exactly
+0, all shifted by the same +4.4e-8, about 7e-6 of their Adam step; fp32 Adam arithmetic alone
+accounts for ~1e-7 of it (emulated on the CPU). The cause is not isolated; logits, loss and every
+touched row stayed inside their bounds, profiles/r06g_dmp_kjt_adam_bound.log.)"""
 import os
 import socket
 import subprocess
