@@ -998,7 +998,8 @@ def run_multi(args, world, rank, local_rank):
             "exchange_A_bytes_sent": 4 * step.A_total,
             "exchange_B_bytes_sent": 2 * D * world * step.S[r],
             "collectives_per_step": 2, "mode": mode,
-            "exchange": xdesc,
+            "exchange": xdesc + ("; producers store at the destinations" if getattr(step, "direct", False) else "")
+                        + ("; launch U / Adam signal and wait in-launch" if getattr(step, "merged", False) else ""),
             "overlap": "T2 (tower weight gradients) on a parallel graph branch beside exchange A + the owner's "
                        "update" if step.overlap else "none (one stream)"}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline

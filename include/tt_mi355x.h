@@ -79,7 +79,29 @@ typedef struct {
   const void* copy_src[TT_PEER_MAXW];    /* 16-B aligned; NULL / copy_len 0: nothing to copy */
   void* copy_dst[TT_PEER_MAXW];          /* 16-B aligned mapped address at destination d */
   int64_t copy_len[TT_PEER_MAXW];        /* bytes, a multiple of 16 */
+  int32_t* epoch;                        /* nullable: the exchange's epoch word (this rank's), advanced
+                                            by one by the producer (a tt_peer_wait_t consumer follows) */
 } tt_peer_direct_t;
+
+/* The consumer of such an exchange signals and waits INSIDE its own launch instead of a separate
+ * signal / wait kernel: workgroup 0's first W threads store the epoch into the peers' flag words
+ * for this source (release: system scope when sys, else a relaxed agent-scope store after the
+ * producer's kernel boundary), and every workgroup that reads the received blocks polls this
+ * rank's W flag words (relaxed, bounded by timeout_ticks of s_memrealtime, 100 MHz; a wait that
+ * gives up sets *err, sticky) and then acquires (system scope when sys) before its reads — the
+ * consumer's other roles start at once. The epoch is the one the producer advanced
+ * (tt_peer_direct_t.epoch). Only for ranks on different devices or a single rank: ranks sharing a
+ * device could fill every CU with spinning workgroups (the caller uses the signal / wait kernel
+ * there). */
+typedef struct {
+  int32_t W;                             /* ranks, 1..TT_PEER_MAXW */
+  int32_t sys;                           /* 1: system-scope release / acquire */
+  int32_t* flag[TT_PEER_MAXW];           /* mapped: peer d's flag word for this source */
+  const int32_t* flags;                  /* this rank's W flag words */
+  const int32_t* epoch;                  /* this rank's epoch word of the exchange */
+  int32_t* err;                          /* sticky: a wait gave up */
+  int64_t timeout_ticks;
+} tt_peer_wait_t;
 
 /* status codes (besides hipError_t values, which are all < 1000) */
 #define TT_OK 0
@@ -538,7 +560,10 @@ int tt_tower_grads_replicated(const tt_tower_shape_t* shape, int64_t B, float* p
  * or launch U of the pipelined sharded step) wrote into the workspace: no pow() per thread. */
 int tt_tower_adam_pre_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
                                 int64_t src_stride, float* exp_avg, float* exp_avg_sq, float eps, float beta1,
-                                float beta2, float weight_decay, void* workspace, size_t ws_bytes, void* stream);
+                                float beta2, float weight_decay, void* workspace, size_t ws_bytes,
+                                const tt_peer_wait_t* wait, void* stream);
+/* (wait, nullable, ABI 4: every workgroup waits for the exchange that brought the W gradients;
+ * workgroup 0 signals it first — tt_peer_wait_t) */
 
 /* T3 with the gradient taken from `grads` (data-parallel towers: the all-reduced gradient) instead
  * of T2's partials: Adam + the bf16 weight copies. */
@@ -721,6 +746,9 @@ typedef struct {
   tt_adagrad_role_t adagrad;
   tt_route_role_t route;          /* ROUTE_COUNT / ROUTE_PLACE */
   tt_gather_role_t gather;        /* F and W: the route's */
+  const tt_peer_wait_t* wait;     /* nullable (ABI 4): the ADAGRAD role's workgroups of launch U wait for
+                                     the exchange that brought their gradient rows (the others start
+                                     at once); workgroup 0 signals it first */
 } tt_launch_plan_t;
 
 int tt_launch(const tt_launch_plan_t* plan, void* stream);

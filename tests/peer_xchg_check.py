@@ -48,7 +48,9 @@ def main():
     a = FusedShardedTwoTowerStep(pc, N, D, [128, 64], B, device, full_tables=full, capacity=cap)
     ref_comm = TorchComm() if launched else ThreadComm.group(1)[0]
     b = FusedShardedTwoTowerStep(ref_comm, N, D, [128, 64], B, device, full_tables=full, capacity=cap)
-    print(f"rank {r}: PeerComm memory {pc.memory}", flush=True)
+    print(f"rank {r}: PeerComm memory {pc.memory}, direct {a.direct}, in-launch waits {a.merged}", flush=True)
+    if os.environ.get("TT_PEER_EXPECT_MERGED"):
+        assert a.merged == (os.environ["TT_PEER_EXPECT_MERGED"] == "1"), "in-launch waits not as expected"
     stage("synchronous step")
     a.load_batch(*batches[0])
     a.step()

@@ -52,7 +52,7 @@ def test_launch_plan_layout_matches_the_header(tmp_path):
                "tt_update_role_t": _lib.UpdateRole, "tt_insert_role_t": _lib.InsertRole,
                "tt_resolve_role_t": _lib.ResolveRole, "tt_adagrad_role_t": _lib.AdagradRole,
                "tt_route_role_t": _lib.RouteRole, "tt_gather_role_t": _lib.GatherRole, "tt_peer_put_t": _lib.PeerPut,
-               "tt_peer_direct_t": _lib.PeerDirect}
+               "tt_peer_direct_t": _lib.PeerDirect, "tt_peer_wait_t": _lib.PeerWait}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "tt_mi355x.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} sizeof %zu\\n", sizeof({cname}));')

@@ -25,7 +25,7 @@ def _comm(monkeypatch, W, rank, peers, out):
     monkeypatch.setattr(_lib, "load", lambda path=None: rec)
     monkeypatch.setattr(sharded, "stream_handle", lambda device=None: 0)
     pc = object.__new__(sharded.PeerComm)
-    pc.world, pc.rank, pc.timeout_s, pc.same_device = W, rank, 5.0, False
+    pc.world, pc.rank, pc.timeout_s, pc.same_device, pc.shared_gpu = W, rank, 5.0, False, False
     pc.err = torch.zeros(1, dtype=torch.int32)
     pc._puts = {}
     pc._bufs = {out.data_ptr(): {"peers": peers, "flags": torch.zeros(W, dtype=torch.int32),
@@ -129,6 +129,35 @@ def test_direct_descriptor_addresses_rows_and_copies(monkeypatch):
         pc.direct(out, inp, rowb, out_splits=[rows[r]] * W, in_splits=rows, copy=[(4, 16)] * W)
     with pytest.raises(_lib.TTError, match="do not match"):
         pc.block_dst(out, inp, out_splits=[rows[r] + 1] * W, in_splits=rows)
+
+
+def test_in_launch_wait_descriptor(monkeypatch):
+    """PeerComm.wait_desc (tt_peer_wait_t): the consumer signals peer d's flag word for this source and
+    polls this rank's W flag words against the exchange's epoch word — the one the producer's
+    descriptor (direct(..., epoch=True)) advances; refused when the ranks share a GPU."""
+    W, r, D = 3, 1, 4
+    rows = [8, 8, 8]
+    inp = torch.zeros(sum(rows), D)
+    out = torch.zeros(W * rows[r], D)
+    peers = [(1 << 24, 4096), (2 << 24, 8192), (3 << 24, 1024)]
+    pc, _ = _comm(monkeypatch, W, r, peers, out)
+    e = pc._bufs[out.data_ptr()]
+    x = pc.direct(out, inp, 4 * D, epoch=True)
+    assert x.epoch == e["state"].data_ptr() and not pc.direct(out, inp, 4 * D).epoch
+    assert pc.in_launch_wait
+    w = pc.wait_desc(out)
+    assert (w.W, w.sys) == (W, 1)
+    assert [w.flag[d] for d in range(W)] == [peers[d][0] + peers[d][1] + 4 * r for d in range(W)]
+    assert (w.flags, w.epoch, w.err) == (e["flags"].data_ptr(), e["state"].data_ptr(), pc.err.data_ptr())
+    assert w.timeout_ticks == int(5.0 * 1e8)
+    with pytest.raises(_lib.TTError, match="recv_buffer"):
+        pc.wait_desc(torch.zeros(4))
+    pc.shared_gpu = True  # ranks on one GPU (the scope may still be forced to system): kernels only
+    assert not pc.in_launch_wait
+    with pytest.raises(_lib.TTError, match="share a device"):
+        pc.wait_desc(out)
+    pc.world = 1
+    assert pc.in_launch_wait
 
 
 def test_exchange_comm_falls_back_to_rccl_when_the_self_test_fails(monkeypatch):

@@ -126,7 +126,14 @@ class PeerDirect(C.Structure):
     """tt_peer_direct_t (ABI 4): a producer's stores straight into the destinations' receive buffers."""
     _fields_ = [("W", C.c_int32), ("_pad", C.c_int32), ("first_row", C.c_int64 * TT_PEER_MAXW),
                 ("row0", C.c_void_p * TT_PEER_MAXW), ("copy_src", C.c_void_p * TT_PEER_MAXW),
-                ("copy_dst", C.c_void_p * TT_PEER_MAXW), ("copy_len", C.c_int64 * TT_PEER_MAXW)]
+                ("copy_dst", C.c_void_p * TT_PEER_MAXW), ("copy_len", C.c_int64 * TT_PEER_MAXW),
+                ("epoch", C.c_void_p)]
+
+
+class PeerWait(C.Structure):
+    """tt_peer_wait_t (ABI 4): a consumer launch's in-launch signal / wait of such an exchange."""
+    _fields_ = [("W", C.c_int32), ("sys", C.c_int32), ("flag", C.c_void_p * TT_PEER_MAXW), ("flags", C.c_void_p),
+                ("epoch", C.c_void_p), ("err", C.c_void_p), ("timeout_ticks", C.c_int64)]
 
 
 class GatherRole(C.Structure):
@@ -141,7 +148,7 @@ class LaunchPlan(C.Structure):
     _fields_ = [("roles", C.c_uint32), ("shape", C.POINTER(TowerShape)), ("B", C.c_int64),
                 ("workspace", C.c_void_p), ("ws_bytes", C.c_size_t), ("wgrad", WgradRole), ("update", UpdateRole),
                 ("insert", InsertRole), ("resolve", ResolveRole), ("adagrad", AdagradRole), ("route", RouteRole),
-                ("gather", GatherRole)]
+                ("gather", GatherRole), ("wait", C.POINTER(PeerWait))]
 
 
 class PeerPut(C.Structure):
@@ -300,7 +307,7 @@ SIGNATURES = {
          _i64, _pvp, _vp, _sz, _vp],
     ),
     "tt_tower_adam_pre_grads_sum": (
-        _int, [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _sz, _vp],
+        _int, [_psh, _i64, _vp, _vp, _int, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _sz, C.POINTER(PeerWait), _vp],
     ),
     "tt_tower_fwd_bwd_indexed_multi_bf16": (
         _int,

@@ -154,6 +154,7 @@ struct GatherSegArgs {
   int32_t* bad;
   // direct exchange (dW > 0): source s's slot j -> dblk[s] + j * D (s's mapped receive buffer)
   int dW;
+  int32_t* epoch;  // nullable: exchange B's epoch word, advanced by launch G's workgroup 0
   __bf16* dblk[TT_PEER_MAXW];
 };
 

@@ -1456,6 +1456,7 @@ struct UpdateArgs {
   int in_srcs;
   int64_t in_stride;
   char* wimg;  // nullable: the row-owned T1's weight image (rk_off), written beside the other copies
+  PxWait wt;   // W > 0: every workgroup waits for the exchange that brought grads_in (workgroup 0 signals)
 #if TT_EXPERIMENTS
   int64_t* stamps;  // EXPERIMENT (TT_RING_STAMPS): [workgroups][4] s_memrealtime per phase
 #endif
@@ -1953,6 +1954,10 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
         if (px_copy_unit(a.xd, u, s2, d2)) *d2 = *s2;
       }
     }
+    // the exchange's epoch advances with its producer (a consumer that signals / waits in-launch
+    // reads it after this kernel's boundary)
+    if (a.xd.epoch && blockIdx.x == 0 && threadIdx.x == 0)
+      __hip_atomic_fetch_add(a.xd.epoch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   RK_STAMP(15);
 }
@@ -2505,9 +2510,16 @@ __global__ void __launch_bounds__(256) tower_wgrad_insert_kernel(WgradArgs a, co
 // ~4.5 us late), then the T2 tiles, then the route count
 __global__ void __launch_bounds__(256, 3) tower_wgrad_route_rowwise_kernel(WgradArgs a, const WgradTile* __restrict__ tiles,
                                                                         RouteArgs r, DdUpdateArgs d, int n_t2,
-                                                                        int n_cnt, int n_dd) {
+                                                                        int n_cnt, int n_dd, PxWait w) {
   __shared__ __attribute__((aligned(16))) char smem[T2_SMEM];
   int b = (int)blockIdx.x;
+  if (w.W) {
+    // in-launch exchange A: workgroup 0 signals; it and the owner's update workgroups (the only
+    // readers of the received blocks) wait — workgroup 0 always, so a rank with no update
+    // workgroups still holds launch G back until every peer consumed its exchange-B buffer
+    if (b == 0) px_signal(w);
+    if (b == 0 || (n_dd > 0 ? b < n_dd : b >= n_t2 + n_cnt)) px_wait(w);
+  }
   if (n_dd > 0) {
     if (b < n_dd) {
       dd_update_block(d, b, smem);
@@ -2528,6 +2540,10 @@ __global__ void __launch_bounds__(256, 3) tower_wgrad_route_rowwise_kernel(Wgrad
 
 __device__ __forceinline__ void update_block(const UpdateArgs& a, int bid, int nblocks) {
   T3_STAMP(0);
+  if (a.wt.W) {
+    if (bid == 0) px_signal(a.wt);
+    px_wait(a.wt);
+  }
   const int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   int64_t t_step = 0;
   float step_size = 0.f, bc2_sqrt = 1.f;
@@ -2597,6 +2613,8 @@ __global__ void __launch_bounds__(256) tower_grads_place_gather_kernel(UpdateArg
   __shared__ int base[RT_MAXW];
   __shared__ int wc[RT_BLOCK / 64][RT_MAXW];
   const int b = (int)blockIdx.x;
+  if (g.epoch && b == 0 && threadIdx.x == 0)  // exchange B's epoch advances with its producer
+    __hip_atomic_fetch_add(g.epoch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (b < n_upd) {
     update_block(a, b, n_upd);
   } else if (b < n_upd + n_place) {
@@ -3359,13 +3377,15 @@ static int launch_t3(const tt_tower_shape_t* shape, int64_t B, float* params, fl
                      int do_adam, float* grads_out, const float* grads_in, void* workspace, size_t ws_bytes,
                      void* stream, const float* adam_pre = nullptr, const DdUpdateArgs* dd = nullptr,
                      int64_t dd_grid = 0, int out_copies = 1, const int64_t* out_off = nullptr,
-                     float out_scale = 1.f, int in_srcs = 1, int64_t in_stride = 0) {
+                     float out_scale = 1.f, int in_srcs = 1, int64_t in_stride = 0,
+                     const tt_peer_wait_t* wait = nullptr) {
   UpdateArgs a;
   int64_t g3 = 0;
   int rc = t3_args(shape, B, params, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_state, do_adam,
                    grads_out, grads_in, workspace, ws_bytes, adam_pre, out_copies, out_off, out_scale, in_srcs,
                    in_stride, a, &g3);
   if (rc) return rc;
+  if ((rc = peer_wait_args(wait, a.wt, "tower_update"))) return rc;
   if (dd) {
     if (dd_grid + g3 > INT32_MAX) return fail(TT_EINVAL, "tower_update_rowwise_adagrad: grid too large");
     tower_update_dedup_kernel<<<dim3((unsigned)(dd_grid + g3)), dim3(256), 0, as_stream(stream)>>>(a, *dd, (int)dd_grid);
@@ -3452,15 +3472,17 @@ int tt_tower_grads_replicated(const tt_tower_shape_t* shape, int64_t B, float* p
 
 int tt_tower_adam_pre_grads_sum(const tt_tower_shape_t* shape, int64_t B, float* params, const float* grads, int nsrc,
                                 int64_t src_stride, float* exp_avg, float* exp_avg_sq, float eps, float beta1,
-                                float beta2, float weight_decay, void* workspace, size_t ws_bytes, void* stream) {
+                                float beta2, float weight_decay, void* workspace, size_t ws_bytes,
+                                const tt_peer_wait_t* wait, void* stream) {
   TowerLayout L;
   int rc = tower_layout(shape, B, &L);
   if (rc) return rc;
   if (!workspace || ws_bytes < L.total) return fail(TT_ECAPACITY, "tower: workspace too small");
   if (!grads || nsrc < 1 || (nsrc > 1 && src_stride < L.P)) return fail(TT_EINVAL, "tower_adam_pre_grads_sum: bad gradient");
+  if (wait && wait->W != nsrc) return fail(TT_EINVAL, "tower_adam_pre_grads_sum: wait.W must be nsrc");
   const float* pre = reinterpret_cast<const float*>(reinterpret_cast<const char*>(workspace) + L.o_counter);
   return launch_t3(shape, B, params, exp_avg, exp_avg_sq, 0.f, beta1, beta2, eps, weight_decay, nullptr, 1, nullptr,
-                   grads, workspace, ws_bytes, stream, pre, nullptr, 0, 1, nullptr, 1.f, nsrc, src_stride);
+                   grads, workspace, ws_bytes, stream, pre, nullptr, 0, 1, nullptr, 1.f, nsrc, src_stride, wait);
 }
 
 }  // extern "C"
@@ -3521,8 +3543,10 @@ static int fused_wgrad_route_count_adagrad(const tt_tower_shape_t* shape, int64_
                                            const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
                                            const float* emb_grad, int64_t ldg, float* weights, float* state,
                                            float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                           int64_t dedup_max_lookups, void* stream) {
+                                           int64_t dedup_max_lookups, const tt_peer_wait_t* wait, void* stream) {
   if (!adam_step_state) return fail(TT_EINVAL, "tower_wgrad_route_rowwise: null Adam step state");
+  PxWait pw;
+  if (int rc = peer_wait_args(wait, pw, "tower_wgrad_route_rowwise")) return rc;
   WgradArgs a{};
   int64_t wgs = 0;
   int rc = wgrad_args(shape, B, loss, workspace, ws_bytes, a, &wgs);
@@ -3552,7 +3576,7 @@ static int fused_wgrad_route_count_adagrad(const tt_tower_shape_t* shape, int64_
 #endif
   tower_wgrad_route_rowwise_kernel<<<dim3((unsigned)(wgs + n_cnt + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
       a, reinterpret_cast<const WgradTile*>(reinterpret_cast<char*>(workspace) + a.tiles_off), r, d, (int)wgs,
-      (int)n_cnt, dd_first ? (int)dd_grid : 0);
+      (int)n_cnt, dd_first ? (int)dd_grid : 0, pw);
   return check_launch("tower_wgrad_route_count_rowwise_adagrad");
 }
 
@@ -3564,7 +3588,9 @@ static int fused_route_count_adagrad(int F, int64_t B, const void* const* cols, 
                                      const tt_feature_meta_t* features, int Fsrc, int64_t emb_B,
                                      const float* emb_grad, int64_t ldg, float* weights, float* state,
                                      float emb_lr, float emb_eps, void* dedup_ws, size_t dedup_ws_bytes,
-                                     int64_t dedup_max_lookups, void* stream) {
+                                     int64_t dedup_max_lookups, const tt_peer_wait_t* wait, void* stream) {
+  PxWait pw;
+  if (int rc = peer_wait_args(wait, pw, "shard_route_count_rowwise_adagrad")) return rc;
   // launch U of the pipelined sharded step without its T2 tiles (those run on a parallel branch of
   // the step graph, beside exchange A): the owner's update workgroups first, then the route count
   RouteArgs r{};
@@ -3580,7 +3606,7 @@ static int fused_route_count_adagrad(int F, int64_t B, const void* const* cols, 
   if (n_cnt + dd_grid > INT32_MAX) return fail(TT_EINVAL, "shard_route_count_rowwise_adagrad: grid too large");
   WgradArgs a{};
   tower_wgrad_route_rowwise_kernel<<<dim3((unsigned)(n_cnt + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
-      a, nullptr, r, d, 0, (int)n_cnt, (int)dd_grid);
+      a, nullptr, r, d, 0, (int)n_cnt, (int)dd_grid, pw);
   return check_launch("shard_route_count_rowwise_adagrad");
 }
 
@@ -3614,6 +3640,7 @@ static int fused_grads_route_place_gather(const tt_tower_shape_t* shape, int64_t
       g.dblk[s] = reinterpret_cast<__bf16*>(direct->row0[s]);
     }
     g.dW = W;
+    g.epoch = direct->epoch;
   }
   int64_t off[16];
   for (int q = 0; q < copies; ++q) off[q] = offsets[q];
@@ -3879,6 +3906,10 @@ int tt_launch(const tt_launch_plan_t* p, void* stream) {
                                                          "(adagrad.multi_only = 1)"
                                                        : "launch: this plan updates every row (adagrad.multi_only = 0)");
   };
+  // the in-launch exchange wait is launch U's alone
+  if (p->wait && p->roles != (TT_ROLE_WGRAD | TT_ROLE_ROUTE_COUNT | TT_ROLE_ADAGRAD) &&
+      p->roles != (TT_ROLE_ROUTE_COUNT | TT_ROLE_ADAGRAD))
+    return fail(TT_EINVAL, "launch: only launch U (ROUTE_COUNT | ADAGRAD [| WGRAD]) takes a wait");
   auto adam_mode = [&]() {
     return u.replicated ? fail(TT_EINVAL, "launch: this plan's UPDATE role runs Adam (update.replicated = 0)") : TT_OK;
   };
@@ -3927,13 +3958,13 @@ int tt_launch(const tt_launch_plan_t* p, void* stream) {
                                              r.num_embeddings, r.block_sizes, r.owners, r.W, r.segs, r.send, r.pos_in,
                                              r.pos_out, r.overflow, r.route_ws, r.route_ws_bytes, g.tables, g.T,
                                              g.features, g.F, g.B, g.grad, g.ldg, g.weights, g.state, g.lr, g.eps,
-                                             g.dedup_ws, g.dedup_ws_bytes, g.dedup_max_lookups, stream);
+                                             g.dedup_ws, g.dedup_ws_bytes, g.dedup_max_lookups, p->wait, stream);
     case TT_ROLE_ROUTE_COUNT | TT_ROLE_ADAGRAD:
       if ((rc = need_multi(0))) return rc;
       return fused_route_count_adagrad(r.F, B, r.cols, r.id_dtype, r.num_embeddings, r.block_sizes, r.owners, r.W,
                                        r.segs, r.send, r.pos_in, r.pos_out, r.overflow, r.route_ws, r.route_ws_bytes,
                                        g.tables, g.T, g.features, g.F, g.B, g.grad, g.ldg, g.weights, g.state, g.lr,
-                                       g.eps, g.dedup_ws, g.dedup_ws_bytes, g.dedup_max_lookups, stream);
+                                       g.eps, g.dedup_ws, g.dedup_ws_bytes, g.dedup_max_lookups, p->wait, stream);
     case TT_ROLE_UPDATE | TT_ROLE_ROUTE_PLACE | TT_ROLE_GATHER:
       if (!u.replicated) return fail(TT_EINVAL, "launch: launch G's UPDATE role writes the replicated gradient "
                                                 "(update.replicated = 1)");

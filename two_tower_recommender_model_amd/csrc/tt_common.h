@@ -44,6 +44,75 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// a consumer launch's in-launch signal / wait of a device-initiated exchange (tt_peer_wait_t),
+// by value in the kernel arguments; W = 0: none
+struct PxWait {
+  int32_t W, sys;
+  int32_t* flag[TT_PEER_MAXW];
+  const int32_t* flags;
+  const int32_t* epoch;
+  int32_t* err;
+  int64_t ticks;
+};
+// workgroup 0, threads [0, W): store the epoch into every peer's flag word for this source
+__device__ __forceinline__ void px_signal(const PxWait& w) {
+  const int s = (int)threadIdx.x;
+  if (s < w.W) {
+    const int e = __hip_atomic_load(w.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w.sys)
+      __hip_atomic_store(w.flag[s], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      __hip_atomic_store(w.flag[s], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// every thread of the workgroup: threads [0, W) poll (relaxed) until source s's flag holds the
+// epoch, then acquire; the workgroup's barrier releases the others. A wait past the timeout sets
+// *err (sticky) and goes on (the data is then invalid).
+__device__ __forceinline__ void px_wait(const PxWait& w) {
+  const int s = (int)threadIdx.x;
+  if (s < w.W) {
+    // the epoch and the first poll of the flag in flight together (one round trip, not two)
+    const int e = __hip_atomic_load(w.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int f = __hip_atomic_load(w.flags + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+    bool late = false;
+    while (f < e) {
+      if ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 > w.ticks) {
+        late = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      f = __hip_atomic_load(w.flags + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (late) __hip_atomic_fetch_or(w.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w.sys)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// host: a tt_peer_wait_t into kernel arguments (W = 0 for none)
+inline int peer_wait_args(const tt_peer_wait_t* p, PxWait& w, const char* who) {
+  w = PxWait{};
+  if (!p) return TT_OK;
+  const std::string s(who);
+  if (p->W < 1 || p->W > TT_PEER_MAXW || !p->flags || !p->epoch || !p->err || p->timeout_ticks <= 0)
+    return fail(TT_EINVAL, s + ": wait.W 1..TT_PEER_MAXW, flags, epoch, err and a timeout");
+  w.W = p->W;
+  w.sys = p->sys ? 1 : 0;
+  for (int d = 0; d < p->W; ++d) {
+    if (!p->flag[d]) return fail(TT_EINVAL, s + ": wait.flag[d] is null");
+    w.flag[d] = p->flag[d];
+  }
+  w.flags = p->flags;
+  w.epoch = p->epoch;
+  w.err = p->err;
+  w.ticks = p->timeout_ticks;
+  return TT_OK;
+}
+
 // host: a direct-exchange descriptor (tt_peer_direct_t) the kernels can follow blindly
 inline int peer_direct_check(const tt_peer_direct_t& x, const char* who) {
   const std::string w(who);

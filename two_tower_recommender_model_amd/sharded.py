@@ -227,6 +227,7 @@ class PeerComm(TorchComm):
         else:
             idents[0] = ident
         self.same_device = ident is not None and all(i == ident for i in idents)
+        self.shared_gpu = self.same_device  # the truth, whatever scope the signalling is forced to
         if os.environ.get("TT_PEER_SYSTEM_SCOPE") == "1":  # tests / measurement: the multi-device signalling
             self.same_device = False
         if self.memory == "device" and not self.same_device:
@@ -418,14 +419,19 @@ class PeerComm(TorchComm):
         return res
 
     def direct(self, out: torch.Tensor, inp: torch.Tensor, unit_bytes: int, out_splits: Optional[List[int]] = None,
-               in_splits: Optional[List[int]] = None, copy: Optional[Sequence[Tuple[int, int]]] = None):
+               in_splits: Optional[List[int]] = None, copy: Optional[Sequence[Tuple[int, int]]] = None,
+               epoch: bool = False):
         """tt_peer_direct_t for a producer of ``inp`` (units of ``unit_bytes``, counted from ``inp``'s
         start) whose all-to-all into ``out`` then runs with ``stored=True``: block d's units go to
         their place in rank d's receive buffer. ``copy[d] = (lo, hi)``: bytes [lo, hi) of block d
-        (relative to its start) that the producer copies to rank d beside its units."""
+        (relative to its start) that the producer copies to rank d beside its units. ``epoch``: the
+        producer advances the exchange's epoch, and its consumer signals / waits in-launch
+        (``wait_desc``) instead of the all-to-all call."""
         blocks = self.block_dst(out, inp, out_splits, in_splits)
         x = _lib.PeerDirect()
         x.W = self.world
+        if epoch:
+            x.epoch = self._bufs[out.data_ptr()]["state"].data_ptr()
         for d, (off, n, dst) in enumerate(blocks):
             if off % unit_bytes:
                 raise _lib.TTError("PeerComm.direct: a block does not start on a unit")
@@ -439,6 +445,30 @@ class PeerComm(TorchComm):
                 x.copy_dst[d] = dst + lo
                 x.copy_len[d] = hi - lo
         return x
+
+    @property
+    def in_launch_wait(self) -> bool:
+        """Whether a consumer launch may signal / wait in-launch (tt_peer_wait_t): ranks on different
+        devices or one rank. Ranks sharing a device are excluded: one rank's spinning workgroups
+        could hold every CU while a peer's producer waits for one."""
+        return self.world == 1 or not self.shared_gpu
+
+    def wait_desc(self, out: torch.Tensor):
+        """tt_peer_wait_t of the exchange into ``out`` (a buffer from recv_buffer) for a consumer
+        launch that signals / waits in-launch; its producer took ``direct(..., epoch=True)``."""
+        e = self._bufs.get(out.data_ptr())
+        if e is None:
+            raise _lib.TTError("PeerComm.wait_desc: the receive buffer was not allocated by recv_buffer()")
+        if not self.in_launch_wait:
+            raise _lib.TTError("PeerComm.wait_desc: ranks share a device (use the all-to-all's signal / wait)")
+        w = _lib.PeerWait()
+        w.W, w.sys = self.world, 0 if self.same_device else 1
+        for d in range(self.world):
+            base, body = e["peers"][d]
+            w.flag[d] = base + body + 4 * self.rank
+        w.flags, w.epoch, w.err = e["flags"].data_ptr(), e["state"].data_ptr(), self.err.data_ptr()
+        w.timeout_ticks = int(min(self.timeout_s * 1e8, 9e17))  # s_memrealtime: 100 MHz
+        return w
 
     def close(self) -> None:
         """Unmap the peers' buffers and free this rank's (the buffers from recv_buffer are invalid after)."""
@@ -776,12 +806,19 @@ class FusedShardedTwoTowerStep:
         # signal / wait (TT_PEER_DIRECT=0: the put kernels instead)
         self.direct = (getattr(comm, "supports_direct", False) and not self.multi
                        and os.environ.get("TT_PEER_DIRECT", "1") != "0")
+        # ... and, opt-in (TT_PEER_MERGED=1; ranks on different devices, or one rank), with in-launch
+        # waits: no exchange kernel at all — launch U signals / waits exchange A, Adam exchange B.
+        # Same-box A/B at world 1: 53.2 vs 52.6 us (agent scope), 53.3 vs 53.5 us (system scope)
+        # against the signal / wait kernels (profiles/r06i_ab_in_launch_waits.log): not the default
+        # until a multi-GPU run shows the overlap it buys there
+        self.merged = (self.direct and getattr(comm, "in_launch_wait", False)
+                       and os.environ.get("TT_PEER_MERGED", "0") == "1")
         if self.direct:
             self._dA = comm.direct(self.recvA, self.sendA, 4 * D, out_splits=[self.Asz[r]] * W,
                                    in_splits=list(self.Asz),
-                                   copy=[(4 * self.S[d] * D, 4 * self.Asz[d]) for d in range(W)])
+                                   copy=[(4 * self.S[d] * D, 4 * self.Asz[d]) for d in range(W)], epoch=self.merged)
             self._dB = comm.direct(self.rows_in, self.rows_out, 2 * D, out_splits=[self.RSTR] * W,
-                                   in_splits=[self.RSTR] * W)
+                                   in_splits=[self.RSTR] * W, epoch=self.merged)
             base = self.rows_out.data_ptr()
             offs = []
             for d in range(W):
@@ -790,6 +827,9 @@ class FusedShardedTwoTowerStep:
                     raise _lib.TTError("sharded step: exchange B's tower block is not 4-B aligned")
                 offs.append((addr - base) // 4)
             self._tw_off_direct = (C.c_int64 * W)(*offs)
+        if self.merged:
+            self._wA = comm.wait_desc(self.recvA)
+            self._wB = comm.wait_desc(self.rows_in)
         self.overlap = bool(overlap)
         self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         self.pool_graphs: list = []
@@ -934,22 +974,25 @@ class FusedShardedTwoTowerStep:
                                                   ptr(ws), ws.numel(), self.max_lookups, stream_handle(self.device)),
               "dedup_rowwise_adagrad")
 
-    def _adam(self) -> None:
+    def _adam(self, wait=None) -> None:
         """Adam on the fixed-order sum of the W tower gradients received in exchange B, with the
-        step scalars T2 wrote (launch U / tt_tower_wgrad_pre advanced the step)."""
+        step scalars T2 wrote (launch U / tt_tower_wgrad_pre advanced the step). ``wait``: exchange
+        B's in-launch signal / wait (tt_peer_wait_t)."""
         tw = self.towers
         grads = self.rows_in.data_ptr() + 4 * self._tw_in
         check(_lib.load().tt_tower_adam_pre_grads_sum(
             C.byref(tw.shape), self.B, ptr(self.params), grads, self.W, self._tw_stride, ptr(self.exp_avg),
-            ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(tw.ws), tw.nbytes, stream_handle(self.device)),
-            "tower_adam_pre_grads_sum")
+            ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(tw.ws), tw.nbytes,
+            C.byref(wait) if wait is not None else None, stream_handle(self.device)), "tower_adam_pre_grads_sum")
 
-    def _plan(self, roles: int, route, ws: torch.Tensor) -> "_lib.LaunchPlan":
+    def _plan(self, roles: int, route, ws: torch.Tensor, wait: bool = False) -> "_lib.LaunchPlan":
         """A tt_launch plan for the pipelined step's launches U / G: the towers, the WGRAD role, the
         route of a later batch (``route`` = _route_args) and the owner's ADAGRAD role over the received
-        gradient rows (one pseudo-feature per source rank) in dedup workspace ``ws``."""
+        gradient rows (one pseudo-feature per source rank) in dedup workspace ``ws``; ``wait``:
+        launch U signals / waits exchange A in-launch."""
         tw, ts, r = self.towers, self.tables, self.rank
         return _lib.LaunchPlan(
+            wait=C.pointer(self._wA) if wait else None,
             roles=roles, shape=C.pointer(tw.shape), B=self.B, workspace=ptr(tw.ws), ws_bytes=tw.nbytes,
             wgrad=_lib.WgradRole(loss=ptr(self.loss), adam_step_state=ptr(self.adam_state), adam_lr=self.lr_dense,
                                  adam_beta1=0.9, adam_beta2=0.999),
@@ -1006,7 +1049,7 @@ class FusedShardedTwoTowerStep:
         """Step on the staged batch i (rows in place, parity ``parity``; batch i+1's keys placed),
         staging batch i+1's rows and routing ``next2_cols`` (batch i+2, same parity)."""
         lib, tw, ts, r, B, dev = _lib.load(), self.towers, self.tables, self.rank, self.B, self.device
-        direct = self.direct
+        direct, merged = self.direct, self.merged
         self._t1(parity, labels, direct=direct)
         route = self._route_args(next2_cols, parity)
         ws = self.dd_ws[parity]
@@ -1020,15 +1063,17 @@ class FusedShardedTwoTowerStep:
                 check(lib.tt_tower_wgrad_pre(C.byref(tw.shape), B, ptr(self.loss), ptr(tw.ws), tw.nbytes,
                                              ptr(self.adam_state), self.lr_dense, 0.9, 0.999, None, 0, 0,
                                              stream_handle(dev)), "tower_wgrad_pre")
-            self._exchange_a(stored=direct)
+            if not merged:
+                self._exchange_a(stored=direct)
             # launch U without T2: the owner's row-wise Adagrad + the count pass of batch i+2's route
-            _lib.launch(self._plan(_lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws), stream_handle(dev),
+            _lib.launch(self._plan(_lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws, merged), stream_handle(dev),
                         "shard_route_count_rowwise_adagrad")
             main.wait_stream(self.side)
         else:
-            self._exchange_a(stored=direct)
+            if not merged:
+                self._exchange_a(stored=direct)
             # launch U: T2 + the count pass of batch i+2's route + the owner's row-wise Adagrad
-            _lib.launch(self._plan(_lib.ROLE_WGRAD | _lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws),
+            _lib.launch(self._plan(_lib.ROLE_WGRAD | _lib.ROLE_ROUTE_COUNT | _lib.ROLE_ADAGRAD, route, ws, merged),
                         stream_handle(dev), "tower_wgrad_route_count_rowwise_adagrad")
         # launch G: the tower gradient x 1/W into every destination block + the route's place pass +
         # the owner's gather of batch i+1's rows
@@ -1042,8 +1087,11 @@ class FusedShardedTwoTowerStep:
                                       dedup_ws=g[13], dedup_ws_bytes=g[14], dedup_max_lookups=g[15],
                                       direct=C.pointer(self._dB) if direct else None)
         _lib.launch(plan, stream_handle(dev), "tower_grads_replicated_route_place_gather")
-        self._exchange_b(stored=direct)
-        self._adam()
+        if merged:
+            self._adam(self._wB)
+        else:
+            self._exchange_b(stored=direct)
+            self._adam()
 
     # ---- checkpoint (03_model_training.py:474-502 / :1015-1054 format) -------------------------
     def spans(self, f: int) -> List[Tuple[int, int]]:

@@ -278,7 +278,7 @@ class FusedShardedKJTStep:
         check(_lib.load().tt_tower_adam_pre_grads_sum(
             C.byref(tw.shape), self.B, ptr(self.params), self.recvC.data_ptr() + 4 * self.B * self.Fmax * self.D,
             self.W, self.strideC, ptr(self.exp_avg), ptr(self.exp_avg_sq), 1e-8, 0.9, 0.999, 0.0, ptr(tw.ws),
-            tw.nbytes, stream_handle(self.device)), "tower_adam_pre_grads_sum")
+            tw.nbytes, None, stream_handle(self.device)), "tower_adam_pre_grads_sum")
 
     def step(self, values: torch.Tensor, offsets: torch.Tensor, labels: torch.Tensor) -> None:
         """One training step on this rank's KJT batch (key-major bags of F features x B, ids in range
