@@ -935,7 +935,10 @@ def run_multi(args, world, rank, local_rank):
     N, Fq, D, B, layers, sharding, owners, ids, seed, plan = sharded_spec(args, world)
     F = len(N)
     dev = torch.device("cuda", local_rank % torch.cuda.device_count())  # (rehearsal: ranks may share one GPU)
-    comm, xdesc = exchange_comm(args.exchange, device=dev)
+    # the exchanges' per-destination blocks (gradient rows fp32, returned rows bf16): "auto" times
+    # both exchanges on them and keeps RCCL where the device-initiated stores do not pay
+    per_dest = -(-F * B // world)
+    comm, xdesc = exchange_comm(args.exchange, device=dev, probe=[per_dest * D * 4, per_dest * D * 2])
     peer = isinstance(comm, PeerComm)
     k = args.steps_per_graph or 8
     nb = max(2 * k, args.batches // (2 * k) * (2 * k))  # even and a multiple of k

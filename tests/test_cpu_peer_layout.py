@@ -195,3 +195,23 @@ def test_exchange_comm_falls_back_to_rccl_when_the_self_test_fails(monkeypatch):
     FakePeer.self_test = lambda self: (True, "")
     comm, desc = sharded.exchange_comm("auto")
     assert isinstance(comm, FakePeer) and desc.startswith("device-initiated")
+    # the probe (auto, RCCL backend, block sizes given): RCCL kept when the device-initiated
+    # exchange is more than 10 % slower, never probed for "peer" or without sizes
+    monkeypatch.setattr(sharded.dist, "get_backend", lambda group=None: "nccl")
+    times = {"t": (2.0, 1.0)}
+    probed = []
+
+    def fake_probe(pc, group, device, sizes, iters=10):
+        probed.append(list(sizes))
+        return times["t"]
+
+    monkeypatch.setattr(sharded, "_probe_exchanges", fake_probe)
+    comm, desc = sharded.exchange_comm("auto", probe=[1024, 512])
+    assert isinstance(comm, FakeTorch) and made[-1].closed and "2000.0 us" in desc and probed == [[1024, 512]]
+    times["t"] = (1.05, 1.0)
+    comm, desc = sharded.exchange_comm("auto", probe=[1024])
+    assert isinstance(comm, FakePeer) and "probe 1050.0 us" in desc
+    n = len(probed)
+    comm, _ = sharded.exchange_comm("peer", probe=[1024])
+    comm2, _ = sharded.exchange_comm("auto")
+    assert isinstance(comm, FakePeer) and isinstance(comm2, FakePeer) and len(probed) == n

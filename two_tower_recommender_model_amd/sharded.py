@@ -484,12 +484,49 @@ class PeerComm(TorchComm):
         self._own.clear()
 
 
-def exchange_comm(kind: str = "auto", group=None, device=None, verbose: bool = True):
+def _probe_exchanges(pc: "PeerComm", group, device, block_bytes: Sequence[int], iters: int = 10):
+    """Collective: the mean time (ms) of one round of all-to-alls with destination blocks of
+    ``block_bytes`` each, through ``pc`` and through RCCL (all_to_all_single), max over the ranks."""
+    tc = TorchComm(group, always_collective=True)
+    W = pc.world
+    res = []
+    for comm in (pc, tc):
+        tot = 0.0
+        for nb in block_bytes:
+            n = max(64, int(nb) // 4 // 64 * 64)  # int32 words per destination block
+            inp = torch.zeros(W * n, dtype=torch.int32, device=device)
+            out = (pc.recv_buffer((W * n,), torch.int32, device) if comm is pc
+                   else torch.empty(W * n, dtype=torch.int32, device=device))
+            for _ in range(3):
+                comm.all_to_all(out, inp)
+            torch.cuda.synchronize(device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                comm.all_to_all(out, inp)
+            e1.record()
+            torch.cuda.synchronize(device)
+            tot += e0.elapsed_time(e1) / iters
+        res.append(tot)
+    tc.retire()
+    t = torch.tensor(res, dtype=torch.float64, device=device)
+    if W > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    if int(pc.err.item()):
+        raise _lib.TTError("PeerComm: a wait timed out in the exchange probe")
+    return float(t[0]), float(t[1])
+
+
+def exchange_comm(kind: str = "auto", group=None, device=None, verbose: bool = True,
+                  probe: Optional[Sequence[int]] = None):
     """The sharded steps' comm (collective: every rank calls it with the same ``kind``).
     "rccl": TorchComm (all_to_all_single, RCCL over xGMI with backend "nccl"); "peer": PeerComm, the
     device-initiated exchange, after its startup ``self_test`` — raises if the test fails; "auto"
     (the default): PeerComm when its self-test passes on every rank, else TorchComm on every rank
-    (the reason printed on rank 0). Returns (comm, description)."""
+    (the reason printed on rank 0). ``probe`` (auto, backend "nccl"): the step's per-destination
+    block bytes; after the self-test both exchanges are timed on them (eager, max over ranks) and
+    RCCL is taken if the device-initiated one is more than 10 % slower — a guard for interconnects
+    where its stores do not pay. Returns (comm, description)."""
     if kind not in ("auto", "peer", "rccl"):
         raise _lib.TTError(f"exchange_comm: kind is auto, peer or rccl, got {kind!r}")
     if kind == "rccl":
@@ -501,6 +538,19 @@ def exchange_comm(kind: str = "auto", group=None, device=None, verbose: bool = T
         pc, why = None, str(e)
     if pc is not None:
         ok, why = pc.self_test()
+        if ok and kind == "auto" and probe and dist.get_backend(group) == "nccl":
+            tp, tr = _probe_exchanges(pc, group, device, probe)
+            timing = f"probe {tp * 1e3:.1f} us against RCCL {tr * 1e3:.1f} us"
+            if tp > 1.1 * tr:
+                pc.close()
+                if verbose and dist.get_rank(group) == 0:
+                    import sys
+
+                    print(f"exchange_comm: device-initiated exchange slower ({timing}); RCCL all-to-alls",
+                          file=sys.stderr)
+                return TorchComm(group, always_collective=True), f"RCCL all_to_all_single (peer {timing})"
+            return pc, (f"device-initiated puts into IPC-mapped peer buffers ({pc.memory} memory, self-test "
+                        f"passed, {timing})")
         if ok:
             return pc, f"device-initiated puts into IPC-mapped peer buffers ({pc.memory} memory, self-test passed)"
         pc.close()
