@@ -157,3 +157,19 @@ def test_bench_config5_peer_exchange_rehearsal():
     sh = d["config"]["sharded"]
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["loss"] == d["loss"]
     assert sh["mode"] == "hipgraph" and sh["exchange"].startswith("device-initiated"), sh
+
+
+def test_bench_sharded_world1_probes_the_exchange():
+    """`bench.py --sharded` at world 1 (backend "nccl"): exchange_comm("auto") runs the PeerComm
+    self-test, then times both exchanges on the step's block sizes and keeps the faster; the line
+    names the choice and both probe times, and the step runs as HIP graphs."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT",
+                                                              "TT_REHEARSE_GLOO")}
+    cmd = [sys.executable, "bench.py", "--sharded", "--steps", "8", "--warmup", "2", "--batches", "8",
+           "--steps-per-graph", "2", "--workload", "config2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    sh = d["config"]["sharded"]
+    assert d["n_gpus"] == 1 and d["value"] > 0 and sh["mode"] == "hipgraph", sh
+    assert "probe" in sh["exchange"] and "against RCCL" in sh["exchange"], sh["exchange"]
