@@ -77,6 +77,28 @@ def test_bench_gpus2_northstar_table_wise_as_driver_runs_it():
     assert d["value"] > 0 and d["loss"] == d["loss"]
 
 
+def test_bench_gpus4_northstar_row_wise_peer_rehearsal():
+    """The driver's N = 4 line on the north star (`bench.py --gpus 4`): the row-wise plan (both
+    tables split in 4 blocks, 19.2 GB per rank on the shared GPU), four processes storing straight
+    into each other's IPC-mapped exchange buffers (the default exchange after its self-test), HIP
+    graphs, flags checked on every rank, one JSON line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TT_REHEARSE_GLOO="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "4", "--steps", "16", "--warmup", "4", "--batches", "16",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=250)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    print(lines[0][:600], flush=True)
+    sh = d["config"]["sharded"]
+    assert d["n_gpus"] == 4 and d["config"]["per_gpu_batch"] == 8192
+    assert sh["plan"].startswith("row-wise") and sh["mode"] == "hipgraph", sh
+    assert sh["exchange"].startswith("device-initiated") and "producers store" in sh["exchange"], sh
+    assert d["value"] > 0 and d["loss"] == d["loss"]
+
+
 def test_bench_dropin_n2_rehearsal():
     """`bench.py --gpus 2 --path dropin`: the reference's DMP + TrainPipelineSparseDist loop in two
     processes (gloo, sharing the GPU) dispatched to the fused sharded step on every rank."""
