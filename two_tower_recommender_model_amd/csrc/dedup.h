@@ -20,6 +20,8 @@ constexpr int DD_CNT_BITS = 18;     // slot word = key << 18 | count; a step has
 constexpr uint64_t DD_CNT_MASK = (1ull << DD_CNT_BITS) - 1;
 constexpr int DD_INL = 30;          // lookups stored inline per slot (128-B slot: word + 30 items)
 constexpr int DD_SPH = 4;           // slots per half-wave in the update launch
+constexpr int DD_SEGW = 20;         // ints per T1 list segment: [0] count, [1 .. 16] slots (80 B: one
+                                    // 16-B load reads the count and the first three entries)
 #ifndef DD_MR
 #define DD_MR 4                     // gradient rows of a multi-lookup slot in flight per half-wave
 #endif
@@ -33,6 +35,7 @@ struct DedupWs {
   DSlot* slots;    // [cap], clean (key EMPTY, cnt 0) between steps
   uint64_t* lkey;  // [L] key of each lookup (DD_EMPTY: dropped / padding)
   int32_t* hot;    // [L / (DD_INL + 1) + 1] slots with cnt > DD_INL
+  uint64_t* hkey;  // [same] their keys, filed beside them (the hot role's first hop is the key)
   int32_t* ctr;    // [4] {hot rows, hot-workgroup ticket, hot rows as the row-owned T1 found them, -}
   int64_t cap;
   int64_t L;
@@ -56,10 +59,10 @@ struct DedupWs {
   float* hotp;
   int32_t* hcnt;
   // the ring's rows looked up 2..DD_INL times, listed by the row-owned T1 (which updates the rows
-  // looked up once and frees their slots): per T1 wave (segment) of 16 lookups, mcnt[seg] slots at
-  // multi[16 seg ..], written every step (no reset); the tail's list role updates them
-  int32_t* multi;  // [nseg * 16]
-  int32_t* mcnt;   // [nseg]
+  // looked up once and frees their slots): per T1 wave (segment) of 16 lookups, its count at
+  // multi[DD_SEGW seg] and its slots behind it, written every step (no reset); the tail's list role
+  // updates them
+  int32_t* multi;  // [nseg * DD_SEGW]
   int32_t nseg;    // capacity in segments: ceil(L / 16)
 };
 #if TT_EXPERIMENTS
@@ -127,7 +130,10 @@ __device__ __forceinline__ void dd_insert_finish(const DedupWs& ws, const DdPend
     ws.slots[h].item[k] = i;
   } else if (k == DD_INL) {
     const int q = atomicAdd(&ws.ctr[0], 1);
-    if (q < ws.hot_cap) ws.hot[q] = (int32_t)h;  // bound holds unless inserts skip an update
+    if (q < ws.hot_cap) {  // bound holds unless inserts skip an update
+      ws.hot[q] = (int32_t)h;
+      ws.hkey[q] = p.key;
+    }
   }
 }
 
@@ -304,7 +310,7 @@ __device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs) {
 __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
                                             float* __restrict__ weights, float* __restrict__ state, float lr,
                                             float eps, const DedupWs& ws, int hot_wgs, int bid, char* smem, int nh,
-                                            bool ticket, int32_t hc) {
+                                            bool ticket, int32_t hc, uint64_t hk) {
   f32x4v (*part)[32] = reinterpret_cast<f32x4v (*)[32]>(smem);       // [8][32], 16-B aligned
   int* list = reinterpret_cast<int*>(smem + 8 * 32 * 16);             // [DD_HOT_CH]
   int* qc = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4);  // [PT][4] matches per (q, wave)
@@ -316,9 +322,10 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
   const int K = dd_hot_team(nh, n, hot_wgs);
   for (int w = bid; w < nh * K; w += hot_wgs) {
     const int j = w / K, k = w - j * K;
-    // hc: lane l holds hot[bid / (l + 1)], loaded beside the count (the first item for team size K)
+    // hc / hk: lane l holds hot[bid / (l + 1)] and its key, loaded beside the count (the first item
+    // for team size K): the key scan starts one round trip after the launch, not two
     const int32_t h = w == bid ? __shfl(hc, K - 1, 64) : ws.hot[j];
-    const uint64_t key = ws.slots[h].word >> DD_CNT_BITS;
+    const uint64_t key = w == bid ? (uint64_t)__shfl((long long)hk, K - 1, 64) : ws.hkey[j];
     const int t = (int)(key >> DD_TABLE_SHIFT);
     const int64_t r = (int64_t)(key & ((1ull << DD_TABLE_SHIFT) - 1));
     const int D = gm.lm->dim[t];
@@ -572,36 +579,30 @@ __device__ __forceinline__ void dd_slots_finish(const DdUpdateArgs& a, const Gra
   DD_STAMP(3);
 }
 
-// the list role (DdUpdateArgs::multi_nseg): every workgroup scans the segment counts (thread t owns
-// segments t, t + 256, ...), takes the equal share [lb per, (lb + 1) per) of the listed slots in
-// that order (per <= 256: the host sizes nlb >= lookups / 512), gathers their slot indices into LDS
-// and updates those slots, DD_SPH per half-wave per round. Sparse steps (at most one listed slot per
-// workgroup on average: uniform ids list one or two a step) skip that gather's round trip: workgroup
-// lb takes the slots of its own 8 segments, whose counts and entries it loaded beside the scan's
-// counts (skewed steps cluster their slots in few segments: they keep the equal share). Each slot's
-// update is the same whichever half-wave takes it.
+// the list role (DdUpdateArgs::multi_nseg): every workgroup reads the head of every T1 segment
+// (thread t owns segments t, t + 256, ...: one 16-B load = the segment's count and its first three
+// slots), takes the equal share [lb per, (lb + 1) per) of the listed slots in that order (per <= 256:
+// the host sizes nlb >= lookups / 512), files their slot indices into LDS (an entry past a head's
+// three is loaded then: rare, a segment is one T1 wave of 16 lookups) and updates those slots,
+// DD_SPH per half-wave per round. Counts and first entries in one round trip: the slot words follow
+// at the second, not the third. Each slot's update is the same whichever half-wave takes it.
 __device__ __forceinline__ void dd_multi_block(const DdUpdateArgs& a, const GradMap& gm, DdMeta* lm, int lb, int nlb,
                                                char* smem, int bid) {
   const DedupWs& ws = a.ws;
   int* lst = reinterpret_cast<int*>(smem);  // [256]
-  int* wsum = lst + 256;                    // [4] wave totals, then [8] own segment counts
+  int* wsum = lst + 256;                    // [4] wave totals
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nseg = a.multi_nseg;
   constexpr int SPT = 8;  // segments per thread (nseg <= 2048)
-  int c[SPT];
+  int4 hd[SPT];
 #pragma unroll
-  for (int k = 0; k < SPT; ++k) c[k] = tid + 256 * k < nseg ? ws.mcnt[tid + 256 * k] : 0;
-  // the sparse form's own segments, beside the counts: thread tid < 128 holds entry tid & 15 of
-  // segment lb * 8 + (tid >> 4) and that segment's count
-  const bool own_form = nlb * 8 >= nseg;  // every segment belongs to some workgroup's 8
-  const int oseg = lb * 8 + (tid >> 4);
-  const bool own_ok = own_form && tid < 128 && oseg < nseg;
-  const int own_ent = own_ok ? ws.multi[(int64_t)oseg * 16 + (tid & 15)] : -1;
-  const int own_cnt = own_ok ? ws.mcnt[oseg] : 0;
+  for (int k = 0; k < SPT; ++k)
+    hd[k] = tid + 256 * k < nseg ? *reinterpret_cast<const int4*>(ws.multi + (int64_t)(tid + 256 * k) * DD_SEGW)
+                                 : make_int4(0, -1, -1, -1);
   dd_meta_fill(a.m, lm);
   int mine = 0;
 #pragma unroll
-  for (int k = 0; k < SPT; ++k) mine += c[k];
+  for (int k = 0; k < SPT; ++k) mine += hd[k].x;
   int inc = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -616,31 +617,17 @@ __device__ __forceinline__ void dd_multi_block(const DdUpdateArgs& a, const Grad
     base += w < wid ? wsum[w] : 0;
     total += wsum[w];
   }
-  int len;
-  if (own_form && total <= nlb) {  // sparse (workgroup-uniform)
-    int* oc = wsum + 4;  // [8] own segment counts
-    if (tid < 128 && (tid & 15) == 0) oc[tid >> 4] = own_cnt;
-    __syncthreads();
-    int ob = 0, ot = 0;
+  const int per = (total + nlb - 1) / nlb;
+  const int r0 = lb * per, r1 = min(total, r0 + per);
+  int p = base;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int cj = oc[j];
-      ob += j < (tid >> 4) ? cj : 0;
-      ot += cj;
-    }
-    if (tid < 128 && (tid & 15) < own_cnt) lst[ob + (tid & 15)] = own_ent;
-    len = ot;
-  } else {
-    const int per = (total + nlb - 1) / nlb;
-    const int r0 = lb * per, r1 = min(total, r0 + per);
-    int p = base;
-#pragma unroll
-    for (int k = 0; k < SPT; ++k) {
-      for (int e = 0; e < c[k]; ++e, ++p)
-        if (p >= r0 && p < r1) lst[p - r0] = ws.multi[(int64_t)(tid + 256 * k) * 16 + e];
-    }
-    len = max(0, r1 - r0);
+  for (int k = 0; k < SPT; ++k) {
+    const int seg = tid + 256 * k;
+    for (int e = 0; e < hd[k].x; ++e, ++p)
+      if (p >= r0 && p < r1)
+        lst[p - r0] = e == 0 ? hd[k].y : e == 1 ? hd[k].z : e == 2 ? hd[k].w : ws.multi[(int64_t)seg * DD_SEGW + 1 + e];
   }
+  const int len = max(0, r1 - r0);
   __syncthreads();
   const int hl = lane & 31;
   const int hw = wid * 2 + ((lane & 32) >> 5);  // half-wave of the workgroup (8)
@@ -685,7 +672,9 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     const bool ticket = !a.skip_single;
     // beside the count: the hot-list entry this workgroup takes first for each team size it can get
     // (lane l: team size l + 1), so the slot word is the next hop, not the list entry
-    const int32_t hc = ws.hot[min(bid / (min((int)(threadIdx.x & 63), DD_HOT_TEAM - 1) + 1), ws.hot_cap - 1)];
+    const int hi = min(bid / (min((int)(threadIdx.x & 63), DD_HOT_TEAM - 1) + 1), ws.hot_cap - 1);
+    const int32_t hc = ws.hot[hi];
+    const uint64_t hk = ws.hkey[hi];
     const int nh = min(ticket ? __hip_atomic_load(&ws.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ws.ctr[2],
                        ws.hot_cap);
     if (bid >= nh * dd_hot_team(nh, a.n, a.hot_wgs)) {
@@ -694,7 +683,7 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     }
     dd_meta_fill(m, lm);
     __syncthreads();
-    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem, nh, ticket, hc);
+    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem, nh, ticket, hc, hk);
     return;
   }
   if (LIST_ONLY || a.multi_nseg > 0) {

@@ -64,8 +64,9 @@ size_t dedup_layout(void* base, int64_t L, DedupWs* w) {
   t.hotp = reinterpret_cast<float*>(take(sizeof(float) * 128 * DD_HOT_TEAM * hot_cap));
   t.hcnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * hot_cap));
   t.nseg = (int32_t)((L + 15) / 16);
-  t.multi = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 16 * (size_t)t.nseg));
-  t.mcnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)t.nseg));
+  t.multi = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * DD_SEGW * (size_t)t.nseg));
+  t.hkey = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * (L / (DD_INL + 1) + 1)));  // (last: the
+  // layout before it is what tests/test_gpu_dedup.py inspects)
   t.cap = cap;
   t.L = L;
   t.hot_cap = (int32_t)(L / (DD_INL + 1) + 1);

@@ -1867,9 +1867,9 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
       const bool mul = q == 0 && r >= 0 && cl >= 0 && cnt >= 2u && cnt <= (uint32_t)DD_INL;
       const uint64_t bal = __ballot(mul);
       const int seg = (int)blockIdx.x * 4 + wid;
-      if (seg < a.dd.nseg) {
-        if (mul) a.dd.multi[(int64_t)seg * 16 + __popcll(bal & ((1ull << lane) - 1))] = cl;
-        if (lane == 0) a.dd.mcnt[seg] = __popcll(bal);
+      if (seg < a.dd.nseg) {  // [count, slots...] (DD_SEGW): the list role reads count + 3 slots at once
+        if (mul) a.dd.multi[(int64_t)seg * DD_SEGW + 1 + __popcll(bal & ((1ull << lane) - 1))] = cl;
+        if (lane == 0) a.dd.multi[(int64_t)seg * DD_SEGW] = __popcll(bal);
       }
     }
     // the updated rows go back through the wave's LDS rows (same chunk swizzle) and out as two
@@ -2747,7 +2747,10 @@ __device__ __forceinline__ void insert_next_full_block(const InsertArgs& ins, in
       ws.slots[h].item[k] = (int32_t)i;
     } else if (k == DD_INL) {
       const int q = atomicAdd(&ws.ctr[0], 1);
-      if (q < ws.hot_cap) ws.hot[q] = h;
+      if (q < ws.hot_cap) {
+        ws.hot[q] = h;
+        ws.hkey[q] = key[u];
+      }
     }
   }
 }
