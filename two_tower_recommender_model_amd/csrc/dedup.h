@@ -310,7 +310,8 @@ __device__ __forceinline__ void dd_hot_ticket(const DedupWs& ws, int hot_wgs) {
 __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
                                             float* __restrict__ weights, float* __restrict__ state, float lr,
                                             float eps, const DedupWs& ws, int hot_wgs, int bid, char* smem, int nh,
-                                            bool ticket, int32_t hc, uint64_t hk) {
+                                            bool ticket, int32_t hc, uint64_t hk,
+                                            const uint64_t (&kspec)[DD_HOT_PT], int ks) {
   f32x4v (*part)[32] = reinterpret_cast<f32x4v (*)[32]>(smem);       // [8][32], 16-B aligned
   int* list = reinterpret_cast<int*>(smem + 8 * 32 * 16);             // [DD_HOT_CH]
   int* qc = reinterpret_cast<int*>(smem + 8 * 32 * 16 + DD_HOT_CH * 4);  // [PT][4] matches per (q, wave)
@@ -339,11 +340,17 @@ __device__ __forceinline__ void dd_hot_role(const GradMap& gm, int64_t n,
     f32x4v acc = (f32x4v)(0.f);
     uint64_t kc[DD_HOT_PT], kn[DD_HOT_PT];
     // thread tid holds lookups pass * CH + 256 q + tid (q < PT): every key load instruction reads
-    // 512 contiguous bytes (16 consecutive keys per thread made each instruction touch 64 lines)
+    // 512 contiguous bytes (16 consecutive keys per thread made each instruction touch 64 lines).
+    // The first pass of the first item comes from kspec when the speculation held (pass ks)
+    if (w == bid && k == ks) {
 #pragma unroll
-    for (int q = 0; q < DD_HOT_PT; ++q) {
-      const int i = k * DD_HOT_CH + 256 * q + tid;
-      kc[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
+      for (int q = 0; q < DD_HOT_PT; ++q) kc[q] = kspec[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < DD_HOT_PT; ++q) {
+        const int i = k * DD_HOT_CH + 256 * q + tid;
+        kc[q] = i < nn ? ws.lkey[i] : DD_EMPTY;
+      }
     }
     const uint64_t lt = (1ull << lane) - 1;
     for (int p = k; p < npass; p += K) {
@@ -665,6 +672,16 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   if ((a.exp_skip & 2) && bid >= a.hot_wgs) return;
 #endif
   if (bid < a.hot_wgs) {
+    // speculative: the keys of the first pass a member of a two-workgroup team scans (teams of two
+    // are the skewed steps' usual case: 17..32 hot rows over 64 hot workgroups), issued beside the
+    // count instead of a round trip after it; any other team size loads its own
+    const int ks = bid & 1;
+    uint64_t kspec[DD_HOT_PT];
+#pragma unroll
+    for (int q = 0; q < DD_HOT_PT; ++q) {
+      const int64_t i = (int64_t)ks * DD_HOT_CH + 256 * q + threadIdx.x;
+      kspec[q] = i < a.n ? ws.lkey[i] : DD_EMPTY;
+    }
     // a workgroup with no hot work item (most of them at uniform ids) only checks in: the ticket
     // that resets the hot-row count once every hot workgroup has read it. skip_single: the row-owned
     // T1 moved the count to ctr[2] and zeroed ctr[0] (no ticket: 64 returning atomics on one word
@@ -683,7 +700,7 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
     }
     dd_meta_fill(m, lm);
     __syncthreads();
-    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem, nh, ticket, hc, hk);
+    dd_hot_role(gm, a.n, weights, state, lr, eps, ws, a.hot_wgs, bid, smem, nh, ticket, hc, hk, kspec, ks);
     return;
   }
   if (LIST_ONLY || a.multi_nseg > 0) {
