@@ -1342,6 +1342,13 @@ __device__ __forceinline__ void rk_strip(const bf16x8 (&v)[4], __bf16* row, int 
   for (int s = 0; s < NS; ++s) *reinterpret_cast<bf16x8*>(row + 32 * s + 8 * q) = v[s];
 }
 
+// workgroups are dealt round-robin over the 8 XCDs (bid % 8): logical index of workgroup bid
+// among n so that each XCD runs one contiguous 1/8 of [0, n) (any n)
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int x = bid & 7, loc = bid >> 3, q = n >> 3, r = n & 7;
+  return x * q + min(x, r) + loc;
+}
+
 // direct exchange (tt_peer_direct_t): where send-buffer row `row` lands (the destination block's
 // mapped receive buffer); a uniform loop with scalar kernarg loads selects the block
 __device__ __forceinline__ char* px_row(const tt_peer_direct_t& x, int64_t row, int64_t row_bytes) {
@@ -1552,7 +1559,10 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
                                                                     // (fp32, 16-B chunk c of row n at c ^ n)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = wid >> 1, h = wid & 1, q = lane >> 4, n = lane & 15;
-  const int64_t B = a.B, m0 = (int64_t)blockIdx.x * TR, m = m0 + 16 * h + n;
+  // the tile: XCD x runs tiles [x n / 8, (x + 1) n / 8) (xcd_remap), so the 256-row slices the
+  // tail's T2 tiles read (also placed a contiguous 1/8 per XCD) were written through that XCD's L2
+  const int tile = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int64_t B = a.B, m0 = (int64_t)tile * TR, m = m0 + 16 * h + n;
   const bool live = m < B;
   RK_STAMP(0);
   // ---- 0. loads in dependency order (vmcnt retires in issue order: a wait for a load also waits
@@ -1866,7 +1876,7 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
       // updates them (segment = the wave; plain stores, the count written every step)
       const bool mul = q == 0 && r >= 0 && cl >= 0 && cnt >= 2u && cnt <= (uint32_t)DD_INL;
       const uint64_t bal = __ballot(mul);
-      const int seg = (int)blockIdx.x * 4 + wid;
+      const int seg = tile * 4 + wid;
       if (seg < a.dd.nseg) {  // [count, slots...] (DD_SEGW): the list role reads count + 3 slots at once
         if (mul) a.dd.multi[(int64_t)seg * DD_SEGW + 1 + __popcll(bal & ((1ull << lane) - 1))] = cl;
         if (lane == 0) a.dd.multi[(int64_t)seg * DD_SEGW] = __popcll(bal);
@@ -1931,20 +1941,20 @@ __device__ __forceinline__ void tower_rows_body(const TowerArgs& a) {
   __syncthreads();
   RK_STAMP(14);
   if (h == 0) {
-    float* db0 = a.dbpart + (((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW;
-    float* db1 = a.dbpart + (((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW;
+    float* db0 = a.dbpart + (((int64_t)t * MAXL + 0) * a.nwg + tile) * MAXW;  // by tile: T2 sums them in tile order
+    float* db1 = a.dbpart + (((int64_t)t * MAXL + 1) * a.nwg + tile) * MAXW;
     db0[feat(2 * n)] = z0[0] + bsum[t][feat(2 * n)];
     db0[feat(2 * n + 1)] = z0[1] + bsum[t][feat(2 * n + 1)];
     db1[feat(n)] = z1[0] + bsum[t][RK_W0 + feat(n)];
     if (t == 0 && lane == 0) {
       float p = 0.f;
       for (int i = 0; i < TR; ++i) p += lrow[i];
-      a.loss_part[blockIdx.x] = p;
+      a.loss_part[tile] = p;
     }
   }
   // every row's overflow entry is written (EMPTY for a dropped id or a dead row of a ragged tile):
   // the resolver reads all 64 entries of the group
-  if (!UPD && a.dd_on && q == 0) dd_insert_defer_finish_at(a.dd, pend, li, (int)blockIdx.x, 16 * wid + n);
+  if (!UPD && a.dd_on && q == 0) dd_insert_defer_finish_at(a.dd, pend, li, tile, 16 * wid + n);
   if constexpr (IDX) {
     if (cpd) *cpd = cpv;
     if (a.xd.W) {  // a share past 256 units (not at the sharded steps' sizes)
@@ -2036,12 +2046,6 @@ constexpr int T2_RED = 3 * 64 * 16 * 4;                // bytes of the register-
 constexpr int T2_SMEM0 = T2_LDS > T2_RED ? T2_LDS : T2_RED;
 constexpr int T2_SMEM = T2_SMEM0 > DD_SMEM ? T2_SMEM0 : DD_SMEM;  // the combined launch shares it with dedup.h
 
-// workgroups are dealt round-robin over the 8 XCDs (bid % 8): logical index of workgroup bid
-// among n so that each XCD runs one contiguous 1/8 of [0, n) (any n)
-__device__ __forceinline__ int xcd_remap(int bid, int n) {
-  const int x = bid & 7, loc = bid >> 3, q = n >> 3, r = n & 7;
-  return x * q + min(x, r) + loc;
-}
 
 __device__ __forceinline__ void wgrad_lds_block(const WgradArgs& a, int lb, char* smem) {
   __bf16* buf = reinterpret_cast<__bf16*>(smem);
@@ -2451,8 +2455,8 @@ struct InsertArgs {
                 // per (XCD class, tower); 0: 256 consecutive lookups per workgroup
 };
 // lookup of thread tid in insert workgroup blk (blk < 2B / 256). xcd_wpt > 0 (B % 2048 == 0): the
-// workgroup takes only rows of T1 tiles b (32 rows each) with b = blk (mod 8) — T1's workgroup for
-// tile b runs on XCD b % 8, as this workgroup runs on XCD blk % 8 — so the next batch's ids and the
+// workgroup takes only rows of the T1 tiles (32 rows each) that run on its own XCD (blk % 8): T1
+// places tiles [c B / 256, (c + 1) B / 256) on XCD c (xcd_remap), so the next batch's ids and the
 // claims T1 reads first are in that XCD's L2 when its T1 tile starts (plain loads and stores keep
 // their lines there). Lookup order is irrelevant to the results: every row's lookups are summed in
 // ascending lookup order whatever their slot positions.
@@ -2460,7 +2464,8 @@ __device__ __forceinline__ int64_t ins_lookup(const InsertArgs& ins, int blk, in
   if (ins.xcd_wpt <= 0) return (int64_t)blk * 256 + tid;
   const int c = blk & 7, j = blk >> 3;
   const int t = j / ins.xcd_wpt, qi = j - t * ins.xcd_wpt;
-  const int64_t b = c + 8 * (8 * qi + (tid >> 5));
+  // T1 tile b runs on XCD c for b in [c B / 256, (c + 1) B / 256) (tower_rows_body's xcd_remap)
+  const int64_t b = (int64_t)c * (ins.B / 256) + 8 * qi + (tid >> 5);
   return (int64_t)t * ins.B + 32 * b + (tid & 31);
 }
 
