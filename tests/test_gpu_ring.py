@@ -51,6 +51,29 @@ def test_ring_equals_classic_step(device, D, mode):
     assert torch.equal(a.logits, b.logits)
 
 
+@pytest.mark.parametrize("B", [2136, 2400])
+def test_ring_ragged_grid_equals_classic_step(device, B):
+    """T1 grids that are not a multiple of 8 workgroups (67 tiles, the last one partial at B = 2136;
+    75 at 2400): T1's XCD tile placement (xcd_remap, uneven blocks per XCD) and the insert's plain
+    filing (B % 2048 != 0) — bit for bit the classic step."""
+    from two_tower_recommender_model_amd.fused import FusedTwoTowerStep
+
+    N = [30_000, 50_000]
+    batches = _batches(N, B, 4, seed=B, device=device)
+    a = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=3)
+    b = FusedTwoTowerStep(N, [128, 128], [0], [1], [128, 64], B, device, seed=3)
+    assert a.ring_supported()
+    a.capture_ring(batches, steps_per_graph=2)
+    a.run(4)
+    for cols, lab in batches:
+        b.load_batch(cols, lab)
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.tables.weights, b.tables.weights) and torch.equal(a.tables.state, b.tables.state)
+    assert torch.equal(a.params, b.params) and float(a.loss) == float(b.loss)
+    assert torch.equal(a.logits, b.logits)
+
+
 def test_ring_large_batch_equals_classic_step(device):
     """B = 32,768 (65,536 lookups, 4096 T1 segments: past the tail list role's 2048) — the tail's slot
     role walks every claiming lookup instead of T1's list; bit for bit the classic step."""
