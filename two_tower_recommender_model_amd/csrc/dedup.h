@@ -202,6 +202,8 @@ struct DdUpdateArgs {
   int hot_wgs;         // workgroups of the hot role; the slot role has slot_hw / 8 more
   int64_t slot_hw;     // half-waves of the slot role: ceil(L / DD_SPH), a multiple of 8
   int skip_single;     // rows looked up once were updated by T1 (dd_mode 2): only free their slots
+  int xcd;             // 1: the slot role's workgroups start at a multiple of 8 in their launch: they
+                       // take the claiming lookups a contiguous 1/8 per XCD (xcd_remap)
   int multi_nseg;      // > 0: the slot role walks the T1 list of multi-lookup rows (DedupWs::multi, this
                        // many segments) instead of every claiming lookup; T1 freed the single slots
 #if TT_EXPERIMENTS
@@ -712,7 +714,12 @@ __device__ __forceinline__ void dd_update_block(const DdUpdateArgs& a, int bid, 
   // DD_SPH claiming lookups per half-wave (i and i + nhw, ...), their dependent loads interleaved:
   // the slot a lookup claimed (claim[i] >= 0) is updated by that lookup's half-wave; the grid covers
   // the step's lookups (not the cap slots) in one round of resident waves
-  const int64_t hw = ((int64_t)(bid - a.hot_wgs) * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
+  int sb = bid - a.hot_wgs;
+  if (a.xcd) {  // (a uniform remap of the slot workgroups: which workgroup takes a lookup is free)
+    const int ns = (int)(a.slot_hw / 8), x = sb & 7, loc = sb >> 3, q = ns >> 3, r = ns & 7;
+    sb = x * q + min(x, r) + loc;
+  }
+  const int64_t hw = ((int64_t)sb * 4 + (threadIdx.x >> 6)) * 2 + (hb >> 5);
   const int64_t nhw = a.slot_hw;
   int hq[DD_SPH];
   uint64_t lk[DD_SPH];

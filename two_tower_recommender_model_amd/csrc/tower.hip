@@ -2626,7 +2626,7 @@ __global__ void __launch_bounds__(256) tower_grads_place_gather_kernel(UpdateArg
   if (g.epoch && b == 0 && threadIdx.x == 0)  // exchange B's epoch advances with its producer
     __hip_atomic_fetch_add(g.epoch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (b < n_upd) {
-    update_block(a, b, n_upd);
+    update_block(a, xcd_remap(b, n_upd), n_upd);  // a contiguous 1/8 per XCD, as T3
   } else if (b < n_upd + n_place) {
     const int j = b - n_upd;
     route_place_block<true>(r, j % r.nblk, j / r.nblk, base, wc);
@@ -3582,6 +3582,7 @@ static int fused_wgrad_route_count_adagrad(const tt_tower_shape_t* shape, int64_
   if (rc) return rc;
   const int64_t n_cnt = (int64_t)r.nblk * F;
   if (wgs + n_cnt + dd_grid > INT32_MAX) return fail(TT_EINVAL, "tower_wgrad_route_rowwise: grid too large");
+  d.xcd = d.hot_wgs % 8 == 0 ? 1 : 0;  // the owner's update workgroups first (dd_first): slot role aligned
 #if TT_EXPERIMENTS
   static const bool dd_first = !getenv("TT_U_DD_FIRST") || atoi(getenv("TT_U_DD_FIRST")) != 0;  // A/B switch
 #else
@@ -3617,6 +3618,7 @@ static int fused_route_count_adagrad(int F, int64_t B, const void* const* cols, 
   if (rc) return rc;
   const int64_t n_cnt = (int64_t)r.nblk * F;
   if (n_cnt + dd_grid > INT32_MAX) return fail(TT_EINVAL, "shard_route_count_rowwise_adagrad: grid too large");
+  d.xcd = d.hot_wgs % 8 == 0 ? 1 : 0;  // the owner's update workgroups first: slot role aligned
   WgradArgs a{};
   tower_wgrad_route_rowwise_kernel<<<dim3((unsigned)(n_cnt + dd_grid)), dim3(256), 0, as_stream(stream)>>>(
       a, nullptr, r, d, 0, (int)n_cnt, (int)dd_grid, pw);
