@@ -875,7 +875,8 @@ __global__ void __launch_bounds__(256) bwd_adagrad_direct_kernel(EmbMeta m, cons
   __shared__ LdsMeta lm;
   const int tid = threadIdx.x;
   const int64_t NB = (int64_t)m.F * m.B;
-  const int64_t b0 = (int64_t)blockIdx.x * TILE_BAGS;
+  // bag tiles a contiguous 1/8 per XCD (xcd_remap): every tile's lookups are independent
+  const int64_t b0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * TILE_BAGS;
   const int nb = (int)min((int64_t)TILE_BAGS, NB - b0);
   if (tid <= nb) off[tid] = offsets[b0 + tid];
   stage_meta(m, lm);

@@ -1342,12 +1342,6 @@ __device__ __forceinline__ void rk_strip(const bf16x8 (&v)[4], __bf16* row, int 
   for (int s = 0; s < NS; ++s) *reinterpret_cast<bf16x8*>(row + 32 * s + 8 * q) = v[s];
 }
 
-// workgroups are dealt round-robin over the 8 XCDs (bid % 8): logical index of workgroup bid
-// among n so that each XCD runs one contiguous 1/8 of [0, n) (any n)
-__device__ __forceinline__ int xcd_remap(int bid, int n) {
-  const int x = bid & 7, loc = bid >> 3, q = n >> 3, r = n & 7;
-  return x * q + min(x, r) + loc;
-}
 
 // direct exchange (tt_peer_direct_t): where send-buffer row `row` lands (the destination block's
 // mapped receive buffer); a uniform loop with scalar kernarg loads selects the block

@@ -44,6 +44,13 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// workgroups are dealt round-robin over the 8 XCDs (bid % 8): logical index of workgroup bid
+// among n so that each XCD runs one contiguous 1/8 of [0, n) (any n)
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int x = bid & 7, loc = bid >> 3, q = n >> 3, r = n & 7;
+  return x * q + min(x, r) + loc;
+}
+
 // a consumer launch's in-launch signal / wait of a device-initiated exchange (tt_peer_wait_t),
 // by value in the kernel arguments; W = 0: none
 struct PxWait {
