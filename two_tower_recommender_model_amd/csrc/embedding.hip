@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(256) bwd_tile_hash_kernel(EmbMeta m, const voi
   __shared__ int red[4];
   const int tid = threadIdx.x;
   const int64_t NB = (int64_t)m.F * m.B;
-  const int64_t b0 = (int64_t)blockIdx.x * TILE_BAGS;
+  const int64_t b0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * TILE_BAGS;  // a contiguous 1/8 per XCD
   const int nb = (int)min((int64_t)TILE_BAGS, NB - b0);
   if (tid <= nb) off[tid] = offsets[b0 + tid];
   for (int i = tid; i < TILE_HS; i += 256) {
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(256) bwd_tile_scatter_kernel(EmbMeta m, const 
   __shared__ int lbase[TILE_CH];
   const int tid = threadIdx.x;
   const int64_t NB = (int64_t)m.F * m.B;
-  const int64_t b0 = (int64_t)blockIdx.x * TILE_BAGS;
+  const int64_t b0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * TILE_BAGS;  // as the hash kernel
   const int nb = (int)min((int64_t)TILE_BAGS, NB - b0);
   if (tid <= nb) off[tid] = offsets[b0 + tid];
   __syncthreads();

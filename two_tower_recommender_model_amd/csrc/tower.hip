@@ -698,7 +698,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     // batch's id) finish before barrier 1: the compute waves spend ~5 us gathering there, while a
     // round trip after barrier 1 made this wave the last arrival at barrier 2 (by 0.8-1.2 us).
     const int tq = lane / TR, row = lane % TR;
-    const int64_t gm = (int64_t)blockIdx.x * TR + row;
+    const int64_t gm = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * TR + row;
     const bool pref = a.pcol[0] != nullptr;
     int64_t r = -1;
     int32_t cl = -1;
@@ -776,7 +776,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     // table; its CAS round trips count only in ITS vmcnt, so the 8 compute waves never wait on
     // them. It passes the compute waves' barriers (T1_BARRIERS, all unconditional) in step.
     const int tq = lane / TR, row = lane % TR;
-    const int64_t gm = (int64_t)blockIdx.x * TR + row;
+    const int64_t gm = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * TR + row;
     const bool own = a.dd_on && gm < a.B;
     DdPend p;
     if (own) {
@@ -794,7 +794,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
     // probing here (dd_insert_defer_finish): this wave's tail is one atomic round trip
     __syncthreads();
     __syncthreads();
-    if (a.dd_on) dd_insert_defer_finish(a.dd, p, (int32_t)(tq * a.B + gm), (int)blockIdx.x);
+    if (a.dd_on) dd_insert_defer_finish(a.dd, p, (int32_t)(tq * a.B + gm), xcd_remap((int)blockIdx.x, (int)gridDim.x));
 #if TT_EXPERIMENTS
     if (a.stamps && lane == 0) a.stamps[(int64_t)blockIdx.x * 16 + 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -808,17 +808,19 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   const int tt = threadIdx.x & 255;  // thread index inside the tower group
   const int r16 = lane & 15, q4 = lane >> 4;
   const int64_t B = a.B;
-  const int64_t m0 = (int64_t)blockIdx.x * TR;
+  // the tile: a contiguous 1/8 per XCD (xcd_remap), as tower_rows_body; per-tile partials by tile
+  const int tl2 = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int64_t m0 = (int64_t)tl2 * TR;
   const int nval = (int)min((int64_t)TR, B - m0);  // valid rows of this tile (32-bit row tests)
   // this tile's run of each T1 -> T2 strip (tile-major, strip_at): wave-uniform bases, so a
   // store's address is base + (feature * TR + row) in 32 bits
-  const int64_t tile_el = (int64_t)blockIdx.x * TR;
+  const int64_t tile_el = (int64_t)tl2 * TR;
   __bf16* const xt_tile = a.xt + (int64_t)t * a.in_max * a.Bp + tile_el * a.in_max;
   __bf16* const act_tile = a.act + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + tile_el * MAXW;
   __bf16* const dz0_tile = a.dzt + ((int64_t)t * MAXL + 0) * MAXW * a.Bp + tile_el * MAXW;
   __bf16* const dz1_tile = a.dzt + ((int64_t)t * MAXL + 1) * MAXW * a.Bp + tile_el * MAXW;
-  float* const db0 = a.dbpart + (((int64_t)t * MAXL + 0) * a.nwg + blockIdx.x) * MAXW;
-  float* const db1 = a.dbpart + (((int64_t)t * MAXL + 1) * a.nwg + blockIdx.x) * MAXW;
+  float* const db0 = a.dbpart + (((int64_t)t * MAXL + 0) * a.nwg + tl2) * MAXW;
+  float* const db1 = a.dbpart + (((int64_t)t * MAXL + 1) * a.nwg + tl2) * MAXW;
   const int in = IN_ ? IN_ : a.s.in_dim[t];
   const int W0 = W0_ ? W0_ : a.s.width[0];
   const int W1 = W1_ ? W1_ : a.s.width[1];
@@ -1142,7 +1144,7 @@ __global__ void __launch_bounds__(T1_THREADS) tower_l2_kernel(TowerArgs a) {
   if (threadIdx.x == 0) {
     float p = 0.f;
     for (int i = 0; i < TR; ++i) p += lpart[i];
-    a.loss_part[blockIdx.x] = p;
+    a.loss_part[tl2] = p;
   }
   T1_WSTAMP(7);
   __syncthreads();
