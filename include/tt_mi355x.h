@@ -582,6 +582,14 @@ int tt_kjt_admit(int F, int64_t B, const void* values, int id_dtype, int64_t nnz
                  const int64_t* num_embeddings, const int64_t* block_sizes, const int32_t* owners, int W, int32_t* out,
                  void* stream);
 
+/* Setup helper, no reference counterpart (TorchRec's tables pay the same cold page-table walks in
+ * their first training iterations, 03_model_training.py:648's loop): one 4-byte load per page_bytes
+ * of [base, base + bytes) (bytes / 4 words, the tail page included), asynchronous on `stream`. It
+ * warms the address translations of the embedding tables before the first step; nothing is
+ * written except, never in practice, one word of `sink` (device, 4 bytes). page_bytes: a multiple
+ * of 4 (4096 = the GPU page). ABI 4. */
+int tt_table_prefault(const void* base, size_t bytes, size_t page_bytes, uint32_t* sink, void* stream);
+
 /* ---- multi-hot sharded step (config 5, sharded_kjt.py): fixed-size exchanges ------------------------
  * TorchRec's KJTAllToAll / PooledEmbeddingsAllToAll / reduce-scatter (torchrec/distributed/embeddingbag.py,
  * reached from 03_model_training.py:812-815) exchange variable split sizes the host reads every batch;

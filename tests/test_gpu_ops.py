@@ -384,3 +384,29 @@ def test_linear_fp32_parity_mode(ops, device, M, N, K, groups):
         dz = dys[i] * pos
         close(dxs[i].cpu(), dz, ws[i])
         close(dws[i].cpu(), dz.T.contiguous(), xs[i])
+
+
+@pytest.mark.parametrize("rows,dim", [(1, 4), (3, 7), (5000, 128), (1 << 17, 64)])
+def test_table_prefault_reads_only(ops, device, rows, dim):
+    """TableSet.prefault (tt_table_prefault): one load per page of the weights and the state, the
+    last partial page included; nothing of the tables changes and the sink stays 0."""
+    ts = ops.TableSet([rows, 3], [dim, dim], [0, 1], device)
+    ts.init_uniform_(torch.Generator(device=device).manual_seed(0))
+    ts.state.uniform_()
+    w0, s0 = ts.weights.clone(), ts.state.clone()
+    for page in (4096, 4, 65536):
+        ts.prefault(page)
+    torch.cuda.synchronize()
+    assert torch.equal(ts.weights, w0) and torch.equal(ts.state, s0)
+    assert int(ts._sink[0]) == 0
+
+
+def test_table_prefault_argument_errors(ops, device):
+    from two_tower_recommender_model_amd import _lib
+
+    lib = _lib.load()
+    sink = torch.zeros(1, dtype=torch.int32, device=device)
+    buf = torch.zeros(16, dtype=torch.float32, device=device)
+    assert lib.tt_table_prefault(buf.data_ptr(), 64, 6, sink.data_ptr(), None) != 0
+    assert lib.tt_table_prefault(buf.data_ptr(), 64, 4096, None, None) != 0
+    assert lib.tt_table_prefault(None, 0, 4096, sink.data_ptr(), None) == 0

@@ -324,6 +324,7 @@ SIGNATURES = {
     "tt_peer_unimport": (_int, [_vp]),
     "tt_peer_exchange": (_int, [C.c_void_p, _vp, _vp, C.c_double, _vp]),
     "tt_kjt_admit": (_int, [_int, _i64, _vp, _int, _i64, _vp, _pi64, _pi64, _pi32, _int, _vp, _vp]),
+    "tt_table_prefault": (_int, [_vp, _sz, _sz, _vp, _vp]),
 }
 
 COMPUTE_ENTRY_POINTS = [
@@ -379,6 +380,7 @@ COMPUTE_ENTRY_POINTS = [
     "tt_launch",
     "tt_peer_exchange",
     "tt_kjt_admit",
+    "tt_table_prefault",
 ]
 
 _lib = None

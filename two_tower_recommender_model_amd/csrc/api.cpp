@@ -59,6 +59,7 @@ int tt_abi_version(void) { return TT_ABI_VERSION; }
 // tt_bwd_rowwise_adagrad_part
 // tt_peer_exchange
 // tt_kjt_admit
-int tt_num_entry_points(void) { return 52; }
+// tt_table_prefault
+int tt_num_entry_points(void) { return 53; }
 
 }  // extern "C"

@@ -260,6 +260,7 @@ class FusedTwoTowerStep:
             raise _lib.TTError("capture_pool_kjt(ahead=True): the batch count must be even")
         if k > 1 and (not ahead or n % k or k % 2):
             raise _lib.TTError("capture_pool_kjt: steps_per_graph > 1 needs ahead=True, an even k dividing the pool")
+        self._prefault_due = True  # the next replay walks the tables' pages first (TableSet.prefault)
         self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]
         keep = self.values, self.offsets, self.labels
         self.pool_graphs = []
@@ -361,6 +362,9 @@ class FusedTwoTowerStep:
     def replay_pool(self, n: int) -> None:
         """Replay n pool graphs in pool order, continuing at the cursor (the pipelined pool needs
         the order: graph i expects batch i's grouping from graph i-1)."""
+        if getattr(self, "_prefault_due", False):  # first replay after a capture: the tables' pages
+            self._prefault_due = False  # walked right before it (TableSet.prefault; r06pf_* profiles)
+            self.tables.prefault()
         i, nb = self.pool_cursor, len(self.pool_graphs)
         k = getattr(self, "steps_per_graph", 1)
         mid = getattr(self, "pool_mid", {})
@@ -752,6 +756,7 @@ class FusedTwoTowerStep:
                     raise _lib.TTError("capture_ring: batch columns must match the step's id dtype and batch")
             staged.append((list(cols), labels.to(torch.int32).contiguous()))
         self._ring_inputs = staged
+        self._prefault_due = True  # the next replay walks the tables' pages first (TableSet.prefault)
         self.ring_reset()
         self.sync_weights()
         self.ring_prime(staged[0][0], 0)
@@ -787,6 +792,7 @@ class FusedTwoTowerStep:
         self.ring_offset = offset % n
         self.ring_graphs = [self._ring_graph(span(j, k)) for j in range(0, n, k)] if k > 1 else list(self.ring_small)
         self.ring_mid = {}
+        self._prefault_due = True  # the next replay walks the tables' pages first (TableSet.prefault)
         sz = k // 2 if k & (k - 1) == 0 else 0
         while sz >= 2:
             self.ring_mid[sz] = [self._ring_graph(span(j, sz)) for j in range(0, n, sz)]
@@ -805,6 +811,9 @@ class FusedTwoTowerStep:
 
     def run(self, n: int) -> None:
         """Replay n production steps from the ring, continuing at the cursor."""
+        if getattr(self, "_prefault_due", False):  # first replay after a capture: the tables' pages
+            self._prefault_due = False  # walked right before it (TableSet.prefault; r06pf_* profiles)
+            self.tables.prefault()
         i, nb, k = self.ring_cursor, len(self.ring_small), self.ring_k
         mid = self.ring_mid
         while n > 0:
@@ -872,6 +881,9 @@ class FusedTwoTowerStep:
 
     def replay(self, i: Optional[int] = None) -> None:
         """Replay the single-step graph, or pool graph ``i`` (which runs ``steps_per_graph`` steps)."""
+        if getattr(self, "_prefault_due", False):  # first replay after a capture: the tables' pages
+            self._prefault_due = False  # walked right before it (TableSet.prefault; r06pf_* profiles)
+            self.tables.prefault()
         if i is None:
             self.graph.replay()
         else:
@@ -913,6 +925,7 @@ class FusedTwoTowerStep:
                     raise _lib.TTError("capture_pool: batch columns must match the step's id dtype and batch")
             staged.append((list(cols), labels.to(torch.int32).contiguous()))
         self._pool_inputs = getattr(self, "_pool_inputs", []) + [staged]  # alive as long as any graph
+        self._prefault_due = True  # the next replay walks the tables' pages first (TableSet.prefault)
         self.pool_graphs = []
         for j in range(0, len(staged), k):
             self.capture(staged[j:j + k], keep_graph=keep_graph)

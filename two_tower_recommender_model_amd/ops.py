@@ -272,6 +272,17 @@ class TableSet:
             a = (1.0 / max(1, self.rows[t])) ** 0.5
             self.table_view(t).uniform_(-a, a, generator=generator)
 
+    def prefault(self, page_bytes: int = 4096) -> None:
+        """Walk every page of the weights and the row-wise state once (tt_table_prefault, one 4-byte
+        load per page, on the current stream): setup before a run's first step, so its first ~30
+        steps do not pay the cold page-table walks (profiles/r06dr_overhead4.log: +2 us a step over
+        a 20-step run in a fresh process)."""
+        if not hasattr(self, "_sink"):
+            self._sink = torch.zeros(1, dtype=torch.int32, device=self.device)
+        for buf in (self.weights, self.state):
+            check(_lib_().tt_table_prefault(ptr(buf), buf.numel() * buf.element_size(), page_bytes, ptr(self._sink),
+                                            stream_handle(self.device)), "table_prefault")
+
     # -- forward
     def pooled_fwd(self, values: torch.Tensor, offsets: torch.Tensor, B: int, pooling: int = TT_POOL_SUM,
                    out: Optional[torch.Tensor] = None, bounds_check: bool = False) -> torch.Tensor:

@@ -1287,6 +1287,7 @@ class FusedShardedTwoTowerStep:
         staged = self._staged(batches)
         self._pool_inputs = [staged]
         self.pool_k = k
+        self._prefault_due = True  # the next replay walks the tables' pages first (TableSet.prefault)
         # stage batch 0 (and place batch 1's keys) eagerly, then retire every eager collective
         self.prime(staged[0][0], 0, staged[1][0])
         self.cursor = 0
@@ -1312,6 +1313,9 @@ class FusedShardedTwoTowerStep:
     def run(self, n: int) -> None:
         """Replay n pipelined steps from the pool, continuing at the cursor (re-primed at the pool's
         first batch after ``reset_pipeline`` / ``load_state_dict``)."""
+        if getattr(self, "_prefault_due", False):  # first replay after a capture: the tables' pages
+            self._prefault_due = False  # walked right before it (TableSet.prefault; r06pf_* profiles)
+            self.tables.prefault()
         if not self.small_graphs:
             raise _lib.TTError("run: no captured pool (capture_pool first)")
         if self.cursor is None:

@@ -307,6 +307,7 @@ class FusedShardedKJTStep:
             raise _lib.TTError("capture_pool: the comm is not graph-capturable")
         staged = [(v, o.to(torch.int32).contiguous(), l.to(torch.int32).contiguous()) for v, o, l in batches]
         self._pool_inputs = staged
+        self._prefault_due = True  # the next replay walks the tables' pages first (TableSet.prefault)
         self.warmup()
         self.comm.retire()
         self.graphs = []
@@ -340,6 +341,9 @@ class FusedShardedKJTStep:
         torch.cuda.synchronize(self.device)
 
     def run(self, n: int) -> None:
+        if getattr(self, "_prefault_due", False):  # first replay after a capture: the tables' pages
+            self._prefault_due = False  # walked right before it (TableSet.prefault; r06pf_* profiles)
+            self.tables.prefault()
         for _ in range(n):
             self.graphs[self.cursor].replay()
             self.cursor = (self.cursor + 1) % len(self.graphs)
