@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--sweep", default="none", choices=["none", "page", "frag", "pf", "busy", "busyread"],
                     help="before anything: read one float per 4 KB page / per 2 MB of the tables")
     ap.add_argument("--perstep", type=int, default=0, help="first: this many single-step graphs, timed each")
+    ap.add_argument("--passes", type=int, default=None, help="TableSet.prefault passes (default: the library's)")
     a = ap.parse_args()
+    if a.passes is not None:
+        from two_tower_recommender_model_amd import ops
+        ops.TableSet.prefault.__defaults__ = (4096, a.passes)
     num_users, num_items, D, B, layers = bench.WORKLOADS["northstar"]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)

@@ -272,14 +272,16 @@ class TableSet:
             a = (1.0 / max(1, self.rows[t])) ** 0.5
             self.table_view(t).uniform_(-a, a, generator=generator)
 
-    def prefault(self, page_bytes: int = 4096) -> None:
-        """Walk every page of the weights and the row-wise state once (tt_table_prefault, one 4-byte
-        load per page, on the current stream): setup before a run's first step, so its first ~30
-        steps do not pay the cold page-table walks (profiles/r06dr_overhead4.log: +2 us a step over
-        a 20-step run in a fresh process)."""
+    def prefault(self, page_bytes: int = 4096, passes: int = 2) -> None:
+        """Walk every page of the weights and the row-wise state (tt_table_prefault, one 4-byte load
+        per page, on the current stream), ``passes`` times: setup before a run's first step, so its
+        first ~30 steps do not pay the cold page-table walks (profiles/r06dr_overhead4.log: +2 us a
+        step over a 20-step run in a fresh process). One pass from cold took 1.4 ms and left the
+        first run ~1 us a step slow; a second (0.4 ms) took off ~0.4 us more, four passes were
+        worse than two (the walks' lines displace the run's own; profiles/r06pf6_overhead.log)."""
         if not hasattr(self, "_sink"):
             self._sink = torch.zeros(1, dtype=torch.int32, device=self.device)
-        for buf in (self.weights, self.state):
+        for buf in [self.weights, self.state] * passes:
             check(_lib_().tt_table_prefault(ptr(buf), buf.numel() * buf.element_size(), page_bytes, ptr(self._sink),
                                             stream_handle(self.device)), "table_prefault")
 
