@@ -429,6 +429,21 @@ def synth_kjt_batches(num_users, num_items, B, maxlen, n, device, ids, seed):
     return out
 
 
+def end_timed_region(t0: float, dev) -> tuple:
+    """Close a multi-rank timed region: this rank's clock is read right after its device
+    synchronize, then the closing barrier runs, then the MAX over ranks. Every rank started its
+    clock on leaving the same opening barrier, so max(end - t0) is when the last rank's steps were
+    done; the closing barrier's own collective (35-60 us over RCCL even at world 1,
+    profiles/r06sh_barrier.log) is not the job's work. Returns (seconds, seconds with the closing
+    barrier), both max over ranks; the second is reported beside the line."""
+    t1 = time.perf_counter()
+    dist.barrier()
+    t2 = time.perf_counter()
+    dt = torch.tensor([t1 - t0, t2 - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    return float(dt[0]), float(dt[1])
+
+
 def run_multihot(args):
     """SURVEY 8(d) config 5 shape at N = 1: the fused step on multi-hot KJT input (tt_pooled_fwd ->
     fused towers T1 -> tiled tt_bwd_prepare (side stream) -> T2/T3 (side stream) ->
@@ -587,10 +602,7 @@ def run_multi_kjt(args, world, rank, local_rank):
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
-    dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], device=dev)
-    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt)
+    dt, dt_barrier = end_timed_region(t0, dev)
     step.check()
     loss = float(step.loss)
     step.release_graphs()
@@ -614,7 +626,8 @@ def run_multi_kjt(args, world, rank, local_rank):
     info = {"plan": f"users table-wise (rank {world - 1}) + items row-wise", "ids": args.ids, "capacity": cap,
             "exchange_bytes_per_rank": {"A_ids": 4 * step.sendA.numel(), "B_pooled": 4 * step.sendB.numel(),
                                         "C_grads": 4 * step.sendC.numel()},
-            "collectives_per_step": 3, "mode": "hipgraph" if graphs else "eager", "exchange": xdesc}
+            "collectives_per_step": 3, "mode": "hipgraph" if graphs else "eager", "exchange": xdesc,
+            "ms_per_step_with_closing_barrier": round(dt_barrier / args.steps * 1e3, 5)}
     return world * args.steps * B / dt, dt / args.steps * 1e3, loss, info, roofline
 
 
@@ -852,11 +865,8 @@ def run_dropin(args, world=1, rank=0, local_rank=0):
             loss, _, _ = pipeline.progress(it)
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
-        dt = torch.tensor([time.perf_counter() - t0], device=dev)
-        if world > 1:
-            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        return float(dt), float(loss)
+            return end_timed_region(t0, dev)[0], float(loss)
+        return time.perf_counter() - t0, float(loss)
 
     pipeline = TrainPipelineSparseDist(model, optimizer, dev)
     pipeline._model.train()
@@ -973,10 +983,7 @@ def run_multi(args, world, rank, local_rank):
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
-    dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], device=dev)
-    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt)
+    dt, dt_barrier = end_timed_region(t0, dev)
     step.check()
     loss = float(step.loss)
     step.release_graphs()  # before the process group is destroyed
@@ -1001,6 +1008,7 @@ def run_multi(args, world, rank, local_rank):
             "exchange_A_bytes_sent": 4 * step.A_total,
             "exchange_B_bytes_sent": 2 * D * world * step.S[r],
             "collectives_per_step": 2, "mode": mode,
+            "ms_per_step_with_closing_barrier": round(dt_barrier / args.steps * 1e3, 5),
             "exchange": xdesc + ("; producers store at the destinations" if getattr(step, "direct", False) else "")
                         + ("; launch U / Adam signal and wait in-launch" if getattr(step, "merged", False) else ""),
             "overlap": "T2 (tower weight gradients) on a parallel graph branch beside exchange A + the owner's "
