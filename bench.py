@@ -16,8 +16,9 @@ data-parallel towers, two fixed-size all-to-alls per step captured into the HIP 
 kernels; config 5: `sharded_kjt.FusedShardedKJTStep`, three). `python bench.py --gpus N` without a
 launcher starts `torch.distributed.run --nproc-per-node N` itself as a child process (before any GPU
 call), relays its output and exits with its status; under a launcher the world size must equal
---gpus. Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize + barrier, max over
-ranks; rank 0 prints ONE JSON line.
+--gpus. Timing: W untimed steps, synchronize + barrier, K timed steps, synchronize (each rank's clock
+read here) + barrier, max over ranks (the closing barrier's collective outside the interval, its
+inclusive figure reported beside: end_timed_region); rank 0 prints ONE JSON line.
 Also reported: the embedding path's dominant kernel against the HBM roofline (HIP events on its
 own stream) and the CPU restatement's pairs/s on this host (rank 0, N = 1, bounded sample).
 """
