@@ -590,6 +590,15 @@ int tt_kjt_admit(int F, int64_t B, const void* values, int id_dtype, int64_t nnz
  * of 4 (4096 = the GPU page). ABI 4. */
 int tt_table_prefault(const void* base, size_t bytes, size_t page_bytes, uint32_t* sink, void* stream);
 
+/* SETUP ONLY (allocating, synchronising): device memory for embedding tables on the current
+ * device, physically contiguous when the driver can give it (hipDeviceMallocContiguous: the largest
+ * page fragments for the random row gathers; *contiguous = 1), plain device memory otherwise
+ * (*contiguous = 0; contiguous may be NULL). Uninitialised. Free with tt_table_free (NULL is a
+ * no-op). No reference counterpart: FBGEMM's TBE allocates its weights through the caching
+ * allocator (torchrec, reached from 03_model_training.py:812-815). ABI 4. */
+int tt_table_alloc(size_t bytes, void** out, int* contiguous);
+int tt_table_free(void* p);
+
 /* ---- multi-hot sharded step (config 5, sharded_kjt.py): fixed-size exchanges ------------------------
  * TorchRec's KJTAllToAll / PooledEmbeddingsAllToAll / reduce-scatter (torchrec/distributed/embeddingbag.py,
  * reached from 03_model_training.py:812-815) exchange variable split sizes the host reads every batch;

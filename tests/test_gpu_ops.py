@@ -410,3 +410,27 @@ def test_table_prefault_argument_errors(ops, device):
     assert lib.tt_table_prefault(buf.data_ptr(), 64, 6, sink.data_ptr(), None) != 0
     assert lib.tt_table_prefault(buf.data_ptr(), 64, 4096, None, None) != 0
     assert lib.tt_table_prefault(None, 0, 4096, sink.data_ptr(), None) == 0
+
+
+def test_table_alloc_large_tableset_matches_caching_allocator(ops, device):
+    """TableSet buffers >= TABLE_ALLOC_MIN_BYTES come from tt_table_alloc (contiguous when the
+    driver can); the same weights in caching-allocator memory give bit-identical pooled sums, and
+    the memory is released with the last view (a second allocation of the same size succeeds)."""
+    rows = ops.TABLE_ALLOC_MIN_BYTES // (128 * 4) + 1000
+    for _ in range(2):
+        ts = ops.TableSet([rows, 64], [128, 128], [0, 1], device)
+        assert isinstance(ts.weights, torch.Tensor) and ts.weights.dtype == torch.float32
+        assert ts.weights.numel() >= rows * 128 and float(ts.state.abs().sum()) == 0.0
+        ts.init_uniform_(torch.Generator(device=device).manual_seed(3))
+        ref_ts = ops.TableSet([rows, 64], [128, 128], [0, 1], device, weights=ts.weights.clone())
+        g = torch.Generator(device=device).manual_seed(4)
+        B = 512
+        values = torch.cat([torch.randint(0, rows, (B,), device=device, generator=g),
+                            torch.randint(0, 64, (B,), device=device, generator=g)])
+        offsets = torch.arange(0, 2 * B + 1, dtype=torch.int32, device=device)
+        a = ts.pooled_fwd(values, offsets, B)
+        b = ref_ts.pooled_fwd(values, offsets, B)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        del ts, ref_ts, a, b
+        torch.cuda.synchronize()

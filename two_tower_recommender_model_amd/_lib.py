@@ -325,6 +325,8 @@ SIGNATURES = {
     "tt_peer_exchange": (_int, [C.c_void_p, _vp, _vp, C.c_double, _vp]),
     "tt_kjt_admit": (_int, [_int, _i64, _vp, _int, _i64, _vp, _pi64, _pi64, _pi32, _int, _vp, _vp]),
     "tt_table_prefault": (_int, [_vp, _sz, _sz, _vp, _vp]),
+    "tt_table_alloc": (_int, [_sz, _pvp, C.POINTER(C.c_int)]),
+    "tt_table_free": (_int, [_vp]),
 }
 
 COMPUTE_ENTRY_POINTS = [

@@ -1367,6 +1367,34 @@ int tt_table_prefault(const void* base, size_t bytes, size_t page_bytes, uint32_
   return check_launch("table_prefault");
 }
 
+int tt_table_alloc(size_t bytes, void** out, int* contiguous) {
+  if (!out || bytes == 0) return fail(TT_EINVAL, "table_alloc: null output or zero bytes");
+  *out = nullptr;
+  // one physically contiguous range when the driver has it: the largest page fragments, so the
+  // random row gathers walk fewer translation levels (profiles/r06al_alloc.log)
+  hipError_t e = hipExtMallocWithFlags(out, bytes, hipDeviceMallocContiguous);
+  int contig = 1;
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    contig = 0;
+    e = hipMalloc(out, bytes);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return fail((int)e, std::string("table_alloc: ") + hipGetErrorString(e));
+  }
+  if (contiguous) *contiguous = contig;
+  return TT_OK;
+}
+
+int tt_table_free(void* p) {
+  if (!p) return TT_OK;
+  hipError_t e = hipFree(p);
+  return e == hipSuccess ? TT_OK : fail((int)e, std::string("table_free: ") + hipGetErrorString(e));
+}
+
 int tt_pooled_fwd(const float* weights, const tt_table_meta_t* tables, int T,
                   const tt_feature_meta_t* features, int F, int64_t B, const void* values,
                   int id_dtype, const int32_t* offsets, int pooling, float* out, int64_t ldo,

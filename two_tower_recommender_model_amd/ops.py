@@ -171,6 +171,42 @@ def block_bucketize(lengths: torch.Tensor, offsets: torch.Tensor, values: torch.
 # ---- a4 / a8: embedding tables ----------------------------------------------------------------
 
 
+# TableSet buffers of at least this many bytes come from tt_table_alloc (physically contiguous when
+# the driver can: -0.45 us a north-star step against the caching allocator, profiles/r06al_alloc.log)
+TABLE_ALLOC_MIN_BYTES = 256 << 20
+
+
+class _TableMemory:
+    """One tt_table_alloc allocation as __cuda_array_interface__ bytes for torch.as_tensor; the
+    tensor keeps this object alive and it frees the memory with the last view."""
+
+    def __init__(self, nbytes: int, device: torch.device):
+        p, flag = C.c_void_p(), C.c_int(0)
+        with torch.cuda.device(device):
+            check(_lib_().tt_table_alloc(nbytes, C.byref(p), C.byref(flag)), "table_alloc")
+        self.ptr, self.contiguous = p.value, bool(flag.value)
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                         "version": 2}
+
+    def __del__(self):
+        if self.ptr:
+            try:
+                _lib_().tt_table_free(self.ptr)
+            except Exception:  # interpreter shutdown: the process frees it
+                pass
+            self.ptr = None
+
+
+def table_empty(n: int, device: torch.device, dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """An uninitialised 1-D device tensor for table storage: tt_table_alloc memory at
+    TABLE_ALLOC_MIN_BYTES and above, the caching allocator below."""
+    nbytes = n * torch.tensor([], dtype=dtype).element_size()
+    if nbytes < TABLE_ALLOC_MIN_BYTES or torch.device(device).type != "cuda":
+        return torch.empty(n, dtype=dtype, device=device)
+    mem = _TableMemory(nbytes, torch.device(device))
+    return torch.as_tensor(mem, device=device).view(dtype)
+
+
 class TableSet:
     """Flat fp32 weight buffer + flat row-wise state for T local tables (FBGEMM-TBE-style layout:
     one allocation, per-table element offsets), with the feature->table map of a KJT.
@@ -202,9 +238,9 @@ class TableSet:
         self.total_weights = w
         self.total_rows = s
         if weights is None:
-            weights = torch.empty(max(1, w), dtype=torch.float32, device=self.device)
+            weights = table_empty(max(1, w), self.device)
         self.weights = weights
-        self.state = torch.zeros(max(1, s), dtype=torch.float32, device=self.device)
+        self.state = table_empty(max(1, s), self.device).zero_()
         if out_offsets is None:
             out_offsets, o = [], 0
             for t in self.feature_table:
