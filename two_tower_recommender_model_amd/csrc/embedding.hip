@@ -1334,15 +1334,11 @@ static int pack_cols(ColArgs& ca, int F, const void* const* cols, const int64_t*
 
 static int check_ws(void* workspace, size_t ws_bytes, int64_t max_lookups, const char* what);
 
-}  // namespace tt
-
-using namespace tt;
-
 // One 4-byte load per page of the tables (tt_table_prefault): the address translations of every
 // page walked once at setup, so the first training steps do not pay the page-table misses a cold
 // process otherwise takes ~30 steps to absorb (profiles/r06dr_overhead4.log). The loads are
-// XOR-folded and stored only if the fold equals a value no sum of table words is expected to give,
-// so they cannot be dropped; the sink is written by at most a lane (vector store).
+// XOR-folded and stored only if the fold equals one fixed value, so they cannot be dropped; in
+// practice the sink is never written (and if so, by a vector store).
 __global__ void __launch_bounds__(256) table_prefault_kernel(const uint32_t* __restrict__ base, int64_t words,
                                                              int64_t stride, uint32_t* sink) {
   const int64_t n = (words + stride - 1) / stride;
@@ -1351,6 +1347,10 @@ __global__ void __launch_bounds__(256) table_prefault_kernel(const uint32_t* __r
     acc ^= base[p * stride];
   if (acc == 0x7fc0dead) sink[0] = acc;
 }
+
+}  // namespace tt
+
+using namespace tt;
 
 extern "C" {
 
