@@ -28,9 +28,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--alloc", default="torch", choices=["torch", "contiguous"])
     ap.add_argument("--runs", type=int, default=5)
+    ap.add_argument("--workload", default="northstar")
+    ap.add_argument("--min-bytes", type=int, default=None, help="ops.TABLE_ALLOC_MIN_BYTES for this run")
     ap.add_argument("--steps", type=int, default=200)
     a = ap.parse_args()
-    num_users, num_items, D, B, layers = bench.WORKLOADS["northstar"]
+    num_users, num_items, D, B, layers = bench.WORKLOADS[a.workload]
+    if a.min_bytes is not None:
+        ops.TABLE_ALLOC_MIN_BYTES = a.min_bytes
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     Ns = [num_users, num_items]
