@@ -433,4 +433,8 @@ def test_table_alloc_large_tableset_matches_caching_allocator(ops, device):
         torch.cuda.synchronize()
         assert torch.equal(a, b)
         del ts, ref_ts, a, b
-        torch.cuda.synchronize()
+        import gc
+        gc.collect()
+        assert len(ops._PENDING_FREE) >= 1  # the weights (the state is below the threshold), freed later
+    ops.free_tables()
+    assert not ops._PENDING_FREE

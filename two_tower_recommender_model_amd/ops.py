@@ -176,24 +176,41 @@ def block_bucketize(lengths: torch.Tensor, offsets: torch.Tensor, values: torch.
 TABLE_ALLOC_MIN_BYTES = 256 << 20
 
 
+# tt_table_alloc memory whose last view is gone, freed at the next table allocation (or free_tables)
+# rather than in __del__: a garbage collection can run inside a graph capture or while a stream
+# still reads the buffer, and hipFree there would break the capture
+_PENDING_FREE: List[Tuple[int, int]] = []
+
+
+def free_tables() -> None:
+    """Free the table memory no tensor refers to any more (synchronises the devices involved).
+    Outside a capture only; table_empty calls it before allocating."""
+    if not _PENDING_FREE or torch.cuda.is_current_stream_capturing():
+        return
+    for dev in sorted({d for _, d in _PENDING_FREE}):
+        torch.cuda.synchronize(dev)
+    while _PENDING_FREE:
+        p, _ = _PENDING_FREE.pop()
+        check(_lib_().tt_table_free(p), "table_free")
+
+
 class _TableMemory:
     """One tt_table_alloc allocation as __cuda_array_interface__ bytes for torch.as_tensor; the
-    tensor keeps this object alive and it frees the memory with the last view."""
+    tensor keeps this object alive, and with the last view the memory joins _PENDING_FREE."""
 
     def __init__(self, nbytes: int, device: torch.device):
+        free_tables()
         p, flag = C.c_void_p(), C.c_int(0)
         with torch.cuda.device(device):
             check(_lib_().tt_table_alloc(nbytes, C.byref(p), C.byref(flag)), "table_alloc")
         self.ptr, self.contiguous = p.value, bool(flag.value)
+        self.device = device.index if device.index is not None else torch.cuda.current_device()
         self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False),
                                          "version": 2}
 
     def __del__(self):
         if self.ptr:
-            try:
-                _lib_().tt_table_free(self.ptr)
-            except Exception:  # interpreter shutdown: the process frees it
-                pass
+            _PENDING_FREE.append((self.ptr, self.device))
             self.ptr = None
 
 
